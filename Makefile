@@ -1,0 +1,36 @@
+# Build: the HIP engine (gfx950) and the CPU oracle (test infrastructure only).
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+ARCH    ?= gfx950
+JOBS    ?= 8
+
+LIB     := wiser_amd/_lib/libwiser_hip.so
+ORACLE  := oracle/_build/liboracle.so
+SRCS    := wiser_amd/csrc/writer.cc wiser_amd/csrc/index.cc wiser_amd/csrc/engine.cc \
+           wiser_amd/csrc/kernels.hip
+HDRS    := $(wildcard wiser_amd/csrc/*.h) include/wiser_hip.h
+OBJDIR  := wiser_amd/_lib/obj
+OBJS    := $(patsubst wiser_amd/csrc/%,$(OBJDIR)/%.o,$(SRCS))
+
+# -ffp-contract=off everywhere: the reference build has no FMA (CMakeLists.txt:6,12)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall \
+            -Wno-unused-function
+ORAFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -shared
+
+all: $(LIB) $(ORACLE)
+
+$(OBJDIR)/%.o: wiser_amd/csrc/% $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+
+$(ORACLE): oracle/oracle.cc oracle/oracle.h
+	@mkdir -p oracle/_build
+	$(CXX) $(ORAFLAGS) -o $@ oracle/oracle.cc -lpthread
+
+clean:
+	rm -rf wiser_amd/_lib oracle/_build
+
+.PHONY: all clean

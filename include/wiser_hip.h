@@ -1,0 +1,144 @@
+/*
+ * wiser_hip.h -- C ABI of the MI355X conjunctive-query + BM25 top-k engine for
+ * the Vacuum (WiSER) index.  Plain pointers and sizes only; no C++ or torch
+ * types cross this boundary.  Every function returns 0 (WSR_OK) or a negative
+ * WSR_E_* code and never aborts; wsr_last_error() gives a thread-local message.
+ *
+ * Reference interfaces replaced (paths under /root/reference/src/qq_mem/src):
+ *   wsr_open / wsr_close ...... VacuumEngine::Load (vacuum_engine.h:144-180) and
+ *                               CreateSearchEngine("vacuum:vacuum_dump:<dir>")
+ *                               (engine_factory.h:21-50)
+ *   wsr_term_count ............ SearchEngineServiceNew::TermCount (engine_services.h:20,
+ *                               vacuum_engine.h:182-185)
+ *   wsr_lookup ................ VacuumInvertedIndex::FindTermIndexResult +
+ *                               VacuumPostingListIterator::Size
+ *                               (vacuum_engine.h:75-99,187-199, flash_iterators.h:1030-1032)
+ *   wsr_search_batch .......... VacuumEngine::Search (vacuum_engine.h:201-258) ->
+ *                               qq_search::ProcessQueryDelta (query_processing.h:956-979),
+ *                               n queries per call instead of one
+ *   wsr_batch_* ............... the same, split into upload / enqueue / fetch so that a
+ *                               serving loop (grpc_server_impl.h:382-389) or a bench
+ *                               (engine_bench.cc:255-279) can keep query batches
+ *                               resident in HBM and overlap them
+ *   wsr_build_* / wsr_gen_* ... index writer FlashEngineDumper::{LoadLocalDocuments,Dump}
+ *                               (flash_engine_dumper.h:674-744) and the query generator
+ *                               tools/gen_synthetic_log.py:191-214 (host only, no GPU)
+ *
+ * Threading: a handle may be used from several threads; calls on one handle
+ * are serialised internally (the reference's engine is shared read-only by
+ * its gRPC threads, grpc_server_impl.h:260-263).
+ */
+#ifndef WISER_HIP_H
+#define WISER_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSR_MAX_TERMS 8
+#define WSR_MAX_K 64
+
+enum {
+  WSR_OK = 0,
+  WSR_E_INVALID = -1,   /* bad argument */
+  WSR_E_IO = -2,        /* missing / malformed index files */
+  WSR_E_HIP = -3,       /* HIP runtime error (no device, out of memory, ...) */
+  WSR_E_LIMIT = -4,     /* n_terms > WSR_MAX_TERMS or k > WSR_MAX_K */
+  WSR_E_INTERNAL = -5
+};
+
+typedef struct wsr_handle wsr_handle;
+typedef struct wsr_batch wsr_batch;
+
+typedef struct wsr_open_opts {
+  int32_t device;     /* HIP device ordinal */
+  uint32_t doc_lo;    /* doc-id shard [doc_lo, doc_hi); doc_hi = 0 means all docs */
+  uint32_t doc_hi;
+  int32_t threads;    /* host threads for the load-time directory build (0 = all) */
+} wsr_open_opts;
+
+/* A query with its terms already resolved by wsr_lookup (list id per term, in
+ * query order; -1 = term not in the index => empty result, as the reference). */
+typedef struct wsr_query {
+  int32_t n_terms;
+  int32_t k;          /* n_results; 0 => empty result */
+  int32_t list_ids[WSR_MAX_TERMS];
+} wsr_query;
+
+typedef struct wsr_hit {
+  int32_t doc_id;
+  int32_t pad;
+  double score;       /* f64 BM25, bit-identical to the reference engine */
+} wsr_hit;
+
+/* Per-batch counters of the last run (for the roofline / profiles). */
+typedef struct wsr_batch_stats {
+  uint64_t work_items;       /* segments processed */
+  uint64_t survivors;        /* docs in every list (scored) */
+  uint64_t driver_blocks;    /* 128-posting blocks decoded from driver lists */
+  uint64_t other_blocks;     /* blocks decoded from the other lists */
+  uint64_t algo_bytes;       /* sum over queries of docid+tf span bytes of its lists
+                                + survivors * 1 B + k * 12 B */
+  double plan_ms, segment_ms, replay_ms;  /* HIP-event times on the engine stream */
+} wsr_batch_stats;
+
+const char* wsr_last_error(void);
+const char* wsr_version(void);
+
+/* ---- engine ---------------------------------------------------------- */
+int wsr_open(const char* vacuum_dir, const wsr_open_opts* opts, wsr_handle** out);
+void wsr_close(wsr_handle* h);
+int wsr_term_count(wsr_handle* h, int32_t* out);
+int wsr_n_docs(wsr_handle* h, int32_t* out);
+/* list id (or -1) and document frequency (0 if absent) of one term */
+int wsr_lookup(wsr_handle* h, const char* term, int32_t* list_id, int32_t* doc_freq);
+/* bytes of docid+tf span held in HBM for a list (0 if absent from this shard) */
+int wsr_list_bytes(wsr_handle* h, int32_t list_id, uint64_t* out);
+
+/* Run nq queries synchronously.  hits: nq * hit_stride entries (hit_stride >=
+ * every query's k); n_hits[q] = entries written for query q. */
+int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t hit_stride,
+                     wsr_hit* hits, int32_t* n_hits);
+
+/* ---- resident batches ------------------------------------------------ */
+int wsr_batch_create(wsr_handle* h, int32_t max_queries, int32_t hit_stride, wsr_batch** out);
+void wsr_batch_destroy(wsr_handle* h, wsr_batch* b);
+/* copy queries to HBM (synchronous) and size the event workspace */
+int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq);
+/* enqueue plan + segment + replay kernels on the engine stream (asynchronous) */
+int wsr_batch_run(wsr_handle* h, wsr_batch* b);
+/* wait for the engine stream */
+int wsr_sync(wsr_handle* h);
+/* copy results to the host (waits for the stream) */
+int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits);
+int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
+/* device pointers of the batch's results (for collectives on the caller's side) */
+int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits);
+
+/* Decode one block of a list on the device (test hook for the decoder):
+ * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */
+int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,
+                           uint32_t* out, int32_t* count);
+
+/* ---- index building (host only; no GPU needed) ----------------------- */
+typedef struct wsr_build_stats {
+  int64_t n_docs, n_terms, n_postings, vacuum_bytes, docs_char4_ge_0x80;
+  double avg_length;
+} wsr_build_stats;
+
+/* format: "TOKEN_ONLY" or "WITH_POSITIONS"; n_rows < 0 reads every row */
+int wsr_build_from_linedoc(const char* linedoc, int64_t n_rows, const char* format,
+                           const char* out_dir, wsr_build_stats* st);
+int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, double zipf_s,
+                        uint64_t seed, int32_t with_positions, int32_t threads,
+                        wsr_build_stats* st);
+int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                         const char* out_path, int64_t* n_written);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WISER_HIP_H */

@@ -1,0 +1,765 @@
+// TEST INFRASTRUCTURE ONLY -- see oracle.h.  A single-threaded-per-query CPU
+// restatement of the reference's query path, written from its behaviour; each
+// piece cites the reference file:line it restates (paths relative to
+// /root/reference/src/qq_mem/src).  Deliberately iterator-shaped like the
+// reference (linear skip-row walk, whole-pack unpack, per-posting heap test)
+// so that it doubles as the CPU baseline timed by bench.py.
+#include "oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <fcntl.h>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <thread>
+#include <unistd.h>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int64_t> g_ub_neg{0};
+
+constexpr int kPack = 128;                 // PACK_ITEM_CNT, packed_value.h:13
+constexpr uint8_t kSkipMagic = 0xA3;       // types.h:44
+constexpr uint8_t kPostingMagic = 0xF4;    // types.h:46
+constexpr uint8_t kPackMagic = 0xD6;       // types.h:47
+constexpr uint8_t kVIntsMagic = 0x9B;      // types.h:48
+constexpr uint8_t kVacuumMagic = 0x88;     // types.h:50
+
+// utils.h:249-266 varint_decode_64bit
+int varint_decode(const uint8_t* b, uint64_t* v) {
+  uint64_t r = b[0] & 0x7f;
+  int i = 1;
+  if (b[0] < 0x80) { *v = b[0]; return 1; }
+  while (b[i - 1] & 0x80) { r += static_cast<uint64_t>(b[i] & 0x7f) << (7 * i); ++i; }
+  *v = r;
+  return i;
+}
+
+// utils.cc:257-270 varint_encode
+int varint_encode(uint64_t v, uint8_t* out) {
+  int i = 0;
+  while (i == 0 || v > 0) { out[i++] = static_cast<uint8_t>((v & 0x7f) | 0x80); v >>= 7; }
+  out[i - 1] &= 0x7f;
+  return i;
+}
+
+// utils.h:286-294
+int num_bits(uint32_t v) { int n = 0; while (v) { v >>= 1; ++n; } return n; }
+
+// utils.h:301-313 UintToChar4 (returns the char's bit pattern)
+uint8_t char4_encode(uint32_t val) {
+  if (val < 0x08) return static_cast<uint8_t>(val & 0xff);
+  int shift = num_bits(val) - 4;
+  uint32_t enc = (val >> shift) & 0x07;
+  enc |= static_cast<uint32_t>(shift + 1) << 3;
+  return static_cast<uint8_t>(enc);
+}
+
+// utils.h:315-329 Char4ToUint
+uint32_t char4_decode(uint8_t c) {
+  uint32_t bits = c & 0x07;
+  int shift = ((c & 0xff) >> 3) - 1;
+  if (shift == -1) return bits;
+  return (bits | 0x08) << shift;
+}
+
+// LittleIntPacker turbounpack32 (turbobitpacking32.c:3863-3868, layout from
+// scripts/turbopacking32.py:83-112): value j at bits [j*b, j*b+b) of the
+// little-endian stream of 64-bit words.
+void turbo_unpack(const uint8_t* in, int b, uint32_t* out) {
+  for (int j = 0; j < kPack; ++j) {
+    uint64_t v = 0;
+    for (int k = 0; k < b; ++k) {
+      uint64_t bit = static_cast<uint64_t>(j) * b + k;
+      v |= static_cast<uint64_t>((in[bit >> 3] >> (bit & 7)) & 1) << k;
+    }
+    out[j] = static_cast<uint32_t>(v);
+  }
+}
+
+// turbopack32 restated the same way (packed_value.h:87-128 caller)
+void turbo_pack(const uint32_t* in, int b, uint8_t* out) {
+  std::memset(out, 0, 16 * b);
+  for (int j = 0; j < kPack; ++j)
+    for (int k = 0; k < b; ++k)
+      if ((in[j] >> k) & 1) {
+        uint64_t bit = static_cast<uint64_t>(j) * b + k;
+        out[bit >> 3] |= static_cast<uint8_t>(1u << (bit & 7));
+      }
+}
+
+// scoring.h:21-25
+double es_idf(int doc_count, int doc_freq) {
+  return std::log(1 + (doc_count - doc_freq + 0.5) / (doc_freq + 0.5));
+}
+
+// Bm25Similarity (scoring.h:43-97)
+struct Bm25 {
+  static constexpr double k1 = 1.2, b = 0.75;
+  double avg = 1;
+  double cache[256];
+  void reset(double a) {
+    avg = a;
+    for (int i = 0; i < 256; ++i) {
+      uint32_t fl = char4_decode(static_cast<uint8_t>(i & 0xff));
+      cache[i] = k1 * (1 - b + b * fl / avg);
+    }
+  }
+  double tfnorm_lossy(int freq, uint8_t c) const {
+    // cache_[field_length] with a signed char index: negative for c >= 0x80 (UB in
+    // the reference).  Counted, and read as the unsigned byte like the GPU path.
+    if (static_cast<signed char>(c) < 0) ++g_ub_neg;
+    return (freq * (k1 + 1)) / (freq + cache[c]);
+  }
+};
+
+// --------------------------------------------------------------- codecs --
+// LittlePackedIntsReader (packed_value.h:184-235)
+struct PackReader {
+  const uint8_t* buf = nullptr;
+  int bits = 0;
+  uint32_t cache[kPack];
+  void reset(const uint8_t* p) {
+    buf = p;
+    if (p[0] != kPackMagic) throw std::runtime_error("pack magic");
+    bits = p[1];
+  }
+  void decode() { turbo_unpack(buf + 2, bits, cache); }
+};
+
+// VIntsIterator (packed_value.h:400-460) over VarintIteratorEndBound (compression.h:131-196)
+struct VIntsIter {
+  const uint8_t* data = nullptr;
+  int cur = 0, end = 0, next_index = 0;
+  void reset(const uint8_t* p) {
+    if (p[0] != kVIntsMagic) throw std::runtime_error("vints magic");
+    uint64_t nb;
+    int l = varint_decode(p + 1, &nb);
+    data = p + 1 + l;
+    cur = 0;
+    end = static_cast<int>(nb);
+    next_index = 0;
+  }
+  bool is_end() const { return cur >= end; }
+  uint64_t peek() const { uint64_t v; varint_decode(data + cur, &v); return v; }
+  uint64_t pop() { uint64_t v; cur += varint_decode(data + cur, &v); ++next_index; return v; }
+  int index() const { return next_index; }
+  void skip_to(int i) { while (index() < i) pop(); }
+};
+
+// SkipList::Load (flash_containers.h:354-391); only the docid/tf columns are kept.
+struct SkipEntry { uint32_t prev_doc; uint64_t doc_off, tf_off; };
+std::vector<SkipEntry> load_skip_list(const uint8_t* buf) {
+  if (buf[0] != kSkipMagic) throw std::runtime_error("skip list magic");
+  uint64_t n;
+  int l = varint_decode(buf + 1, &n);
+  const uint8_t* p = buf + 1 + l;
+  std::vector<SkipEntry> rows;
+  rows.reserve(n);
+  uint32_t pd = 0;
+  uint64_t pdo = 0, pto = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t f[7];
+    for (int k = 0; k < 7; ++k) p += varint_decode(p, &f[k]);
+    uint32_t prev = static_cast<uint32_t>(f[0] + pd);
+    uint64_t dof = f[1] + pdo, tof = f[2] + pto;
+    rows.push_back(SkipEntry{prev, dof, tof});
+    pd = prev; pdo = dof; pto = tof;
+  }
+  return rows;
+}
+
+// DocIdIterator (flash_iterators.h:121-262) with DeltaEncodedPackedIntsIterator /
+// DeltaEncodedVIntsIterator (packed_value.h:320-369,463-507).
+class DocIdIter {
+ public:
+  void reset(const uint8_t* file, const std::vector<SkipEntry>* sl, int n) {
+    file_ = file; sl_ = sl; n_ = n; fmt_ = 0; cur_ = 0;
+    skip_to(0);
+  }
+  int posting_index() const { return cur_; }
+  bool is_end() const { return cur_ == n_; }
+  uint32_t value() const {
+    if (fmt_ == 1) return static_cast<uint32_t>(pack_prev_ + pack_.cache[pack_idx_]);
+    return static_cast<uint32_t>(vprev_ + vints_.peek());
+  }
+  void advance() { skip_to(cur_ + 1); }
+  void skip_to(int posting) {
+    const int blob = posting / kPack, off = posting % kPack;
+    if (fmt_ == 0 || cur_blob() != blob) {
+      if (posting >= n_) { cur_ = n_; return; }
+      setup(blob);
+    }
+    if (fmt_ == 2) { while (vints_.index() < off) vprev_ += vints_.pop(); }
+    else { while (pack_idx_ < off) { pack_prev_ = value(); ++pack_idx_; } }
+    cur_ = posting;
+  }
+  // flash_iterators.h:181-199: linear walk over skip rows, then in-blob scan
+  void skip_forward(uint32_t val) {
+    int blob_to_go = cur_blob();
+    const int last = (n_ - 1) / kPack;
+    while (blob_to_go + 1 <= last && (*sl_)[blob_to_go + 1].prev_doc < val) ++blob_to_go;
+    const int base = blob_to_go * kPack;
+    if (blob_to_go != cur_blob()) skip_to(base);
+    if (fmt_ == 2) {
+      while (!vints_.is_end() && vprev_ + vints_.peek() < val) vprev_ += vints_.pop();
+      cur_ = base + vints_.index();
+    } else {
+      while (pack_idx_ != kPack && value() < val) { pack_prev_ = value(); ++pack_idx_; }
+      cur_ = base + pack_idx_;
+    }
+  }
+
+ private:
+  int cur_blob() const { return cur_ / kPack; }
+  void setup(int blob) {
+    const SkipEntry& e = (*sl_)[blob];
+    const uint8_t* p = file_ + e.doc_off;
+    if (p[0] == kPackMagic) {
+      fmt_ = 1; pack_.reset(p); pack_.decode(); pack_idx_ = 0; pack_prev_ = e.prev_doc;
+    } else if (p[0] == kVIntsMagic) {
+      fmt_ = 2; vints_.reset(p); vprev_ = e.prev_doc;
+    } else {
+      throw std::runtime_error("docid blob format");
+    }
+  }
+  const uint8_t* file_ = nullptr;
+  const std::vector<SkipEntry>* sl_ = nullptr;
+  int n_ = 0, cur_ = 0, fmt_ = 0;  // fmt: 0 none, 1 pack, 2 vints
+  PackReader pack_;
+  int pack_idx_ = 0;
+  long pack_prev_ = 0;
+  VIntsIter vints_;
+  long vprev_ = 0;
+};
+
+// TermFreqIterator (flash_iterators.h:43-118)
+class TfIter {
+ public:
+  void reset(const uint8_t* file, const std::vector<SkipEntry>* sl) { file_ = file; sl_ = sl; fmt_ = 0; cur_ = 0; }
+  uint32_t at(int posting) {
+    const int blob = posting / kPack, off = posting % kPack;
+    if (fmt_ == 0 || cur_ / kPack != blob) {
+      const uint8_t* p = file_ + (*sl_)[blob].tf_off;
+      if (p[0] == kPackMagic) { fmt_ = 1; pack_.reset(p); pack_.decode(); }
+      else { fmt_ = 2; vints_.reset(p); }
+    }
+    cur_ = posting;
+    if (fmt_ == 1) return pack_.cache[off];
+    vints_.skip_to(off);
+    return static_cast<uint32_t>(vints_.peek());
+  }
+
+ private:
+  const uint8_t* file_ = nullptr;
+  const std::vector<SkipEntry>* sl_ = nullptr;
+  int fmt_ = 0, cur_ = 0;
+  PackReader pack_;
+  VIntsIter vints_;
+};
+
+// VacuumPostingListIterator (flash_iterators.h:893-1079), no bloom / positions.
+class VacuumIter {
+ public:
+  VacuumIter(const uint8_t* file, uint64_t off) {
+    const uint8_t* buf = file + off;
+    if (buf[0] != kPostingMagic) throw std::runtime_error("posting list magic");
+    uint64_t df;
+    int l = varint_decode(buf + 1, &df);
+    n_ = static_cast<int>(df);
+    skip_ = std::make_shared<std::vector<SkipEntry>>(load_skip_list(buf + 1 + l + 8));
+    doc_.reset(file, skip_.get(), n_);
+    tf_.reset(file, skip_.get());
+  }
+  int size() const { return n_; }
+  bool is_end() const { return doc_.is_end(); }
+  int doc_id() const { return static_cast<int>(doc_.value()); }
+  int term_freq() { return static_cast<int>(tf_.at(doc_.posting_index())); }
+  void advance() { doc_.advance(); }
+  void skip_forward(uint32_t d) { doc_.skip_forward(d); }
+
+ private:
+  int n_ = 0;
+  std::shared_ptr<std::vector<SkipEntry>> skip_;
+  DocIdIter doc_;
+  TfIter tf_;
+};
+
+// In-memory posting list iterator for the QqMem restatement (posting_list_delta.h:161-394:
+// SkipForward = first posting >= doc id; the result set is codec-independent).
+class MemIter {
+ public:
+  MemIter(const std::vector<uint32_t>* d, const std::vector<uint32_t>* t) : d_(d), t_(t) {}
+  int size() const { return static_cast<int>(d_->size()); }
+  bool is_end() const { return i_ >= d_->size(); }
+  int doc_id() const { return static_cast<int>((*d_)[i_]); }
+  int term_freq() const { return static_cast<int>((*t_)[i_]); }
+  void advance() { ++i_; }
+  void skip_forward(uint32_t v) { while (i_ < d_->size() && (*d_)[i_] < v) ++i_; }
+
+ private:
+  const std::vector<uint32_t>* d_;
+  const std::vector<uint32_t>* t_;
+  size_t i_ = 0;
+};
+
+// ----------------------------------------------------------- the heap ----
+// std::priority_queue<unique_ptr<ResultDocEntry>, vector, EntryGreater>
+// (query_processing.h:510-524) with libstdc++'s __push_heap / __adjust_heap /
+// __pop_heap restated; comp(a, b) = a.score > b.score.
+struct Entry { int doc; double score; };
+class MinHeap {
+ public:
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  const Entry& top() const { return v_[0]; }
+  void push(const Entry& e) {
+    v_.push_back(e);
+    push_hole(static_cast<long>(v_.size()) - 1, 0, e);
+  }
+  void pop() {
+    if (v_.size() > 1) {
+      const long len = static_cast<long>(v_.size()) - 1;
+      Entry value = v_[len];
+      v_[len] = v_[0];
+      adjust(0, len, value);
+    }
+    v_.pop_back();
+  }
+
+ private:
+  static bool comp(const Entry& a, const Entry& b) { return a.score > b.score; }
+  void push_hole(long hole, long top, Entry value) {
+    long parent = (hole - 1) / 2;
+    while (hole > top && comp(v_[parent], value)) {
+      v_[hole] = v_[parent];
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    v_[hole] = value;
+  }
+  void adjust(long hole, long len, Entry value) {
+    const long top = hole;
+    long child = hole;
+    while (child < (len - 1) / 2) {
+      child = 2 * (child + 1);
+      if (comp(v_[child], v_[child - 1])) --child;
+      v_[hole] = v_[child];
+      hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+      child = 2 * (child + 1);
+      v_[hole] = v_[child - 1];
+      hole = child - 1;
+    }
+    push_hole(hole, top, value);
+  }
+  std::vector<Entry> v_;
+};
+
+// ProcessorBase / NonPhraseProcessorBase / *QueryProcessor (query_processing.h:527-950)
+template <class It>
+class Processor {
+ public:
+  Processor(const Bm25& sim, std::vector<It>* its, const std::vector<uint8_t>& lens, int n_docs, int k)
+      : sim_(sim), its_(*its), lens_(lens), k_(k) {
+    for (auto& it : its_) idf_.push_back(es_idf(n_docs, it.size()));   // :544-547
+  }
+  std::vector<Entry> run() {  // qq_search::ProcessQueryDelta dispatch (:966-978)
+    if (its_.size() == 1) single();
+    else if (its_.size() == 2) two();
+    else multi();
+    return sort_heap();
+  }
+
+ private:
+  // CalcDocScoreLossy (scoring.h:124-145), terms in query order
+  double score(int doc) {
+    double s = 0;
+    const uint8_t c = static_cast<size_t>(doc) < lens_.size() ? lens_[doc] : 0;
+    for (size_t i = 0; i < its_.size(); ++i) {
+      const int tf = its_[i].term_freq();
+      double tfn = sim_.tfnorm_lossy(tf, c);
+      double t = idf_[i] * tfn;
+      s += t;
+    }
+    return s;
+  }
+  // RankDoc (query_processing.h:588-603)
+  void rank(int doc) {
+    const double s = score(doc);
+    if (heap_.size() < static_cast<size_t>(k_)) heap_.push(Entry{doc, s});
+    else if (s > heap_.top().score) { heap_.pop(); heap_.push(Entry{doc, s}); }
+  }
+  void single() {  // :632-641
+    auto& it = its_[0];
+    while (!it.is_end()) { rank(it.doc_id()); it.advance(); }
+  }
+  void two() {  // TwoTermNonPhraseQueryProcessor::Process :656-677
+    auto& a = its_[0];
+    auto& b = its_[1];
+    while (!a.is_end() && !b.is_end()) {
+      const int d0 = a.doc_id(), d1 = b.doc_id();
+      if (d0 > d1) b.skip_forward(d0);
+      else if (d0 < d1) a.skip_forward(d1);
+      else { rank(d0); a.advance(); b.advance(); }
+    }
+  }
+  void multi() {  // ProcessMultipleTerms / FindMax / FindMatch :710-728,810-852
+    for (;;) {
+      int mx = -1;
+      bool fin = false;
+      for (auto& it : its_) {
+        if (it.is_end()) { fin = true; break; }
+        if (it.doc_id() > mx) mx = it.doc_id();
+      }
+      if (fin) break;
+      for (size_t i = 0; i < its_.size(); ++i) {
+        auto& it = its_[i];
+        it.skip_forward(static_cast<uint32_t>(mx));
+        if (it.is_end()) { fin = true; break; }
+        if (it.doc_id() != mx) break;
+        if (i == its_.size() - 1) {
+          rank(mx);
+          for (auto& x : its_) x.advance();
+        }
+      }
+      if (fin) break;
+    }
+  }
+  std::vector<Entry> sort_heap() {  // :551-562
+    std::vector<Entry> r;
+    int kk = k_;
+    while (!heap_.empty() && kk != 0) { r.push_back(heap_.top()); heap_.pop(); --kk; }
+    std::reverse(r.begin(), r.end());
+    return r;
+  }
+  const Bm25& sim_;
+  std::vector<It>& its_;
+  const std::vector<uint8_t>& lens_;
+  int k_;
+  std::vector<double> idf_;
+  MinHeap heap_;
+};
+
+int emit(const std::vector<Entry>& r, int32_t* docs, double* scores) {
+  for (size_t i = 0; i < r.size(); ++i) { docs[i] = r[i].doc; scores[i] = r[i].score; }
+  return static_cast<int>(r.size());
+}
+
+std::vector<std::string> explode(const std::string& s, char c) {  // utils.cc:29-42
+  std::vector<std::string> v;
+  std::string cur;
+  for (char ch : s) {
+    if (ch != c) cur += ch;
+    else if (!cur.empty()) { v.push_back(cur); cur.clear(); }
+  }
+  if (!cur.empty()) v.push_back(cur);
+  return v;
+}
+
+std::vector<std::string> explode_strict(const std::string& s, char c) {  // utils.cc:52-67
+  std::vector<std::string> v;
+  std::string cur;
+  for (char ch : s) {
+    if (ch != c) cur += ch;
+    else { v.push_back(cur); cur.clear(); }
+  }
+  v.push_back(cur);
+  return v;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ handles ----
+struct orc_vacuum {
+  uint8_t* map = nullptr;
+  size_t len = 0;
+  std::unordered_map<std::string, uint64_t> tip;  // term -> posting list offset
+  std::vector<uint8_t> lens;                      // DocLengthCharStore
+  int n_docs = 0;
+  Bm25 sim;
+};
+
+struct orc_qqmem {
+  std::map<std::string, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> index;
+  std::vector<uint8_t> lens;
+  double avg = 0;
+  int n_docs = 0;
+  Bm25 sim;
+};
+
+extern "C" {
+
+const char* orc_last_error(void) { return g_err.c_str(); }
+int orc_num_bits(uint32_t v) { return num_bits(v); }
+uint8_t orc_char4_encode(uint32_t v) { return char4_encode(v); }
+uint32_t orc_char4_decode(uint8_t c) { return char4_decode(c); }
+int orc_varint_encode(uint64_t v, uint8_t* out) { return varint_encode(v, out); }
+int orc_varint_decode(const uint8_t* in, uint64_t* v) { return varint_decode(in, v); }
+int64_t orc_ub_negative_char_index(void) { return g_ub_neg.load(); }
+
+int orc_pack128(const uint32_t* values, uint8_t* out) {  // packed_value.h:93-116
+  int b = 0;
+  for (int i = 0; i < kPack; ++i) { int n = num_bits(values[i]); n = n == 0 ? 1 : n; b = std::max(b, n); }
+  out[0] = kPackMagic;
+  out[1] = static_cast<uint8_t>(b);
+  turbo_pack(values, b, out + 2);
+  return 2 + (b * kPack + 7) / 8;
+}
+
+int orc_unpack128(const uint8_t* pack, uint32_t* out) {
+  try {
+    PackReader r;
+    r.reset(pack);
+    r.decode();
+    std::memcpy(out, r.cache, sizeof r.cache);
+    return r.bits;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+double orc_es_idf(int n, int df) { return es_idf(n, df); }
+
+double orc_es_tfnorm(int freq, int field_length, double avg) {  // scoring.h:28-40
+  const double k1 = 1.2, b = 0.75;
+  return (freq * (k1 + 1)) / (freq + k1 * (1 - b + ((b * field_length) / avg)));
+}
+
+double orc_tfnorm_lossy(double avg, int freq, uint8_t c) {
+  Bm25 s;
+  s.reset(avg);
+  return s.tfnorm_lossy(freq, c);
+}
+
+// VacuumEngine::Load (vacuum_engine.h:144-180) minus doc store / mlock / profiler
+orc_vacuum* orc_vacuum_open(const char* dir) {
+  std::unique_ptr<orc_vacuum> h(new orc_vacuum());
+  try {
+    const std::string d(dir);
+    {  // DocLengthCharStore::Deserialize (doc_length_store.h:163-190)
+      std::ifstream f(d + "/my.doc_length", std::ios::binary);
+      if (!f) throw std::runtime_error("cannot open my.doc_length");
+      int32_t count;
+      double avg;
+      f.read(reinterpret_cast<char*>(&count), 4);
+      f.read(reinterpret_cast<char*>(&avg), 8);
+      for (int32_t i = 0; i < count; ++i) {
+        int32_t id;
+        char c;
+        f.read(reinterpret_cast<char*>(&id), 4);
+        f.read(&c, 1);
+        if (!f) throw std::runtime_error("truncated my.doc_length");
+        if (static_cast<size_t>(id) >= h->lens.size()) h->lens.resize(id + 1, 0);
+        h->lens[id] = static_cast<uint8_t>(c);
+      }
+      h->n_docs = count;
+      h->sim.reset(avg);  // similarity_.Reset(doc_lengths_.GetAvgLength())
+    }
+    {  // TermTrieIndex::Load (term_index.h:106-159)
+      std::ifstream f(d + "/my.tip", std::ios::binary);
+      if (!f) throw std::runtime_error("cannot open my.tip");
+      for (;;) {
+        uint32_t n;
+        if (!f.read(reinterpret_cast<char*>(&n), 4)) break;
+        std::string t(n, '\0');
+        int64_t v;
+        f.read(&t[0], n);
+        f.read(reinterpret_cast<char*>(&v), 8);
+        // DecodePrefetchZoneAndOffset (flash_containers.h:14-19)
+        h->tip[t] = static_cast<uint64_t>(v) & ((~0ull << 16) >> 16);
+      }
+    }
+    {  // MapPostingLists + VacuumHeader::Load (flash_iterators.h:826-873)
+      int fd = ::open((d + "/my.vacuum").c_str(), O_RDONLY);
+      if (fd < 0) throw std::runtime_error("cannot open my.vacuum");
+      struct stat sb;
+      fstat(fd, &sb);
+      h->len = sb.st_size;
+      void* p = mmap(nullptr, h->len, PROT_READ, MAP_PRIVATE, fd, 0);
+      ::close(fd);
+      if (p == MAP_FAILED) throw std::runtime_error("mmap");
+      h->map = static_cast<uint8_t*>(p);
+      if (h->map[0] != kVacuumMagic) throw std::runtime_error("Vacuum's first byte is wrong");
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+  return h.release();
+}
+
+void orc_vacuum_close(orc_vacuum* h) {
+  if (!h) return;
+  if (h->map) munmap(h->map, h->len);
+  delete h;
+}
+
+int orc_vacuum_term_count(orc_vacuum* h) { return static_cast<int>(h->tip.size()); }
+int orc_vacuum_n_docs(orc_vacuum* h) { return h->n_docs; }
+
+int orc_vacuum_df(orc_vacuum* h, const char* term) {
+  auto it = h->tip.find(term);
+  if (it == h->tip.end()) return 0;
+  return VacuumIter(h->map, it->second).size();
+}
+
+int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* tfs, int cap) {
+  auto f = h->tip.find(term);
+  if (f == h->tip.end()) return 0;
+  try {
+    VacuumIter it(h->map, f->second);
+    int n = 0;
+    while (!it.is_end()) {
+      if (n < cap) { docs[n] = it.doc_id(); tfs[n] = it.term_freq(); }
+      ++n;
+      it.advance();
+    }
+    return n;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// VacuumEngine::Search (vacuum_engine.h:201-258), non-phrase, no snippets
+int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k, int32_t* docs,
+                      double* scores, int32_t* doc_freqs) {
+  if (k == 0) return 0;
+  try {
+    std::vector<VacuumIter> its;
+    for (int i = 0; i < n_terms; ++i) {  // FindIteratorsSolid (vacuum_engine.h:89-99)
+      auto f = h->tip.find(terms[i]);
+      if (f != h->tip.end()) its.emplace_back(h->map, f->second);
+    }
+    if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
+    if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
+    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k);
+    return emit(p.run(), docs, scores);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads, int32_t* docs,
+                            double* scores, int32_t* n_out, int max_q) {
+  std::vector<std::string> lines = explode(text, '\n');
+  const int nq = std::min<int>(static_cast<int>(lines.size()), max_q);
+  std::atomic<int> next{0};
+  auto work = [&] {
+    for (int q; (q = next++) < nq;) {
+      std::vector<std::string> t = explode(lines[q], ' ');
+      std::vector<const char*> tp;
+      for (auto& s : t) tp.push_back(s.c_str());
+      n_out[q] = orc_vacuum_search(h, tp.data(), static_cast<int>(tp.size()), k,
+                                   docs + static_cast<int64_t>(q) * k,
+                                   scores + static_cast<int64_t>(q) * k, nullptr);
+    }
+  };
+  if (threads <= 1) work();
+  else {
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+  }
+  return nq;
+}
+
+// QqMemEngineDelta::LoadLocalDocuments / AddDocument (qq_mem_engine.h:271-305):
+// TOKEN_ONLY: tokens = body = column 2, tf = token count (utils.cc:167-180),
+// length = count_terms(body); WITH_POSITIONS: tokens column 2, tf = offset pairs
+// of the term (column 3), length = count_terms(column 1) (types.cc:38-40).
+orc_qqmem* orc_qqmem_load(const char* linedoc, int64_t n_rows, const char* format) {
+  std::unique_ptr<orc_qqmem> h(new orc_qqmem());
+  try {
+    const std::string fmt(format);
+    const bool tok_only = fmt == "TOKEN_ONLY";
+    if (!tok_only && fmt != "WITH_POSITIONS") throw std::runtime_error("format");
+    std::ifstream in(linedoc);
+    if (!in) throw std::runtime_error("cannot open linedoc");
+    std::string line;
+    std::getline(in, line);  // LineDoc header (utils.h:54-67)
+    int doc = 0;
+    int cnt = 0;
+    while ((n_rows < 0 || doc < n_rows) && std::getline(in, line)) {
+      auto items = explode_strict(line, '\t');
+      int length;
+      if (tok_only) {
+        std::map<std::string, int> counts;
+        auto toks = explode(items[2], ' ');
+        for (auto& t : toks) ++counts[t];
+        for (auto& kv : counts) {
+          auto& pl = h->index[kv.first];
+          pl.first.push_back(doc);
+          pl.second.push_back(kv.second);
+        }
+        length = static_cast<int>(toks.size());
+      } else {
+        auto toks = explode(items[2], ' ');
+        // utils::parse_offsets (utils.cc:105-141): groups by '.', pairs end with ';'
+        std::vector<int> tf;
+        std::string grp;
+        for (char ch : items[3]) {
+          if (ch != '.') grp += ch;
+          else if (!grp.empty()) {
+            int n = 0;
+            for (char c2 : grp) if (c2 == ';') ++n;
+            tf.push_back(n);
+            grp.clear();
+          }
+        }
+        for (size_t i = 0; i < toks.size(); ++i) {
+          auto& pl = h->index[toks[i]];
+          pl.first.push_back(doc);
+          pl.second.push_back(tf.at(i));
+        }
+        length = static_cast<int>(explode(items[1], ' ').size());
+      }
+      // DocLengthCharStore::AddLength (doc_length_store.h:104-112)
+      h->avg = h->avg + (length - h->avg) / (cnt + 1);
+      if (static_cast<size_t>(doc) >= h->lens.size()) h->lens.resize(doc + 1, 0);
+      h->lens[doc] = char4_encode(static_cast<uint32_t>(length));
+      ++cnt;
+      ++doc;
+    }
+    h->n_docs = cnt;
+    h->sim.reset(h->avg);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+  return h.release();
+}
+
+void orc_qqmem_close(orc_qqmem* h) { delete h; }
+int orc_qqmem_term_count(orc_qqmem* h) { return static_cast<int>(h->index.size()); }
+
+// QqMemEngineDelta::Search (qq_mem_engine.h:335-368)
+int orc_qqmem_search(orc_qqmem* h, const char* const* terms, int n_terms, int k, int32_t* docs,
+                     double* scores, int32_t* doc_freqs) {
+  if (k == 0) return 0;
+  std::vector<MemIter> its;
+  for (int i = 0; i < n_terms; ++i) {
+    auto f = h->index.find(terms[i]);
+    if (f != h->index.end()) its.emplace_back(&f->second.first, &f->second.second);
+  }
+  if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
+  if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
+  Processor<MemIter> p(h->sim, &its, h->lens, h->n_docs, k);
+  return emit(p.run(), docs, scores);
+}
+
+}  // extern "C"

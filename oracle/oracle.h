@@ -1,0 +1,74 @@
+/*
+ * oracle.h -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference
+ * (tailuzhecom/wiser, src/qq_mem/src) conjunctive-query + BM25 + top-k path,
+ * used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as
+ * the checker.  The product (wiser_amd, libwiser_hip.so) never links or calls
+ * this library.
+ *
+ * Parity pinning: the reference C++ could not be built or run here (the
+ * environment refused it), so this restatement is pinned
+ * by the reference's own known-answer tests (tests/test_oracle_kat.py cites
+ * each one) and by the Vacuum == QqMem differential test of tests_15.cc:158-210
+ * re-run over the reference's own fixture files.
+ */
+#ifndef WISER_ORACLE_H
+#define WISER_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_vacuum orc_vacuum;
+typedef struct orc_qqmem orc_qqmem;
+
+const char* orc_last_error(void);
+
+/* ---- codecs (known-answer tests) ------------------------------------- */
+int orc_num_bits(uint32_t v);
+uint8_t orc_char4_encode(uint32_t v);
+uint32_t orc_char4_decode(uint8_t c);
+int orc_varint_encode(uint64_t v, uint8_t* out);               /* returns bytes */
+int orc_varint_decode(const uint8_t* in, uint64_t* v);          /* returns bytes */
+/* LittlePackedIntsWriter::Serialize: 2-byte header + 16*b bytes; returns size */
+int orc_pack128(const uint32_t* values, uint8_t* out);
+/* LittlePackedIntsReader::DecodeToCache over a serialised pack */
+int orc_unpack128(const uint8_t* pack, uint32_t* out);
+double orc_es_idf(int doc_count, int doc_freq);
+double orc_es_tfnorm(int freq, int field_length, double avg);  /* calc_es_tfnorm */
+double orc_tfnorm_lossy(double avg, int freq, uint8_t char4);   /* Bm25Similarity */
+
+/* ---- Vacuum engine restatement --------------------------------------- */
+orc_vacuum* orc_vacuum_open(const char* dir);
+void orc_vacuum_close(orc_vacuum* h);
+int orc_vacuum_term_count(orc_vacuum* h);
+int orc_vacuum_n_docs(orc_vacuum* h);
+/* posting list size (0 if absent) */
+int orc_vacuum_df(orc_vacuum* h, const char* term);
+/* iterate a whole list through DocIdIterator / TermFreqIterator */
+int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* tfs, int cap);
+/* VacuumEngine::Search: returns n entries (<= k), fills docs/scores and doc_freqs
+ * (doc_freqs filled only when every term exists, as the reference). */
+int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k,
+                      int32_t* docs, double* scores, int32_t* doc_freqs);
+/* Many queries: queries are '\n'-separated lines of ' '-separated terms.
+ * Outputs are nq*k arrays plus n per query.  threads >= 1.  Returns nq. */
+int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads,
+                            int32_t* docs, double* scores, int32_t* n_out, int max_q);
+
+/* ---- QqMem (in-memory, varint postings) engine restatement ----------- */
+orc_qqmem* orc_qqmem_load(const char* linedoc, int64_t n_rows, const char* format);
+void orc_qqmem_close(orc_qqmem* h);
+int orc_qqmem_term_count(orc_qqmem* h);
+int orc_qqmem_search(orc_qqmem* h, const char* const* terms, int n_terms, int k,
+                     int32_t* docs, double* scores, int32_t* doc_freqs);
+
+/* counters of reference-UB situations hit so far (negative cache index) */
+int64_t orc_ub_negative_char_index(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

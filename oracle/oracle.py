@@ -1,0 +1,177 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so, the CPU
+restatement of the reference query path (see oracle.h).  Imported only by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.dirname(HERE), "oracle/_build/liboracle.so"])
+
+
+if not os.path.exists(LIB_PATH):
+    build()
+
+lib = C.CDLL(LIB_PATH)
+_P = C.c_void_p
+_I32P = C.POINTER(C.c_int32)
+_F64P = C.POINTER(C.c_double)
+for name, res, args in [
+    ("orc_last_error", C.c_char_p, []),
+    ("orc_num_bits", C.c_int, [C.c_uint32]),
+    ("orc_char4_encode", C.c_uint8, [C.c_uint32]),
+    ("orc_char4_decode", C.c_uint32, [C.c_uint8]),
+    ("orc_varint_encode", C.c_int, [C.c_uint64, C.POINTER(C.c_uint8)]),
+    ("orc_varint_decode", C.c_int, [C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]),
+    ("orc_pack128", C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint8)]),
+    ("orc_unpack128", C.c_int, [C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)]),
+    ("orc_es_idf", C.c_double, [C.c_int, C.c_int]),
+    ("orc_es_tfnorm", C.c_double, [C.c_int, C.c_int, C.c_double]),
+    ("orc_tfnorm_lossy", C.c_double, [C.c_double, C.c_int, C.c_uint8]),
+    ("orc_vacuum_open", _P, [C.c_char_p]),
+    ("orc_vacuum_close", None, [_P]),
+    ("orc_vacuum_term_count", C.c_int, [_P]),
+    ("orc_vacuum_n_docs", C.c_int, [_P]),
+    ("orc_vacuum_df", C.c_int, [_P, C.c_char_p]),
+    ("orc_vacuum_list", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                  C.c_int]),
+    ("orc_vacuum_search", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, _I32P, _F64P,
+                                    _I32P]),
+    ("orc_vacuum_search_lines", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, _I32P, _F64P, _I32P,
+                                          C.c_int]),
+    ("orc_qqmem_load", _P, [C.c_char_p, C.c_int64, C.c_char_p]),
+    ("orc_qqmem_close", None, [_P]),
+    ("orc_qqmem_term_count", C.c_int, [_P]),
+    ("orc_qqmem_search", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, _I32P, _F64P,
+                                   _I32P]),
+    ("orc_ub_negative_char_index", C.c_int64, []),
+]:
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = args
+
+
+def _err():
+    return lib.orc_last_error().decode(errors="replace")
+
+
+def _search(fn, h, terms, k):
+    arr = (C.c_char_p * max(len(terms), 1))(*[t.encode() for t in terms])
+    kk = max(k, 1)
+    docs = (C.c_int32 * kk)()
+    scores = (C.c_double * kk)()
+    freqs = (C.c_int32 * max(len(terms), 1))(*([-1] * max(len(terms), 1)))
+    n = fn(h, arr, len(terms), k, docs, scores, freqs)
+    if n < 0:
+        raise RuntimeError(_err())
+    dfs = [freqs[i] for i in range(len(terms))] if n > 0 or (len(terms) and freqs[0] >= 0) else []
+    if any(d < 0 for d in dfs):
+        dfs = []
+    return [(docs[i], scores[i]) for i in range(n)], dfs
+
+
+class OracleVacuum:
+    """VacuumEngine restatement reading my.vacuum / my.tip / my.doc_length."""
+
+    def __init__(self, index_dir: str):
+        self.h = lib.orc_vacuum_open(index_dir.encode())
+        if not self.h:
+            raise RuntimeError(_err())
+
+    def close(self):
+        if self.h:
+            lib.orc_vacuum_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def term_count(self):
+        return lib.orc_vacuum_term_count(self.h)
+
+    def n_docs(self):
+        return lib.orc_vacuum_n_docs(self.h)
+
+    def df(self, term):
+        return lib.orc_vacuum_df(self.h, term.encode())
+
+    def postings(self, term):
+        n = self.df(term)
+        d = (C.c_uint32 * max(n, 1))()
+        t = (C.c_uint32 * max(n, 1))()
+        m = lib.orc_vacuum_list(self.h, term.encode(), d, t, n)
+        if m < 0:
+            raise RuntimeError(_err())
+        return list(d[:m]), list(t[:m])
+
+    def search(self, terms, k):
+        """-> ([(doc, score)], doc_freqs)"""
+        return _search(lib.orc_vacuum_search, self.h, terms, k)
+
+    def search_lines(self, lines, k, threads=1):
+        """Many queries; returns list of [(doc, score)]."""
+        text = "\n".join(" ".join(t) for t in lines).encode()
+        nq = len(lines)
+        docs = (C.c_int32 * (nq * k))()
+        scores = (C.c_double * (nq * k))()
+        nout = (C.c_int32 * nq)()
+        lib.orc_vacuum_search_lines(self.h, text, k, threads, docs, scores, nout, nq)
+        return [[(docs[q * k + i], scores[q * k + i]) for i in range(nout[q])] for q in range(nq)]
+
+
+class OracleQqMem:
+    """QqMemEngineDelta restatement built straight from a linedoc."""
+
+    def __init__(self, linedoc: str, fmt: str, n_rows: int = -1):
+        self.h = lib.orc_qqmem_load(linedoc.encode(), n_rows, fmt.encode())
+        if not self.h:
+            raise RuntimeError(_err())
+
+    def close(self):
+        if self.h:
+            lib.orc_qqmem_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def term_count(self):
+        return lib.orc_qqmem_term_count(self.h)
+
+    def search(self, terms, k):
+        return _search(lib.orc_qqmem_search, self.h, terms, k)
+
+
+def pack128(values):
+    v = (C.c_uint32 * 128)(*values)
+    out = (C.c_uint8 * (2 + 512 + 8))()
+    n = lib.orc_pack128(v, out)
+    return bytes(out[:n])
+
+
+def unpack128(data: bytes):
+    buf = (C.c_uint8 * (len(data) + 16)).from_buffer_copy(data + b"\0" * 16)
+    out = (C.c_uint32 * 128)()
+    b = lib.orc_unpack128(buf, out)
+    if b < 0:
+        raise RuntimeError(_err())
+    return list(out), b
+
+
+def varint_encode(v):
+    out = (C.c_uint8 * 10)()
+    n = lib.orc_varint_encode(v, out)
+    return bytes(out[:n])
+
+
+def varint_decode(data: bytes):
+    buf = (C.c_uint8 * (len(data) + 10)).from_buffer_copy(data + b"\0" * 10)
+    v = C.c_uint64()
+    n = lib.orc_varint_decode(buf, C.byref(v))
+    return v.value, n

@@ -1,0 +1,11 @@
+"""wiser_amd: MI355X-native conjunctive-query + BM25 top-k engine for the
+Vacuum (WiSER) index.  The compute path is libwiser_hip.so (hand-written HIP
+for gfx950) behind the C ABI in include/wiser_hip.h; this package is the thin
+Python mirror of the reference's SearchEngineServiceNew surface."""
+from .engine import (CreateSearchEngine, ResidentBatch, SearchQuery, SearchResult,  # noqa: F401
+                     SearchResultEntry, VacuumEngine, build_from_linedoc, build_synthetic,
+                     gen_two_term_log, sync)
+
+__all__ = ["CreateSearchEngine", "VacuumEngine", "SearchQuery", "SearchResult",
+           "SearchResultEntry", "ResidentBatch", "build_from_linedoc", "build_synthetic",
+           "gen_two_term_log", "sync"]

@@ -1,0 +1,107 @@
+"""ctypes binding of include/wiser_hip.h (the engine's C ABI).
+
+Loads the in-tree ``wiser_amd/_lib/libwiser_hip.so`` built by ``make`` (or
+``__graft_entry__.build()``).  There is no fallback: if the library is missing
+the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libwiser_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "wiser_hip.h")
+
+MAX_TERMS = 8
+MAX_K = 64
+
+WSR_OK = 0
+ERRORS = {-1: "WSR_E_INVALID", -2: "WSR_E_IO", -3: "WSR_E_HIP", -4: "WSR_E_LIMIT",
+          -5: "WSR_E_INTERNAL"}
+
+
+class OpenOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("doc_lo", C.c_uint32), ("doc_hi", C.c_uint32),
+                ("threads", C.c_int32)]
+
+
+class Query(C.Structure):
+    _fields_ = [("n_terms", C.c_int32), ("k", C.c_int32), ("list_ids", C.c_int32 * MAX_TERMS)]
+
+
+class Hit(C.Structure):
+    _fields_ = [("doc_id", C.c_int32), ("pad", C.c_int32), ("score", C.c_double)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("work_items", C.c_uint64), ("survivors", C.c_uint64),
+                ("driver_blocks", C.c_uint64), ("other_blocks", C.c_uint64),
+                ("algo_bytes", C.c_uint64), ("plan_ms", C.c_double),
+                ("segment_ms", C.c_double), ("replay_ms", C.c_double)]
+
+
+class BuildStats(C.Structure):
+    _fields_ = [("n_docs", C.c_int64), ("n_terms", C.c_int64), ("n_postings", C.c_int64),
+                ("vacuum_bytes", C.c_int64), ("docs_char4_ge_0x80", C.c_int64),
+                ("avg_length", C.c_double)]
+
+
+class WiserError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build() "
+                      "(the HIP engine has no CPU fallback)")
+
+lib = C.CDLL(LIB_PATH)
+
+_P = C.c_void_p
+_sigs = {
+    "wsr_last_error": (C.c_char_p, []),
+    "wsr_version": (C.c_char_p, []),
+    "wsr_open": (C.c_int, [C.c_char_p, C.POINTER(OpenOpts), C.POINTER(_P)]),
+    "wsr_close": (None, [_P]),
+    "wsr_term_count": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "wsr_n_docs": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "wsr_lookup": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "wsr_list_bytes": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_uint64)]),
+    "wsr_search_batch": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.POINTER(Hit),
+                                   C.POINTER(C.c_int32)]),
+    "wsr_batch_create": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    "wsr_batch_destroy": (None, [_P, _P]),
+    "wsr_batch_upload": (C.c_int, [_P, _P, C.POINTER(Query), C.c_int32]),
+    "wsr_batch_run": (C.c_int, [_P, _P]),
+    "wsr_sync": (C.c_int, [_P]),
+    "wsr_batch_fetch": (C.c_int, [_P, _P, C.POINTER(Hit), C.POINTER(C.c_int32)]),
+    "wsr_batch_stats_get": (C.c_int, [_P, _P, C.POINTER(BatchStats)]),
+    "wsr_batch_device_results": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_P)]),
+    "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
+                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]),
+    "wsr_build_from_linedoc": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_char_p,
+                                         C.POINTER(BuildStats)]),
+    "wsr_build_synthetic": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_double, C.c_uint64,
+                                      C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
+    "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
+                                       C.POINTER(C.c_int64)]),
+}
+for _name, (_res, _args) in _sigs.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def check(rc):
+    if rc != WSR_OK:
+        raise WiserError(rc, lib.wsr_last_error().decode(errors="replace"))
+    return rc
+
+
+def header_symbols(path: str = HEADER):
+    """Function names declared in include/wiser_hip.h."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(wsr_\w+)\s*\(", text, re.M)))

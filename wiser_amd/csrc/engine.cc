@@ -1,0 +1,438 @@
+// C ABI (include/wiser_hip.h) over the HIP engine: index load + HBM upload,
+// resident query batches, kernel launches, result download.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/wiser_hip.h"
+#include "engine_types.h"
+#include "index.h"
+#include "kernels.h"
+#include "writer.h"
+
+namespace wiser {
+constexpr int kSegCostMax = kSegCost;
+}  // namespace wiser
+
+using namespace wiser;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+template <class T>
+void dev_upload(T** dst, const std::vector<T>& src) {
+  const size_t n = std::max<size_t>(src.size(), 1) * sizeof(T);
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(dst), n));
+  if (!src.empty()) HIP_OK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
+}  // namespace
+
+struct wsr_handle {
+  std::mutex mu;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  VacuumIndex idx;
+  IndexArgs args{};
+  uint8_t* d_blob = nullptr;
+  ListDev* d_lists = nullptr;
+  BlockDev* d_blocks = nullptr;
+  uint32_t* d_last = nullptr;
+  uint8_t* d_c4 = nullptr;
+  double* d_cache = nullptr;
+  std::vector<ListDev> lists;       // host copy of the directory heads
+  std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
+  std::vector<BlockDev> blocks;     // host copy (debug decode)
+  int grid = 0;
+};
+
+struct wsr_batch {
+  int max_q = 0, stride = 0, nq = 0;
+  QueryIn* d_q = nullptr;
+  QueryPlan* d_plan = nullptr;
+  uint32_t* d_ctr = nullptr;
+  Event* d_events = nullptr;
+  uint64_t ev_cap = 0;
+  uint32_t* d_evcnt = nullptr;
+  uint64_t item_cap = 0;
+  HitDev* d_hits = nullptr;
+  int32_t* d_nhits = nullptr;
+  uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ran = false;
+};
+
+extern "C" {
+
+const char* wsr_last_error(void) { return g_err.c_str(); }
+const char* wsr_version(void) { return "wiser-hip 0.1 (gfx950)"; }
+
+int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
+  if (!dir || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = nullptr;
+  std::unique_ptr<wsr_handle> h(new wsr_handle());
+  try {
+    h->idx.open(dir);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  try {
+    const int dev = opts ? opts->device : 0;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= dev)
+      return fail(WSR_E_HIP, "no HIP device " + std::to_string(dev) + " (MI355X required; no CPU fallback)");
+    HIP_OK(hipSetDevice(dev));
+    h->device = dev;
+    uint32_t lo = opts ? opts->doc_lo : 0, hi = opts ? opts->doc_hi : 0;
+    if (hi == 0) hi = 0xFFFFFFFFu;
+    int threads = opts && opts->threads > 0 ? opts->threads : static_cast<int>(std::thread::hardware_concurrency());
+    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32));
+    dev_upload(&h->d_blob, img.blob);
+    dev_upload(&h->d_lists, img.lists);
+    dev_upload(&h->d_blocks, img.blocks);
+    dev_upload(&h->d_last, img.blk_last);
+    dev_upload(&h->d_c4, h->idx.char4_lengths());
+    std::vector<double> cache(h->idx.bm25_cache(), h->idx.bm25_cache() + 256);
+    dev_upload(&h->d_cache, cache);
+    h->lists = img.lists;
+    h->blocks = img.blocks;
+    h->list_bytes = img.list_bytes;
+    h->args.blob = h->d_blob;
+    h->args.lists = h->d_lists;
+    h->args.blocks = h->d_blocks;
+    h->args.blk_last = h->d_last;
+    h->args.c4 = h->d_c4;
+    h->args.cache = h->d_cache;
+    h->args.n_c4 = static_cast<uint32_t>(h->idx.char4_lengths().size());
+    h->args.n_lists = static_cast<uint32_t>(img.lists.size());
+    h->args.doc_lo = lo;
+    h->args.doc_hi = hi;
+    HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIP_OK(hipGetDeviceProperties(&prop, dev));
+    int occ = segment_kernel_occupancy();
+    if (occ < 1) occ = 1;
+    h->grid = prop.multiProcessorCount * std::min(occ, 16);
+  } catch (const std::exception& e) {
+    wsr_close(h.release());
+    return fail(WSR_E_HIP, e.what());
+  }
+  *out = h.release();
+  return WSR_OK;
+}
+
+void wsr_close(wsr_handle* h) {
+  if (!h) return;
+  if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
+  for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
+                  static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
+                  static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache)})
+    if (p) (void)hipFree(p);
+  delete h;
+}
+
+int wsr_term_count(wsr_handle* h, int32_t* out) {
+  if (!h || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = h->idx.n_lists();
+  return WSR_OK;
+}
+
+int wsr_n_docs(wsr_handle* h, int32_t* out) {
+  if (!h || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = h->idx.n_docs();
+  return WSR_OK;
+}
+
+int wsr_lookup(wsr_handle* h, const char* term, int32_t* list_id, int32_t* df) {
+  if (!h || !term) return fail(WSR_E_INVALID, "null argument");
+  const int32_t id = h->idx.find(term);
+  if (list_id) *list_id = id;
+  if (df) *df = id < 0 ? 0 : static_cast<int32_t>(h->idx.df(id));
+  return WSR_OK;
+}
+
+int wsr_list_bytes(wsr_handle* h, int32_t id, uint64_t* out) {
+  if (!h || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = (id >= 0 && id < static_cast<int32_t>(h->list_bytes.size())) ? h->list_bytes[id] : 0;
+  return WSR_OK;
+}
+
+int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** out) {
+  if (!h || !out || max_q <= 0 || stride <= 0 || stride > WSR_MAX_K)
+    return fail(WSR_E_INVALID, "bad batch arguments");
+  std::lock_guard<std::mutex> g(h->mu);
+  std::unique_ptr<wsr_batch> b(new wsr_batch());
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    b->max_q = max_q;
+    b->stride = stride;
+    HIP_OK(hipMalloc(&b->d_q, sizeof(QueryIn) * max_q));
+    HIP_OK(hipMalloc(&b->d_plan, sizeof(QueryPlan) * max_q));
+    HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
+    HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
+    HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
+    for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
+  } catch (const std::exception& e) {
+    wsr_batch_destroy(h, b.release());
+    return fail(WSR_E_HIP, e.what());
+  }
+  *out = b.release();
+  return WSR_OK;
+}
+
+void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
+  if (!b) return;
+  if (h && h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
+                  static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
+                  static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
+                  static_cast<void*>(b->d_nhits)})
+    if (p) (void)hipFree(p);
+  for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
+  delete b;
+}
+
+int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq) {
+  if (!h || !b || (nq > 0 && !q) || nq < 0 || nq > b->max_q)
+    return fail(WSR_E_INVALID, "bad upload arguments");
+  std::lock_guard<std::mutex> g(h->mu);
+  std::vector<QueryIn> in(nq);
+  uint64_t ev_need = 0, items_need = 0, algo = 0;
+  for (int i = 0; i < nq; ++i) {
+    const wsr_query& s = q[i];
+    if (s.n_terms > WSR_MAX_TERMS || s.k > WSR_MAX_K || s.k > b->stride)
+      return fail(WSR_E_LIMIT, "query " + std::to_string(i) + ": n_terms or k over the limit");
+    QueryIn& d = in[i];
+    d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
+    d.k = s.k < 0 ? 0 : s.k;
+    uint32_t nbmin = 0xFFFFFFFFu;
+    bool ok = d.n_terms > 0 && d.k > 0;
+    for (int t = 0; t < WSR_MAX_TERMS; ++t) {
+      d.list[t] = t < d.n_terms ? s.list_ids[t] : -1;
+      if (t < d.n_terms) {
+        const int32_t id = s.list_ids[t];
+        if (id < 0 || id >= static_cast<int32_t>(h->lists.size())) { ok = false; continue; }
+        nbmin = std::min(nbmin, h->lists[id].nblk);
+      }
+    }
+    if (ok && nbmin > 0) {
+      ev_need += (static_cast<uint64_t>(nbmin) + kSegCostMax) * 128;
+      items_need += nbmin;
+      for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[d.list[t]];
+      algo += 12ull * d.k;
+    }
+  }
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    if (ev_need > b->ev_cap) {
+      if (b->d_events) HIP_OK(hipFree(b->d_events));
+      b->ev_cap = ev_need + ev_need / 4 + 4096;
+      HIP_OK(hipMalloc(&b->d_events, sizeof(Event) * b->ev_cap));
+    }
+    if (items_need > b->item_cap || !b->d_evcnt) {
+      if (b->d_evcnt) HIP_OK(hipFree(b->d_evcnt));
+      b->item_cap = items_need + items_need / 4 + 1024;
+      HIP_OK(hipMalloc(&b->d_evcnt, sizeof(uint32_t) * b->item_cap));
+    }
+    if (nq) HIP_OK(hipMemcpy(b->d_q, in.data(), sizeof(QueryIn) * nq, hipMemcpyHostToDevice));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  b->nq = nq;
+  b->algo_static = algo;
+  b->ran = false;
+  return WSR_OK;
+}
+
+int wsr_batch_run(wsr_handle* h, wsr_batch* b) {
+  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * kNumCounters, st));
+    HIP_OK(hipEventRecord(b->ev[0], st));
+    HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
+                       static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)), st));
+    HIP_OK(hipEventRecord(b->ev[1], st));
+    HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
+                           h->grid, st));
+    HIP_OK(hipEventRecord(b->ev[2], st));
+    HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
+                         b->d_nhits, st));
+    HIP_OK(hipEventRecord(b->ev[3], st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  b->ran = true;
+  return WSR_OK;
+}
+
+int wsr_sync(wsr_handle* h) {
+  if (!h) return fail(WSR_E_INVALID, "null argument");
+  hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return fail(WSR_E_HIP, hipGetErrorString(e));
+  return WSR_OK;
+}
+
+int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits) {
+  if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    uint32_t ctr[kNumCounters];
+    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (ctr[4]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[4]));
+    if (b->nq) {
+      if (hits) HIP_OK(hipMemcpy(hits, b->d_hits, sizeof(HitDev) * b->nq * b->stride, hipMemcpyDeviceToHost));
+      if (n_hits) HIP_OK(hipMemcpy(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost));
+    }
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
+  if (!h || !b || !out || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipStreamSynchronize(h->stream));
+    uint32_t ctr[kNumCounters];
+    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    out->work_items = ctr[0];
+    out->survivors = ctr[3];
+    out->driver_blocks = ctr[5];
+    out->other_blocks = ctr[6];
+    out->algo_bytes = b->algo_static + ctr[3];
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, b->ev[0], b->ev[1])); out->plan_ms = ms;
+    HIP_OK(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); out->segment_ms = ms;
+    HIP_OK(hipEventElapsedTime(&ms, b->ev[2], b->ev[3])); out->replay_ms = ms;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits) {
+  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  if (hits) *hits = b->d_hits;
+  if (n_hits) *n_hits = b->d_nhits;
+  return WSR_OK;
+}
+
+int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stride, wsr_hit* hits,
+                     int32_t* n_hits) {
+  if (!h || nq < 0 || (nq && (!q || !hits || !n_hits))) return fail(WSR_E_INVALID, "bad arguments");
+  if (nq == 0) return WSR_OK;
+  wsr_batch* b = nullptr;
+  int rc = wsr_batch_create(h, nq, stride, &b);
+  if (rc) return rc;
+  rc = wsr_batch_upload(h, b, q, nq);
+  if (!rc) rc = wsr_batch_run(h, b);
+  if (!rc) rc = wsr_batch_fetch(h, b, hits, n_hits);
+  wsr_batch_destroy(h, b);
+  return rc;
+}
+
+int wsr_debug_decode_block(wsr_handle* h, int32_t id, int32_t block, int32_t which, uint32_t* out,
+                           int32_t* count) {
+  if (!h || !out || id < 0 || id >= static_cast<int32_t>(h->lists.size()))
+    return fail(WSR_E_INVALID, "bad list id");
+  const ListDev& L = h->lists[id];
+  if (block < 0 || static_cast<uint32_t>(block) >= L.nblk) return fail(WSR_E_INVALID, "bad block");
+  std::lock_guard<std::mutex> g(h->mu);
+  const BlockDev& bd = h->blocks[L.blk0 + block];
+  const uint32_t cnt = static_cast<uint32_t>(block) == L.nblk - 1 ? L.tail_cnt : 128u;
+  try {
+    uint32_t* d_out = nullptr;
+    HIP_OK(hipMalloc(&d_out, 128 * sizeof(uint32_t)));
+    const uint8_t* p = h->d_blob + L.base + (which ? bd.tf_rel : bd.doc_rel);
+    hipError_t e = launch_decode_probe(p, cnt, which == 0, bd.prev, d_out, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, 128 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    HIP_OK(e);
+  } catch (const std::exception& ex) {
+    return fail(WSR_E_HIP, ex.what());
+  }
+  if (count) *count = static_cast<int32_t>(cnt);
+  return WSR_OK;
+}
+
+// ------------------------------------------------------------ building --
+static void fill_stats(const BuildStats& s, wsr_build_stats* st) {
+  if (!st) return;
+  st->n_docs = s.n_docs;
+  st->n_terms = s.n_terms;
+  st->n_postings = s.n_postings;
+  st->vacuum_bytes = s.vacuum_bytes;
+  st->docs_char4_ge_0x80 = s.docs_char4_ge_0x80;
+  st->avg_length = s.avg_length;
+}
+
+int wsr_build_from_linedoc(const char* linedoc, int64_t n_rows, const char* format,
+                           const char* out_dir, wsr_build_stats* st) {
+  if (!linedoc || !format || !out_dir) return fail(WSR_E_INVALID, "null argument");
+  try {
+    fill_stats(build_from_linedoc(linedoc, n_rows, format, out_dir), st);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, double zipf_s,
+                        uint64_t seed, int32_t with_positions, int32_t threads,
+                        wsr_build_stats* st) {
+  if (!out_dir || n_docs <= 0 || vocab <= 0) return fail(WSR_E_INVALID, "bad arguments");
+  try {
+    SyntheticSpec sp;
+    sp.n_docs = n_docs;
+    sp.vocab = vocab;
+    sp.zipf_s = zipf_s;
+    sp.seed = seed;
+    sp.with_positions = with_positions != 0;
+    sp.threads = threads;
+    fill_stats(build_synthetic(sp, out_dir), st);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                         const char* out_path, int64_t* n_written) {
+  if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
+  try {
+    int64_t n = gen_two_term_log(index_dir, n_queries, seed, out_path);
+    if (n_written) *n_written = n;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+}  // extern "C"

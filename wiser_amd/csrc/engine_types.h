@@ -1,0 +1,65 @@
+// Plain structs shared by the host planner and the HIP kernels.  All of them
+// live in HBM; sizes are fixed so the host and device agree byte for byte.
+#pragma once
+
+#include <cstdint>
+
+namespace wiser {
+
+constexpr int kMaxTerms = 8;    // terms per conjunctive query (reference phrase cap, query_processing.h:695)
+constexpr int kMaxK = 64;       // n_results per query: the running top-k lives in one wave's lanes
+
+// One posting list in the HBM image.
+struct ListDev {
+  uint64_t base;      // byte offset of the list's docid span in the blob
+  uint32_t blk0;      // first entry in the block directory
+  uint32_t nblk;      // blocks of this list in the image
+  uint32_t df;        // GLOBAL document frequency (drives idf and planning)
+  uint32_t tail_cnt;  // postings in the image's last block (128 unless a VInts tail)
+  double idf;         // calc_es_idf(N, df) computed on the host with libm log
+};
+static_assert(sizeof(ListDev) == 32, "ListDev layout");
+
+// One 128-posting block (= one skip-list row, flash_containers.h:312-350).
+struct BlockDev {
+  uint32_t prev;      // previous_doc_id: delta seed, doc id of posting 128*i - 1
+  uint32_t last;      // doc id of the block's last posting
+  uint32_t doc_rel;   // docid blob offset relative to ListDev::base
+  uint32_t tf_rel;    // tf blob offset relative to ListDev::base
+};
+static_assert(sizeof(BlockDev) == 16, "BlockDev layout");
+
+struct QueryIn {
+  int32_t n_terms;          // 0 => empty result
+  int32_t k;                // n_results (0 => empty result)
+  int32_t list[kMaxTerms];  // list ids in query order; -1 => term missing => empty
+};
+static_assert(sizeof(QueryIn) == 40, "QueryIn layout");
+
+// Written by the plan kernel for every query of a batch.
+struct QueryPlan {
+  uint32_t item_base;   // first work item of this query
+  uint32_t n_items;     // segments (0 for empty queries)
+  uint32_t seg_blocks;  // driver blocks per segment
+  uint32_t driver;      // query slot of the shortest list
+  uint64_t ev_base;     // first event slot (capacity = driver blocks * 128)
+};
+static_assert(sizeof(QueryPlan) == 24, "QueryPlan layout");
+
+// A heap-insertion event: a survivor that a top-k heap run from empty over its
+// segment inserts (query_processing.h:595-602).
+struct Event {
+  double score;
+  int32_t doc;
+  int32_t pad;
+};
+static_assert(sizeof(Event) == 16, "Event layout");
+
+struct HitDev {
+  int32_t doc;
+  int32_t pad;
+  double score;
+};
+static_assert(sizeof(HitDev) == 16, "HitDev layout");
+
+}  // namespace wiser

@@ -1,0 +1,287 @@
+#include "index.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <fcntl.h>
+#include <fstream>
+#include <stdexcept>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <thread>
+#include <unistd.h>
+
+#include "format.h"
+
+namespace wiser {
+
+VacuumIndex::~VacuumIndex() {
+  if (map_) ::munmap(map_, map_len_);
+}
+
+int32_t VacuumIndex::find(const std::string& term) const {
+  auto it = lookup_.find(term);
+  return it == lookup_.end() ? -1 : it->second;
+}
+
+void VacuumIndex::open(const std::string& dir) {
+  // --- my.doc_length (doc_length_store.h:163-190)
+  {
+    std::ifstream f(dir + "/my.doc_length", std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open " + dir + "/my.doc_length");
+    int32_t count = 0;
+    f.read(reinterpret_cast<char*>(&count), 4);
+    f.read(reinterpret_cast<char*>(&avg_), 8);
+    if (!f || count < 0) throw std::runtime_error("truncated my.doc_length");
+    std::string rec(static_cast<size_t>(count) * 5, '\0');
+    f.read(&rec[0], rec.size());
+    if (!f) throw std::runtime_error("truncated my.doc_length records");
+    for (int32_t i = 0; i < count; ++i) {
+      int32_t id;
+      std::memcpy(&id, &rec[5 * i], 4);
+      if (id < 0) throw std::runtime_error("negative doc id in my.doc_length");
+      if (static_cast<size_t>(id) >= c4_.size()) c4_.resize(static_cast<size_t>(id) + 1, 0);
+      c4_[id] = static_cast<uint8_t>(rec[5 * i + 4]);
+    }
+    n_docs_ = count;
+  }
+  // Bm25Similarity::BuildCache (scoring.h:85-90): k1 * (1 - b + b * len / avg)
+  {
+    const double k1 = 1.2, b = 0.75;
+    for (int i = 0; i < 256; ++i) {
+      const uint32_t fl = char4_to_length(static_cast<uint8_t>(i));
+      cache_[i] = k1 * (1 - b + b * fl / avg_);
+    }
+  }
+  // --- my.vacuum
+  {
+    int fd = ::open((dir + "/my.vacuum").c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open " + dir + "/my.vacuum");
+    struct stat sb;
+    if (::fstat(fd, &sb) != 0) { ::close(fd); throw std::runtime_error("stat my.vacuum"); }
+    map_len_ = static_cast<uint64_t>(sb.st_size);
+    void* p = map_len_ ? ::mmap(nullptr, map_len_, PROT_READ, MAP_PRIVATE, fd, 0) : nullptr;
+    ::close(fd);
+    if (map_len_ && p == MAP_FAILED) throw std::runtime_error("mmap my.vacuum failed");
+    map_ = static_cast<uint8_t*>(p);
+    if (map_len_ < 1 || map_[0] != kVacuumMagic)
+      throw std::runtime_error("my.vacuum: wrong first byte (expected 0x88)");
+    // Bloom fields: has_bloom_begin, bytes, entries, f32 ratio; same for end.
+    const uint8_t* q = map_ + 1;
+    const uint8_t* e = map_ + std::min<uint64_t>(map_len_, kVacuumHeaderBytes);
+    uint64_t has_bloom[2] = {0, 0};
+    for (int s = 0; s < 2; ++s) {
+      uint64_t v;
+      int l = get_varint(q, e, &has_bloom[s]); q += l;
+      l = get_varint(q, e, &v); q += l;
+      l = get_varint(q, e, &v); q += l;
+      q += 4;
+      if (q > e) throw std::runtime_error("my.vacuum: truncated header");
+    }
+    if (has_bloom[1])
+      throw std::runtime_error("my.vacuum carries bloom filters: the phrase/bloom path is not built yet");
+  }
+  // --- my.tip (term_index.h:147-159)
+  {
+    std::ifstream f(dir + "/my.tip", std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open " + dir + "/my.tip");
+    std::string all((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    size_t at = 0;
+    while (at < all.size()) {
+      if (at + 4 > all.size()) throw std::runtime_error("truncated my.tip");
+      uint32_t len;
+      std::memcpy(&len, &all[at], 4);
+      at += 4;
+      if (at + len + 8 > all.size()) throw std::runtime_error("truncated my.tip entry");
+      std::string term = all.substr(at, len);
+      at += len;
+      int64_t v;
+      std::memcpy(&v, &all[at], 8);
+      at += 8;
+      const uint64_t off = tip_offset(v);
+      if (off + 2 > map_len_ || map_[off] != kPostingListMagic)
+        throw std::runtime_error("posting list of '" + term + "' has a wrong magic byte");
+      uint64_t df = 0;
+      if (!get_varint(map_ + off + 1, map_ + map_len_, &df) || df == 0)
+        throw std::runtime_error("posting list of '" + term + "' has a bad doc freq");
+      auto ins = lookup_.emplace(term, static_cast<int32_t>(terms_.size()));
+      if (!ins.second) { // later entries win, as htrie_map assignment does
+        const int32_t id = ins.first->second;
+        off_[id] = off;
+        df_[id] = static_cast<uint32_t>(df);
+        continue;
+      }
+      terms_.push_back(term);
+      off_.push_back(off);
+      df_.push_back(static_cast<uint32_t>(df));
+    }
+  }
+  // calc_es_idf (scoring.h:21-25) with N = doc_lengths.Size() (vacuum_engine.h:240)
+  idf_.resize(df_.size());
+  for (size_t i = 0; i < df_.size(); ++i) {
+    const int N = n_docs_, d = static_cast<int>(df_[i]);
+    idf_[i] = std::log(1 + (N - d + 0.5) / (d + 0.5));
+  }
+}
+
+std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
+  const uint8_t* end = map_ + map_len_;
+  const uint8_t* p = map_ + off_[id];
+  uint64_t v;
+  int l = get_varint(p + 1, end, &v);
+  if (!l) throw std::runtime_error("bad df varint");
+  p += 1 + l + 8;  // magic | df | 8 reserved bytes (bloom section pointers)
+  if (p >= end || p[0] != kSkipListMagic) throw std::runtime_error("bad skip list magic");
+  uint64_t n = 0;
+  l = get_varint(p + 1, end, &n);
+  p += 1 + l;
+  std::vector<SkipRow> out(n);
+  // fields: d prev_doc, d docid off, d tf off, d pos off, pos idx, d off off, off idx
+  uint64_t pd = 0, pdo = 0, pto = 0;
+  for (uint64_t r = 0; r < n; ++r) {
+    uint64_t f[7];
+    for (int k = 0; k < 7; ++k) {
+      l = get_varint(p, end, &f[k]);
+      if (!l) throw std::runtime_error("truncated skip list");
+      p += l;
+    }
+    pd = static_cast<uint32_t>(pd + f[0]);
+    pdo += f[1]; pto += f[2];
+    out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto};
+  }
+  return out;
+}
+
+bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta,
+                       uint32_t prev, uint32_t* out) {
+  if (p >= end) return false;
+  if (p[0] == kPackMagic) {
+    if (cnt != kPackSize || p + 2 > end) return false;
+    const int b = p[1];
+    if (b < 1 || b > 32 || p + 2 + 16 * b > end) return false;
+    const uint8_t* d = p + 2;
+    for (int j = 0; j < kPackSize; ++j) {
+      uint64_t bit = static_cast<uint64_t>(j) * b, val = 0;
+      for (int k = 0; k < b; ++k, ++bit) val |= static_cast<uint64_t>((d[bit >> 3] >> (bit & 7)) & 1) << k;
+      out[j] = static_cast<uint32_t>(val);
+    }
+  } else if (p[0] == kVIntsMagic) {
+    uint64_t nb = 0;
+    int l = get_varint(p + 1, end, &nb);
+    if (!l) return false;
+    const uint8_t* q = p + 1 + l;
+    const uint8_t* qe = q + nb;
+    if (qe > end) return false;
+    for (int j = 0; j < cnt; ++j) {
+      uint64_t v;
+      int m = get_varint(q, qe, &v);
+      if (!m) return false;
+      q += m;
+      out[j] = static_cast<uint32_t>(v);
+    }
+  } else {
+    return false;
+  }
+  if (delta) {
+    uint32_t acc = prev;
+    for (int j = 0; j < cnt; ++j) { acc += out[j]; out[j] = acc; }
+  }
+  return true;
+}
+
+HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads) {
+  const int32_t L = idx.n_lists();
+  const uint8_t* file = idx.file();
+  const uint8_t* fend = file + idx.file_bytes();
+  struct Part {
+    std::vector<BlockDev> blocks;  // doc_rel / tf_rel relative to the list's span
+    std::vector<uint8_t> bytes;    // docid span followed by tf span
+    uint32_t tail_cnt = 0;
+  };
+  std::vector<Part> parts(L);
+  std::atomic<int32_t> next{0};
+  std::atomic<bool> failed{false};
+  std::string err;
+  auto work = [&] {
+    try {
+      for (int32_t id; (id = next++) < L && !failed;) {
+        const std::vector<SkipRow> rows = idx.rows(id);
+        const uint32_t df = idx.df(id);
+        const uint64_t nrows = rows.size();
+        if (nrows != (df + kPackSize - 1) / kPackSize)
+          throw std::runtime_error("skip rows do not match df for '" + idx.term(id) + "'");
+        // last doc of each block: prev of the next row; decode the final block.
+        std::vector<uint32_t> last(nrows);
+        for (uint64_t r = 0; r + 1 < nrows; ++r) last[r] = rows[r + 1].prev_doc;
+        const int fcnt = static_cast<int>(df - kPackSize * (nrows - 1));
+        {
+          uint32_t tmp[kPackSize];
+          if (!host_decode_block(file + rows[nrows - 1].doc_off, fend, fcnt, true,
+                                 rows[nrows - 1].prev_doc, tmp))
+            throw std::runtime_error("cannot decode the last block of '" + idx.term(id) + "'");
+          last[nrows - 1] = tmp[fcnt - 1];
+        }
+        // blocks whose docs can fall into [doc_lo, doc_hi): docs of block r lie in
+        // (prev_doc, last] (block 0: [first, last]).
+        uint64_t r0 = nrows, r1 = 0;
+        for (uint64_t r = 0; r < nrows; ++r) {
+          const bool below_hi = (r == 0) || (static_cast<uint64_t>(rows[r].prev_doc) + 1 < doc_hi);
+          if (below_hi && last[r] >= doc_lo) { r0 = std::min(r0, r); r1 = r + 1; }
+        }
+        Part& pt = parts[id];
+        if (r0 >= r1) continue;  // list has no docs in this shard
+        const uint64_t d0 = rows[r0].doc_off;
+        const uint64_t d1 = rows[r1 - 1].doc_off + blob_bytes(file + rows[r1 - 1].doc_off, fend);
+        const uint64_t t0 = rows[r0].tf_off;
+        const uint64_t t1 = rows[r1 - 1].tf_off + blob_bytes(file + rows[r1 - 1].tf_off, fend);
+        if (d1 <= d0 || t1 <= t0 || d1 > idx.file_bytes() || t1 > idx.file_bytes())
+          throw std::runtime_error("bad blob span for '" + idx.term(id) + "'");
+        pt.bytes.assign(file + d0, file + d1);
+        pt.bytes.insert(pt.bytes.end(), file + t0, file + t1);
+        for (uint64_t r = r0; r < r1; ++r)
+          pt.blocks.push_back(BlockDev{rows[r].prev_doc, last[r],
+                                       static_cast<uint32_t>(rows[r].doc_off - d0),
+                                       static_cast<uint32_t>((d1 - d0) + rows[r].tf_off - t0)});
+        pt.tail_cnt = (r1 == nrows) ? static_cast<uint32_t>(fcnt) : kPackSize;
+      }
+    } catch (const std::exception& ex) {
+      if (!failed.exchange(true)) err = ex.what();
+    }
+  };
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> ts;
+  for (int i = 0; i < threads; ++i) ts.emplace_back(work);
+  for (auto& t : ts) t.join();
+  if (failed) throw std::runtime_error(err);
+
+  HostImage img;
+  img.doc_lo = doc_lo;
+  img.doc_hi = doc_hi;
+  img.lists.resize(L);
+  img.list_bytes.resize(L);
+  uint64_t total = 0, nb = 0;
+  for (auto& p : parts) { total += (p.bytes.size() + 15) & ~15ull; nb += p.blocks.size(); }
+  img.blob.resize(total + 64, 0);  // tail pad: lanes read whole dwords past a blob end
+  img.blocks.reserve(nb);
+  img.blk_last.reserve(nb);
+  uint64_t at = 0;
+  for (int32_t id = 0; id < L; ++id) {
+    Part& p = parts[id];
+    ListDev& ld = img.lists[id];
+    ld.base = at;
+    ld.blk0 = static_cast<uint32_t>(img.blocks.size());
+    ld.nblk = static_cast<uint32_t>(p.blocks.size());
+    ld.df = idx.df(id);
+    ld.tail_cnt = p.tail_cnt;
+    ld.idf = idx.idf(id);
+    if (!p.bytes.empty()) std::memcpy(&img.blob[at], p.bytes.data(), p.bytes.size());
+    img.docid_tf_bytes += p.bytes.size();
+    img.list_bytes[id] = p.bytes.size();
+    at += (p.bytes.size() + 15) & ~15ull;
+    for (auto& b : p.blocks) { img.blocks.push_back(b); img.blk_last.push_back(b.last); }
+    std::vector<uint8_t>().swap(p.bytes);
+  }
+  return img;
+}
+
+}  // namespace wiser

@@ -1,0 +1,89 @@
+// Host-side Vacuum index loader and HBM image builder.
+//
+// VacuumIndex::open() is the equivalent of VacuumEngine::Load()
+// (vacuum_engine.h:144-180) minus the doc store: it reads my.doc_length
+// (doc_length_store.h:163-190), the term dictionary my.tip (term_index.h:106-159)
+// and memory-maps my.vacuum (VacuumHeader::Load, flash_iterators.h:826-873).
+//
+// build_image() decodes every list's skip list ONCE (the reference re-decodes
+// it on every query, flash_iterators.h:946-948) into a struct-of-arrays block
+// directory and copies the [docid | tf] byte span of every list -- the
+// reference's "prefetch zone" minus the header -- unchanged into one blob that
+// is uploaded to HBM.  A doc-id range [lo, hi) restricts the image to the
+// blocks that can hold docs of that range (multi-GPU doc-range shards).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "engine_types.h"
+
+namespace wiser {
+
+struct SkipRow {
+  uint32_t prev_doc;
+  uint64_t doc_off;  // absolute file offsets of the docid / tf blobs of this row
+  uint64_t tf_off;
+};
+
+class VacuumIndex {
+ public:
+  VacuumIndex() = default;
+  ~VacuumIndex();
+  VacuumIndex(const VacuumIndex&) = delete;
+  VacuumIndex& operator=(const VacuumIndex&) = delete;
+
+  void open(const std::string& dir);  // throws std::runtime_error
+
+  int32_t n_lists() const { return static_cast<int32_t>(terms_.size()); }
+  int32_t find(const std::string& term) const;  // -1 when absent
+  const std::string& term(int32_t id) const { return terms_[id]; }
+  uint32_t df(int32_t id) const { return df_[id]; }
+  uint64_t list_offset(int32_t id) const { return off_[id]; }
+  double idf(int32_t id) const { return idf_[id]; }
+
+  // N = number of doc-length records (DocLengthCharStore::Size()).
+  int32_t n_docs() const { return n_docs_; }
+  double avg_length() const { return avg_; }
+  const std::vector<uint8_t>& char4_lengths() const { return c4_; }
+  const double* bm25_cache() const { return cache_; }
+
+  // Skip rows of one list (decoded on demand).
+  std::vector<SkipRow> rows(int32_t id) const;
+  const uint8_t* file() const { return map_; }
+  uint64_t file_bytes() const { return map_len_; }
+
+ private:
+  std::vector<std::string> terms_;
+  std::unordered_map<std::string, int32_t> lookup_;
+  std::vector<uint64_t> off_;
+  std::vector<uint32_t> df_;
+  std::vector<double> idf_;
+  std::vector<uint8_t> c4_;
+  int32_t n_docs_ = 0;
+  double avg_ = 0;
+  double cache_[256] = {0};
+  uint8_t* map_ = nullptr;
+  uint64_t map_len_ = 0;
+};
+
+struct HostImage {
+  std::vector<uint8_t> blob;
+  std::vector<ListDev> lists;   // indexed by list id
+  std::vector<BlockDev> blocks;
+  std::vector<uint32_t> blk_last;
+  std::vector<uint64_t> list_bytes;  // docid+tf span bytes per list in the image
+  uint32_t doc_lo = 0, doc_hi = 0;
+  uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
+};
+
+// Decode one block (pack or VInts) at p into out[0..cnt); delta-coded blocks
+// are seeded with prev.  Returns false on a malformed blob.
+bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta,
+                       uint32_t prev, uint32_t* out);
+
+HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads);
+
+}  // namespace wiser

@@ -1,0 +1,47 @@
+// Launch interface of kernels.hip (host side).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "engine_types.h"
+
+namespace wiser {
+
+// Kernel view of one HBM index image (a whole index or one doc-range shard).
+struct IndexArgs {
+  const uint8_t* blob;      // [docid | tf] spans of every list, byte-exact from my.vacuum
+  const ListDev* lists;
+  const BlockDev* blocks;
+  const uint32_t* blk_last; // dense copy of BlockDev::last for the block searches
+  const uint8_t* c4;        // 1-byte lossy doc length per doc id
+  const double* cache;      // Bm25Similarity cache_[256]
+  uint32_t n_c4;
+  uint32_t n_lists;
+  uint32_t doc_lo, doc_hi;  // doc-id range of this image (shard)
+};
+
+// counters[]: 0 total items, 1 queue head, 2 event capacity used, 3 survivors,
+//             4 error flags, 5 driver blocks decoded, 6 other blocks decoded
+enum { kCtrItems = 0, kCtrHead = 1, kCtrEvCap = 2, kCtrSurvivors = 3, kCtrError = 4,
+       kCtrDriverBlocks = 5, kCtrOtherBlocks = 6, kNumCounters = 8 };
+enum { kErrLimit = 1, kErrCapacity = 2 };
+
+constexpr int kSegCost = 48;  // target block decodes per work item; bounds seg_blocks
+
+hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
+                       uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
+                       hipStream_t st);
+hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
+                           uint32_t* counters, Event* events, uint32_t* ev_cnt, int grid,
+                           hipStream_t st);
+hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
+                         const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
+                         hipStream_t st);
+hipError_t launch_decode_probe(const uint8_t* p, uint32_t cnt, bool delta, uint32_t seed,
+                               uint32_t* out, hipStream_t st);
+// resident 64-thread segment workgroups per CU
+int segment_kernel_occupancy();
+
+}  // namespace wiser

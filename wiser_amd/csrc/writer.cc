@@ -1,0 +1,580 @@
+// Vacuum index writer.  Restates the byte layout produced by the reference's
+// VacuumInvertedIndexDumper (flash_engine_dumper.h:288-411) and friends:
+//
+//   my.vacuum : 0x88 | 2 x (varint has_bloom, varint bit_array_bytes,
+//               varint expected_entries, f32 ratio) | zero pad to byte 100,
+//               then one posting list per term:
+//               0xF4 | varint df | 8 reserved bytes (two varint 0s, zero pad)
+//               | skip list | gap | docid box | tf box | position box | offset box
+//   my.tip    : per term u32 len | bytes | i64 (prefetch pages << 48 | list offset)
+//   my.doc_length : i32 n | f64 incremental-mean avg | n x (i32 doc, i8 char4)
+//
+// A "box" (GeneralTermEntry::GetCozyBoxWriter, flash_engine_dumper.h:78-104) is
+// floor(n/128) bit packs followed by one VInts blob holding the n mod 128 rest.
+// Doc ids are delta coded over the whole list (utils.h:573-584); tf raw;
+// positions / offsets delta coded inside each posting's bag.
+//
+// The skip list is first sized as if the data began 512 KiB later (the
+// reference's FakeFileDumper estimate, flash_engine_dumper.h:528-537), the data
+// is placed after that estimate, and the real (possibly shorter) skip list is
+// written in front, leaving a zero gap -- exactly the reference's placement.
+#include "writer.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <random>
+#include <stdexcept>
+#include <sys/stat.h>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "format.h"
+
+namespace wiser {
+namespace {
+
+// ------------------------------------------------------------ term input --
+struct TermPostings {
+  std::vector<uint32_t> docs;
+  std::vector<uint32_t> tfs;
+  std::vector<uint32_t> pos_vals;   // per-bag delta coded
+  std::vector<uint32_t> pos_sizes;
+  std::vector<uint32_t> off_vals;   // per-bag delta coded [s0,e0,s1,e1..]
+  std::vector<uint32_t> off_sizes;
+};
+
+// One encoded box: the bytes plus, for every skip row, where the row's first
+// posting lives (blob offset relative to box start, in-blob index).
+struct Box {
+  std::string bytes;
+  std::vector<uint64_t> row_off;
+  std::vector<uint32_t> row_idx;
+};
+
+// values + per-posting bag sizes -> packs + vints; rows every 128 postings.
+void encode_box(const std::vector<uint32_t>& vals, const std::vector<uint32_t>* sizes,
+                size_t n_postings, bool delta, Box* box) {
+  const size_t nv = vals.size();
+  std::vector<uint32_t> v(nv);
+  if (delta) {
+    uint32_t prev = 0;
+    for (size_t i = 0; i < nv; ++i) { v[i] = vals[i] - prev; prev = vals[i]; }
+  } else {
+    v = vals;
+  }
+  const size_t n_packs = nv / kPackSize;
+  std::vector<uint64_t> blob_off;
+  blob_off.reserve(n_packs + 1);
+  for (size_t p = 0; p < n_packs; ++p) {
+    blob_off.push_back(box->bytes.size());
+    append_pack(&box->bytes, &v[p * kPackSize]);
+  }
+  const size_t rest = nv - n_packs * kPackSize;
+  if (rest) {
+    blob_off.push_back(box->bytes.size());
+    append_vints(&box->bytes, &v[n_packs * kPackSize], static_cast<int>(rest));
+  }
+  // value index of posting p = sum of bag sizes before p
+  uint64_t vi = 0;
+  for (size_t p = 0; p < n_postings; ++p) {
+    if (p % kPackSize == 0) {
+      const size_t blob = vi / kPackSize;
+      if (blob >= blob_off.size())
+        throw std::runtime_error("posting bag points past the last blob (empty bags at list end)");
+      box->row_off.push_back(blob_off[blob]);
+      box->row_idx.push_back(static_cast<uint32_t>(vi % kPackSize));
+    }
+    vi += sizes ? (*sizes)[p] : 1;
+  }
+}
+
+struct EncodedList {
+  uint32_t df = 0;
+  std::vector<uint32_t> prev_doc;  // per row
+  Box doc, tf, pos, off;
+};
+
+void encode_list(const TermPostings& t, EncodedList* e) {
+  const size_t n = t.docs.size();
+  e->df = static_cast<uint32_t>(n);
+  for (size_t r = 0; r * kPackSize < n; ++r)
+    e->prev_doc.push_back(r == 0 ? 0 : t.docs[r * kPackSize - 1]);
+  encode_box(t.docs, nullptr, n, true, &e->doc);
+  encode_box(t.tfs, nullptr, n, false, &e->tf);
+  encode_box(t.pos_vals, &t.pos_sizes, n, false, &e->pos);
+  encode_box(t.off_vals, &t.off_sizes, n, false, &e->off);
+}
+
+// Skip list with the data sections starting at absolute file offset `data0`.
+std::string encode_skip_list(const EncodedList& e, uint64_t data0) {
+  const uint64_t d0 = data0;
+  const uint64_t t0 = d0 + e.doc.bytes.size();
+  const uint64_t p0 = t0 + e.tf.bytes.size();
+  const uint64_t o0 = p0 + e.pos.bytes.size();
+  std::string s;
+  s.push_back(static_cast<char>(kSkipListMagic));
+  const size_t rows = e.prev_doc.size();
+  put_varint(&s, rows);
+  uint32_t pd = 0;
+  uint64_t pdo = 0, pto = 0, ppo = 0, poo = 0;
+  for (size_t r = 0; r < rows; ++r) {
+    const uint64_t dof = d0 + e.doc.row_off[r], tof = t0 + e.tf.row_off[r];
+    const uint64_t pof = p0 + e.pos.row_off[r], oof = o0 + e.off.row_off[r];
+    put_varint(&s, static_cast<uint32_t>(e.prev_doc[r] - pd));
+    put_varint(&s, dof - pdo);
+    put_varint(&s, tof - pto);
+    put_varint(&s, pof - ppo);
+    put_varint(&s, e.pos.row_idx[r]);
+    put_varint(&s, oof - poo);
+    put_varint(&s, e.off.row_idx[r]);
+    pd = e.prev_doc[r]; pdo = dof; pto = tof; ppo = pof; poo = oof;
+  }
+  return s;
+}
+
+class VacuumFileWriter {
+ public:
+  explicit VacuumFileWriter(const std::string& dir) : dir_(dir) {
+    ::mkdir(dir.c_str(), 0777);
+    vac_.open(dir + "/my.vacuum", std::ios::binary | std::ios::trunc);
+    tip_.open(dir + "/my.tip", std::ios::binary | std::ios::trunc);
+    if (!vac_ || !tip_) throw std::runtime_error("cannot create index files in " + dir);
+    // No bloom filters: has_bloom, bit bytes, expected entries = 0, ratio 0.0f,
+    // for the "begin" and the "end" filter (flash_engine_dumper.h:288-316).
+    std::string h;
+    h.push_back(static_cast<char>(kVacuumMagic));
+    for (int i = 0; i < 2; ++i) {
+      put_varint(&h, 0); put_varint(&h, 0); put_varint(&h, 0);
+      h.append(4, '\0');
+    }
+    h.resize(kVacuumHeaderBytes, '\0');
+    vac_.write(h.data(), h.size());
+    off_ = kVacuumHeaderBytes;
+  }
+
+  void add(const std::string& term, const EncodedList& e) {
+    const uint64_t start = off_;
+    std::string head;
+    head.push_back(static_cast<char>(kPostingListMagic));
+    put_varint(&head, e.df);
+    const size_t resv = head.size();
+    put_varint(&head, 0);
+    put_varint(&head, 0);
+    head.resize(resv + 8, '\0');
+    const uint64_t skip_start = start + head.size();
+    const size_t est = encode_skip_list(e, skip_start + 512 * 1024).size();
+    const std::string skip = encode_skip_list(e, skip_start + est);
+    if (skip.size() > est) throw std::runtime_error("skip list estimate too small");
+    head += skip;
+    head.append(est - skip.size(), '\0');
+    vac_.write(head.data(), head.size());
+    vac_.write(e.doc.bytes.data(), e.doc.bytes.size());
+    vac_.write(e.tf.bytes.data(), e.tf.bytes.size());
+    vac_.write(e.pos.bytes.data(), e.pos.bytes.size());
+    vac_.write(e.off.bytes.data(), e.off.bytes.size());
+    const uint64_t tf_end = skip_start + est + e.doc.bytes.size() + e.tf.bytes.size();
+    off_ = skip_start + est + e.doc.bytes.size() + e.tf.bytes.size() + e.pos.bytes.size() +
+           e.off.bytes.size();
+    const uint32_t pages = static_cast<uint32_t>((tf_end - start) / 4096);
+    const int64_t v = encode_tip_value(pages, start);
+    const uint32_t len = static_cast<uint32_t>(term.size());
+    tip_.write(reinterpret_cast<const char*>(&len), 4);
+    tip_.write(term.data(), term.size());
+    tip_.write(reinterpret_cast<const char*>(&v), 8);
+    ++n_terms_;
+  }
+
+  uint64_t bytes() const { return off_; }
+  int64_t terms() const { return n_terms_; }
+  void close() { vac_.close(); tip_.close(); }
+
+ private:
+  std::string dir_;
+  std::ofstream vac_, tip_;
+  uint64_t off_ = 0;
+  int64_t n_terms_ = 0;
+};
+
+// Incremental mean exactly as DocLengthCharStore::AddLength (doc_length_store.h:104-112).
+struct DocLengths {
+  std::vector<uint8_t> c4;
+  double avg = 0;
+  int64_t cnt = 0, big = 0;
+  void add(uint32_t len) {
+    avg = avg + (static_cast<int>(len) - avg) / (cnt + 1);
+    uint8_t c = length_to_char4(len);
+    if (c >= 0x80) ++big;
+    c4.push_back(c);
+    ++cnt;
+  }
+  void write(const std::string& dir) const {
+    std::ofstream f(dir + "/my.doc_length", std::ios::binary | std::ios::trunc);
+    if (!f) throw std::runtime_error("cannot write my.doc_length");
+    int32_t n = static_cast<int32_t>(c4.size());
+    f.write(reinterpret_cast<const char*>(&n), 4);
+    f.write(reinterpret_cast<const char*>(&avg), 8);
+    std::string rec(5 * c4.size(), '\0');
+    for (int32_t i = 0; i < n; ++i) {
+      std::memcpy(&rec[5 * i], &i, 4);
+      rec[5 * i + 4] = static_cast<char>(c4[i]);
+    }
+    f.write(rec.data(), rec.size());
+  }
+};
+
+// ------------------------------------------------------- linedoc parsing --
+// utils::explode (utils.cc:29-42): split, dropping empty pieces.
+std::vector<std::string> explode(const std::string& s, char c) {
+  std::vector<std::string> v;
+  std::string cur;
+  for (char ch : s) {
+    if (ch != c) cur += ch;
+    else if (!cur.empty()) { v.push_back(cur); cur.clear(); }
+  }
+  if (!cur.empty()) v.push_back(cur);
+  return v;
+}
+
+// utils::explode_strict (utils.cc:52-67): split, keeping empty pieces.
+std::vector<std::string> explode_strict(const std::string& s, char c) {
+  std::vector<std::string> v;
+  std::string cur;
+  for (char ch : s) {
+    if (ch != c) cur += ch;
+    else { v.push_back(cur); cur.clear(); }
+  }
+  v.push_back(cur);
+  return v;
+}
+
+// utils::parse_offsets (utils.cc:105-141): "s,e;s,e;." groups per term.
+std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parse_offsets(const std::string& s) {
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> res;
+  std::string grp;
+  auto flush_group = [&](const std::string& g) {
+    std::vector<std::pair<uint32_t, uint32_t>> term;
+    std::string buf;
+    for (char ch : g) {
+      if (ch != ';') buf += ch;
+      else if (!buf.empty()) {
+        size_t c = buf.find(',');
+        term.emplace_back(std::stoul(buf.substr(0, c)), std::stoul(buf.substr(c + 1)));
+        buf.clear();
+      }
+    }
+    res.push_back(term);
+  };
+  for (char ch : s) {
+    if (ch != '.') grp += ch;
+    else if (!grp.empty()) { flush_group(grp); grp.clear(); }
+  }
+  return res;
+}
+
+void add_bag_delta(std::vector<uint32_t>* vals, std::vector<uint32_t>* sizes,
+                   const std::vector<uint32_t>& raw) {
+  uint32_t prev = 0;
+  for (uint32_t x : raw) { vals->push_back(x - prev); prev = x; }
+  sizes->push_back(static_cast<uint32_t>(raw.size()));
+}
+
+}  // namespace
+
+BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
+                              const std::string& format, const std::string& out_dir) {
+  const bool token_only = format == "TOKEN_ONLY";
+  if (!token_only && format != "WITH_POSITIONS")
+    throw std::runtime_error("unsupported linedoc format " + format);
+  std::ifstream in(linedoc);
+  if (!in) throw std::runtime_error("cannot open linedoc " + linedoc);
+  std::string line;
+  std::getline(in, line);  // header row
+  std::map<std::string, TermPostings> index;  // sorted term order in my.tip / my.vacuum
+  DocLengths lens;
+  uint32_t doc = 0;
+  while ((n_rows < 0 || doc < n_rows) && std::getline(in, line)) {
+    std::vector<std::string> items = explode_strict(line, '\t');
+    if (items.size() < (token_only ? 3u : 5u))
+      throw std::runtime_error("linedoc row " + std::to_string(doc) + " has too few columns");
+    if (token_only) {
+      // Body = tokens = column 2; tf = token count; positions = token ordinals;
+      // offsets = char span (end inclusive) of each occurrence in column 2.
+      const std::string& toks = items[2];
+      std::map<std::string, std::vector<uint32_t>> occ;
+      std::map<std::string, std::vector<uint32_t>> offs;
+      uint32_t ordinal = 0;
+      size_t i = 0;
+      while (i < toks.size()) {
+        if (toks[i] == ' ') { ++i; continue; }
+        size_t j = i;
+        while (j < toks.size() && toks[j] != ' ') ++j;
+        std::string t = toks.substr(i, j - i);
+        occ[t].push_back(ordinal++);
+        offs[t].push_back(static_cast<uint32_t>(i));
+        offs[t].push_back(static_cast<uint32_t>(j - 1));
+        i = j;
+      }
+      for (auto& kv : occ) {
+        TermPostings& tp = index[kv.first];
+        tp.docs.push_back(doc);
+        tp.tfs.push_back(static_cast<uint32_t>(kv.second.size()));
+        add_bag_delta(&tp.pos_vals, &tp.pos_sizes, kv.second);
+        add_bag_delta(&tp.off_vals, &tp.off_sizes, offs[kv.first]);
+      }
+      lens.add(ordinal);
+    } else {
+      std::vector<std::string> toks = explode(items[2], ' ');
+      auto offsets = parse_offsets(items[3]);
+      std::vector<std::string> groups = explode(items[4], '.');
+      if (offsets.size() != toks.size() || groups.size() != toks.size())
+        throw std::runtime_error("linedoc row " + std::to_string(doc) +
+                                 ": token/offset/position column mismatch");
+      std::unordered_set<std::string> seen;
+      for (size_t t = 0; t < toks.size(); ++t) {
+        if (!seen.insert(toks[t]).second)
+          throw std::runtime_error("duplicate token '" + toks[t] + "' in row " + std::to_string(doc));
+        std::vector<uint32_t> pos;
+        for (auto& p : explode(groups[t], ';')) pos.push_back(static_cast<uint32_t>(std::stoul(p)));
+        std::vector<uint32_t> flat;
+        for (auto& pr : offsets[t]) { flat.push_back(pr.first); flat.push_back(pr.second); }
+        TermPostings& tp = index[toks[t]];
+        tp.docs.push_back(doc);
+        tp.tfs.push_back(static_cast<uint32_t>(offsets[t].size()));
+        add_bag_delta(&tp.pos_vals, &tp.pos_sizes, pos);
+        add_bag_delta(&tp.off_vals, &tp.off_sizes, flat);
+      }
+      lens.add(static_cast<uint32_t>(explode(items[1], ' ').size()));
+    }
+    ++doc;
+  }
+  VacuumFileWriter w(out_dir);
+  BuildStats st;
+  for (auto& kv : index) {
+    EncodedList e;
+    encode_list(kv.second, &e);
+    w.add(kv.first, e);
+    st.n_postings += e.df;
+  }
+  w.close();
+  lens.write(out_dir);
+  st.n_docs = doc;
+  st.n_terms = w.terms();
+  st.vacuum_bytes = static_cast<int64_t>(w.bytes());
+  st.docs_char4_ge_0x80 = lens.big;
+  st.avg_length = lens.avg;
+  return st;
+}
+
+// ------------------------------------------------------ synthetic corpus --
+namespace {
+
+std::string synth_term(int64_t id) {
+  char b[32];
+  std::snprintf(b, sizeof b, "t%07lld", static_cast<long long>(id));
+  return b;
+}
+
+// Vose alias table for P(rank r) ~ r^-s, r = 1..V (term id = r - 1).
+struct Alias {
+  std::vector<double> prob;
+  std::vector<uint32_t> alias;
+  explicit Alias(int64_t V, double s) : prob(V), alias(V) {
+    std::vector<double> w(V);
+    double tot = 0;
+    for (int64_t r = 0; r < V; ++r) { w[r] = std::pow(static_cast<double>(r + 1), -s); tot += w[r]; }
+    std::vector<int64_t> small, large;
+    for (int64_t r = 0; r < V; ++r) {
+      w[r] = w[r] * V / tot;
+      (w[r] < 1.0 ? small : large).push_back(r);
+    }
+    while (!small.empty() && !large.empty()) {
+      int64_t a = small.back(); small.pop_back();
+      int64_t g = large.back();
+      prob[a] = w[a]; alias[a] = static_cast<uint32_t>(g);
+      w[g] = (w[g] + w[a]) - 1.0;
+      if (w[g] < 1.0) { large.pop_back(); small.push_back(g); }
+    }
+    for (int64_t g : large) { prob[g] = 1.0; alias[g] = static_cast<uint32_t>(g); }
+    for (int64_t a : small) { prob[a] = 1.0; alias[a] = static_cast<uint32_t>(a); }
+  }
+  uint32_t draw(std::mt19937_64& g) const {
+    const uint64_t V = prob.size();
+    uint64_t col = g() % V;
+    double u = static_cast<double>(g() >> 11) * 0x1.0p-53;
+    return u < prob[col] ? static_cast<uint32_t>(col) : alias[col];
+  }
+};
+
+double unit(std::mt19937_64& g) { return (static_cast<double>(g() >> 11) + 0.5) * 0x1.0p-53; }
+
+}  // namespace
+
+BuildStats build_synthetic(const SyntheticSpec& sp, const std::string& out_dir) {
+  const int64_t N = sp.n_docs, V = sp.vocab;
+  int threads = sp.threads > 0 ? sp.threads : static_cast<int>(std::thread::hardware_concurrency());
+  if (threads < 1) threads = 1;
+  Alias alias(V, sp.zipf_s);
+
+  // 1) doc lengths (one stream, so they do not depend on the thread count)
+  std::vector<uint32_t> len(N);
+  {
+    std::mt19937_64 g(sp.seed);
+    for (int64_t d = 0; d < N; ++d) {
+      double z = std::sqrt(-2.0 * std::log(unit(g))) * std::cos(2.0 * M_PI * unit(g));
+      double l = std::round(std::exp(sp.len_mu + sp.len_sigma * z));
+      if (l < 1) l = 1;
+      if (l > sp.len_max) l = static_cast<double>(sp.len_max);
+      len[d] = static_cast<uint32_t>(l);
+    }
+  }
+  std::vector<uint64_t> doc_start(N + 1, 0);
+  for (int64_t d = 0; d < N; ++d) doc_start[d + 1] = doc_start[d] + len[d];
+  const uint64_t T = doc_start[N];
+
+  // 2) tokens, chunked by 4096 docs with per-chunk seeds
+  std::vector<uint32_t> tok(T);
+  const int64_t CH = 4096, nch = (N + CH - 1) / CH;
+  {
+    std::atomic<int64_t> next{0};
+    auto work = [&] {
+      for (int64_t c; (c = next++) < nch;) {
+        std::mt19937_64 g(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(c + 1)));
+        for (int64_t d = c * CH; d < std::min(N, (c + 1) * CH); ++d)
+          for (uint64_t i = doc_start[d]; i < doc_start[d + 1]; ++i) tok[i] = alias.draw(g);
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+  }
+
+  // 3) term-major occurrence lists (doc order, then position order)
+  std::vector<uint64_t> term_start(V + 1, 0);
+  for (uint64_t i = 0; i < T; ++i) ++term_start[tok[i] + 1];
+  for (int64_t v = 0; v < V; ++v) term_start[v + 1] += term_start[v];
+  std::vector<uint32_t> occ_doc(T), occ_pos(T);
+  {
+    std::vector<uint64_t> fill(term_start.begin(), term_start.end() - 1);
+    for (int64_t d = 0; d < N; ++d)
+      for (uint64_t i = doc_start[d]; i < doc_start[d + 1]; ++i) {
+        uint64_t at = fill[tok[i]]++;
+        occ_doc[at] = static_cast<uint32_t>(d);
+        occ_pos[at] = static_cast<uint32_t>(i - doc_start[d]);
+      }
+  }
+  std::vector<uint32_t>().swap(tok);
+
+  // 4) encode lists in parallel batches, append in term-id order
+  VacuumFileWriter w(out_dir);
+  BuildStats st;
+  const int64_t BATCH = 8192;
+  for (int64_t b0 = 0; b0 < V; b0 += BATCH) {
+    const int64_t b1 = std::min(V, b0 + BATCH);
+    std::vector<std::unique_ptr<EncodedList>> enc(b1 - b0);
+    std::atomic<int64_t> next{b0};
+    auto work = [&] {
+      for (int64_t v; (v = next++) < b1;) {
+        const uint64_t s = term_start[v], e = term_start[v + 1];
+        if (s == e) continue;
+        TermPostings tp;
+        for (uint64_t i = s; i < e;) {
+          uint64_t j = i;
+          while (j < e && occ_doc[j] == occ_doc[i]) ++j;
+          tp.docs.push_back(occ_doc[i]);
+          tp.tfs.push_back(static_cast<uint32_t>(j - i));
+          if (sp.with_positions) {
+            uint32_t pp = 0, po = 0;
+            for (uint64_t k = i; k < j; ++k) {
+              uint32_t p = occ_pos[k];
+              tp.pos_vals.push_back(p - pp); pp = p;
+              // 8-char term + 1 space per token: span [9p, 9p + 7]
+              tp.off_vals.push_back(9 * p - po); tp.off_vals.push_back(7); po = 9 * p + 7;
+            }
+            tp.pos_sizes.push_back(static_cast<uint32_t>(j - i));
+            tp.off_sizes.push_back(static_cast<uint32_t>(2 * (j - i)));
+          } else {
+            // minimal bags: one position (the first) and one offset pair per posting
+            tp.pos_vals.push_back(occ_pos[i]);
+            tp.pos_sizes.push_back(1);
+            tp.off_vals.push_back(9 * occ_pos[i]); tp.off_vals.push_back(7);
+            tp.off_sizes.push_back(2);
+          }
+          i = j;
+        }
+        auto el = std::make_unique<EncodedList>();
+        encode_list(tp, el.get());
+        enc[v - b0] = std::move(el);
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+    for (int64_t v = b0; v < b1; ++v)
+      if (enc[v - b0]) { w.add(synth_term(v), *enc[v - b0]); st.n_postings += enc[v - b0]->df; }
+  }
+  w.close();
+  DocLengths lens;
+  lens.c4.reserve(N);
+  for (int64_t d = 0; d < N; ++d) lens.add(len[d]);
+  lens.write(out_dir);
+  st.n_docs = N;
+  st.n_terms = w.terms();
+  st.vacuum_bytes = static_cast<int64_t>(w.bytes());
+  st.docs_char4_ge_0x80 = lens.big;
+  st.avg_length = lens.avg;
+  return st;
+}
+
+// --------------------------------------------------------- query log gen --
+int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t seed,
+                         const std::string& out_path) {
+  std::ifstream tip(dir + "/my.tip", std::ios::binary);
+  std::ifstream vac(dir + "/my.vacuum", std::ios::binary);
+  if (!tip || !vac) throw std::runtime_error("cannot open index in " + dir);
+  std::vector<std::string> low, high;
+  for (;;) {
+    uint32_t len;
+    if (!tip.read(reinterpret_cast<char*>(&len), 4)) break;
+    std::string term(len, '\0');
+    int64_t v;
+    tip.read(&term[0], len);
+    tip.read(reinterpret_cast<char*>(&v), 8);
+    uint8_t buf[16] = {0};
+    vac.seekg(static_cast<std::streamoff>(tip_offset(v)));
+    vac.read(reinterpret_cast<char*>(buf), sizeof buf);
+    uint64_t df = 0;
+    if (buf[0] != kPostingListMagic || !get_varint(buf + 1, buf + sizeof buf, &df))
+      throw std::runtime_error("bad posting list header for " + term);
+    if (df >= 1 && df < 10000) low.push_back(term);
+    else if (df >= 10000 && df < 10000000) high.push_back(term);
+  }
+  if (low.empty() || high.empty() || low.size() + high.size() < 2)
+    throw std::runtime_error("df table has an empty low or high group");
+  std::mt19937_64 g(seed);
+  std::unordered_set<std::string> seen;
+  std::vector<std::string> out;
+  int64_t guard = 0;
+  while (static_cast<int64_t>(out.size()) < n_queries) {
+    if (++guard > 1000 * n_queries + 1000000) throw std::runtime_error("cannot find enough distinct queries");
+    const auto& g1 = (g() & 1) ? high : low;
+    const auto& g2 = (g() & 1) ? high : low;
+    std::string t1 = g1[g() % g1.size()];
+    std::string t2 = g2[g() % g2.size()];
+    int spins = 0;
+    while (t2 == t1 && spins++ < 1000) t2 = g2[g() % g2.size()];
+    if (t2 == t1) continue;
+    if (t2 < t1) std::swap(t1, t2);
+    std::string q = t1 + " " + t2;
+    if (seen.insert(q).second) out.push_back(q);
+  }
+  std::ofstream f(out_path, std::ios::trunc);
+  for (auto& q : out) f << q << "\n";
+  return static_cast<int64_t>(out.size());
+}
+
+}  // namespace wiser

@@ -1,0 +1,50 @@
+// Vacuum index writer (host, C++17): builds my.vacuum / my.tip / my.doc_length
+// from a linedoc or from a seeded synthetic Zipf corpus.  Off the query hot
+// path; it exists because the reference's own dumper cannot be built here
+//  and the engine needs indexes in the reference layout.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace wiser {
+
+struct SyntheticSpec {
+  int64_t n_docs = 1000000;
+  int64_t vocab = 500000;
+  double zipf_s = 1.07;
+  double len_mu = 5.0;
+  double len_sigma = 0.8;
+  int64_t len_max = 20000;
+  uint64_t seed = 0x5EED2026ull;
+  bool with_positions = true;  // write position + offset sections (reference layout)
+  int threads = 0;             // 0 = hardware concurrency
+};
+
+struct BuildStats {
+  int64_t n_docs = 0;
+  int64_t n_terms = 0;
+  int64_t n_postings = 0;
+  int64_t vacuum_bytes = 0;
+  int64_t docs_char4_ge_0x80 = 0;  // lengths >= 2^18: reference indexes its cache with a
+                                   // negative signed char (UB, scoring.h:65-69)
+  double avg_length = 0;
+};
+
+// format: "TOKEN_ONLY" or "WITH_POSITIONS" (engine_loader.h:53-96).
+// Throws std::runtime_error on malformed input.
+BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
+                              const std::string& format, const std::string& out_dir);
+
+BuildStats build_synthetic(const SyntheticSpec& spec, const std::string& out_dir);
+
+// Two-term query log restating tools/gen_synthetic_log.py:191-214 over the
+// df table of an index: group "low" = floor(log10 df) in 0..3, "high" = 4..6;
+// each term picks a group uniformly then a term uniformly; t1 != t2; the pair
+// is sorted; duplicates are dropped until n_queries distinct queries exist.
+// Written one query per line (query_pool.h:319-378 format).
+int64_t gen_two_term_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
+                         const std::string& out_path);
+
+}  // namespace wiser

@@ -1,0 +1,257 @@
+"""Python mirror of the reference operator surface for the Vacuum engine.
+
+Same names, argument meaning and error behaviour as the reference's
+``SearchEngineServiceNew`` implemented by ``VacuumEngine``
+(src/qq_mem/src/engine_services.h:14-27, vacuum_engine.h:119-258) and its
+``SearchQuery`` / ``SearchResult`` types (types.h:205-346); every call goes
+through the C ABI of libwiser_hip.so into the HIP kernels.
+
+    engine = CreateSearchEngine("vacuum:vacuum_dump:/path/to/index")
+    engine.Load()
+    result = engine.Search(SearchQuery(["hello", "world"], n_results=10))
+
+Behaviour kept from the reference:
+  * ``n_results == 0`` -> empty result (vacuum_engine.h:206-208);
+  * any term missing from the dictionary -> empty result, ``doc_freqs`` left
+    empty (vacuum_engine.h:210-215);
+  * entries ordered as the reference heap pops them (SortHeap), f64 scores.
+Not built in this round (raise ``NotImplementedError`` rather than answer
+differently): phrase queries of two or more terms, snippets.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from . import _capi
+from ._capi import check, lib
+
+
+@dataclass
+class SearchQuery:
+    """types.h:205-256"""
+    terms: List[str]
+    n_results: int = 5
+    return_snippets: bool = False
+    n_snippet_passages: int = 3
+    is_phrase: bool = False
+
+
+@dataclass
+class SearchResultEntry:
+    """types.h:259-274 (snippet stays empty: the doc store is out of scope)"""
+    doc_id: int
+    doc_score: float
+    snippet: str = ""
+
+
+@dataclass
+class SearchResult:
+    """types.h:297-346"""
+    entries: List[SearchResultEntry] = field(default_factory=list)
+    doc_freqs: List[int] = field(default_factory=list)
+
+    def Size(self) -> int:
+        return len(self.entries)
+
+    def __getitem__(self, i):
+        return self.entries[i]
+
+
+def ParseUrl(url: str):
+    """engine_factory.h:21-31: ``vacuum:<source_type>:<path>``."""
+    parts = url.split(":", 2)
+    if len(parts) != 3 or parts[0] != "vacuum":
+        raise ValueError(f"not a vacuum url: {url}")
+    return parts[1], parts[2]
+
+
+def CreateSearchEngine(url: str, bloom_factor: int = 1, device: int = 0) -> "VacuumEngine":
+    """engine_factory.h:33-50 (only ``vacuum:vacuum_dump:<dir>`` is served here)."""
+    source, path = ParseUrl(url)
+    if source != "vacuum_dump":
+        raise ValueError(f"unsupported vacuum source type: {source}")
+    return VacuumEngine(path, bloom_factor=bloom_factor, device=device)
+
+
+class VacuumEngine:
+    """SearchEngineServiceNew over the HIP engine (vacuum_engine.h:119-258)."""
+
+    def __init__(self, engine_dir_path: str, bloom_factor: int = 1, device: int = 0,
+                 doc_range: Optional[Sequence[int]] = None, threads: int = 0):
+        self.engine_dir_path = engine_dir_path
+        self.bloom_factor = bloom_factor
+        self.device = device
+        self.doc_range = doc_range
+        self.threads = threads
+        self._h = None
+
+    # ---- SearchEngineServiceNew -------------------------------------
+    def Load(self) -> None:
+        if self._h is not None:
+            raise RuntimeError("Engine is already loaded.")  # vacuum_engine.h:145
+        opts = _capi.OpenOpts()
+        opts.device = self.device
+        opts.doc_lo, opts.doc_hi = (self.doc_range if self.doc_range else (0, 0))
+        opts.threads = self.threads
+        h = C.c_void_p()
+        check(lib.wsr_open(self.engine_dir_path.encode(), C.byref(opts), C.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if self._h is not None:
+            lib.wsr_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def TermCount(self) -> int:
+        n = C.c_int32()
+        check(lib.wsr_term_count(self._h, C.byref(n)))
+        return n.value
+
+    def NumDocs(self) -> int:
+        n = C.c_int32()
+        check(lib.wsr_n_docs(self._h, C.byref(n)))
+        return n.value
+
+    def PostinglistSizes(self, terms: Sequence[str]) -> Dict[str, int]:
+        out = {}
+        for t in terms:
+            lid, df = self.lookup(t)
+            if lid >= 0:
+                out[t] = df
+        return out
+
+    def Search(self, query: SearchQuery) -> SearchResult:
+        return self.SearchBatch([query])[0]
+
+    # ---- batched extension -----------------------------------------
+    def lookup(self, term: str):
+        lid, df = C.c_int32(), C.c_int32()
+        check(lib.wsr_lookup(self._h, term.encode(), C.byref(lid), C.byref(df)))
+        return lid.value, df.value
+
+    def resolve(self, query: SearchQuery):
+        """-> (wsr_query, doc_freqs or None) with the reference's empty-result rules."""
+        if query.is_phrase and len(query.terms) > 1:
+            raise NotImplementedError("phrase queries (position intersect + bloom) are not built yet")
+        if len(query.terms) > _capi.MAX_TERMS:
+            raise NotImplementedError(f"more than {_capi.MAX_TERMS} terms per query")
+        if query.n_results > _capi.MAX_K:
+            raise NotImplementedError(f"n_results above {_capi.MAX_K}")
+        q = _capi.Query()
+        q.k = max(0, int(query.n_results))
+        ids, dfs = [], []
+        for t in query.terms:
+            lid, df = self.lookup(t)
+            ids.append(lid)
+            dfs.append(df)
+        missing = any(i < 0 for i in ids) or not ids
+        q.n_terms = 0 if (missing or q.k == 0) else len(ids)
+        for i, lid in enumerate(ids):
+            q.list_ids[i] = lid
+        freqs = None if (missing or q.k == 0) else dfs
+        return q, freqs
+
+    def SearchBatch(self, queries: Sequence[SearchQuery]) -> List[SearchResult]:
+        if not queries:
+            return []
+        arr = (_capi.Query * len(queries))()
+        freqs = []
+        stride = 1
+        for i, sq in enumerate(queries):
+            q, f = self.resolve(sq)
+            arr[i] = q
+            freqs.append(f)
+            stride = max(stride, q.k)
+        hits = (_capi.Hit * (len(queries) * stride))()
+        nh = (C.c_int32 * len(queries))()
+        check(lib.wsr_search_batch(self._h, arr, len(queries), stride, hits, nh))
+        out = []
+        for i in range(len(queries)):
+            r = SearchResult()
+            if freqs[i] is not None:
+                r.doc_freqs = list(freqs[i])
+                for j in range(nh[i]):
+                    h = hits[i * stride + j]
+                    r.entries.append(SearchResultEntry(h.doc_id, h.score))
+            out.append(r)
+        return out
+
+    def decode_block(self, list_id: int, block: int, which: int = 0):
+        """Device decode of one block (test hook) -> list of values."""
+        buf = (C.c_uint32 * 128)()
+        cnt = C.c_int32()
+        check(lib.wsr_debug_decode_block(self._h, list_id, block, which, buf, C.byref(cnt)))
+        return list(buf[: cnt.value])
+
+
+class ResidentBatch:
+    """A query batch kept in HBM (wsr_batch_*): upload once, run many times."""
+
+    def __init__(self, engine: VacuumEngine, max_queries: int, hit_stride: int):
+        self.engine = engine
+        self.stride = hit_stride
+        b = C.c_void_p()
+        check(lib.wsr_batch_create(engine._h, max_queries, hit_stride, C.byref(b)))
+        self._b = b
+        self.nq = 0
+
+    def upload(self, queries) -> None:
+        """queries: ctypes array of _capi.Query."""
+        check(lib.wsr_batch_upload(self.engine._h, self._b, queries, len(queries)))
+        self.nq = len(queries)
+
+    def run(self) -> None:
+        check(lib.wsr_batch_run(self.engine._h, self._b))
+
+    def fetch(self):
+        hits = (_capi.Hit * (max(self.nq, 1) * self.stride))()
+        nh = (C.c_int32 * max(self.nq, 1))()
+        check(lib.wsr_batch_fetch(self.engine._h, self._b, hits, nh))
+        return hits, nh
+
+    def stats(self) -> _capi.BatchStats:
+        st = _capi.BatchStats()
+        check(lib.wsr_batch_stats_get(self.engine._h, self._b, C.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if self._b is not None:
+            lib.wsr_batch_destroy(self.engine._h, self._b)
+            self._b = None
+
+
+def sync(engine: VacuumEngine) -> None:
+    check(lib.wsr_sync(engine._h))
+
+
+# ---- index building (host only) -------------------------------------------
+def build_from_linedoc(linedoc: str, out_dir: str, fmt: str = "WITH_POSITIONS",
+                       n_rows: int = -1) -> _capi.BuildStats:
+    st = _capi.BuildStats()
+    check(lib.wsr_build_from_linedoc(linedoc.encode(), n_rows, fmt.encode(), out_dir.encode(),
+                                     C.byref(st)))
+    return st
+
+
+def build_synthetic(out_dir: str, n_docs: int = 1_000_000, vocab: int = 500_000,
+                    zipf_s: float = 1.07, seed: int = 0x5EED2026, with_positions: bool = True,
+                    threads: int = 0) -> _capi.BuildStats:
+    st = _capi.BuildStats()
+    check(lib.wsr_build_synthetic(out_dir.encode(), n_docs, vocab, zipf_s, seed,
+                                  1 if with_positions else 0, threads, C.byref(st)))
+    return st
+
+
+def gen_two_term_log(index_dir: str, out_path: str, n_queries: int = 100_000, seed: int = 7) -> int:
+    n = C.c_int64()
+    check(lib.wsr_gen_two_term_log(index_dir.encode(), n_queries, seed, out_path.encode(),
+                                   C.byref(n)))
+    return n.value
