@@ -57,11 +57,13 @@ struct wsr_handle {
   ListDev* d_lists = nullptr;
   BlockDev* d_blocks = nullptr;
   uint32_t* d_last = nullptr;
+  uint32_t* d_meta = nullptr;
   uint8_t* d_c4 = nullptr;
   double* d_cache = nullptr;
   std::vector<ListDev> lists;       // host copy of the directory heads
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
   std::vector<BlockDev> blocks;     // host copy (debug decode)
+  std::vector<uint32_t> meta;
   int grid = 0;
 };
 
@@ -110,16 +112,19 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     dev_upload(&h->d_lists, img.lists);
     dev_upload(&h->d_blocks, img.blocks);
     dev_upload(&h->d_last, img.blk_last);
+    dev_upload(&h->d_meta, img.blk_meta);
     dev_upload(&h->d_c4, h->idx.char4_lengths());
     std::vector<double> cache(h->idx.bm25_cache(), h->idx.bm25_cache() + 256);
     dev_upload(&h->d_cache, cache);
     h->lists = img.lists;
     h->blocks = img.blocks;
+    h->meta = img.blk_meta;
     h->list_bytes = img.list_bytes;
     h->args.blob = h->d_blob;
     h->args.lists = h->d_lists;
     h->args.blocks = h->d_blocks;
     h->args.blk_last = h->d_last;
+    h->args.blk_meta = h->d_meta;
     h->args.c4 = h->d_c4;
     h->args.cache = h->d_cache;
     h->args.n_c4 = static_cast<uint32_t>(h->idx.char4_lengths().size());
@@ -131,7 +136,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     HIP_OK(hipGetDeviceProperties(&prop, dev));
     int occ = segment_kernel_occupancy();
     if (occ < 1) occ = 1;
-    h->grid = prop.multiProcessorCount * std::min(occ, 16);
+    h->grid = prop.multiProcessorCount * std::min(occ, 32);
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -145,6 +150,7 @@ void wsr_close(wsr_handle* h) {
   if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
   for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
+                  static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache)})
     if (p) (void)hipFree(p);
   delete h;
@@ -370,7 +376,8 @@ int wsr_debug_decode_block(wsr_handle* h, int32_t id, int32_t block, int32_t whi
     uint32_t* d_out = nullptr;
     HIP_OK(hipMalloc(&d_out, 128 * sizeof(uint32_t)));
     const uint8_t* p = h->d_blob + L.base + (which ? bd.tf_rel : bd.doc_rel);
-    hipError_t e = launch_decode_probe(p, cnt, which == 0, bd.prev, d_out, h->stream);
+    const uint32_t bits = which ? (h->meta[L.blk0 + block] >> 8) : (h->meta[L.blk0 + block] & 0xFF);
+    hipError_t e = launch_decode_probe(p, bits, cnt, which == 0, bd.prev, d_out, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess) e = hipMemcpy(out, d_out, 128 * sizeof(uint32_t), hipMemcpyDeviceToHost);
     (void)hipFree(d_out);

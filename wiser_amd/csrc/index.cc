@@ -195,6 +195,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   const uint8_t* fend = file + idx.file_bytes();
   struct Part {
     std::vector<BlockDev> blocks;  // doc_rel / tf_rel relative to the list's span
+    std::vector<uint32_t> meta;
     std::vector<uint8_t> bytes;    // docid span followed by tf span
     uint32_t tail_cnt = 0;
   };
@@ -238,10 +239,19 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
           throw std::runtime_error("bad blob span for '" + idx.term(id) + "'");
         pt.bytes.assign(file + d0, file + d1);
         pt.bytes.insert(pt.bytes.end(), file + t0, file + t1);
-        for (uint64_t r = r0; r < r1; ++r)
+        for (uint64_t r = r0; r < r1; ++r) {
           pt.blocks.push_back(BlockDev{rows[r].prev_doc, last[r],
                                        static_cast<uint32_t>(rows[r].doc_off - d0),
                                        static_cast<uint32_t>((d1 - d0) + rows[r].tf_off - t0)});
+          const uint8_t* pd = file + rows[r].doc_off;
+          const uint8_t* pf = file + rows[r].tf_off;
+          const uint32_t bd = pd[0] == kPackMagic ? pd[1] : 0u;
+          const uint32_t bf = pf[0] == kPackMagic ? pf[1] : 0u;
+          if ((pd[0] != kPackMagic && pd[0] != kVIntsMagic) || (pf[0] != kPackMagic && pf[0] != kVIntsMagic) ||
+              bd > 32 || bf > 32 || (pd[0] == kPackMagic && bd == 0) || (pf[0] == kPackMagic && bf == 0))
+            throw std::runtime_error("bad blob header in '" + idx.term(id) + "'");
+          pt.meta.push_back(bd | (bf << 8));
+        }
         pt.tail_cnt = (r1 == nrows) ? static_cast<uint32_t>(fcnt) : kPackSize;
       }
     } catch (const std::exception& ex) {
@@ -264,6 +274,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.blob.resize(total + 64, 0);  // tail pad: lanes read whole dwords past a blob end
   img.blocks.reserve(nb);
   img.blk_last.reserve(nb);
+  img.blk_meta.reserve(nb);
   uint64_t at = 0;
   for (int32_t id = 0; id < L; ++id) {
     Part& p = parts[id];
@@ -279,6 +290,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     img.list_bytes[id] = p.bytes.size();
     at += (p.bytes.size() + 15) & ~15ull;
     for (auto& b : p.blocks) { img.blocks.push_back(b); img.blk_last.push_back(b.last); }
+    img.blk_meta.insert(img.blk_meta.end(), p.meta.begin(), p.meta.end());
     std::vector<uint8_t>().swap(p.bytes);
   }
   return img;

@@ -74,6 +74,7 @@ struct HostImage {
   std::vector<ListDev> lists;   // indexed by list id
   std::vector<BlockDev> blocks;
   std::vector<uint32_t> blk_last;
+  std::vector<uint32_t> blk_meta;    // docid pack bits | tf pack bits << 8 (0 = VInts)
   std::vector<uint64_t> list_bytes;  // docid+tf span bytes per list in the image
   uint32_t doc_lo = 0, doc_hi = 0;
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image

@@ -15,6 +15,7 @@ struct IndexArgs {
   const ListDev* lists;
   const BlockDev* blocks;
   const uint32_t* blk_last; // dense copy of BlockDev::last for the block searches
+  const uint32_t* blk_meta; // docid pack bits | tf pack bits << 8 (0 = VInts blob)
   const uint8_t* c4;        // 1-byte lossy doc length per doc id
   const double* cache;      // Bm25Similarity cache_[256]
   uint32_t n_c4;
@@ -39,8 +40,8 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);
-hipError_t launch_decode_probe(const uint8_t* p, uint32_t cnt, bool delta, uint32_t seed,
-                               uint32_t* out, hipStream_t st);
+hipError_t launch_decode_probe(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
+                               uint32_t seed, uint32_t* out, hipStream_t st);
 // resident 64-thread segment workgroups per CU
 int segment_kernel_occupancy();
 

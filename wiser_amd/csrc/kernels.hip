@@ -24,9 +24,10 @@
 //                   fp64 in query-term order, and keep a running top-k (one f64
 //                   per lane) to emit the survivors a heap started empty at the
 //                   segment start would insert ("events", in doc-id order).
-//   replay_kernel   one lane per query: replays the events of its segments, in
-//                   doc-id order, through a restatement of libstdc++'s
-//                   push_heap/pop_heap with the reference comparator, then SortHeap.
+//   replay_kernel   one wave per query: filters the events of its segments, in
+//                   doc-id order, down to the reference heap's insertions and
+//                   applies them to a restatement of libstdc++'s push_heap /
+//                   pop_heap with the reference comparator, then SortHeap.
 //
 // Exactness of the event filter: survivor i is inserted by a heap run from
 // empty over a sequence iff fewer than k earlier survivors have a score >= s_i.
@@ -61,23 +62,53 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
-    if (l >= d) x += y;
-  }
+// DPP lane shuffles (no LDS crossbar, no per-width address registers).
+// Lanes whose source is outside the row / wave read 0.
+template <int CTRL, int ROWMASK = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROWMASK, 0xF, false));
+}
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143, kWaveShr1 = 0x138;
+
+// inclusive sum inside aligned groups of W lanes (W = 2..64)
+template <int W>
+__device__ __forceinline__ uint32_t group_incl_scan(uint32_t x) {
+  const uint32_t r = threadIdx.x & ((W < 16 ? W : 16) - 1);
+  uint32_t y;
+  y = dpp<kRowShr1>(x); if (r >= 1) x += y;
+  if (W > 2) { y = dpp<kRowShr2>(x); if (r >= 2) x += y; }
+  if (W > 4) { y = dpp<kRowShr4>(x); if (r >= 4) x += y; }
+  if (W > 8) { y = dpp<kRowShr8>(x); if (r >= 8) x += y; }
+  if (W > 16) { y = dpp<kRowBcast15, 0xA>(x); x += y; }
+  if (W > 32) { y = dpp<kRowBcast31, 0xC>(x); x += y; }
   return x;
 }
 
-__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    uint32_t y = __shfl_xor(x, d, 64);
-    x = x > y ? x : y;
-  }
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) { return group_incl_scan<64>(x); }
+
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// max over the lanes below this one (0 for lane 0)
+__device__ __forceinline__ uint32_t wave_excl_max(uint32_t x) {
+  const uint32_t r = threadIdx.x & 15;
+  x = dpp<kWaveShr1>(x);
+  uint32_t y;
+  y = dpp<kRowShr1>(x); if (r >= 1) x = umax(x, y);
+  y = dpp<kRowShr2>(x); if (r >= 2) x = umax(x, y);
+  y = dpp<kRowShr4>(x); if (r >= 4) x = umax(x, y);
+  y = dpp<kRowShr8>(x); if (r >= 8) x = umax(x, y);
+  y = dpp<kRowBcast15, 0xA>(x); x = umax(x, y);
+  y = dpp<kRowBcast31, 0xC>(x); x = umax(x, y);
   return x;
+}
+
+// value of lane l-1 (lane 0 reads 0)
+__device__ __forceinline__ double wave_shr1_f64(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = dpp<kWaveShr1>(static_cast<uint32_t>(u));
+  const uint32_t hi = dpp<kWaveShr1>(static_cast<uint32_t>(u >> 32));
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
 }
 
 // Value j of a 128-value pack whose data bytes start at d (bit width b):
@@ -101,17 +132,16 @@ __device__ __forceinline__ uint32_t load_byte(const uint8_t* p) {
 
 // Wave-cooperative decode of one block (pack of 128 or VInts tail of cnt) into
 // out[0..cnt); delta blocks are prefix-summed from `seed` (doc ids), raw blocks
-// are term frequencies.  Values past cnt are written as the last value (delta)
-// or 0 (raw).  Ends with the wave's LDS writes visible to every lane.
-__device__ void decode_block(const uint8_t* p, uint32_t cnt, bool delta, uint32_t seed,
-                             uint32_t* out) {
+// are term frequencies.  `bits` is the pack width from the block directory
+// (0 = VInts blob), so no dependent header load precedes the data loads.
+// Ends with the wave's LDS writes visible to every lane.
+__device__ void decode_block(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
+                             uint32_t seed, uint32_t* out) {
   const uint32_t l = threadIdx.x & 63;
   uint32_t x0, x1;
-  const uint32_t magic = uni(load_byte(p));
-  if (magic == 0xD6) {
-    const uint32_t b = uni(load_byte(p + 1));
-    x0 = pack_value(p + 2, b, 2 * l);
-    x1 = pack_value(p + 2, b, 2 * l + 1);
+  if (bits) {
+    x0 = pack_value(p + 2, bits, 2 * l);
+    x1 = pack_value(p + 2, bits, 2 * l + 1);
   } else {
     // 0x9B | varint nbytes | LEB128 values.  Terminator bytes (MSB clear) are
     // found with a ballot per 64-byte chunk; a terminator's rank is its value
@@ -173,23 +203,42 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t* s, uint32_t 
 }
 
 // First block j in [cur, nblk) of a list with last[j] >= x (nblk if none):
-// the block DocIdIterator::GetBlobIndexToGo walks to (flash_iterators.h:218-227),
-// found by galloping from the cursor.
+// the block DocIdIterator::GetBlobIndexToGo walks to (flash_iterators.h:218-227).
+// Doc ids of a list are spread over the id space, so one interpolation probe
+// between the cursor block and the list's last block lands next to the answer;
+// galloping from the probe and a short bisection finish it.  This keeps the
+// chain of dependent directory loads short for the far jumps of skewed pairs.
 __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cur, uint32_t nblk,
                                                uint32_t x) {
   if (cur >= nblk) return nblk;
-  if (last[cur] >= x) return cur;
-  uint32_t lo = cur + 1, step = 1, hi;
-  for (;;) {
-    const uint32_t probe = cur + step;
-    if (probe >= nblk) { hi = nblk; break; }
-    if (last[probe] >= x) { hi = probe; break; }
-    lo = probe + 1;
-    step <<= 1;
-  }
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (last[mid] < x) lo = mid + 1; else hi = mid;
+  const uint32_t a = last[cur];
+  const uint32_t z = last[nblk - 1];
+  if (a >= x) return cur;
+  if (z < x) return nblk;
+  uint32_t lo = cur + 1, hi = nblk - 1;  // last[lo-1] < x <= last[hi]
+  if (lo < hi) {
+    const float f = static_cast<float>(x - a) * __frcp_rn(static_cast<float>(z - a) + 1.0f);
+    uint32_t g = lo + static_cast<uint32_t>(static_cast<float>(hi - lo) * f);
+    g = g < lo ? lo : (g > hi ? hi : g);
+    if (last[g] >= x) {
+      hi = g;
+      for (uint32_t s = 1; hi >= lo + s; s <<= 1) {
+        const uint32_t p = hi - s;
+        if (last[p] < x) { lo = p + 1; break; }
+        hi = p;
+      }
+    } else {
+      lo = g + 1;
+      for (uint32_t s = 1; lo + s - 1 < hi; s <<= 1) {
+        const uint32_t p = lo + s - 1;
+        if (last[p] >= x) { hi = p; break; }
+        lo = p + 1;
+      }
+    }
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (last[mid] < x) lo = mid + 1; else hi = mid;
+    }
   }
   return lo;
 }
@@ -266,33 +315,90 @@ __global__ __launch_bounds__(1024) void plan_kernel(IndexArgs ix, const QueryIn*
 
 // -------------------------------------------------------------- segment --
 struct WaveLds {
-  uint32_t doc[128];                 // decoded doc ids of the current other-list block
-  uint32_t tf[128];                  // decoded tf block (other list, then driver)
-  uint32_t tfq[kMaxTerms][128];      // tf per query slot per driver posting of the block
+  uint32_t mb[8][128];   // doc ids of up to 8 other-list blocks decoded side by side
+  uint32_t tf[128];      // cooperative decode of a VInts tf tail
+  uint32_t dl[128];      // distinct other-list blocks probed by the driver block
 };
 
-__global__ __launch_bounds__(64) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+// tf of posting `pos` of a block: packs are raw (not delta coded), so a lane
+// reads its value directly; VInts tails are decoded by the whole wave.
+__device__ __forceinline__ uint32_t pack_tf(const uint8_t* p, uint32_t bits, uint32_t pos) {
+  return pack_value(p + 2, bits, pos);
+}
+
+// G packed blocks side by side: group g (64/G lanes) unpacks block dl[base+g],
+// 2G values per lane, prefix-sums them from the block's previous doc id and
+// writes them to mb[g].  Skewed pairs probe many blocks with few docs each;
+// decoding them together turns G dependent rounds into one.
+template <int G>
+__device__ __forceinline__ void grouped_decode(const IndexArgs& ix, const ListDev& B, const uint32_t* dl,
+                                               uint32_t base, uint32_t n, uint32_t (*mb)[128]) {
+  constexpr int W = 64 / G, V = 2 * G;
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t g = l / W, li = l % W;
+  const bool act = base + g < n;
+  const uint32_t jj = act ? dl[base + g] : dl[base];
+  const BlockDev bb = ix.blocks[B.blk0 + jj];
+  const uint32_t bits = ix.blk_meta[B.blk0 + jj] & 0xFF;
+  const uint8_t* p = ix.blob + B.base + bb.doc_rel;
+  uint32_t* out = mb[g];
+  uint32_t sum = 0;
+#pragma unroll 2
+  for (int t = 0; t < V; ++t) {
+    const uint32_t x = pack_value(p + 2, bits, li * V + t);
+    if (act) out[li * V + t] = x;   // raw deltas first: keeps them out of registers
+    sum += x;
+  }
+  const uint32_t inc = group_incl_scan<W>(sum);
+  uint32_t run = bb.prev + (inc - sum);
+  if (act) {
+#pragma unroll 4
+    for (int t = 0; t < V; ++t) { run += out[li * V + t]; out[li * V + t] = run; }
+  }
+}
+
+__device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double cache) {
+  // Bm25Similarity::TfNormLossy (scoring.h:65-69) times idf (scoring.h:136-140)
+  const double f = static_cast<double>(static_cast<int32_t>(tf));
+  const double k1p1 = 1.2 + 1;
+  const double tfn = (f * k1p1) / (f + cache);
+  return idf * tfn;
+}
+
+__global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
                                                      Event* __restrict__ events,
                                                      uint32_t* __restrict__ ev_cnt) {
   __shared__ WaveLds S;
   const uint32_t l = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt();
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0, n_oblk = 0;
   for (;;) {
     uint32_t item = 0;
     if (l == 0) item = atomicAdd(&counters[kCtrHead], 1u);
-    item = uni(__shfl(item, 0, 64));
+    item = uni(item);
     if (item >= total) break;
-    // query of this item: last q with plan[q].item_base <= item
-    uint32_t lo = 0, hi = static_cast<uint32_t>(nq);
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (plan[mid].item_base <= item) lo = mid; else hi = mid;
+    // query of this item: last q with plan[q].item_base <= item (bases are
+    // non-decreasing), found with two wave-wide probes instead of a binary search
+    uint32_t qi;
+    {
+      const uint32_t stride = (static_cast<uint32_t>(nq) + 63) / 64;
+      const uint32_t q1 = l * stride;
+      const uint64_t m1 = __ballot(q1 < static_cast<uint32_t>(nq) && plan[q1].item_base <= item);
+      const uint32_t lo = (63 - __clzll(m1)) * stride;
+      const uint32_t hi = min(lo + stride, static_cast<uint32_t>(nq));
+      uint32_t best = lo;
+      for (uint32_t c = lo; c < hi; c += 64) {
+        const uint32_t q2 = c + l;
+        const uint64_t m2 = __ballot(q2 < hi && plan[q2].item_base <= item);
+        if (m2) best = c + 63 - __clzll(m2);
+        if (m2 != ~0ull) break;
+      }
+      qi = uni(best);
     }
-    const uint32_t qi = uni(lo);
     const QueryPlan P = plan[qi];
     const int32_t* qlist = qs[qi].list;
     const uint32_t r = item - P.item_base;
@@ -308,7 +414,9 @@ __global__ __launch_bounds__(64) void segment_kernel(IndexArgs ix, const QueryIn
 
     // per other slot: cursor into its block directory, seeded at the segment's first doc
     uint32_t cur[kMaxTerms];
-    const uint32_t first_doc = b0 == 0 ? 0u : ix.blocks[A.blk0 + b0].prev + 1u;
+    BlockDev blk = ix.blocks[A.blk0 + b0];
+    uint32_t meta = ix.blk_meta[A.blk0 + b0];
+    const uint32_t first_doc = b0 == 0 ? 0u : blk.prev + 1u;
     bool done = false;   // some other list has no doc >= the next driver doc
 #pragma unroll
     for (uint32_t s = 0; s < kMaxTerms; ++s) {
@@ -324,95 +432,141 @@ __global__ __launch_bounds__(64) void segment_kernel(IndexArgs ix, const QueryIn
     uint32_t pt_n = 0;   // valid entries (uniform)
 
     for (uint32_t b = b0; b < b1 && !done; ++b) {
-      const BlockDev blk = ix.blocks[A.blk0 + b];
+      // prefetch the next driver block's directory entry
+      const uint32_t bn = b + 1 < b1 ? b + 1 : b;
+      const BlockDev blk_next = ix.blocks[A.blk0 + bn];
+      const uint32_t meta_next = ix.blk_meta[A.blk0 + bn];
+      const BlockDev blk_cur = blk;
+      const uint32_t meta_cur = meta;
+      blk = blk_next;
+      meta = meta_next;
       const uint32_t cnt = (b == A.nblk - 1) ? A.tail_cnt : 128u;
-      decode_block(ix.blob + A.base + blk.doc_rel, cnt, true, blk.prev, S.tfq[d]);
-      ++n_dblk;
-      const uint32_t a0 = S.tfq[d][2 * l], a1 = S.tfq[d][2 * l + 1];
       __syncthreads();
+      decode_block(ix.blob + A.base + blk_cur.doc_rel, meta_cur & 0xFF, cnt, true, blk_cur.prev,
+                   S.mb[0]);
+      ++n_dblk;
+      const uint32_t a0 = S.mb[0][2 * l], a1 = S.mb[0][2 * l + 1];
       bool al0 = 2 * l < cnt && a0 >= ix.doc_lo && a0 < ix.doc_hi;
       bool al1 = 2 * l + 1 < cnt && a1 >= ix.doc_lo && a1 < ix.doc_hi;
+      const uint32_t c0 = al0 && a0 < ix.n_c4 ? ix.c4[a0] : 0u;
+      const uint32_t c1 = al1 && a1 < ix.n_c4 ? ix.c4[a1] : 0u;
+      double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
 
       for (uint32_t s = 0; s < nt; ++s) {
-        if (s == d) continue;
         if (__ballot(al0 || al1) == 0) break;
-        const ListDev B = ix.lists[qlist[s]];
+        const ListDev L = ix.lists[qlist[s]];
+        if (s == d) {  // the driver's own tf
+          uint32_t ta0 = 0, ta1 = 0;
+          const uint32_t tbits = meta_cur >> 8;
+          const uint8_t* tp = ix.blob + A.base + blk_cur.tf_rel;
+          if (tbits) {
+            if (al0) ta0 = pack_tf(tp, tbits, 2 * l);
+            if (al1) ta1 = pack_tf(tp, tbits, 2 * l + 1);
+          } else {
+            __syncthreads();
+            decode_block(tp, 0, cnt, false, 0, S.tf);
+            ta0 = S.tf[2 * l];
+            ta1 = S.tf[2 * l + 1];
+          }
+          if (al0) s0 += bm25_term(L.idf, ta0, ix.cache[c0]);
+          if (al1) s1 += bm25_term(L.idf, ta1, ix.cache[c1]);
+          continue;
+        }
+        const ListDev& B = L;
         const uint32_t* last = ix.blk_last + B.blk0;
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kMaxTerms; ++u) if (u == s) c = cur[u];
         const uint32_t j0 = al0 ? find_block(last, c, B.nblk, a0) : kNoBlock;
         const uint32_t j1 = al1 ? find_block(last, c, B.nblk, a1) : kNoBlock;
-        bool pd0 = al0 && j0 < B.nblk, pd1 = al1 && j1 < B.nblk;
         // a doc beyond the list's last block cannot match, nor can any later doc
         if (__ballot((al0 && j0 >= B.nblk) || (al1 && j1 >= B.nblk))) done = true;
-        al0 = pd0; al1 = pd1;
+        al0 = al0 && j0 < B.nblk;
+        al1 = al1 && j1 < B.nblk;
+        // distinct blocks probed, in order (probe blocks are non-decreasing)
+        const uint32_t k0 = al0 ? j0 + 1 : 0u, k1 = al1 ? j1 + 1 : 0u;
+        const uint32_t pre = wave_excl_max(k0 > k1 ? k0 : k1);
+        const bool st0 = k0 && k0 > pre;
+        const bool st1 = k1 && k1 > (pre > k0 ? pre : k0);
+        const uint64_t m0 = __ballot(st0), m1 = __ballot(st1);
+        const uint32_t nd = __popcll(m0) + __popcll(m1);
+        const uint32_t before = __popcll(m0 & lt) + __popcll(m1 & lt);
+        const uint32_t r0 = before + (st0 ? 1u : 0u) - 1u;              // rank of value (l,0)'s block
+        const uint32_t r1 = before + (st0 ? 1u : 0u) + (st1 ? 1u : 0u) - 1u;
+        __syncthreads();
+        if (st0) S.dl[before] = j0;
+        if (st1) S.dl[before + (st0 ? 1u : 0u)] = j1;
+        __syncthreads();
+        // the list's VInts tail (if probed) is the last distinct block
+        const bool tail_vints = nd && B.tail_cnt < 128u &&
+                                S.dl[nd - 1] == B.nblk - 1;
+        const uint32_t npk = tail_vints ? nd - 1 : nd;
         uint32_t t0 = 0, t1 = 0;
-        for (;;) {
-          const uint64_t any0 = __ballot(pd0), any1 = __ballot(pd1);
-          if ((any0 | any1) == 0) break;
-          const int fl = __builtin_ctzll(any0 | any1);
-          const uint32_t cand = ((any0 >> fl) & 1) ? j0 : j1;
-          const uint32_t jj = uni(__builtin_amdgcn_readlane(cand, fl));
-          const BlockDev bb = ix.blocks[B.blk0 + jj];
-          const uint32_t bc = (jj == B.nblk - 1) ? B.tail_cnt : 128u;
-          decode_block(ix.blob + B.base + bb.doc_rel, bc, true, bb.prev, S.doc);
-          ++n_oblk;
-          uint32_t p0 = 0, p1 = 0;
-          bool h0 = false, h1 = false;
-          if (pd0 && j0 == jj) {
-            p0 = lds_lower_bound(S.doc, bc, a0);
-            h0 = p0 < bc && S.doc[p0] == a0;
-            pd0 = false;
-            al0 = h0;
+        bool h0 = false, h1 = false;
+        uint32_t p0 = 0, p1 = 0;
+        for (uint32_t base = 0; base < npk;) {
+          const uint32_t rem = npk - base;
+          uint32_t G;
+          if (rem >= 8) { G = 8; grouped_decode<8>(ix, B, S.dl, base, npk, S.mb); }
+          else if (rem >= 4) { G = 4; grouped_decode<4>(ix, B, S.dl, base, npk, S.mb); }
+          else if (rem >= 2) { G = 2; grouped_decode<2>(ix, B, S.dl, base, npk, S.mb); }
+          else { G = 1; grouped_decode<1>(ix, B, S.dl, base, npk, S.mb); }
+          n_oblk += min(G, rem);
+          __syncthreads();
+          if (al0 && r0 >= base && r0 < base + G) {
+            p0 = lds_lower_bound(S.mb[r0 - base], 128, a0);
+            h0 = p0 < 128 && S.mb[r0 - base][p0] == a0;
           }
-          if (pd1 && j1 == jj) {
-            p1 = lds_lower_bound(S.doc, bc, a1);
-            h1 = p1 < bc && S.doc[p1] == a1;
-            pd1 = false;
-            al1 = h1;
+          if (al1 && r1 >= base && r1 < base + G) {
+            p1 = lds_lower_bound(S.mb[r1 - base], 128, a1);
+            h1 = p1 < 128 && S.mb[r1 - base][p1] == a1;
           }
           __syncthreads();
-          if (__ballot(h0 || h1)) {
-            decode_block(ix.blob + B.base + bb.tf_rel, bc, false, 0, S.tf);
-            if (h0) t0 = S.tf[p0];
-            if (h1) t1 = S.tf[p1];
-            __syncthreads();
-          }
+          base += G;
         }
-        if (al0) S.tfq[s][2 * l] = t0;
-        if (al1) S.tfq[s][2 * l + 1] = t1;
+        if (tail_vints) {
+          const uint32_t jt = B.nblk - 1;
+          const BlockDev bb = ix.blocks[B.blk0 + jt];
+          decode_block(ix.blob + B.base + bb.doc_rel, 0, B.tail_cnt, true, bb.prev, S.mb[0]);
+          ++n_oblk;
+          if (al0 && r0 == nd - 1) {
+            p0 = lds_lower_bound(S.mb[0], B.tail_cnt, a0);
+            h0 = p0 < B.tail_cnt && S.mb[0][p0] == a0;
+          }
+          if (al1 && r1 == nd - 1) {
+            p1 = lds_lower_bound(S.mb[0], B.tail_cnt, a1);
+            h1 = p1 < B.tail_cnt && S.mb[0][p1] == a1;
+          }
+          const bool tv0 = h0 && r0 == nd - 1, tv1 = h1 && r1 == nd - 1;
+          if (__ballot(tv0 || tv1)) {
+            __syncthreads();
+            decode_block(ix.blob + B.base + bb.tf_rel, (ix.blk_meta[B.blk0 + jt] >> 8), B.tail_cnt,
+                         false, 0, S.tf);
+            if (tv0) t0 = S.tf[p0];
+            if (tv1) t1 = S.tf[p1];
+          }
+          __syncthreads();
+        }
+        // tf of matched postings held in packs: direct per-lane read
+        if (h0 && !(tail_vints && r0 == nd - 1)) {
+          const uint32_t tb = ix.blk_meta[B.blk0 + j0] >> 8;
+          t0 = pack_tf(ix.blob + B.base + ix.blocks[B.blk0 + j0].tf_rel, tb, p0);
+        }
+        if (h1 && !(tail_vints && r1 == nd - 1)) {
+          const uint32_t tb = ix.blk_meta[B.blk0 + j1] >> 8;
+          t1 = pack_tf(ix.blob + B.base + ix.blocks[B.blk0 + j1].tf_rel, tb, p1);
+        }
+        al0 = h0;
+        al1 = h1;
+        if (al0) s0 += bm25_term(B.idf, t0, ix.cache[c0]);
+        if (al1) s1 += bm25_term(B.idf, t1, ix.cache[c1]);
         // advance the cursor to the furthest block queried (docs only increase)
-        const uint32_t q0 = j0 != kNoBlock ? j0 : 0u, q1 = j1 != kNoBlock ? j1 : 0u;
-        const uint32_t jm = uni(wave_max(q0 > q1 ? q0 : q1));
+        const uint32_t jm = nd ? uni(S.dl[nd - 1]) : 0u;
 #pragma unroll
         for (uint32_t u = 0; u < kMaxTerms; ++u)
           if (u == s && jm > cur[u]) cur[u] = jm;
       }
-      __syncthreads();
       if (__ballot(al0 || al1) == 0) continue;
-
-      // driver tf
-      decode_block(ix.blob + A.base + blk.tf_rel, cnt, false, 0, S.tf);
-      const uint32_t ta0 = S.tf[2 * l], ta1 = S.tf[2 * l + 1];
-      __syncthreads();
-      // BM25 in query-term order (scoring.h:124-145), fp64, no contraction
-      double s0 = 0.0, s1 = 0.0;
-      const uint32_t c0 = al0 && a0 < ix.n_c4 ? ix.c4[a0] : 0u;
-      const uint32_t c1 = al1 && a1 < ix.n_c4 ? ix.c4[a1] : 0u;
-      const double cache0 = ix.cache[c0], cache1 = ix.cache[c1];
-      for (uint32_t s = 0; s < nt; ++s) {
-        const double idf = ix.lists[qlist[s]].idf;
-        const uint32_t f0 = s == d ? ta0 : S.tfq[s][2 * l];
-        const uint32_t f1 = s == d ? ta1 : S.tfq[s][2 * l + 1];
-        const double k1p1 = 1.2 + 1;
-        const double n0 = (static_cast<double>(static_cast<int32_t>(f0)) * k1p1) /
-                          (static_cast<double>(static_cast<int32_t>(f0)) + cache0);
-        const double n1 = (static_cast<double>(static_cast<int32_t>(f1)) * k1p1) /
-                          (static_cast<double>(static_cast<int32_t>(f1)) + cache1);
-        s0 += idf * n0;
-        s1 += idf * n1;
-      }
       n_surv += __popcll(__ballot(al0)) + __popcll(__ballot(al1));
 
       // running top-k: candidates beat the k-th best at block start
@@ -435,7 +589,7 @@ __global__ __launch_bounds__(64) void segment_kernel(IndexArgs ix, const QueryIn
             ev_out[ev_n] = e;
           }
           ++ev_n;
-          const double up = __shfl_up(pt, 1, 64);
+          const double up = wave_shr1_f64(pt);
           if (l > pos) pt = up;
           else if (l == pos) pt = sv;
           pt_n = pt_n + 1 > k ? k : pt_n + 1;
@@ -495,48 +649,75 @@ struct HeapView {
   }
 };
 
+// One wave per query.  The query's events (its segments in doc-id order) are
+// filtered 64 at a time with the same running top-k test the segment kernel
+// uses -- fewer than k earlier events with a score >= s -- which selects exactly
+// the survivors the reference heap inserts (the top-k multiset of any prefix
+// is carried by its events).  Lane 0 applies each of them to the restated heap
+// as RankDoc does, then SortHeap writes the result.
 __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
                                                     const QueryPlan* __restrict__ plan, int nq,
                                                     const Event* __restrict__ events,
                                                     const uint32_t* __restrict__ ev_cnt,
                                                     HitDev* __restrict__ hits, int hit_stride,
                                                     int32_t* __restrict__ n_hits) {
-  __shared__ double s_sc[kMaxK * 64];
-  __shared__ int32_t s_dc[kMaxK * 64];
-  const int t = threadIdx.x;
-  const int qi = blockIdx.x * 64 + t;
+  __shared__ double s_sc[kMaxK];
+  __shared__ int32_t s_dc[kMaxK];
+  const uint32_t l = threadIdx.x & 63;
+  const int qi = blockIdx.x;
   if (qi >= nq) return;
-  const QueryIn Q = qs[qi];
   const QueryPlan P = plan[qi];
-  HeapView H{s_sc + t, s_dc + t, 64};
-  uint32_t n = 0;
-  const uint32_t k = Q.k > 0 ? static_cast<uint32_t>(Q.k) : 0u;
+  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  HeapView H{s_sc, s_dc, 1};
+  uint32_t n = 0;       // heap size (uniform)
+  double pt = 0.0;      // running top-k of events, lane t = rank t
+  uint32_t pt_n = 0;
   for (uint32_t r = 0; r < P.n_items; ++r) {
     const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
-    const uint32_t ne = ev_cnt[P.item_base + r];
-    for (uint32_t i = 0; i < ne; ++i) {
-      const double sc = ev[i].score;
-      const int32_t dc = ev[i].doc;
-      if (n < k) {
-        H.push(n, sc, dc);
-      } else if (sc > H.s(0)) {
-        H.pop(n);
-        H.push(n, sc, dc);
+    const uint32_t ne = uni(ev_cnt[P.item_base + r]);
+    for (uint32_t c = 0; c < ne; c += 64) {
+      const uint32_t i = c + l;
+      const bool valid = i < ne;
+      double sc = 0.0;
+      int32_t dc = 0;
+      if (valid) { sc = ev[i].score; dc = ev[i].doc; }
+      const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+      uint64_t cm = __ballot(valid && (pt_n < k || sc > kth));
+      while (cm) {
+        const int fl = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const double sv = readlane_f64(sc, fl);
+        const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
+        const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
+        if (pos < k) {
+          if (l == 0) {  // RankDoc (query_processing.h:595-602)
+            uint32_t m = n;
+            if (m < k) H.push(m, sv, dv);
+            else if (sv > H.s(0)) { H.pop(m); H.push(m, sv, dv); }
+          }
+          n = n < k ? n + 1 : n;
+          const double up = wave_shr1_f64(pt);
+          if (l > pos) pt = up;
+          else if (l == pos) pt = sv;
+          pt_n = pt_n + 1 > k ? k : pt_n + 1;
+        }
       }
     }
   }
-  // SortHeap (query_processing.h:551-562): pop to ascending, then reverse
-  const uint32_t m = n;
-  HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
-  for (uint32_t i = 0; i < m; ++i) {
-    HitDev h;
-    h.doc = H.d(0);
-    h.pad = 0;
-    h.score = H.s(0);
-    out[m - 1 - i] = h;
-    H.pop(n);
+  if (l == 0) {
+    // SortHeap (query_processing.h:551-562): pop to ascending, then reverse
+    const uint32_t m = n;
+    HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
+    for (uint32_t i = 0; i < m; ++i) {
+      HitDev h;
+      h.doc = H.d(0);
+      h.pad = 0;
+      h.score = H.s(0);
+      out[m - 1 - i] = h;
+      H.pop(n);
+    }
+    n_hits[qi] = static_cast<int32_t>(m);
   }
-  n_hits[qi] = static_cast<int32_t>(m);
 }
 
 // ------------------------------------------------------------ launchers --
@@ -560,7 +741,7 @@ hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const 
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(replay_kernel, dim3((nq + 63) / 64), dim3(64), 0, st, q, plan, nq, events,
+  hipLaunchKernelGGL(replay_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events,
                      ev_cnt, hits, hit_stride, n_hits);
   return hipGetLastError();
 }
@@ -572,19 +753,19 @@ int segment_kernel_occupancy() {
 }
 
 // Test hook: decode one block of the image on the device (wave-cooperative).
-__global__ __launch_bounds__(64) void decode_probe_kernel(const uint8_t* p, uint32_t cnt,
-                                                          uint32_t delta, uint32_t seed,
-                                                          uint32_t* out) {
+__global__ __launch_bounds__(64) void decode_probe_kernel(const uint8_t* p, uint32_t bits,
+                                                          uint32_t cnt, uint32_t delta,
+                                                          uint32_t seed, uint32_t* out) {
   __shared__ uint32_t buf[128];
-  decode_block(p, cnt, delta != 0, seed, buf);
+  decode_block(p, bits, cnt, delta != 0, seed, buf);
   out[2 * threadIdx.x] = buf[2 * threadIdx.x];
   out[2 * threadIdx.x + 1] = buf[2 * threadIdx.x + 1];
 }
 
-hipError_t launch_decode_probe(const uint8_t* p, uint32_t cnt, bool delta, uint32_t seed,
-                               uint32_t* out, hipStream_t st) {
-  hipLaunchKernelGGL(decode_probe_kernel, dim3(1), dim3(64), 0, st, p, cnt, delta ? 1u : 0u, seed,
-                     out);
+hipError_t launch_decode_probe(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
+                               uint32_t seed, uint32_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(decode_probe_kernel, dim3(1), dim3(64), 0, st, p, bits, cnt, delta ? 1u : 0u,
+                     seed, out);
   return hipGetLastError();
 }
 
