@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-query-class kernel times on the C2 index (diagnostic, not the bench)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import wiser_amd as w
+from wiser_amd import _capi
+
+import argparse
+ap = argparse.ArgumentParser()
+ap.add_argument("--index", default="/tmp/wiser_bench/c2_1000000_500000")
+ap.add_argument("--only", default="")
+ap.add_argument("--repeat", type=int, default=1)
+args = ap.parse_args()
+idx = args.index
+if not os.path.exists(os.path.join(idx, "READY")):
+    os.makedirs(idx, exist_ok=True)
+    w.build_synthetic(idx, threads=16)
+    w.gen_two_term_log(idx, os.path.join(idx, "two_term_100000.log"), 100000, 7)
+    open(os.path.join(idx, "READY"), "w").write("ok")
+eng = w.VacuumEngine(idx)
+eng.Load()
+lines = [l.split() for l in open(os.path.join(idx, "two_term_100000.log")).read().splitlines()]
+cls = {"low-low": [], "low-high": [], "high-high": []}
+for t in lines:
+    h = sum(1 for x in t if eng.lookup(x)[1] >= 10000)
+    cls[["low-low", "low-high", "high-high"][h]].append(t)
+for name, qs in cls.items():
+    if args.only and name != args.only:
+        continue
+    qs = qs[:4096]
+    arr = (_capi.Query * len(qs))()
+    for i, t in enumerate(qs):
+        arr[i] = eng.resolve(w.SearchQuery(t, n_results=10))[0]
+    b = w.ResidentBatch(eng, len(qs), 10)
+    b.upload(arr)
+    for _ in range(3):
+        b.run()
+    w.sync(eng)
+    for _ in range(args.repeat):
+        b.run()
+    st = b.stats()
+    print(f"{name:10s} n={len(qs)} plan={st.plan_ms:.3f} seg={st.segment_ms:.3f} replay={st.replay_ms:.3f} "
+          f"items={st.work_items} surv={st.survivors} dblk={st.driver_blocks} oblk={st.other_blocks} "
+          f"algoMB={st.algo_bytes/1e6:.1f}", flush=True)
+    b.close()
+print("class sizes:", {k: len(v) for k, v in cls.items()})

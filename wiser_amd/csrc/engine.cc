@@ -78,6 +78,8 @@ struct wsr_batch {
   uint64_t item_cap = 0;
   HitDev* d_hits = nullptr;
   int32_t* d_nhits = nullptr;
+  uint32_t* d_stats = nullptr;   // per segment workgroup: survivors, blocks
+  int seg_grid = 0;
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ran = false;
@@ -131,6 +133,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.n_lists = static_cast<uint32_t>(img.lists.size());
     h->args.doc_lo = lo;
     h->args.doc_hi = hi;
+    h->args.avg = h->idx.avg_length();
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
@@ -196,6 +199,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
+    HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride * std::max(h->grid, 1)));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
@@ -211,7 +215,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
-                  static_cast<void*>(b->d_nhits)})
+                  static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
   delete b;
@@ -265,6 +269,8 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     return fail(WSR_E_HIP, e.what());
   }
   b->nq = nq;
+  // persistent grid: never more workgroups than work items can exist
+  b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->grid, items_need)));
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -279,10 +285,11 @@ int wsr_batch_run(wsr_handle* h, wsr_batch* b) {
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * kNumCounters, st));
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
-                       static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)), st));
+                       static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
+                       b->seg_grid, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                           h->grid, st));
+                           b->d_stats, b->seg_grid, st));
     HIP_OK(hipEventRecord(b->ev[2], st));
     HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
                          b->d_nhits, st));
@@ -309,7 +316,7 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
     HIP_OK(hipStreamSynchronize(h->stream));
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    if (ctr[4]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[4]));
+    if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
     if (b->nq) {
       if (hits) HIP_OK(hipMemcpy(hits, b->d_hits, sizeof(HitDev) * b->nq * b->stride, hipMemcpyDeviceToHost));
       if (n_hits) HIP_OK(hipMemcpy(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost));
@@ -327,11 +334,17 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     HIP_OK(hipStreamSynchronize(h->stream));
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    out->work_items = ctr[0];
-    out->survivors = ctr[3];
-    out->driver_blocks = ctr[5];
-    out->other_blocks = ctr[6];
-    out->algo_bytes = b->algo_static + ctr[3];
+    std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * b->seg_grid);
+    HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t sv = 0, db = 0, ob = 0;
+    for (int i = 0; i < b->seg_grid; ++i) {
+      sv += ws[kStatStride * i]; db += ws[kStatStride * i + 1]; ob += ws[kStatStride * i + 2];
+    }
+    out->work_items = ctr[kCtrItems];
+    out->survivors = sv;
+    out->driver_blocks = db;
+    out->other_blocks = ob;
+    out->algo_bytes = b->algo_static + sv;
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[0], b->ev[1])); out->plan_ms = ms;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); out->segment_ms = ms;

@@ -21,22 +21,28 @@ struct IndexArgs {
   uint32_t n_c4;
   uint32_t n_lists;
   uint32_t doc_lo, doc_hi;  // doc-id range of this image (shard)
+  double avg;               // average doc length stored in my.doc_length
 };
 
-// counters[]: 0 total items, 1 queue head, 2 event capacity used, 3 survivors,
-//             4 error flags, 5 driver blocks decoded, 6 other blocks decoded
-enum { kCtrItems = 0, kCtrHead = 1, kCtrEvCap = 2, kCtrSurvivors = 3, kCtrError = 4,
-       kCtrDriverBlocks = 5, kCtrOtherBlocks = 6, kNumCounters = 8 };
+// counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
+// 4 error flags; the work queue has one head per XCD-sized shard, each on its
+// own 64-byte line (kCtrHead0 + 16*s), so the dequeues of the persistent
+// segment waves do not serialise on a single cache line.
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrHead0 = 16, kQueueShards = 8,
+       kNumCounters = kCtrHead0 + 16 * kQueueShards };
+// per-workgroup statistics written by the segment kernel (no atomics):
+// stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
+constexpr int kStatStride = 4;
 enum { kErrLimit = 1, kErrCapacity = 2 };
 
 constexpr int kSegCost = 48;  // target block decodes per work item; bounds seg_blocks
 
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       hipStream_t st);
+                       int seg_grid, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
-                           uint32_t* counters, Event* events, uint32_t* ev_cnt, int grid,
-                           hipStream_t st);
+                           uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                           int grid, hipStream_t st);
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);

@@ -114,20 +114,26 @@ __device__ __forceinline__ double wave_shr1_f64(double v) {
 // Value j of a 128-value pack whose data bytes start at d (bit width b):
 // bits [j*b, j*b+b) of an LSB-first little-endian stream.  Reads the two
 // aligned dwords that cover the value (the blob is padded at its end).
+// (Addresses are formed from the global blob pointer with __builtin_align_down,
+// not through integer casts, so the loads stay global_load and never become flat.)
 __device__ __forceinline__ uint32_t pack_value(const uint8_t* d, uint32_t b, uint32_t j) {
   const uint32_t bit = j * b;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(d) + (bit >> 3);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
-  const uint32_t sh = static_cast<uint32_t>((a & 3) << 3) + (bit & 7);
+  const uint8_t* a = d + (bit >> 3);
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a) & 3);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(a, 4));
+  const uint32_t sh = (mis << 3) + (bit & 7);
   const uint64_t v = (static_cast<uint64_t>(w[1]) << 32) | w[0];
   const uint32_t mask = b >= 32 ? 0xFFFFFFFFu : ((1u << b) - 1u);
   return static_cast<uint32_t>(v >> sh) & mask;
 }
 
+// (__builtin_align_down keeps the pointer's provenance, so the load stays
+// global and a uniform byte is never fetched by a scalar load whose base is
+// misaligned with the alignment folded into its immediate offset.)
 __device__ __forceinline__ uint32_t load_byte(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t w = *reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
-  return (w >> ((a & 3) << 3)) & 0xFFu;
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(__builtin_align_down(p, 4));
+  return (w >> (mis << 3)) & 0xFFu;
 }
 
 // Wave-cooperative decode of one block (pack of 128 or VInts tail of cnt) into
@@ -247,7 +253,8 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
 __global__ __launch_bounds__(1024) void plan_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                     int nq, QueryPlan* __restrict__ plan,
                                                     uint32_t* __restrict__ counters,
-                                                    uint64_t ev_capacity, uint32_t item_capacity) {
+                                                    uint64_t ev_capacity, uint32_t item_capacity,
+                                                    uint32_t seg_grid) {
   __shared__ uint32_t s_items[1024];
   __shared__ uint64_t s_cap[1024];
   const int t = threadIdx.x, T = blockDim.x;
@@ -305,19 +312,24 @@ __global__ __launch_bounds__(1024) void plan_kernel(IndexArgs ix, const QueryIn*
     const bool fits = s_cap[t] <= ev_capacity && s_items[t] <= item_capacity;
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
     counters[kCtrItems] = fits ? s_items[t] : 0u;  // never write past the workspace
-    counters[kCtrHead] = 0;
     counters[kCtrEvCap] = static_cast<uint32_t>(s_cap[t] > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap[t]);
-    counters[kCtrSurvivors] = 0;
-    counters[kCtrDriverBlocks] = 0;
-    counters[kCtrOtherBlocks] = 0;
   }
+  // Work queue: shard s serves items s, s+8, s+16, ...; workgroup w starts on
+  // item w without a dequeue, so shard s's head starts past those first items.
+  if (t < kQueueShards)
+    counters[kCtrHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
 }
 
 // -------------------------------------------------------------- segment --
+constexpr uint32_t kWin = 64;  // directory window: one entry per lane
+
 struct WaveLds {
   uint32_t mb[8][128];   // doc ids of up to 8 other-list blocks decoded side by side
   uint32_t tf[128];      // cooperative decode of a VInts tf tail
   uint32_t dl[128];      // distinct other-list blocks probed by the driver block
+  BlockDev wblk[kWin];   // directory window of the current other list: entries cur..cur+63
+  uint32_t wlast[kWin];
+  uint32_t wmeta[kWin];
 };
 
 // tf of posting `pos` of a block: packs are raw (not delta coded), so a lane
@@ -326,60 +338,128 @@ __device__ __forceinline__ uint32_t pack_tf(const uint8_t* p, uint32_t bits, uin
   return pack_value(p + 2, bits, pos);
 }
 
+// Directory entry j of list B: from the LDS window when it covers j.
+// (Address-space-typed pointers keep the compiler from merging the two loads
+// into one flat load of a selected pointer.)
+#define WSR_LDS __attribute__((address_space(3)))
+#define WSR_GLB __attribute__((address_space(1)))
+__device__ __forceinline__ void dir_entry(const IndexArgs& ix, const ListDev& B, const WaveLds& S,
+                                          uint32_t c, uint32_t wn, uint32_t j, BlockDev* bd,
+                                          uint32_t* meta) {
+  if (j - c < wn) {
+    const WSR_LDS BlockDev* wb = (const WSR_LDS BlockDev*)(S.wblk);
+    const WSR_LDS uint32_t* wm = (const WSR_LDS uint32_t*)(S.wmeta);
+    const WSR_LDS BlockDev& e = wb[j - c];
+    bd->prev = e.prev; bd->last = e.last; bd->doc_rel = e.doc_rel; bd->tf_rel = e.tf_rel;
+    *meta = wm[j - c];
+  } else {
+    const WSR_GLB BlockDev* gb = (const WSR_GLB BlockDev*)(ix.blocks);
+    const WSR_GLB uint32_t* gm = (const WSR_GLB uint32_t*)(ix.blk_meta);
+    const WSR_GLB BlockDev& e = gb[B.blk0 + j];
+    bd->prev = e.prev; bd->last = e.last; bd->doc_rel = e.doc_rel; bd->tf_rel = e.tf_rel;
+    *meta = gm[B.blk0 + j];
+  }
+}
+
 // G packed blocks side by side: group g (64/G lanes) unpacks block dl[base+g],
 // 2G values per lane, prefix-sums them from the block's previous doc id and
 // writes them to mb[g].  Skewed pairs probe many blocks with few docs each;
 // decoding them together turns G dependent rounds into one.
 template <int G>
-__device__ __forceinline__ void grouped_decode(const IndexArgs& ix, const ListDev& B, const uint32_t* dl,
-                                               uint32_t base, uint32_t n, uint32_t (*mb)[128]) {
+__device__ __forceinline__ void grouped_decode(const IndexArgs& ix, const ListDev& B, WaveLds& S,
+                                               uint32_t c, uint32_t wn, uint32_t base, uint32_t n) {
   constexpr int W = 64 / G, V = 2 * G;
   const uint32_t l = threadIdx.x & 63;
   const uint32_t g = l / W, li = l % W;
   const bool act = base + g < n;
-  const uint32_t jj = act ? dl[base + g] : dl[base];
-  const BlockDev bb = ix.blocks[B.blk0 + jj];
-  const uint32_t bits = ix.blk_meta[B.blk0 + jj] & 0xFF;
+  const uint32_t jj = act ? S.dl[base + g] : S.dl[base];
+  BlockDev bb;
+  uint32_t bm;
+  dir_entry(ix, B, S, c, wn, jj, &bb, &bm);
+  const uint32_t bits = bm & 0xFF;
   const uint8_t* p = ix.blob + B.base + bb.doc_rel;
-  uint32_t* out = mb[g];
+  uint32_t* out = &S.mb[0][0];   // [t][lane]: conflict-free rows of 64 dwords
   uint32_t sum = 0;
 #pragma unroll 2
   for (int t = 0; t < V; ++t) {
     const uint32_t x = pack_value(p + 2, bits, li * V + t);
-    if (act) out[li * V + t] = x;   // raw deltas first: keeps them out of registers
+    out[t * 64 + l] = x;   // raw deltas first: keeps them out of registers
     sum += x;
   }
   const uint32_t inc = group_incl_scan<W>(sum);
   uint32_t run = bb.prev + (inc - sum);
-  if (act) {
 #pragma unroll 4
-    for (int t = 0; t < V; ++t) { run += out[li * V + t]; out[li * V + t] = run; }
-  }
+  for (int t = 0; t < V; ++t) { run += out[t * 64 + l]; out[t * 64 + l] = run; }
 }
 
-__device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double cache) {
-  // Bm25Similarity::TfNormLossy (scoring.h:65-69) times idf (scoring.h:136-140)
+// lower_bound over the 128 doc ids of group g of a grouped decode
+template <int G>
+__device__ __forceinline__ uint32_t grouped_lower_bound(const WaveLds& S, uint32_t g, uint32_t x) {
+  constexpr int W = 64 / G, V = 2 * G;
+  const uint32_t* m = &S.mb[0][0];
+  uint32_t lo = 0, n = 128;
+  while (n > 0) {
+    const uint32_t h = n >> 1, i = lo + h;
+    if (m[(i % V) * 64 + g * W + i / V] < x) { lo = i + 1; n -= h + 1; } else { n = h; }
+  }
+  return lo;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t grouped_at(const WaveLds& S, uint32_t g, uint32_t i) {
+  constexpr int W = 64 / G, V = 2 * G;
+  return (&S.mb[0][0])[(i % V) * 64 + g * W + i / V];
+}
+
+// Bm25Similarity: cache_[c] = k1 * (1 - b + b * Char4ToUint(c) / avg) (scoring.h:85-90),
+// evaluated with the same operations in the same order as the host table.
+__device__ __forceinline__ double length_norm(uint32_t c4, double avg) {
+  const uint32_t mant = c4 & 0x07;
+  const int sh = static_cast<int>(c4 >> 3) - 1;
+  const uint32_t fl = sh < 0 ? mant : ((mant | 0x08u) << sh);
+  const double k1 = 1.2, b = 0.75;
+  return k1 * (1 - b + b * fl / avg);
+}
+
+__device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm) {
+  // TfNormLossy (scoring.h:65-69) times idf (scoring.h:136-140)
   const double f = static_cast<double>(static_cast<int32_t>(tf));
   const double k1p1 = 1.2 + 1;
-  const double tfn = (f * k1p1) / (f + cache);
+  const double tfn = (f * k1p1) / (f + norm);
   return idf * tfn;
 }
 
-__global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+__global__ __launch_bounds__(64, 4) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
                                                      Event* __restrict__ events,
-                                                     uint32_t* __restrict__ ev_cnt) {
+                                                     uint32_t* __restrict__ ev_cnt,
+                                                     uint32_t* __restrict__ stats) {
   __shared__ WaveLds S;
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0, n_oblk = 0;
+  // first item: this workgroup's own index; then dequeue from the shard heads,
+  // starting with the shard of the workgroup and stealing from the others
+  uint32_t shard = blockIdx.x % kQueueShards;
+  uint32_t tried = 0;
+  uint32_t item = blockIdx.x;
   for (;;) {
-    uint32_t item = 0;
-    if (l == 0) item = atomicAdd(&counters[kCtrHead], 1u);
-    item = uni(item);
+    while (item >= total && tried < kQueueShards) {
+      uint32_t* head = &counters[kCtrHead0 + 16 * shard];
+      const uint32_t limit = (total + kQueueShards - 1 - shard) / kQueueShards;
+      uint32_t local = 0;
+      if (l == 0) {
+        local = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (local < limit) local = atomicAdd(head, 1u);
+      }
+      local = uni(local);
+      if (local < limit) { item = shard + kQueueShards * local; break; }
+      shard = (shard + 1) % kQueueShards;
+      ++tried;
+    }
     if (item >= total) break;
     // query of this item: last q with plan[q].item_base <= item (bases are
     // non-decreasing), found with two wave-wide probes instead of a binary search
@@ -430,9 +510,14 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
 
     double pt = 0.0;     // running top-k scores, lane t holds rank t (descending)
     uint32_t pt_n = 0;   // valid entries (uniform)
+    // raw pack words of the next driver block, fetched one block ahead
+    uint32_t nx0 = 0, nx1 = 0;
+    if ((meta & 0xFF) && b0 < b1) {
+      nx0 = pack_value(ix.blob + A.base + blk.doc_rel + 2, meta & 0xFF, 2 * l);
+      nx1 = pack_value(ix.blob + A.base + blk.doc_rel + 2, meta & 0xFF, 2 * l + 1);
+    }
 
     for (uint32_t b = b0; b < b1 && !done; ++b) {
-      // prefetch the next driver block's directory entry
       const uint32_t bn = b + 1 < b1 ? b + 1 : b;
       const BlockDev blk_next = ix.blocks[A.blk0 + bn];
       const uint32_t meta_next = ix.blk_meta[A.blk0 + bn];
@@ -442,34 +527,58 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
       meta = meta_next;
       const uint32_t cnt = (b == A.nblk - 1) ? A.tail_cnt : 128u;
       __syncthreads();
-      decode_block(ix.blob + A.base + blk_cur.doc_rel, meta_cur & 0xFF, cnt, true, blk_cur.prev,
-                   S.mb[0]);
+      uint32_t a0, a1;
+      if (meta_cur & 0xFF) {
+        const uint32_t x0 = nx0, x1 = nx1;
+        const uint32_t sm = x0 + x1;
+        const uint32_t inc = wave_incl_scan(sm);
+        a0 = blk_cur.prev + (inc - sm) + x0;
+        a1 = a0 + x1;
+      } else {
+        decode_block(ix.blob + A.base + blk_cur.doc_rel, 0, cnt, true, blk_cur.prev, S.mb[0]);
+        a0 = S.mb[0][2 * l];
+        a1 = S.mb[0][2 * l + 1];
+      }
+      // prefetch the next driver block's pack words
+      if (b + 1 < b1 && (meta_next & 0xFF)) {
+        nx0 = pack_value(ix.blob + A.base + blk_next.doc_rel + 2, meta_next & 0xFF, 2 * l);
+        nx1 = pack_value(ix.blob + A.base + blk_next.doc_rel + 2, meta_next & 0xFF, 2 * l + 1);
+      }
       ++n_dblk;
-      const uint32_t a0 = S.mb[0][2 * l], a1 = S.mb[0][2 * l + 1];
       bool al0 = 2 * l < cnt && a0 >= ix.doc_lo && a0 < ix.doc_hi;
       bool al1 = 2 * l + 1 < cnt && a1 >= ix.doc_lo && a1 < ix.doc_hi;
+      // issued now, consumed at scoring time: doc lengths and the driver's tf
       const uint32_t c0 = al0 && a0 < ix.n_c4 ? ix.c4[a0] : 0u;
       const uint32_t c1 = al1 && a1 < ix.n_c4 ? ix.c4[a1] : 0u;
+      uint32_t ta0 = 0, ta1 = 0;
+      {
+        const uint32_t tbits = meta_cur >> 8;
+        const uint8_t* tp = ix.blob + A.base + blk_cur.tf_rel;
+        if (tbits) {
+          ta0 = pack_tf(tp, tbits, 2 * l);
+          ta1 = pack_tf(tp, tbits, 2 * l + 1);
+        } else {
+          __syncthreads();
+          decode_block(tp, 0, cnt, false, 0, S.tf);
+          ta0 = S.tf[2 * l];
+          ta1 = S.tf[2 * l + 1];
+        }
+      }
       double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
+      bool scored_norm = false;
+      double nrm0 = 0.0, nrm1 = 0.0;
 
       for (uint32_t s = 0; s < nt; ++s) {
         if (__ballot(al0 || al1) == 0) break;
         const ListDev L = ix.lists[qlist[s]];
+        if (!scored_norm) {
+          nrm0 = length_norm(c0, ix.avg);
+          nrm1 = length_norm(c1, ix.avg);
+          scored_norm = true;
+        }
         if (s == d) {  // the driver's own tf
-          uint32_t ta0 = 0, ta1 = 0;
-          const uint32_t tbits = meta_cur >> 8;
-          const uint8_t* tp = ix.blob + A.base + blk_cur.tf_rel;
-          if (tbits) {
-            if (al0) ta0 = pack_tf(tp, tbits, 2 * l);
-            if (al1) ta1 = pack_tf(tp, tbits, 2 * l + 1);
-          } else {
-            __syncthreads();
-            decode_block(tp, 0, cnt, false, 0, S.tf);
-            ta0 = S.tf[2 * l];
-            ta1 = S.tf[2 * l + 1];
-          }
-          if (al0) s0 += bm25_term(L.idf, ta0, ix.cache[c0]);
-          if (al1) s1 += bm25_term(L.idf, ta1, ix.cache[c1]);
+          if (al0) s0 += bm25_term(L.idf, ta0, nrm0);
+          if (al1) s1 += bm25_term(L.idf, ta1, nrm1);
           continue;
         }
         const ListDev& B = L;
@@ -477,8 +586,21 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kMaxTerms; ++u) if (u == s) c = cur[u];
-        const uint32_t j0 = al0 ? find_block(last, c, B.nblk, a0) : kNoBlock;
-        const uint32_t j1 = al1 ? find_block(last, c, B.nblk, a1) : kNoBlock;
+        // directory window cur..cur+63 into LDS (one coalesced round)
+        const uint32_t wn = min(kWin, B.nblk - c);
+        uint32_t wl = 0;
+        __syncthreads();
+        if (l < wn) {
+          wl = last[c + l];
+          S.wlast[l] = wl;
+          S.wblk[l] = ix.blocks[B.blk0 + c + l];
+          S.wmeta[l] = ix.blk_meta[B.blk0 + c + l];
+        }
+        const uint32_t wmax = uni(__builtin_amdgcn_readlane(wl, static_cast<int>(wn) - 1));
+        __syncthreads();
+        uint32_t j0 = kNoBlock, j1 = kNoBlock;
+        if (al0) j0 = a0 <= wmax ? c + lds_lower_bound(S.wlast, wn, a0) : find_block(last, c + wn, B.nblk, a0);
+        if (al1) j1 = a1 <= wmax ? c + lds_lower_bound(S.wlast, wn, a1) : find_block(last, c + wn, B.nblk, a1);
         // a doc beyond the list's last block cannot match, nor can any later doc
         if (__ballot((al0 && j0 >= B.nblk) || (al1 && j1 >= B.nblk))) done = true;
         al0 = al0 && j0 < B.nblk;
@@ -493,40 +615,45 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
         const uint32_t before = __popcll(m0 & lt) + __popcll(m1 & lt);
         const uint32_t r0 = before + (st0 ? 1u : 0u) - 1u;              // rank of value (l,0)'s block
         const uint32_t r1 = before + (st0 ? 1u : 0u) + (st1 ? 1u : 0u) - 1u;
-        __syncthreads();
         if (st0) S.dl[before] = j0;
         if (st1) S.dl[before + (st0 ? 1u : 0u)] = j1;
         __syncthreads();
         // the list's VInts tail (if probed) is the last distinct block
-        const bool tail_vints = nd && B.tail_cnt < 128u &&
-                                S.dl[nd - 1] == B.nblk - 1;
+        const uint32_t jlast = nd ? uni(S.dl[nd - 1]) : 0u;
+        const bool tail_vints = nd && B.tail_cnt < 128u && jlast == B.nblk - 1;
         const uint32_t npk = tail_vints ? nd - 1 : nd;
         uint32_t t0 = 0, t1 = 0;
         bool h0 = false, h1 = false;
         uint32_t p0 = 0, p1 = 0;
         for (uint32_t base = 0; base < npk;) {
           const uint32_t rem = npk - base;
-          uint32_t G;
-          if (rem >= 8) { G = 8; grouped_decode<8>(ix, B, S.dl, base, npk, S.mb); }
-          else if (rem >= 4) { G = 4; grouped_decode<4>(ix, B, S.dl, base, npk, S.mb); }
-          else if (rem >= 2) { G = 2; grouped_decode<2>(ix, B, S.dl, base, npk, S.mb); }
-          else { G = 1; grouped_decode<1>(ix, B, S.dl, base, npk, S.mb); }
-          n_oblk += min(G, rem);
-          __syncthreads();
-          if (al0 && r0 >= base && r0 < base + G) {
-            p0 = lds_lower_bound(S.mb[r0 - base], 128, a0);
-            h0 = p0 < 128 && S.mb[r0 - base][p0] == a0;
-          }
-          if (al1 && r1 >= base && r1 < base + G) {
-            p1 = lds_lower_bound(S.mb[r1 - base], 128, a1);
-            h1 = p1 < 128 && S.mb[r1 - base][p1] == a1;
-          }
-          __syncthreads();
-          base += G;
+#define WSR_PROBE(GG)                                                             \
+  {                                                                               \
+    grouped_decode<GG>(ix, B, S, c, wn, base, npk);                               \
+    n_oblk += min(static_cast<uint32_t>(GG), rem);                                \
+    __syncthreads();                                                              \
+    if (al0 && r0 >= base && r0 < base + GG) {                                    \
+      p0 = grouped_lower_bound<GG>(S, r0 - base, a0);                             \
+      h0 = p0 < 128 && grouped_at<GG>(S, r0 - base, p0) == a0;                    \
+    }                                                                             \
+    if (al1 && r1 >= base && r1 < base + GG) {                                    \
+      p1 = grouped_lower_bound<GG>(S, r1 - base, a1);                             \
+      h1 = p1 < 128 && grouped_at<GG>(S, r1 - base, p1) == a1;                    \
+    }                                                                             \
+    __syncthreads();                                                              \
+    base += GG;                                                                   \
+  }
+          if (rem >= 8) WSR_PROBE(8)
+          else if (rem >= 4) WSR_PROBE(4)
+          else if (rem >= 2) WSR_PROBE(2)
+          else WSR_PROBE(1)
+#undef WSR_PROBE
         }
         if (tail_vints) {
           const uint32_t jt = B.nblk - 1;
-          const BlockDev bb = ix.blocks[B.blk0 + jt];
+          BlockDev bb;
+          uint32_t bm;
+          dir_entry(ix, B, S, c, wn, jt, &bb, &bm);
           decode_block(ix.blob + B.base + bb.doc_rel, 0, B.tail_cnt, true, bb.prev, S.mb[0]);
           ++n_oblk;
           if (al0 && r0 == nd - 1) {
@@ -540,8 +667,7 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
           const bool tv0 = h0 && r0 == nd - 1, tv1 = h1 && r1 == nd - 1;
           if (__ballot(tv0 || tv1)) {
             __syncthreads();
-            decode_block(ix.blob + B.base + bb.tf_rel, (ix.blk_meta[B.blk0 + jt] >> 8), B.tail_cnt,
-                         false, 0, S.tf);
+            decode_block(ix.blob + B.base + bb.tf_rel, bm >> 8, B.tail_cnt, false, 0, S.tf);
             if (tv0) t0 = S.tf[p0];
             if (tv1) t1 = S.tf[p1];
           }
@@ -549,22 +675,25 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
         }
         // tf of matched postings held in packs: direct per-lane read
         if (h0 && !(tail_vints && r0 == nd - 1)) {
-          const uint32_t tb = ix.blk_meta[B.blk0 + j0] >> 8;
-          t0 = pack_tf(ix.blob + B.base + ix.blocks[B.blk0 + j0].tf_rel, tb, p0);
+          BlockDev bb;
+          uint32_t bm;
+          dir_entry(ix, B, S, c, wn, j0, &bb, &bm);
+          t0 = pack_tf(ix.blob + B.base + bb.tf_rel, bm >> 8, p0);
         }
         if (h1 && !(tail_vints && r1 == nd - 1)) {
-          const uint32_t tb = ix.blk_meta[B.blk0 + j1] >> 8;
-          t1 = pack_tf(ix.blob + B.base + ix.blocks[B.blk0 + j1].tf_rel, tb, p1);
+          BlockDev bb;
+          uint32_t bm;
+          dir_entry(ix, B, S, c, wn, j1, &bb, &bm);
+          t1 = pack_tf(ix.blob + B.base + bb.tf_rel, bm >> 8, p1);
         }
         al0 = h0;
         al1 = h1;
-        if (al0) s0 += bm25_term(B.idf, t0, ix.cache[c0]);
-        if (al1) s1 += bm25_term(B.idf, t1, ix.cache[c1]);
+        if (al0) s0 += bm25_term(B.idf, t0, nrm0);
+        if (al1) s1 += bm25_term(B.idf, t1, nrm1);
         // advance the cursor to the furthest block queried (docs only increase)
-        const uint32_t jm = nd ? uni(S.dl[nd - 1]) : 0u;
 #pragma unroll
         for (uint32_t u = 0; u < kMaxTerms; ++u)
-          if (u == s && jm > cur[u]) cur[u] = jm;
+          if (u == s && nd && jlast > cur[u]) cur[u] = jlast;
       }
       if (__ballot(al0 || al1) == 0) continue;
       n_surv += __popcll(__ballot(al0)) + __popcll(__ballot(al1));
@@ -597,11 +726,12 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
       }
     }
     if (l == 0) ev_cnt[item] = ev_n;
+    item = 0xFFFFFFFFu;
   }
   if (l == 0) {
-    atomicAdd(&counters[kCtrSurvivors], n_surv);
-    atomicAdd(&counters[kCtrDriverBlocks], n_dblk);
-    atomicAdd(&counters[kCtrOtherBlocks], n_oblk);
+    stats[blockIdx.x * kStatStride + 0] = n_surv;
+    stats[blockIdx.x * kStatStride + 1] = n_dblk;
+    stats[blockIdx.x * kStatStride + 2] = n_oblk;
   }
 }
 
@@ -723,17 +853,17 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       hipStream_t st) {
+                       int seg_grid, hipStream_t st) {
   hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(1024), 0, st, ix, q, nq, plan, counters,
-                     ev_capacity, item_capacity);
+                     ev_capacity, item_capacity, static_cast<uint32_t>(seg_grid));
   return hipGetLastError();
 }
 
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
-                           uint32_t* counters, Event* events, uint32_t* ev_cnt, int grid,
-                           hipStream_t st) {
+                           uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                           int grid, hipStream_t st) {
   hipLaunchKernelGGL(segment_kernel, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
-                     events, ev_cnt);
+                     events, ev_cnt, stats);
   return hipGetLastError();
 }
 
