@@ -1,0 +1,52 @@
+"""The C-ABI library loads, exports every symbol include/wiser_hip.h declares,
+and fails loudly (no CPU fallback) when there is no HIP device.  CPU only."""
+import ctypes as C
+import os
+
+import pytest
+
+
+def test_exports_every_declared_symbol(built):
+    from wiser_amd import _capi
+    names = _capi.header_symbols()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(_capi.lib, n)]
+    assert not missing, missing
+
+
+def test_version_and_error_string(built):
+    from wiser_amd import _capi
+    assert b"gfx950" in _capi.lib.wsr_version()
+    h = C.c_void_p()
+    rc = _capi.lib.wsr_open(b"/nonexistent/index", None, C.byref(h))
+    assert rc == -2 and not h.value
+    assert b"my.doc_length" in _capi.lib.wsr_last_error()
+
+
+def test_no_cpu_fallback(built, indexes):
+    """On a machine without a HIP device the engine refuses to load."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import wiser_amd as w
+    from wiser_amd._capi import WiserError
+    d = indexes["three"][0]
+    e = w.VacuumEngine(d)
+    with pytest.raises(WiserError) as ei:
+        e.Load()
+    assert ei.value.code == -3 and "no CPU fallback" in str(ei.value)
+
+
+def test_null_arguments_are_errors(built):
+    from wiser_amd import _capi
+    assert _capi.lib.wsr_open(None, None, None) == -1
+    assert _capi.lib.wsr_term_count(None, None) == -1
+    assert _capi.lib.wsr_search_batch(None, None, 1, 1, None, None) == -1
+    _capi.lib.wsr_close(None)  # no-op
+
+
+def test_struct_layouts(built):
+    from wiser_amd import _capi
+    assert C.sizeof(_capi.Query) == 40
+    assert C.sizeof(_capi.Hit) == 16
+    assert C.sizeof(_capi.OpenOpts) == 16
