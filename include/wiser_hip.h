@@ -117,6 +117,31 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
 /* device pointers of the batch's results (for collectives on the caller's side) */
 int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits);
 
+/* ---- doc-range shards (multi-GPU) ------------------------------------
+ * A shard engine (wsr_open_opts.doc_lo/doc_hi) runs every query of a batch over
+ * its doc range.  Queries are owned by contiguous slices of q_per_owner queries
+ * (owner o = query / q_per_owner).  Exchange (caller's collectives, e.g. RCCL
+ * all_to_all): counts and events per owner; the owner then replays the events
+ * of all shards in shard (= doc-id range) order.  Results are bit-identical to
+ * an unsharded run ("Why replaying events is exact").          */
+/* After wsr_batch_run: reduce each query's events to the insertions of a heap
+ * run from empty over the shard; d_counts (device, nq int32) receives the per
+ * query event counts, owner_totals (host, n_owners) the events per owner. */
+int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
+                     int32_t* d_counts, int64_t* owner_totals);
+/* Pack the reduced events owner-major into d_send (device, 16-byte events). */
+int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send);
+/* Owner side: d_rcounts (device, n_shards x nq_owned int32, shard-major),
+ * d_recv (device events: shard 0's block for my queries, then shard 1's, ...;
+ * shard g's block starts at event rbase[g], host array) -> results of the
+ * batch's queries [q0, q0 + nq_owned). */
+int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                     const int32_t* d_rcounts, const void* d_recv, const uint64_t* rbase);
+int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
+                          int32_t* n_hits);
+/* the engine's HIP stream (a hipStream_t) for ordering the caller's work */
+int wsr_stream(wsr_handle* h, void** stream);
+
 /* Decode one block of a list on the device (test hook for the decoder):
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */
 int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,

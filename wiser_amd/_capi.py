@@ -80,6 +80,13 @@ _sigs = {
     "wsr_batch_fetch": (C.c_int, [_P, _P, C.POINTER(Hit), C.POINTER(C.c_int32)]),
     "wsr_batch_stats_get": (C.c_int, [_P, _P, C.POINTER(BatchStats)]),
     "wsr_batch_device_results": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_P)]),
+    "wsr_shard_reduce": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_int64)]),
+    "wsr_shard_pack": (C.c_int, [_P, _P, _P]),
+    "wsr_owner_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, _P, _P,
+                                   C.POINTER(C.c_uint64)]),
+    "wsr_batch_fetch_range": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.POINTER(Hit),
+                                        C.POINTER(C.c_int32)]),
+    "wsr_stream": (C.c_int, [_P, C.POINTER(_P)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]),
     "wsr_build_from_linedoc": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_char_p,

@@ -80,6 +80,13 @@ struct wsr_batch {
   int32_t* d_nhits = nullptr;
   uint32_t* d_stats = nullptr;   // per segment workgroup: survivors, blocks
   int seg_grid = 0;
+  // doc-range shard exchange
+  uint64_t* d_soff = nullptr;     // per query send offset (events)
+  int64_t* d_otot = nullptr;      // per owner totals
+  int32_t* d_scount = nullptr;    // per query reduced event count (last wsr_shard_reduce)
+  uint64_t* d_roff = nullptr;     // owner side per (shard, query) offsets
+  uint64_t* d_rbase = nullptr;
+  size_t roff_cap = 0;
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ran = false;
@@ -215,7 +222,9 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
-                  static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats)})
+                  static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
+                  static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
+                  static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
   delete b;
@@ -374,6 +383,99 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stri
   if (!rc) rc = wsr_batch_fetch(h, b, hits, n_hits);
   wsr_batch_destroy(h, b);
   return rc;
+}
+
+int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
+                     int32_t* d_counts, int64_t* owner_totals) {
+  if (!h || !b || !b->ran || !d_counts || !owner_totals || q_per_owner <= 0 || n_owners <= 0 ||
+      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
+    return fail(WSR_E_INVALID, "bad shard_reduce arguments");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
+    if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
+    if (n_owners > 1024) return fail(WSR_E_LIMIT, "more than 1024 owners");
+    HIP_OK(hipMemsetAsync(b->d_otot, 0, sizeof(int64_t) * n_owners, st));
+    HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
+    HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
+    HIP_OK(hipMemcpyAsync(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    b->d_scount = d_counts;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send) {
+  if (!h || !b || !b->d_scount || !d_send) return fail(WSR_E_INVALID, "call wsr_shard_reduce first");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(launch_pack_events(b->d_plan, b->nq, b->d_events, b->d_scount, b->d_soff,
+                              static_cast<Event*>(d_send), h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                     const int32_t* d_rcounts, const void* d_recv, const uint64_t* rbase) {
+  if (!h || !b || n_shards <= 0 || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq ||
+      (nq_owned && (!d_rcounts || !rbase)))
+    return fail(WSR_E_INVALID, "bad owner_replay arguments");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    const size_t n = static_cast<size_t>(n_shards) * nq_owned;
+    if (n > b->roff_cap) {
+      if (b->d_roff) HIP_OK(hipFree(b->d_roff));
+      b->roff_cap = n + 1024;
+      HIP_OK(hipMalloc(&b->d_roff, sizeof(uint64_t) * b->roff_cap));
+    }
+    if (!b->d_rbase) HIP_OK(hipMalloc(&b->d_rbase, sizeof(uint64_t) * 1024));
+    if (n_shards > 1024) return fail(WSR_E_LIMIT, "more than 1024 shards");
+    HIP_OK(hipMemcpyAsync(b->d_rbase, rbase, sizeof(uint64_t) * n_shards, hipMemcpyHostToDevice, st));
+    // per shard: exclusive scan of its counts over my queries
+    for (int32_t s2 = 0; s2 < n_shards; ++s2)
+      HIP_OK(launch_scan_counts(d_rcounts + static_cast<size_t>(s2) * nq_owned, nq_owned, 0,
+                                b->d_roff + static_cast<size_t>(s2) * nq_owned, nullptr, st));
+    HIP_OK(launch_owner_replay(b->d_q, q0, nq_owned, n_shards, d_rcounts, b->d_roff, b->d_rbase,
+                               static_cast<const Event*>(d_recv), b->d_hits, b->stride, b->d_nhits, st));
+    HIP_OK(hipStreamSynchronize(st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
+                          int32_t* n_hits) {
+  if (!h || !b || q0 < 0 || nq < 0 || q0 + nq > b->nq) return fail(WSR_E_INVALID, "bad range");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    if (nq && hits)
+      HIP_OK(hipMemcpy(hits, b->d_hits + static_cast<size_t>(q0) * b->stride,
+                       sizeof(HitDev) * static_cast<size_t>(nq) * b->stride, hipMemcpyDeviceToHost));
+    if (nq && n_hits)
+      HIP_OK(hipMemcpy(n_hits, b->d_nhits + q0, sizeof(int32_t) * nq, hipMemcpyDeviceToHost));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_stream(wsr_handle* h, void** stream) {
+  if (!h || !stream) return fail(WSR_E_INVALID, "null argument");
+  *stream = h->stream;
+  return WSR_OK;
 }
 
 int wsr_debug_decode_block(wsr_handle* h, int32_t id, int32_t block, int32_t which, uint32_t* out,

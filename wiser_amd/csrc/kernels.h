@@ -48,6 +48,17 @@ hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const 
                          hipStream_t st);
 hipError_t launch_decode_probe(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
                                uint32_t seed, uint32_t* out, hipStream_t st);
+// doc-range shards (multi-GPU)
+hipError_t launch_shard_reduce(const QueryIn* q, const QueryPlan* plan, int nq, Event* events,
+                               const uint32_t* ev_cnt, int32_t* scount, hipStream_t st);
+hipError_t launch_scan_counts(const int32_t* cnt, int n, int seg, uint64_t* off, int64_t* seg_total,
+                              hipStream_t st);
+hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events,
+                              const int32_t* scount, const uint64_t* off, Event* send,
+                              hipStream_t st);
+hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
+                               const uint64_t* roff, const uint64_t* rbase, const Event* recv,
+                               HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st);
 // resident 64-thread segment workgroups per CU
 int segment_kernel_occupancy();
 

@@ -779,32 +779,17 @@ struct HeapView {
   }
 };
 
-// One wave per query.  The query's events (its segments in doc-id order) are
-// filtered 64 at a time with the same running top-k test the segment kernel
-// uses -- fewer than k earlier events with a score >= s -- which selects exactly
-// the survivors the reference heap inserts (the top-k multiset of any prefix
-// is carried by its events).  Lane 0 applies each of them to the restated heap
-// as RankDoc does, then SortHeap writes the result.
-__global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
-                                                    const QueryPlan* __restrict__ plan, int nq,
-                                                    const Event* __restrict__ events,
-                                                    const uint32_t* __restrict__ ev_cnt,
-                                                    HitDev* __restrict__ hits, int hit_stride,
-                                                    int32_t* __restrict__ n_hits) {
-  __shared__ double s_sc[kMaxK];
-  __shared__ int32_t s_dc[kMaxK];
-  const uint32_t l = threadIdx.x & 63;
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const QueryPlan P = plan[qi];
-  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
-  HeapView H{s_sc, s_dc, 1};
-  uint32_t n = 0;       // heap size (uniform)
-  double pt = 0.0;      // running top-k of events, lane t = rank t
+// Running filter over a query's event stream, in doc-id order: an event is
+// one the reference heap inserts iff fewer than k earlier events have a score
+// >= its score (the top-k multiset of any prefix is carried by its events).
+// `emit(score, doc)` is called, wave-uniformly, for exactly those events.
+struct EventFilter {
+  double pt = 0.0;    // running top-k of events, lane t = rank t
   uint32_t pt_n = 0;
-  for (uint32_t r = 0; r < P.n_items; ++r) {
-    const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
-    const uint32_t ne = uni(ev_cnt[P.item_base + r]);
+  uint32_t k = 0;
+  template <class Emit>
+  __device__ __forceinline__ void consume(const Event* ev, uint32_t ne, Emit&& emit) {
+    const uint32_t l = threadIdx.x & 63;
     for (uint32_t c = 0; c < ne; c += 64) {
       const uint32_t i = c + l;
       const bool valid = i < ne;
@@ -820,12 +805,7 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
         const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
         const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
         if (pos < k) {
-          if (l == 0) {  // RankDoc (query_processing.h:595-602)
-            uint32_t m = n;
-            if (m < k) H.push(m, sv, dv);
-            else if (sv > H.s(0)) { H.pop(m); H.push(m, sv, dv); }
-          }
-          n = n < k ? n + 1 : n;
+          emit(sv, dv);
           const double up = wave_shr1_f64(pt);
           if (l > pos) pt = up;
           else if (l == pos) pt = sv;
@@ -834,20 +814,157 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
       }
     }
   }
-  if (l == 0) {
-    // SortHeap (query_processing.h:551-562): pop to ascending, then reverse
-    const uint32_t m = n;
-    HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
-    for (uint32_t i = 0; i < m; ++i) {
-      HitDev h;
-      h.doc = H.d(0);
-      h.pad = 0;
-      h.score = H.s(0);
-      out[m - 1 - i] = h;
-      H.pop(n);
+};
+
+// RankDoc (query_processing.h:595-602) on the restated heap, then SortHeap
+// (query_processing.h:551-562).  Lane 0 owns the heap.
+struct HeapSink {
+  HeapView H;
+  uint32_t n = 0, k = 0;
+  __device__ __forceinline__ void insert(double sv, int32_t dv) {
+    if ((threadIdx.x & 63) == 0) {
+      uint32_t m = n;
+      if (m < k) H.push(m, sv, dv);
+      else if (sv > H.s(0)) { H.pop(m); H.push(m, sv, dv); }
     }
-    n_hits[qi] = static_cast<int32_t>(m);
+    n = n < k ? n + 1 : n;
   }
+  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t m = n;
+      for (uint32_t i = 0; i < m; ++i) {
+        HitDev h;
+        h.doc = H.d(0);
+        h.pad = 0;
+        h.score = H.s(0);
+        out[m - 1 - i] = h;
+        H.pop(n);
+      }
+      *n_out = static_cast<int32_t>(m);
+    }
+  }
+};
+
+// One wave per query: filter the events of its segments (doc-id order) and
+// apply the survivors of the filter to the heap.
+__global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
+                                                    const QueryPlan* __restrict__ plan, int nq,
+                                                    const Event* __restrict__ events,
+                                                    const uint32_t* __restrict__ ev_cnt,
+                                                    HitDev* __restrict__ hits, int hit_stride,
+                                                    int32_t* __restrict__ n_hits) {
+  __shared__ double s_sc[kMaxK];
+  __shared__ int32_t s_dc[kMaxK];
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const QueryPlan P = plan[qi];
+  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  EventFilter F;
+  F.k = k;
+  HeapSink sink{HeapView{s_sc, s_dc, 1}, 0, k};
+  for (uint32_t r = 0; r < P.n_items; ++r) {
+    const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
+    F.consume(ev, uni(ev_cnt[P.item_base + r]), [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+  }
+  sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
+}
+
+// ------------------------------------------------------ doc-range shards --
+// Shard side: reduce each query's segment events to the events of a heap run
+// from empty over the whole shard (a superset of the global insertions inside
+// the shard), compacted in place at the query's event base; count -> scount[q].
+__global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restrict__ qs,
+                                                          const QueryPlan* __restrict__ plan, int nq,
+                                                          Event* __restrict__ events,
+                                                          const uint32_t* __restrict__ ev_cnt,
+                                                          int32_t* __restrict__ scount) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const QueryPlan P = plan[qi];
+  EventFilter F;
+  F.k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  Event* out = events + P.ev_base;
+  uint32_t n = 0;
+  for (uint32_t r = 0; r < P.n_items; ++r) {
+    const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
+    // writes land at index n <= index being read: a chunk is read before any write
+    F.consume(ev, uni(ev_cnt[P.item_base + r]), [&](double sv, int32_t dv) {
+      if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
+      ++n;
+    });
+  }
+  if ((threadIdx.x & 63) == 0) scount[qi] = static_cast<int32_t>(n);
+}
+
+// Exclusive scan of cnt[0..n) -> off[0..n) (64-bit), single workgroup; the
+// total per segment of `seg` consecutive entries -> seg_total[n / seg].
+__global__ __launch_bounds__(1024) void scan_counts_kernel(const int32_t* __restrict__ cnt, int n,
+                                                           int seg, uint64_t* __restrict__ off,
+                                                           int64_t* __restrict__ seg_total) {
+  __shared__ uint64_t s[1024];
+  const int t = threadIdx.x, T = blockDim.x;
+  const int per = (n + T - 1) / T;
+  const int i0 = t * per, i1 = min(n, i0 + per);
+  uint64_t sum = 0;
+  for (int i = i0; i < i1; ++i) sum += static_cast<uint64_t>(cnt[i]);
+  s[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < T; d <<= 1) {
+    uint64_t a = t >= d ? s[t - d] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  uint64_t run = s[t] - sum;
+  for (int i = i0; i < i1; ++i) { off[i] = run; run += static_cast<uint64_t>(cnt[i]); }
+  __syncthreads();
+  if (seg_total && seg > 0)
+    for (int g = t; g * seg < n; g += T) {
+      const int e = min(n, (g + 1) * seg) - 1;
+      seg_total[g] = static_cast<int64_t>(off[e] + static_cast<uint64_t>(cnt[e]) - off[g * seg]);
+    }
+}
+
+// Copy each query's compacted shard events to send[off[q]] (owner-major order).
+__global__ __launch_bounds__(64) void pack_events_kernel(const QueryPlan* __restrict__ plan, int nq,
+                                                         const Event* __restrict__ events,
+                                                         const int32_t* __restrict__ scount,
+                                                         const uint64_t* __restrict__ off,
+                                                         Event* __restrict__ send) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const Event* src = events + plan[qi].ev_base;
+  Event* dst = send + off[qi];
+  const int n = scount[qi];
+  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+
+// Owner side: for each owned query, the events every shard sent, in shard
+// (= doc-id range) order, through the filter and the heap.
+// rcount[g * nq + q], roff[g * nq + q] (offset inside shard g's block), rbase[g].
+__global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
+                                                          int n_shards,
+                                                          const int32_t* __restrict__ rcount,
+                                                          const uint64_t* __restrict__ roff,
+                                                          const uint64_t* __restrict__ rbase,
+                                                          const Event* __restrict__ recv,
+                                                          HitDev* __restrict__ hits, int hit_stride,
+                                                          int32_t* __restrict__ n_hits) {
+  __shared__ double s_sc[kMaxK];
+  __shared__ int32_t s_dc[kMaxK];
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int gq = q0 + qi;
+  const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
+  EventFilter F;
+  F.k = k;
+  HeapSink sink{HeapView{s_sc, s_dc, 1}, 0, k};
+  for (int g = 0; g < n_shards; ++g) {
+    const Event* ev = recv + rbase[g] + roff[static_cast<int64_t>(g) * nq + qi];
+    F.consume(ev, uni(static_cast<uint32_t>(rcount[static_cast<int64_t>(g) * nq + qi])),
+              [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+  }
+  sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
 // ------------------------------------------------------------ launchers --
@@ -880,6 +997,39 @@ int segment_kernel_occupancy() {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, segment_kernel, 64, 0) != hipSuccess) return 1;
   return n;
+}
+
+hipError_t launch_shard_reduce(const QueryIn* q, const QueryPlan* plan, int nq, Event* events,
+                               const uint32_t* ev_cnt, int32_t* scount, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(shard_reduce_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events, ev_cnt,
+                     scount);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_counts(const int32_t* cnt, int n, int seg, uint64_t* off, int64_t* seg_total,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, st, cnt, n, seg, off, seg_total);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events,
+                              const int32_t* scount, const uint64_t* off, Event* send,
+                              hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_events_kernel, dim3(nq), dim3(64), 0, st, plan, nq, events, scount, off,
+                     send);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
+                               const uint64_t* roff, const uint64_t* rbase, const Event* recv,
+                               HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount,
+                     roff, rbase, recv, hits, hit_stride, n_hits);
+  return hipGetLastError();
 }
 
 // Test hook: decode one block of the image on the device (wave-cooperative).
