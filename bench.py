@@ -4,11 +4,17 @@
 Workload (BASELINE.json configs[1], SURVEY.md 8d "C2"): 1M synthetic Zipf docs
 (V=500k, s=1.07, lognormal lengths, seed 0x5EED2026) written in the reference's
 Vacuum layout by the build's writer; 100k two-term queries drawn by the
-gen_synthetic_log.py:191-214 rule (seed 7); batches of 4096 queries; k = 10.
-The English-Wikipedia index of configs[2..4] is not available offline.
+gen_synthetic_log.py:191-214 rule (seed 7); batches of 4096 queries per GPU;
+k = 10.  The English-Wikipedia index of configs[2..4] is not available offline.
 
-A step = one batch (4096 queries per GPU) through plan + segment + replay
-kernels, with the batch's resolved queries already resident in HBM.
+A step = one batch through the engine with the batch's resolved queries
+already resident in HBM:
+  N = 1          plan + segment + replay kernels over the whole index;
+  N > 1 (shard)  every rank holds the doc-id range [N*r/W, N*(r+1)/W); a global
+                 batch of 4096*W queries runs on every shard, shard events are
+                 exchanged with RCCL all_to_all over xGMI and each rank replays
+                 the 4096 queries it owns (per-GPU work ~constant: weak scaling);
+  N > 1 (replica, --mode replica) full index per GPU, 4096 queries per rank.
 value = queries completed by all ranks / max-over-ranks wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -41,8 +47,12 @@ def parse():
     p.add_argument("--docs", type=int, default=1_000_000)
     p.add_argument("--vocab", type=int, default=500_000)
     p.add_argument("--queries", type=int, default=100_000)
-    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--batch", type=int, default=4096, help="queries per GPU per step")
     p.add_argument("--k", type=int, default=10)
+    p.add_argument("--mode", choices=["shard", "replica"], default="shard",
+                   help="N>1: doc-range shards with RCCL merge, or full-index replicas")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="shard exchange backend (nccl = RCCL over xGMI; gloo for 1-GPU rehearsals)")
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="bounded CPU-baseline sample (oracle, 1 thread), rank 0 at N=1")
@@ -51,19 +61,8 @@ def parse():
     return p.parse_args()
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo for the control plane (barrier, max)
-        dist.init_process_group("gloo")
-
+def ensure_index(a, rank, dist):
     import wiser_amd as w
-    from wiser_amd import _capi
-
     idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
     qlog = os.path.join(idx, f"two_term_{a.queries}.log")
     if rank == 0 and not os.path.exists(os.path.join(idx, "READY")):
@@ -76,109 +75,188 @@ def main():
             f"{st.vacuum_bytes/1e9:.2f} GB in {time.time()-t:.1f}s")
     if dist:
         dist.barrier()
+    return idx, qlog
 
-    t = time.time()
-    eng = w.VacuumEngine(idx, device=local, threads=min(16, os.cpu_count()))
-    eng.Load()
-    log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
 
-    lines = [l.split() for l in open(qlog).read().splitlines()]
-    # each rank serves its own replica slice of the log (independent queries)
-    per_rank = (len(lines) + world - 1) // world
-    mine = lines[rank * per_rank:(rank + 1) * per_rank] or lines[:a.batch]
-    batches = []
-    for s in range(0, len(mine), a.batch):
-        chunk = mine[s:s + a.batch]
-        arr = (_capi.Query * len(chunk))()
-        for i, terms in enumerate(chunk):
-            q, _ = eng.resolve(w.SearchQuery(terms, n_results=a.k))
-            arr[i] = q
-        b = w.ResidentBatch(eng, a.batch, a.k)
-        b.upload(arr)
-        batches.append((b, chunk))
-    nb = len(batches)
+def resolve(eng, chunk, k):
+    import wiser_amd as w
+    from wiser_amd import _capi
+    arr = (_capi.Query * len(chunk))()
+    for i, terms in enumerate(chunk):
+        arr[i] = eng.resolve(w.SearchQuery(terms, n_results=k))[0]
+    return arr
 
-    # correctness spot-check against the oracle (checker only)
-    checked = 0
-    if a.check and rank == 0:
-        from oracle.oracle import OracleVacuum
-        orc = OracleVacuum(idx)
-        b, chunk = batches[0]
-        b.run()
-        hits, nh = b.fetch()
-        for i, terms in enumerate(chunk[:a.check]):
-            want, _ = orc.search(terms, a.k)
-            got = [(hits[i * a.k + j].doc_id, hits[i * a.k + j].score) for j in range(nh[i])]
-            if got != want:
-                raise SystemExit(f"parity failure on {terms}: {got[:3]} vs {want[:3]}")
-            checked += 1
-        orc.close()
 
-    for s in range(a.warmup):
-        batches[s % nb][0].run()
-    w.sync(eng)
+def check_against_oracle(idx, chunk, hits, nh, k, n):
+    from oracle.oracle import OracleVacuum
+    orc = OracleVacuum(idx)
+    for i, terms in enumerate(chunk[:n]):
+        want, _ = orc.search(terms, k)
+        got = [(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])]
+        if got != want:
+            raise SystemExit(f"parity failure on {terms}: {got[:3]} vs {want[:3]}")
+    orc.close()
+    return min(n, len(chunk))
 
-    # per-batch latency (each batch alone, submit -> results on the host)
-    lat = []
-    for b, _ in batches:
-        t0 = time.perf_counter()
-        b.run()
-        b.fetch()
-        lat.append((time.perf_counter() - t0) * 1e3)
-    p50 = statistics.median(lat)
 
-    if dist:
-        dist.barrier()
-    w.sync(eng)
-    t0 = time.perf_counter()
-    for s in range(a.steps):
-        batches[s % nb][0].run()
-    w.sync(eng)
-    el = time.perf_counter() - t0
-    queries = sum(batches[s % nb][0].nq for s in range(a.steps))
+def cpu_baseline(idx, lines, k, seconds):
+    from oracle.oracle import OracleVacuum
+    orc = OracleVacuum(idx)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < len(lines):
+        orc.search_lines(lines[done:done + 64], k, threads=1)
+        done += 64
+    cel = time.perf_counter() - t0
+    orc.close()
+    return {"value": round(done / cel, 1), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} queries of the same log, oracle restatement of "
+                      f"VacuumEngine::Search, 1 thread, {cel:.1f}s"}
 
-    # kernel-level accounting over one pass of the batches (HIP events on the engine stream)
-    seg_ms = plan_ms = rep_ms = 0.0
-    algo = surv = dblk = oblk = items = 0
-    for b, _ in batches:
+
+def kernel_accounting(eng, batches):
+    """HIP-event kernel times + algorithmic bytes over one pass of the batches."""
+    import wiser_amd as w
+    acc = dict(seg=0.0, plan=0.0, rep=0.0, algo=0, surv=0, dblk=0, oblk=0, items=0)
+    for b in batches:
         b.run()
         w.sync(eng)
         st = b.stats()
-        seg_ms += st.segment_ms
-        plan_ms += st.plan_ms
-        rep_ms += st.replay_ms
-        algo += st.algo_bytes
-        surv += st.survivors
-        dblk += st.driver_blocks
-        oblk += st.other_blocks
-        items += st.work_items
-    seg_avg_ms = seg_ms / nb
-    achieved = (algo / nb) / (seg_avg_ms * 1e-3) / 1e9
+        acc["seg"] += st.segment_ms
+        acc["plan"] += st.plan_ms
+        acc["rep"] += st.replay_ms
+        acc["algo"] += st.algo_bytes
+        acc["surv"] += st.survivors
+        acc["dblk"] += st.driver_blocks
+        acc["oblk"] += st.other_blocks
+        acc["items"] += st.work_items
+    return acc
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    shard = world > 1 and a.mode == "shard"
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        # one GPU per rank; rehearsals with more ranks than GPUs share devices
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dist.init_process_group(a.dist_backend if shard else "gloo")
+
+    import wiser_amd as w
+    idx, qlog = ensure_index(a, rank, dist)
+    lines = [l.split() for l in open(qlog).read().splitlines()]
+    threads = min(16, os.cpu_count())
+    checked = 0
+
+    if shard:
+        import torch
+        from wiser_amd.shard import ShardedSearcher
+        t = time.time()
+        S = ShardedSearcher(idx, rank, world, device=local, threads=threads)
+        log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
+        eng = S.engine
+        Q = a.batch * world
+        gb = []
+        for s in range(0, len(lines) - Q + 1, Q):
+            chunk = lines[s:s + Q]
+            b = w.ResidentBatch(eng, Q, a.k)
+            b.upload(resolve(eng, chunk, a.k))
+            gb.append((b, chunk))
+        nb = len(gb)
+
+        def step(i, fetch=False):
+            return S.run(gb[i % nb][0], a.batch, fetch=fetch)
+
+        if a.check:   # every rank takes part in the collectives; rank 0 checks
+            hits, nh = step(0, fetch=True)
+            if rank == 0:
+                checked = check_against_oracle(idx, gb[0][1][:a.batch], hits, nh, a.k, a.check)
+        for s in range(a.warmup):
+            step(s)
+        lat = []
+        for i in range(nb):
+            dist.barrier()
+            t0 = time.perf_counter()
+            step(i, fetch=True)
+            lat.append((time.perf_counter() - t0) * 1e3)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(a.steps):
+            step(s)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        queries = a.steps * Q  # every rank completes its owned 1/W of each global batch
+        batches = [b for b, _ in gb]
+        parallelism = f"docshard{world}"
+        global_batch = Q
+    else:
+        t = time.time()
+        eng = w.VacuumEngine(idx, device=local, threads=threads)
+        eng.Load()
+        log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
+        per_rank = (len(lines) + world - 1) // world
+        mine = lines[rank * per_rank:(rank + 1) * per_rank] or lines[:a.batch]
+        batches, chunks = [], []
+        for s in range(0, len(mine), a.batch):
+            chunk = mine[s:s + a.batch]
+            b = w.ResidentBatch(eng, a.batch, a.k)
+            b.upload(resolve(eng, chunk, a.k))
+            batches.append(b)
+            chunks.append(chunk)
+        nb = len(batches)
+        if a.check and rank == 0:
+            batches[0].run()
+            hits, nh = batches[0].fetch()
+            checked = check_against_oracle(idx, chunks[0], hits, nh, a.k, a.check)
+        for s in range(a.warmup):
+            batches[s % nb].run()
+        w.sync(eng)
+        lat = []
+        for b in batches:
+            t0 = time.perf_counter()
+            b.run()
+            b.fetch()
+            lat.append((time.perf_counter() - t0) * 1e3)
+        if dist:
+            dist.barrier()
+        w.sync(eng)
+        t0 = time.perf_counter()
+        for s in range(a.steps):
+            batches[s % nb].run()
+        w.sync(eng)
+        el = time.perf_counter() - t0
+        queries = sum(batches[s % nb].nq for s in range(a.steps))
+        parallelism = f"replicas{world}"
+        global_batch = a.batch * world
+
+    p50 = statistics.median(lat)
+    acc = kernel_accounting(eng, batches)
+    nbk = len(batches)
+    seg_avg_ms = acc["seg"] / nbk
+    achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
 
     if dist:
         import torch
-        tt = torch.tensor([el, float(queries)], dtype=torch.float64)
+        tt = torch.tensor([el, float(queries), p50], dtype=torch.float64)
+        if shard and a.dist_backend == "nccl":
+            tt = tt.cuda()
         mx = tt.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tt.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        el, queries = mx[0].item(), sm[1].item()
+        el, p50 = mx[0].item(), mx[2].item()
+        queries = queries if shard else sm[1].item()
     qps = queries / el
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        from oracle.oracle import OracleVacuum
-        orc = OracleVacuum(idx)
-        done, t0 = 0, time.perf_counter()
-        step = 64
-        while time.perf_counter() - t0 < a.cpu_seconds and done < len(lines):
-            orc.search_lines(lines[done:done + step], a.k, threads=1)
-            done += step
-        cel = time.perf_counter() - t0
-        orc.close()
-        cpu = {"value": round(done / cel, 1), "unit": "queries/s", "cores": 1, "kind": "port",
-               "sample": f"first {done} queries of the same log, oracle restatement of "
-                         f"VacuumEngine::Search, 1 thread, {cel:.1f}s"}
+        cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds)
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_segment.json")
@@ -196,24 +274,24 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), "
                                    f"{len(lines)} two-term AND queries (gen_synthetic_log rule, "
-                                   f"seed 7), batch {a.batch}, top-{a.k}",
-                       "global_batch": a.batch * world, "parallelism": f"replicas{world}",
-                       "k": a.k},
+                                   f"seed 7), {a.batch} queries per GPU per step, top-{a.k}",
+                       "global_batch": global_batch, "parallelism": parallelism, "k": a.k},
             "p50_ms": round(p50, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "segment_kernel", "algo_bytes_per_launch": int(algo / nb),
+                         "kernel": "segment_kernel", "algo_bytes_per_launch": int(acc["algo"] / nbk),
                          "avg_launch_ms": round(seg_avg_ms, 4)},
             "cpu_baseline": cpu,
-            "kernel_ms_per_batch": {"plan": round(plan_ms / nb, 4), "segment": round(seg_avg_ms, 4),
-                                    "replay": round(rep_ms / nb, 4)},
-            "per_batch": {"survivors": int(surv / nb), "driver_blocks": int(dblk / nb),
-                          "other_blocks": int(oblk / nb), "work_items": int(items / nb)},
+            "kernel_ms_per_batch": {"plan": round(acc["plan"] / nbk, 4),
+                                    "segment": round(seg_avg_ms, 4),
+                                    "replay": round(acc["rep"] / nbk, 4)},
+            "per_batch": {"survivors": int(acc["surv"] / nbk), "driver_blocks": int(acc["dblk"] / nbk),
+                          "other_blocks": int(acc["oblk"] / nbk), "work_items": int(acc["items"] / nbk)},
             "parity_checked_queries": checked,
         }
         print(json.dumps(out), flush=True)
-    for b, _ in batches:
+    for b in batches:
         b.close()
     eng.close()
     if dist:

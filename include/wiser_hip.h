@@ -109,6 +109,8 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b);
 int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq);
 /* enqueue plan + segment + replay kernels on the engine stream (asynchronous) */
 int wsr_batch_run(wsr_handle* h, wsr_batch* b);
+/* plan + segment only (a doc-range shard: events go to wsr_shard_reduce) */
+int wsr_batch_run_events(wsr_handle* h, wsr_batch* b);
 /* wait for the engine stream */
 int wsr_sync(wsr_handle* h);
 /* copy results to the host (waits for the stream) */

@@ -31,7 +31,7 @@ def _run_sharded(index_dir, queries, k, world):
             arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
         b = w.ResidentBatch(e, len(queries), k)
         b.upload(arr)
-        check(lib.wsr_batch_run(e._h, b._b))
+        check(lib.wsr_batch_run_events(e._h, b._b))
         cnt = torch.empty(len(queries), dtype=torch.int32, device="cuda")
         tot = (C.c_int64 * world)()
         check(lib.wsr_shard_reduce(e._h, b._b, qpr, world, C.c_void_p(cnt.data_ptr()), tot))

@@ -76,6 +76,7 @@ _sigs = {
     "wsr_batch_destroy": (None, [_P, _P]),
     "wsr_batch_upload": (C.c_int, [_P, _P, C.POINTER(Query), C.c_int32]),
     "wsr_batch_run": (C.c_int, [_P, _P]),
+    "wsr_batch_run_events": (C.c_int, [_P, _P]),
     "wsr_sync": (C.c_int, [_P]),
     "wsr_batch_fetch": (C.c_int, [_P, _P, C.POINTER(Hit), C.POINTER(C.c_int32)]),
     "wsr_batch_stats_get": (C.c_int, [_P, _P, C.POINTER(BatchStats)]),

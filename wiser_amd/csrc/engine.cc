@@ -285,7 +285,12 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   return WSR_OK;
 }
 
-int wsr_batch_run(wsr_handle* h, wsr_batch* b) {
+static int batch_run(wsr_handle* h, wsr_batch* b, bool replay);
+
+int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, true); }
+int wsr_batch_run_events(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, false); }
+
+static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
   try {
@@ -300,8 +305,9 @@ int wsr_batch_run(wsr_handle* h, wsr_batch* b) {
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, st));
     HIP_OK(hipEventRecord(b->ev[2], st));
-    HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
-                         b->d_nhits, st));
+    if (replay)
+      HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
+                           b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());

@@ -12,9 +12,9 @@
 //                                (query_processing.h:510-524,551-562,588-616)
 //
 // Three launches per query batch:
-//   plan_kernel     one workgroup: per query pick the shortest list as driver,
-//                   cut its blocks into segments of similar cost, exclusive-scan
-//                   segment counts and event capacities.
+//   plan_*_kernel   per query pick the shortest list as driver and cut its
+//                   blocks into segments of similar cost (one thread per query),
+//                   then exclusive-scan segment counts and event capacities.
 //   segment_kernel  persistent, one wave per workgroup, segments pulled from an
 //                   atomic queue.  Per driver block (128 postings): wave-decode
 //                   doc ids (2 per lane; bit-unpack or ballot-parallel varint),
@@ -250,11 +250,55 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
 }
 
 // ----------------------------------------------------------------- plan --
-__global__ __launch_bounds__(1024) void plan_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
-                                                    int nq, QueryPlan* __restrict__ plan,
-                                                    uint32_t* __restrict__ counters,
-                                                    uint64_t ev_capacity, uint32_t item_capacity,
-                                                    uint32_t seg_grid) {
+// Pass 1, one thread per query: driver (shortest list here), segment length
+// (driver blocks per work item, so that items cost about kSegCost block
+// decodes) and the item count.  item_base / ev_base are filled by pass 2.
+__global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+                                                         int nq, QueryPlan* __restrict__ plan,
+                                                         uint32_t* __restrict__ counters) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const QueryIn q = qs[i];
+  QueryPlan p{0, 0, 1, 0, 0};
+  bool ok = q.n_terms > 0 && q.k > 0;
+  if (q.n_terms > kMaxTerms || q.k > kMaxK) {
+    ok = false;
+    atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
+  }
+  uint32_t nb[kMaxTerms];
+#pragma unroll
+  for (int s = 0; s < kMaxTerms; ++s) {
+    nb[s] = 0xFFFFFFFFu;
+    if (ok && s < q.n_terms) {
+      const int32_t id = q.list[s];
+      if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) ok = false;
+      else nb[s] = ix.lists[id].nblk;
+      if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
+    }
+  }
+  if (ok) {
+    uint32_t d = 0, nd = nb[0];
+#pragma unroll
+    for (int s = 1; s < kMaxTerms; ++s) if (nb[s] < nd) { d = s; nd = nb[s]; }
+    float cost = 1.0f;
+#pragma unroll
+    for (int s = 0; s < kMaxTerms; ++s)
+      if (s < q.n_terms && s != static_cast<int>(d))
+        cost += fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+    uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
+    seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
+    p.driver = d;
+    p.seg_blocks = seg;
+    p.n_items = (nd + seg - 1) / seg;
+  }
+  plan[i] = p;
+}
+
+// Pass 2, one workgroup: exclusive scans of item counts and event capacities.
+__global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __restrict__ plan,
+                                                         uint32_t* __restrict__ counters,
+                                                         uint64_t ev_capacity, uint32_t item_capacity,
+                                                         uint32_t seg_grid) {
   __shared__ uint32_t s_items[1024];
   __shared__ uint64_t s_cap[1024];
   const int t = threadIdx.x, T = blockDim.x;
@@ -262,52 +306,30 @@ __global__ __launch_bounds__(1024) void plan_kernel(IndexArgs ix, const QueryIn*
   const int q0 = t * per, q1 = min(nq, q0 + per);
   uint32_t items = 0;
   uint64_t cap = 0;
-  uint32_t err = 0;
   for (int i = q0; i < q1; ++i) {
-    const QueryIn q = qs[i];
-    QueryPlan p{0, 0, 1, 0, 0};
-    bool ok = q.n_terms > 0 && q.k > 0;
-    if (q.n_terms > kMaxTerms || q.k > kMaxK) { ok = false; err |= kErrLimit; }
-    uint32_t nb[kMaxTerms];
-    for (int s = 0; ok && s < q.n_terms; ++s) {
-      const int32_t id = q.list[s];
-      if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) { ok = false; break; }
-      nb[s] = ix.lists[id].nblk;
-      if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
-    }
-    if (ok) {
-      uint32_t d = 0;
-      for (int s = 1; s < q.n_terms; ++s) if (nb[s] < nb[d]) d = s;
-      float cost = 1.0f;
-      for (int s = 0; s < q.n_terms; ++s)
-        if (s != static_cast<int>(d)) cost += fminf(static_cast<float>(nb[s]) / nb[d], 64.0f);
-      uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
-      seg = seg < 1 ? 1 : (seg > nb[d] ? nb[d] : seg);
-      p.driver = d;
-      p.seg_blocks = seg;
-      p.n_items = (nb[d] + seg - 1) / seg;
-    }
-    p.item_base = items;          // local, made global after the scan
-    p.ev_base = cap;
+    const QueryPlan p = plan[i];
     items += p.n_items;
     cap += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
-    plan[i] = p;
   }
   s_items[t] = items;
   s_cap[t] = cap;
   __syncthreads();
-  // exclusive scan over threads (Hillis-Steele on LDS; 1024 entries)
-  for (int d = 1; d < T; d <<= 1) {
+  for (int d = 1; d < T; d <<= 1) {  // Hillis-Steele over the thread totals
     uint32_t a = 0; uint64_t c = 0;
     if (t >= d) { a = s_items[t - d]; c = s_cap[t - d]; }
     __syncthreads();
     s_items[t] += a; s_cap[t] += c;
     __syncthreads();
   }
-  const uint32_t ib = s_items[t] - items;
-  const uint64_t cb = s_cap[t] - cap;
-  for (int i = q0; i < q1; ++i) { plan[i].item_base += ib; plan[i].ev_base += cb; }
-  if (err) atomicOr(&counters[kCtrError], err);
+  uint32_t ib = s_items[t] - items;
+  uint64_t cb = s_cap[t] - cap;
+  for (int i = q0; i < q1; ++i) {
+    QueryPlan& p = plan[i];
+    p.item_base = ib;
+    p.ev_base = cb;
+    ib += p.n_items;
+    cb += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
+  }
   if (t == T - 1) {
     const bool fits = s_cap[t] <= ev_capacity && s_items[t] <= item_capacity;
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
@@ -971,8 +993,11 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int seg_grid, hipStream_t st) {
-  hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(1024), 0, st, ix, q, nq, plan, counters,
-                     ev_capacity, item_capacity, static_cast<uint32_t>(seg_grid));
+  if (nq > 0)
+    hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
+                       counters);
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
+                     item_capacity, static_cast<uint32_t>(seg_grid));
   return hipGetLastError();
 }
 

@@ -45,6 +45,10 @@ def exchange(counts, send, owner_totals: Sequence[int], world: int, qpr: int, gr
     import torch
     import torch.distributed as dist
     dev = counts.device
+    if dist.get_backend(group) == "gloo" and dev.type != "cpu":
+        # gloo moves host tensors only (CPU tests, or GPUs sharing one device)
+        rc, rv, rb = exchange(counts.cpu(), send.cpu(), owner_totals, world, qpr, group)
+        return rc.to(dev), rv.to(dev), rb
     rcounts = torch.empty((world, qpr), dtype=torch.int32, device=dev)
     dist.all_to_all_single(rcounts.view(-1), counts.view(-1), group=group)
     tot = torch.tensor(list(owner_totals), dtype=torch.int64, device=dev)
@@ -83,14 +87,15 @@ class ShardedSearcher:
             self._batches[key] = ResidentBatch(self.engine, max_queries, k)
         return self._batches[key]
 
-    def run(self, b, qpr: int):
+    def run(self, b, qpr: int, fetch: bool = True):
         """Run an uploaded global batch (world * qpr queries); returns this
-        rank's owned slice [rank*qpr, (rank+1)*qpr) as (hits, n_hits) ctypes arrays."""
+        rank's owned slice [rank*qpr, (rank+1)*qpr) as (hits, n_hits) ctypes
+        arrays (None when fetch is False: results stay in HBM)."""
         import torch
         eng = self.engine
         Q = b.nq
         assert Q == qpr * self.world
-        check(lib.wsr_batch_run(eng._h, b._b))
+        check(lib.wsr_batch_run_events(eng._h, b._b))
         dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device("cpu")
         counts = torch.empty(Q, dtype=torch.int32, device=dev)
@@ -106,6 +111,8 @@ class ShardedSearcher:
         q0 = self.rank * qpr
         check(lib.wsr_owner_replay(eng._h, b._b, q0, qpr, self.world,
                                    C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr()), rb))
+        if not fetch:
+            return None
         hits = (_capi.Hit * (qpr * b.stride))()
         nh = (C.c_int32 * qpr)()
         check(lib.wsr_batch_fetch_range(eng._h, b._b, q0, qpr, hits, nh))
