@@ -17,7 +17,12 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
             -Wno-unused-function
 ORAFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -shared
 
-all: $(LIB) $(ORACLE)
+CLI     := wiser_amd/_lib/engine_cli
+
+all: $(LIB) $(ORACLE) $(CLI)
+
+$(CLI): tests/cpp/engine_cli.cc include/wiser_hip_engine.hpp include/wiser_hip.h $(LIB)
+	$(CXX) -O2 -std=c++17 -Iinclude -o $@ tests/cpp/engine_cli.cc -Lwiser_amd/_lib -lwiser_hip -Wl,-rpath,'$$ORIGIN'
 
 $(OBJDIR)/%.o: wiser_amd/csrc/% $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -1,0 +1,133 @@
+// wiser_hip_engine.hpp -- C++ host class above the C ABI (wiser_hip.h) that
+// keeps the reference's operator surface:
+//   SearchEngineServiceNew::{Load, Search, TermCount, PostinglistSizes}
+//   (src/qq_mem/src/engine_services.h:14-27, vacuum_engine.h:119-258)
+//   SearchQuery / SearchResultEntry / SearchResult (types.h:205-346)
+// Header-only; link libwiser_hip.so.  Errors: the reference aborts (LOG(FATAL))
+// on corrupt data; this class throws std::runtime_error instead, and keeps the
+// reference's empty-result rules (n_results == 0, any missing term).
+#ifndef WISER_HIP_ENGINE_HPP
+#define WISER_HIP_ENGINE_HPP
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "wiser_hip.h"
+
+namespace wiser_hip {
+
+typedef std::vector<std::string> TermList;
+
+struct SearchQuery {  // types.h:205-256
+  SearchQuery() {}
+  explicit SearchQuery(const TermList& t) : terms(t) {}
+  SearchQuery(const TermList& t, bool snippets) : terms(t), return_snippets(snippets) {}
+  TermList terms;
+  int n_results = 5;
+  bool return_snippets = false;  // snippets are out of scope: entries carry an empty snippet
+  int n_snippet_passages = 3;
+  bool is_phrase = false;        // phrase queries of >= 2 terms are not built yet
+};
+
+struct SearchResultEntry {  // types.h:259-274
+  std::string snippet;
+  int doc_id = 0;
+  double doc_score = 0;
+};
+
+struct SearchResult {  // types.h:297-346
+  std::vector<SearchResultEntry> entries;
+  std::vector<int> doc_freqs;
+  std::size_t Size() const { return entries.size(); }
+  const SearchResultEntry& operator[](int i) const { return entries[i]; }
+};
+
+inline void check(int rc) {
+  if (rc != WSR_OK) throw std::runtime_error(std::string("wiser_hip: ") + wsr_last_error());
+}
+
+class VacuumHipEngine {
+ public:
+  explicit VacuumHipEngine(const std::string& dir, int device = 0) : dir_(dir), device_(device) {}
+  ~VacuumHipEngine() { wsr_close(h_); }
+  VacuumHipEngine(const VacuumHipEngine&) = delete;
+  VacuumHipEngine& operator=(const VacuumHipEngine&) = delete;
+
+  void Load() {
+    if (h_) throw std::runtime_error("Engine is already loaded.");
+    wsr_open_opts o{device_, 0, 0, 0};
+    check(wsr_open(dir_.c_str(), &o, &h_));
+  }
+
+  int TermCount() const {
+    int32_t n = 0;
+    check(wsr_term_count(h_, &n));
+    return n;
+  }
+
+  std::map<std::string, int> PostinglistSizes(const TermList& terms) const {
+    std::map<std::string, int> out;
+    for (const auto& t : terms) {
+      int32_t id, df;
+      check(wsr_lookup(h_, t.c_str(), &id, &df));
+      if (id >= 0) out[t] = df;
+    }
+    return out;
+  }
+
+  SearchResult Search(const SearchQuery& q) { return SearchBatch({q})[0]; }
+
+  std::vector<SearchResult> SearchBatch(const std::vector<SearchQuery>& qs) {
+    std::vector<wsr_query> in(qs.size());
+    std::vector<std::vector<int>> freqs(qs.size());
+    std::vector<bool> empty(qs.size(), false);
+    int stride = 1;
+    for (size_t i = 0; i < qs.size(); ++i) {
+      const SearchQuery& q = qs[i];
+      if (q.is_phrase && q.terms.size() > 1) throw std::runtime_error("phrase queries not built");
+      if (q.terms.size() > WSR_MAX_TERMS || q.n_results > WSR_MAX_K)
+        throw std::runtime_error("query over the engine limits");
+      wsr_query& w = in[i];
+      w.k = q.n_results < 0 ? 0 : q.n_results;
+      bool missing = q.terms.empty();
+      for (size_t t = 0; t < q.terms.size(); ++t) {
+        int32_t id, df;
+        check(wsr_lookup(h_, q.terms[t].c_str(), &id, &df));
+        w.list_ids[t] = id;
+        if (id < 0) missing = true;
+        freqs[i].push_back(df);
+      }
+      empty[i] = missing || w.k == 0;
+      w.n_terms = empty[i] ? 0 : static_cast<int32_t>(q.terms.size());
+      if (w.k > stride) stride = w.k;
+    }
+    std::vector<wsr_hit> hits(qs.size() * stride);
+    std::vector<int32_t> nh(qs.size());
+    if (!qs.empty())
+      check(wsr_search_batch(h_, in.data(), static_cast<int32_t>(qs.size()), stride, hits.data(),
+                             nh.data()));
+    std::vector<SearchResult> out(qs.size());
+    for (size_t i = 0; i < qs.size(); ++i) {
+      if (empty[i]) continue;  // vacuum_engine.h:206-215: nothing, doc_freqs unset
+      out[i].doc_freqs = freqs[i];
+      for (int j = 0; j < nh[i]; ++j) {
+        SearchResultEntry e;
+        e.doc_id = hits[i * stride + j].doc_id;
+        e.doc_score = hits[i * stride + j].score;
+        out[i].entries.push_back(e);
+      }
+    }
+    return out;
+  }
+
+ private:
+  std::string dir_;
+  int device_;
+  wsr_handle* h_ = nullptr;
+};
+
+}  // namespace wiser_hip
+
+#endif
