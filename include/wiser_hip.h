@@ -149,6 +149,15 @@ int wsr_stream(wsr_handle* h, void** stream);
 int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,
                            uint32_t* out, int32_t* count);
 
+/* Host-only check of the dense-list image (no GPU): builds the image of
+ * [doc_lo, doc_hi) (doc_hi 0 = all) with the given dense_div and looks each doc
+ * up in the list's rank bitmap + tf bytes, exactly as the device probe does.
+ * tf_out[i] = tf of docs[i] in the list, -1 when absent; *is_dense = 1 when
+ * the list got a bitmap (otherwise tf_out is all -1). */
+int wsr_debug_dense_lookup(const char* dir, uint32_t doc_lo, uint32_t doc_hi, uint32_t dense_div,
+                           const char* term, const uint32_t* docs, int32_t n, int32_t* tf_out,
+                           int32_t* is_dense);
+
 /* ---- index building (host only; no GPU needed) ----------------------- */
 typedef struct wsr_build_stats {
   int64_t n_docs, n_terms, n_postings, vacuum_bytes, docs_char4_ge_0x80;

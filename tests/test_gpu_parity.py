@@ -16,10 +16,32 @@ pytestmark = pytest.mark.gpu
 SCORE_RTOL = 1e-5  # north_star tolerance; asserted only as a secondary check
 
 
-def _engine(d):
+# Other lists are probed either by decoding their blocks or through the rank
+# bitmap of a dense list; both paths must give the reference's result.
+#   blocks: no bitmaps; dense: the default thresholds; dense_all: every list
+#   gets a bitmap and every other list is probed through it.
+DENSE_MODES = {
+    "blocks": {"WSR_DENSE_DIV": "0"},
+    "dense": {},
+    "dense_all": {"WSR_DENSE_DIV": "1000000000", "WSR_DENSE_RATIO": "0"},
+}
+
+
+def _engine(d, mode="dense"):
     import wiser_amd as w
-    e = w.VacuumEngine(d)
-    e.Load()
+    saved = {k: os.environ.get(k) for k in ("WSR_DENSE_DIV", "WSR_DENSE_RATIO")}
+    try:
+        for k in saved:
+            os.environ.pop(k, None)
+        os.environ.update(DENSE_MODES[mode])
+        e = w.VacuumEngine(d)
+        e.Load()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return e
 
 
@@ -37,12 +59,12 @@ def _check(eng, orc, queries, k):
     assert not bad, f"{len(bad)}/{len(queries)} queries differ, first: {bad[:3]}"
 
 
-@pytest.fixture(scope="module")
-def gpu_indexes(indexes):
+@pytest.fixture(scope="module", params=sorted(DENSE_MODES))
+def gpu_indexes(indexes, request):
     from oracle.oracle import OracleVacuum
     out = {}
     for name, (d, st, linedoc, fmt) in indexes.items():
-        out[name] = (_engine(d), OracleVacuum(d), d)
+        out[name] = (_engine(d, request.param), OracleVacuum(d), d)
     yield out
     for e, o, _ in out.values():
         e.close()
@@ -172,11 +194,12 @@ def test_device_block_decode(gpu_indexes):
         assert got_d == docs and got_t == tfs, term
 
 
-def test_synthetic_parity(synth_small):
+@pytest.mark.parametrize("mode", sorted(DENSE_MODES))
+def test_synthetic_parity(synth_small, mode):
     from oracle.oracle import OracleVacuum
     import wiser_amd as w
     d, st = synth_small
-    eng = _engine(d)
+    eng = _engine(d, mode)
     orc = OracleVacuum(d)
     log = os.path.join(d, "q.log")
     w.gen_two_term_log(d, log, n_queries=3000, seed=7)
@@ -198,3 +221,32 @@ def test_limits_fail_loudly(gpu_indexes):
         eng.Search(w.SearchQuery(["hello", "world"], is_phrase=True))
     with pytest.raises(NotImplementedError):
         eng.Search(w.SearchQuery(["hello"], n_results=65))
+
+
+@pytest.mark.parametrize("mode", sorted(DENSE_MODES))
+def test_large_tf_dense_escape(tmp_path, mode):
+    """tf >= 255 in a bitmap-probed list: the 1-byte tf escapes to the blob
+    (pack blocks and the VInts tail)."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    ld = tmp_path / "big_tf.linedoc"
+    rng = random.Random(5)
+    with open(ld, "w") as f:
+        f.write("FIELDS_HEADER_INDICATOR###\tdoctitle\tbody\ttokenized\n")
+        for i in range(300):
+            toks = ["x"] * rng.choice([1, 2, 254, 255, 256, 600])
+            if i % 2 == 0:
+                toks += ["y"] * rng.randint(1, 3)
+            if i % 7 == 0:
+                toks += ["z"] * 300
+            toks += [f"w{i}"]
+            f.write(f"t\t{' '.join(toks)}\t{' '.join(toks)}\n")
+    d = tmp_path / "idx"
+    d.mkdir()
+    w.build_from_linedoc(str(ld), str(d), "TOKEN_ONLY")
+    eng = _engine(str(d), mode)
+    orc = OracleVacuum(str(d))
+    _check(eng, orc, [["x"], ["y", "x"], ["x", "y"], ["z", "x"], ["y", "z", "x"], ["w7", "x"],
+                      ["x", "w299"]], 64)
+    eng.close()
+    orc.close()

@@ -90,6 +90,9 @@ _sigs = {
     "wsr_stream": (C.c_int, [_P, C.POINTER(_P)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]),
+    "wsr_debug_dense_lookup": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p,
+                                         C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32)]),
     "wsr_build_from_linedoc": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_char_p,
                                          C.POINTER(BuildStats)]),
     "wsr_build_synthetic": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_double, C.c_uint64,

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -45,6 +46,15 @@ void dev_upload(T** dst, const std::vector<T>& src) {
   if (!src.empty()) HIP_OK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
 }
 
+// tuning knobs read once per wsr_open (unset or unparsable: the default)
+double env_number(const char* name, double dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const double x = std::strtod(v, &end);
+  return (end && *end == 0 && x >= 0) ? x : dflt;
+}
+
 }  // namespace
 
 struct wsr_handle {
@@ -60,6 +70,9 @@ struct wsr_handle {
   uint32_t* d_meta = nullptr;
   uint8_t* d_c4 = nullptr;
   double* d_cache = nullptr;
+  DenseEnt* d_dense = nullptr;
+  uint8_t* d_tf8 = nullptr;
+  uint32_t dense_lists = 0;
   std::vector<ListDev> lists;       // host copy of the directory heads
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
   std::vector<BlockDev> blocks;     // host copy (debug decode)
@@ -116,7 +129,18 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     uint32_t lo = opts ? opts->doc_lo : 0, hi = opts ? opts->doc_hi : 0;
     if (hi == 0) hi = 0xFFFFFFFFu;
     int threads = opts && opts->threads > 0 ? opts->threads : static_cast<int>(std::thread::hardware_concurrency());
-    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32));
+    // dense-list bitmaps: lists with >= span/div postings (WSR_DENSE_DIV, 0 = off);
+    // probed by bitmap when >= ratio x the driver's blocks (WSR_DENSE_RATIO)
+    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 128));
+    const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
+    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div);
+    dev_upload(&h->d_dense, img.dense);
+    dev_upload(&h->d_tf8, img.tf8);
+    h->dense_lists = img.dense_lists;
+    h->args.dense = h->d_dense;
+    h->args.tf8 = h->d_tf8;
+    h->args.dense_span = img.dense_span;
+    h->args.dense_ratio = dense_ratio;
     dev_upload(&h->d_blob, img.blob);
     dev_upload(&h->d_lists, img.lists);
     dev_upload(&h->d_blocks, img.blocks);
@@ -161,7 +185,8 @@ void wsr_close(wsr_handle* h) {
   for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
                   static_cast<void*>(h->d_meta),
-                  static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache)})
+                  static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
+                  static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8)})
     if (p) (void)hipFree(p);
   delete h;
 }
@@ -507,6 +532,25 @@ int wsr_debug_decode_block(wsr_handle* h, int32_t id, int32_t block, int32_t whi
     return fail(WSR_E_HIP, ex.what());
   }
   if (count) *count = static_cast<int32_t>(cnt);
+  return WSR_OK;
+}
+
+int wsr_debug_dense_lookup(const char* dir, uint32_t doc_lo, uint32_t doc_hi, uint32_t dense_div,
+                           const char* term, const uint32_t* docs, int32_t n, int32_t* tf_out,
+                           int32_t* is_dense) {
+  if (!dir || !term || (n > 0 && (!docs || !tf_out))) return fail(WSR_E_INVALID, "null argument");
+  try {
+    VacuumIndex idx;
+    idx.open(dir);
+    const HostImage img = build_image(idx, doc_lo, doc_hi ? doc_hi : 0xFFFFFFFFu, 4, dense_div);
+    const int32_t id = idx.find(term);
+    const bool dense = id >= 0 && img.lists[id].bm != kNoDense;
+    if (is_dense) *is_dense = dense ? 1 : 0;
+    for (int32_t i = 0; i < n; ++i)
+      tf_out[i] = dense ? static_cast<int32_t>(dense_lookup_host(img, img.lists[id], docs[i])) : -1;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
   return WSR_OK;
 }
 

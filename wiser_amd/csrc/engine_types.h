@@ -17,8 +17,25 @@ struct ListDev {
   uint32_t df;        // GLOBAL document frequency (drives idf and planning)
   uint32_t tail_cnt;  // postings in the image's last block (128 unless a VInts tail)
   double idf;         // calc_es_idf(N, df) computed on the host with libm log
+  uint64_t bm;        // first DenseEnt of the list's doc bitmap, kNoDense when it has none
+  uint64_t tf8;       // byte offset of the list's 1-byte tf array (posting order)
 };
-static_assert(sizeof(ListDev) == 32, "ListDev layout");
+static_assert(sizeof(ListDev) == 48, "ListDev layout");
+
+constexpr uint64_t kNoDense = ~0ull;
+constexpr uint32_t kDenseDocs = 96;   // doc ids per DenseEnt
+constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
+
+// Dense lists (df >= span / dense_div) also carry a rank bitmap of their doc
+// ids over the image's doc range, 96 docs per 16-byte entry, so that a probe
+// costs one 16-byte load + popcounts instead of decoding the list's blocks.
+// rank = postings of the list (in the image's blocks) before the entry's first
+// doc; posting index = rank + popcount of the lower bits; block = index / 128.
+struct DenseEnt {
+  uint32_t rank;
+  uint32_t w[3];     // bit (d - doc_lo) % 96 of doc d
+};
+static_assert(sizeof(DenseEnt) == 16, "DenseEnt layout");
 
 // One 128-posting block (= one skip-list row, flash_containers.h:312-350).
 struct BlockDev {

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstring>
 #include <fcntl.h>
 #include <fstream>
 #include <stdexcept>
@@ -160,10 +161,13 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
     const int b = p[1];
     if (b < 1 || b > 32 || p + 2 + 16 * b > end) return false;
     const uint8_t* d = p + 2;
+    const uint64_t mask = b == 32 ? 0xFFFFFFFFull : ((1ull << b) - 1);
     for (int j = 0; j < kPackSize; ++j) {
-      uint64_t bit = static_cast<uint64_t>(j) * b, val = 0;
-      for (int k = 0; k < b; ++k, ++bit) val |= static_cast<uint64_t>((d[bit >> 3] >> (bit & 7)) & 1) << k;
-      out[j] = static_cast<uint32_t>(val);
+      const uint64_t bit = static_cast<uint64_t>(j) * b;
+      uint64_t w = 0;
+      const uint64_t at = bit >> 3, avail = 16u * b - at;  // bytes of the pack from `at`
+      std::memcpy(&w, d + at, avail < 8 ? avail : 8);     // little-endian bit order
+      out[j] = static_cast<uint32_t>((w >> (bit & 7)) & mask);
     }
   } else if (p[0] == kVIntsMagic) {
     uint64_t nb = 0;
@@ -189,17 +193,53 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
   return true;
 }
 
-HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads) {
+HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
+                      uint32_t dense_div) {
   const int32_t L = idx.n_lists();
   const uint8_t* file = idx.file();
   const uint8_t* fend = file + idx.file_bytes();
+  // doc ids a bitmap covers: the image's range clipped to the doc-length records
+  const uint64_t span_end = std::min<uint64_t>(doc_hi, static_cast<uint64_t>(std::max(idx.n_docs(), 0)));
+  const uint32_t span = span_end > doc_lo ? static_cast<uint32_t>(span_end - doc_lo) : 0u;
+  const uint64_t n_ent = (static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs;
   struct Part {
     std::vector<BlockDev> blocks;  // doc_rel / tf_rel relative to the list's span
     std::vector<uint32_t> meta;
     std::vector<uint8_t> bytes;    // docid span followed by tf span
     uint32_t tail_cnt = 0;
+    std::vector<DenseEnt> dense;   // rank bitmap (dense lists only)
+    std::vector<uint8_t> tf8;
   };
   std::vector<Part> parts(L);
+  // decode the image's postings of one list and lay down its bitmap + tf bytes
+  auto build_dense = [&](Part& pt, const std::vector<SkipRow>& rows, uint64_t r0, uint64_t r1,
+                         uint64_t n_img) {
+    std::vector<uint32_t> docs(n_img), tfs(n_img);
+    for (uint64_t r = r0; r < r1; ++r) {
+      const int cnt = r + 1 == r1 ? static_cast<int>(pt.tail_cnt) : kPackSize;
+      const uint64_t at = (r - r0) * kPackSize;
+      if (!host_decode_block(file + rows[r].doc_off, fend, cnt, true, rows[r].prev_doc, &docs[at]) ||
+          !host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, &tfs[at]))
+        throw std::runtime_error("cannot decode a block for the dense image");
+    }
+    // a doc inside [doc_lo, doc_hi) but past the doc-length records cannot be
+    // represented: keep the list on the block path
+    for (uint64_t i = 0; i < n_img; ++i)
+      if (docs[i] >= doc_lo && docs[i] < doc_hi && docs[i] - doc_lo >= span) return;
+    pt.dense.assign(n_ent, DenseEnt{0, {0, 0, 0}});
+    uint64_t i = 0;
+    for (uint64_t e = 0; e < n_ent; ++e) {
+      const uint64_t start = doc_lo + e * kDenseDocs;
+      while (i < n_img && docs[i] < start) ++i;
+      pt.dense[e].rank = static_cast<uint32_t>(i);
+      for (uint64_t j = i; j < n_img && docs[j] < start + kDenseDocs; ++j) {
+        const uint32_t bit = static_cast<uint32_t>(docs[j] - start);
+        pt.dense[e].w[bit >> 5] |= 1u << (bit & 31);
+      }
+    }
+    pt.tf8.resize(n_img);
+    for (uint64_t j = 0; j < n_img; ++j) pt.tf8[j] = static_cast<uint8_t>(tfs[j] < kTf8Escape ? tfs[j] : kTf8Escape);
+  };
   std::atomic<int32_t> next{0};
   std::atomic<bool> failed{false};
   std::string err;
@@ -253,6 +293,8 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
           pt.meta.push_back(bd | (bf << 8));
         }
         pt.tail_cnt = (r1 == nrows) ? static_cast<uint32_t>(fcnt) : kPackSize;
+        const uint64_t n_img = (r1 - r0 - 1) * kPackSize + pt.tail_cnt;
+        if (dense_div && span && n_img * dense_div >= span) build_dense(pt, rows, r0, r1, n_img);
       }
     } catch (const std::exception& ex) {
       if (!failed.exchange(true)) err = ex.what();
@@ -267,6 +309,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   HostImage img;
   img.doc_lo = doc_lo;
   img.doc_hi = doc_hi;
+  img.dense_span = span;
   img.lists.resize(L);
   img.list_bytes.resize(L);
   uint64_t total = 0, nb = 0;
@@ -285,6 +328,17 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     ld.df = idx.df(id);
     ld.tail_cnt = p.tail_cnt;
     ld.idf = idx.idf(id);
+    ld.bm = kNoDense;
+    ld.tf8 = 0;
+    if (!p.dense.empty()) {
+      ld.bm = img.dense.size();
+      ld.tf8 = img.tf8.size();
+      img.dense.insert(img.dense.end(), p.dense.begin(), p.dense.end());
+      img.tf8.insert(img.tf8.end(), p.tf8.begin(), p.tf8.end());
+      ++img.dense_lists;
+      std::vector<DenseEnt>().swap(p.dense);
+      std::vector<uint8_t>().swap(p.tf8);
+    }
     if (!p.bytes.empty()) std::memcpy(&img.blob[at], p.bytes.data(), p.bytes.size());
     img.docid_tf_bytes += p.bytes.size();
     img.list_bytes[id] = p.bytes.size();
@@ -294,6 +348,27 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     std::vector<uint8_t>().swap(p.bytes);
   }
   return img;
+}
+
+int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) {
+  if (L.bm == kNoDense || doc < img.doc_lo || doc >= img.doc_hi) return -1;
+  const uint32_t rel = doc - img.doc_lo;
+  if (rel >= img.dense_span) return -1;
+  const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
+  const uint32_t bit = rel % kDenseDocs, w = bit >> 5, sh = bit & 31;
+  if (!((e.w[w] >> sh) & 1u)) return -1;
+  uint32_t idx = e.rank + static_cast<uint32_t>(__builtin_popcount(e.w[w] & ((1u << sh) - 1u)));
+  for (uint32_t i = 0; i < w; ++i) idx += static_cast<uint32_t>(__builtin_popcount(e.w[i]));
+  const uint8_t t = img.tf8[L.tf8 + idx];
+  if (t != kTf8Escape) return t;
+  const uint32_t j = idx / kPackSize;
+  const BlockDev& bd = img.blocks[L.blk0 + j];
+  const uint32_t cnt = j + 1 == L.nblk ? L.tail_cnt : kPackSize;
+  uint32_t out[kPackSize];
+  const uint8_t* p = img.blob.data() + L.base + bd.tf_rel;
+  if (!host_decode_block(p, img.blob.data() + img.blob.size(), static_cast<int>(cnt), false, 0, out))
+    return -1;
+  return out[idx % kPackSize];
 }
 
 }  // namespace wiser

@@ -78,6 +78,10 @@ struct HostImage {
   std::vector<uint64_t> list_bytes;  // docid+tf span bytes per list in the image
   uint32_t doc_lo = 0, doc_hi = 0;
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
+  std::vector<DenseEnt> dense;  // rank bitmaps of the dense lists
+  std::vector<uint8_t> tf8;     // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
+  uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
+  uint32_t dense_lists = 0;
 };
 
 // Decode one block (pack or VInts) at p into out[0..cnt); delta-coded blocks
@@ -85,6 +89,13 @@ struct HostImage {
 bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta,
                        uint32_t prev, uint32_t* out);
 
-HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads);
+// dense_div > 0: lists with at least span / dense_div postings in the image get
+// a rank bitmap + 1-byte tf array (0 disables them).
+HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
+                      uint32_t dense_div = 0);
+
+// Host restatement of the device's dense probe (segment kernel): tf of doc in
+// list L of the image, -1 when absent or when L has no bitmap.
+int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc);
 
 }  // namespace wiser

@@ -249,6 +249,56 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
   return lo;
 }
 
+// ---------------------------------------------------------- dense lists --
+// Other list B is probed through its rank bitmap when it has one and is at
+// least dense_ratio times as long as the driver (then a block decode per
+// probe would mostly decode postings nobody asks for).
+constexpr float kDenseCost = 0.5f;   // plan cost of a bitmap probe round, in block decodes
+
+__device__ __forceinline__ bool use_dense(const IndexArgs& ix, bool has_bm, uint32_t nblk_b,
+                                          uint32_t nblk_driver) {
+  return has_bm && static_cast<float>(nblk_b) >= ix.dense_ratio * static_cast<float>(nblk_driver);
+}
+
+// tf of posting `idx` of B read from the tf blob (tf >= 255): pack value, or
+// a per-lane walk of the VInts tail (0x9B | varint nbytes | LEB128 values).
+__device__ __forceinline__ uint32_t dense_tf_slow(const IndexArgs& ix, const ListDev& B, uint32_t idx) {
+  const uint32_t j = idx >> 7, pos = idx & 127;
+  const BlockDev bb = ix.blocks[B.blk0 + j];
+  const uint32_t tbits = ix.blk_meta[B.blk0 + j] >> 8;
+  const uint8_t* p = ix.blob + B.base + bb.tf_rel;
+  if (tbits) return pack_value(p + 2, tbits, pos);
+  const uint8_t* q = p + 1;
+  for (int i = 0; i < 5 && (*q++ & 0x80); ++i) {}   // nbytes
+  for (uint32_t v = 0; v < pos; ++v)
+    for (int i = 0; i < 5 && (*q++ & 0x80); ++i) {}
+  uint32_t val = 0;
+  for (int i = 0; i < 5; ++i) {
+    const uint8_t c = *q++;
+    val |= static_cast<uint32_t>(c & 0x7F) << (7 * i);
+    if (!(c & 0x80)) break;
+  }
+  return val;
+}
+
+// Is doc a in B?  One 16-byte load; on a hit the posting's rank gives its tf.
+__device__ __forceinline__ bool dense_probe(const IndexArgs& ix, const ListDev& B, uint32_t a,
+                                            uint32_t* tf) {
+  const uint32_t rel = a - ix.doc_lo;
+  if (rel >= ix.dense_span) return false;
+  const uint32_t e = rel / kDenseDocs, bit = rel - e * kDenseDocs;
+  const uint4 v = reinterpret_cast<const uint4*>(ix.dense + B.bm)[e];
+  const uint32_t w = bit >> 5, sh = bit & 31;
+  const uint32_t word = w == 0 ? v.y : (w == 1 ? v.z : v.w);
+  if (!((word >> sh) & 1u)) return false;
+  const uint32_t idx = v.x + (w > 0 ? __popc(v.y) : 0u) + (w > 1 ? __popc(v.z) : 0u) +
+                       __popc(word & ((1u << sh) - 1u));
+  uint32_t t = ix.tf8[B.tf8 + idx];
+  if (t == kTf8Escape) t = dense_tf_slow(ix, B, idx);
+  *tf = t;
+  return true;
+}
+
 // ----------------------------------------------------------------- plan --
 // Pass 1, one thread per query: driver (shortest list here), segment length
 // (driver blocks per work item, so that items cost about kSegCost block
@@ -266,13 +316,15 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
   }
   uint32_t nb[kMaxTerms];
+  bool dn[kMaxTerms];
 #pragma unroll
   for (int s = 0; s < kMaxTerms; ++s) {
     nb[s] = 0xFFFFFFFFu;
+    dn[s] = false;
     if (ok && s < q.n_terms) {
       const int32_t id = q.list[s];
       if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) ok = false;
-      else nb[s] = ix.lists[id].nblk;
+      else { nb[s] = ix.lists[id].nblk; dn[s] = ix.lists[id].bm != kNoDense; }
       if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
     }
   }
@@ -284,7 +336,8 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
 #pragma unroll
     for (int s = 0; s < kMaxTerms; ++s)
       if (s < q.n_terms && s != static_cast<int>(d))
-        cost += fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+        cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
+                                                : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
     uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
     seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
     p.driver = d;
@@ -451,7 +504,7 @@ __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm
   return idf * tfn;
 }
 
-__global__ __launch_bounds__(64, 4) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+__global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
                                                      Event* __restrict__ events,
@@ -604,6 +657,19 @@ __global__ __launch_bounds__(64, 4) void segment_kernel(IndexArgs ix, const Quer
           continue;
         }
         const ListDev& B = L;
+        if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
+          uint32_t t0 = 0, t1 = 0;
+          const bool h0 = al0 && dense_probe(ix, B, a0, &t0);
+          const bool h1 = al1 && dense_probe(ix, B, a1, &t1);
+          // past B's last doc nothing later in the segment can match
+          const uint32_t blast = ix.blk_last[B.blk0 + B.nblk - 1];
+          if (__ballot((al0 && a0 > blast) || (al1 && a1 > blast))) done = true;
+          al0 = h0;
+          al1 = h1;
+          if (al0) s0 += bm25_term(B.idf, t0, nrm0);
+          if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+          continue;
+        }
         const uint32_t* last = ix.blk_last + B.blk0;
         uint32_t c = 0;
 #pragma unroll
