@@ -82,6 +82,8 @@ typedef struct wsr_batch_stats {
   uint64_t algo_bytes;       /* sum over queries of docid+tf span bytes of its lists
                                 + survivors * 1 B + k * 12 B */
   double plan_ms, segment_ms, replay_ms;  /* HIP-event times on the engine stream */
+  uint64_t events;           /* segment heap-insertion events handed to the replay */
+  uint64_t max_query_events; /* the largest per-query event count of the batch */
 } wsr_batch_stats;
 
 const char* wsr_last_error(void);
@@ -148,6 +150,12 @@ int wsr_stream(wsr_handle* h, void** stream);
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */
 int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,
                            uint32_t* out, int32_t* count);
+
+/* Raw per-workgroup counters of the last segment launch (diagnostics):
+ * n_wg rows of `stride` u32 {survivors, driver blocks, other blocks, ...;
+ * section cycle counts in a -DWSR_PROFILE build}.  out may be NULL to query. */
+int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_words,
+                       int32_t* n_wg, int32_t* stride);
 
 /* Host-only check of the dense-list image (no GPU): builds the image of
  * [doc_lo, doc_hi) (doc_hi 0 = all) with the given dense_div and looks each doc

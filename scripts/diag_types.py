@@ -24,10 +24,11 @@ if not os.path.exists(os.path.join(idx, "READY")):
 eng = w.VacuumEngine(idx)
 eng.Load()
 lines = [l.split() for l in open(os.path.join(idx, "two_term_100000.log")).read().splitlines()]
-cls = {"low-low": [], "low-high": [], "high-high": []}
+cls = {"mixed": lines[:4096], "low-low": [], "low-high": [], "high-high": []}
 for t in lines:
     h = sum(1 for x in t if eng.lookup(x)[1] >= 10000)
     cls[["low-low", "low-high", "high-high"][h]].append(t)
+import ctypes as C
 for name, qs in cls.items():
     if args.only and name != args.only:
         continue
@@ -45,6 +46,22 @@ for name, qs in cls.items():
     st = b.stats()
     print(f"{name:10s} n={len(qs)} plan={st.plan_ms:.3f} seg={st.segment_ms:.3f} replay={st.replay_ms:.3f} "
           f"items={st.work_items} surv={st.survivors} dblk={st.driver_blocks} oblk={st.other_blocks} "
-          f"algoMB={st.algo_bytes/1e6:.1f}", flush=True)
+          f"algoMB={st.algo_bytes/1e6:.1f} events={st.events} maxqev={st.max_query_events}", flush=True)
+    n_wg, stride = C.c_int32(), C.c_int32()
+    _capi.check(_capi.lib.wsr_debug_wg_stats(eng._h, b._b, None, 0, C.byref(n_wg), C.byref(stride)))
+    raw = (C.c_uint32 * (n_wg.value * stride.value))()
+    _capi.check(_capi.lib.wsr_debug_wg_stats(eng._h, b._b, raw, len(raw), None, None))
+    rows = [raw[i * stride.value:(i + 1) * stride.value] for i in range(n_wg.value)]
+    db = sorted(r[1] for r in rows)
+    print(f"   wg={n_wg.value} driver blocks per wg: mean={sum(db)/len(db):.1f} max={db[-1]} "
+          f"p50={db[len(db)//2]} p99={db[int(len(db)*0.99)]}")
+    if stride.value >= 10:
+        names = ["setup", "driver", "dense", "blocks", "topk"]
+        tot = [sum(r[4 + i] for r in rows) for i in range(5)]
+        wall = sorted(r[9] for r in rows)
+        allc = sum(tot)
+        print("   sections: " + " ".join(f"{n}={100*t/allc:.1f}%" for n, t in zip(names, tot)) +
+              f" | wg cycles mean={sum(wall)/len(wall):.0f} p50={wall[len(wall)//2]} max={wall[-1]}"
+              f" | cycles/driver block={allc/max(1,sum(db)):.0f}")
     b.close()
 print("class sizes:", {k: len(v) for k, v in cls.items()})

@@ -11,7 +11,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libwiser_hip.so")
+# WISER_HIP_LIB: diagnostics only (the section-timer build, `make prof`)
+LIB_PATH = os.environ.get("WISER_HIP_LIB") or os.path.join(HERE, "_lib", "libwiser_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "wiser_hip.h")
 
 MAX_TERMS = 8
@@ -39,7 +40,8 @@ class BatchStats(C.Structure):
     _fields_ = [("work_items", C.c_uint64), ("survivors", C.c_uint64),
                 ("driver_blocks", C.c_uint64), ("other_blocks", C.c_uint64),
                 ("algo_bytes", C.c_uint64), ("plan_ms", C.c_double),
-                ("segment_ms", C.c_double), ("replay_ms", C.c_double)]
+                ("segment_ms", C.c_double), ("replay_ms", C.c_double),
+                ("events", C.c_uint64), ("max_query_events", C.c_uint64)]
 
 
 class BuildStats(C.Structure):
@@ -88,6 +90,8 @@ _sigs = {
     "wsr_batch_fetch_range": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.POINTER(Hit),
                                         C.POINTER(C.c_int32)]),
     "wsr_stream": (C.c_int, [_P, C.POINTER(_P)]),
+    "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
+                                     C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]),
     "wsr_debug_dense_lookup": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p,

@@ -73,6 +73,8 @@ struct wsr_handle {
   DenseEnt* d_dense = nullptr;
   uint8_t* d_tf8 = nullptr;
   uint32_t dense_lists = 0;
+  bool fuse_replay = true;
+  bool seg_floor = true;
   std::vector<ListDev> lists;       // host copy of the directory heads
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
   std::vector<BlockDev> blocks;     // host copy (debug decode)
@@ -91,6 +93,9 @@ struct wsr_batch {
   uint64_t item_cap = 0;
   HitDev* d_hits = nullptr;
   int32_t* d_nhits = nullptr;
+  uint32_t* d_qdone = nullptr;   // fused replay: completed items per query
+  uint32_t* d_itemq = nullptr;   // item -> query (capacity item_cap)
+  uint64_t* d_pub = nullptr;     // per item score floor (capacity item_cap)
   uint32_t* d_stats = nullptr;   // per segment workgroup: survivors, blocks
   int seg_grid = 0;
   // doc-range shard exchange
@@ -133,6 +138,11 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // probed by bitmap when >= ratio x the driver's blocks (WSR_DENSE_RATIO)
     const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 128));
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
+    // replay inside the segment kernel (WSR_FUSE_REPLAY=0: separate launch)
+    h->fuse_replay = env_number("WSR_FUSE_REPLAY", 1) != 0;
+    // segments start from the score floor of the query's earlier segments
+    // (WSR_SEG_FLOOR=0: every segment from an empty top-k)
+    h->seg_floor = env_number("WSR_SEG_FLOOR", 1) != 0;
     HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div);
     dev_upload(&h->d_dense, img.dense);
     dev_upload(&h->d_tf8, img.tf8);
@@ -231,6 +241,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
+    HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride * std::max(h->grid, 1)));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
   } catch (const std::exception& e) {
@@ -248,6 +259,8 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
                   static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
+                  static_cast<void*>(b->d_qdone), static_cast<void*>(b->d_itemq),
+                  static_cast<void*>(b->d_pub),
                   static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase)})
     if (p) (void)hipFree(p);
@@ -295,8 +308,14 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     }
     if (items_need > b->item_cap || !b->d_evcnt) {
       if (b->d_evcnt) HIP_OK(hipFree(b->d_evcnt));
+      if (b->d_itemq) HIP_OK(hipFree(b->d_itemq));
+      if (b->d_pub) HIP_OK(hipFree(b->d_pub));
+      b->d_itemq = nullptr;
+      b->d_pub = nullptr;
       b->item_cap = items_need + items_need / 4 + 1024;
       HIP_OK(hipMalloc(&b->d_evcnt, sizeof(uint32_t) * b->item_cap));
+      HIP_OK(hipMalloc(&b->d_itemq, sizeof(uint32_t) * b->item_cap));
+      HIP_OK(hipMalloc(&b->d_pub, sizeof(uint64_t) * b->item_cap));
     }
     if (nq) HIP_OK(hipMemcpy(b->d_q, in.data(), sizeof(QueryIn) * nq, hipMemcpyHostToDevice));
   } catch (const std::exception& e) {
@@ -322,15 +341,18 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = h->stream;
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * kNumCounters, st));
+    const bool fused = replay && h->fuse_replay;
+    FusedReplay fr{fused ? b->d_qdone : nullptr, b->d_hits, b->stride, b->d_nhits};
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       b->seg_grid, st));
+                       b->seg_grid, fr, b->d_itemq, h->seg_floor ? b->d_pub : nullptr, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                           b->d_stats, b->seg_grid, st));
+                           b->d_stats, b->seg_grid, fr, b->d_itemq,
+                           h->seg_floor ? b->d_pub : nullptr, st));
     HIP_OK(hipEventRecord(b->ev[2], st));
-    if (replay)
+    if (replay && !fused)
       HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
                            b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
@@ -385,6 +407,22 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     out->driver_blocks = db;
     out->other_blocks = ob;
     out->algo_bytes = b->algo_static + sv;
+    {
+      const uint32_t items = ctr[kCtrItems];
+      std::vector<uint32_t> ec(items);
+      std::vector<QueryPlan> pl(b->nq);
+      if (items) HIP_OK(hipMemcpy(ec.data(), b->d_evcnt, items * sizeof(uint32_t), hipMemcpyDeviceToHost));
+      if (b->nq) HIP_OK(hipMemcpy(pl.data(), b->d_plan, pl.size() * sizeof(QueryPlan), hipMemcpyDeviceToHost));
+      uint64_t tot = 0, mx = 0;
+      for (const QueryPlan& p : pl) {
+        uint64_t e = 0;
+        for (uint32_t r = 0; r < p.n_items && p.item_base + r < items; ++r) e += ec[p.item_base + r];
+        tot += e;
+        mx = std::max(mx, e);
+      }
+      out->events = tot;
+      out->max_query_events = mx;
+    }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[0], b->ev[1])); out->plan_ms = ms;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); out->segment_ms = ms;
@@ -532,6 +570,24 @@ int wsr_debug_decode_block(wsr_handle* h, int32_t id, int32_t block, int32_t whi
     return fail(WSR_E_HIP, ex.what());
   }
   if (count) *count = static_cast<int32_t>(cnt);
+  return WSR_OK;
+}
+
+int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_words,
+                       int32_t* n_wg, int32_t* stride) {
+  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> g(h->mu);
+  if (n_wg) *n_wg = b->seg_grid;
+  if (stride) *stride = kStatStride;
+  if (!out) return WSR_OK;
+  const size_t n = std::min<size_t>(static_cast<size_t>(std::max(max_words, 0)),
+                                    static_cast<size_t>(kStatStride) * b->seg_grid);
+  try {
+    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
   return WSR_OK;
 }
 

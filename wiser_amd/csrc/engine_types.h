@@ -23,19 +23,19 @@ struct ListDev {
 static_assert(sizeof(ListDev) == 48, "ListDev layout");
 
 constexpr uint64_t kNoDense = ~0ull;
-constexpr uint32_t kDenseDocs = 96;   // doc ids per DenseEnt
+constexpr uint32_t kDenseDocs = 32;   // doc ids per DenseEnt
 constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 
 // Dense lists (df >= span / dense_div) also carry a rank bitmap of their doc
-// ids over the image's doc range, 96 docs per 16-byte entry, so that a probe
-// costs one 16-byte load + popcounts instead of decoding the list's blocks.
+// ids over the image's doc range, 32 docs per 8-byte entry, so that a probe
+// costs one 8-byte load + a popcount instead of decoding the list's blocks.
 // rank = postings of the list (in the image's blocks) before the entry's first
 // doc; posting index = rank + popcount of the lower bits; block = index / 128.
 struct DenseEnt {
   uint32_t rank;
-  uint32_t w[3];     // bit (d - doc_lo) % 96 of doc d
+  uint32_t w;        // bit (d - doc_lo) % 32 of doc d
 };
-static_assert(sizeof(DenseEnt) == 16, "DenseEnt layout");
+static_assert(sizeof(DenseEnt) == 8, "DenseEnt layout");
 
 // One 128-posting block (= one skip-list row, flash_containers.h:312-350).
 struct BlockDev {

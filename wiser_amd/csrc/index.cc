@@ -226,7 +226,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     // represented: keep the list on the block path
     for (uint64_t i = 0; i < n_img; ++i)
       if (docs[i] >= doc_lo && docs[i] < doc_hi && docs[i] - doc_lo >= span) return;
-    pt.dense.assign(n_ent, DenseEnt{0, {0, 0, 0}});
+    pt.dense.assign(n_ent, DenseEnt{0, 0});
     uint64_t i = 0;
     for (uint64_t e = 0; e < n_ent; ++e) {
       const uint64_t start = doc_lo + e * kDenseDocs;
@@ -234,7 +234,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       pt.dense[e].rank = static_cast<uint32_t>(i);
       for (uint64_t j = i; j < n_img && docs[j] < start + kDenseDocs; ++j) {
         const uint32_t bit = static_cast<uint32_t>(docs[j] - start);
-        pt.dense[e].w[bit >> 5] |= 1u << (bit & 31);
+        pt.dense[e].w |= 1u << bit;
       }
     }
     pt.tf8.resize(n_img);
@@ -355,10 +355,9 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   const uint32_t rel = doc - img.doc_lo;
   if (rel >= img.dense_span) return -1;
   const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
-  const uint32_t bit = rel % kDenseDocs, w = bit >> 5, sh = bit & 31;
-  if (!((e.w[w] >> sh) & 1u)) return -1;
-  uint32_t idx = e.rank + static_cast<uint32_t>(__builtin_popcount(e.w[w] & ((1u << sh) - 1u)));
-  for (uint32_t i = 0; i < w; ++i) idx += static_cast<uint32_t>(__builtin_popcount(e.w[i]));
+  const uint32_t sh = rel % kDenseDocs;
+  if (!((e.w >> sh) & 1u)) return -1;
+  const uint32_t idx = e.rank + static_cast<uint32_t>(__builtin_popcount(e.w & ((1u << sh) - 1u)));
   const uint8_t t = img.tf8[L.tf8 + idx];
   if (t != kTf8Escape) return t;
   const uint32_t j = idx / kPackSize;

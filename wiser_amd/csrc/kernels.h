@@ -36,17 +36,38 @@ enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrHead0 = 16, kQueueShards
        kNumCounters = kCtrHead0 + 16 * kQueueShards };
 // per-workgroup statistics written by the segment kernel (no atomics):
 // stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
+#ifdef WSR_PROFILE
+constexpr int kStatStride = 16;  // + section cycles: 4 dequeue/setup, 5 driver, 6 dense, 7 blocks, 8 top-k, 9 total
+#else
 constexpr int kStatStride = 4;
+#endif
 enum { kErrLimit = 1, kErrCapacity = 2 };
 
-constexpr int kSegCost = 48;  // target block decodes per work item; bounds seg_blocks
+#ifndef WSR_SEG_COST
+#define WSR_SEG_COST 48
+#endif
+constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
+static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
+
+// Replay fused into the segment kernel: the workgroup that completes a
+// query's last item replays it (q_done: per-query completed items, zeroed by
+// the plan kernel).  q_done == nullptr: no fusion (separate replay launch, or
+// doc-range shard mode where events are exchanged first).
+struct FusedReplay {
+  uint32_t* q_done;
+  HitDev* hits;
+  int hit_stride;
+  int32_t* n_hits;
+};
 
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int seg_grid, hipStream_t st);
+                       int seg_grid, const FusedReplay& fr, uint32_t* item_q, uint64_t* pub,
+                       hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
-                           int grid, hipStream_t st);
+                           int grid, const FusedReplay& fr, const uint32_t* item_q,
+                           uint64_t* pub, hipStream_t st);
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);

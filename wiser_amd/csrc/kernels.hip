@@ -253,11 +253,25 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
 // Other list B is probed through its rank bitmap when it has one and is at
 // least dense_ratio times as long as the driver (then a block decode per
 // probe would mostly decode postings nobody asks for).
-constexpr float kDenseCost = 0.5f;   // plan cost of a bitmap probe round, in block decodes
+#ifndef WSR_DENSE_COST
+#define WSR_DENSE_COST 0.5f
+#endif
+constexpr float kDenseCost = WSR_DENSE_COST;   // plan cost of a bitmap probe round, in block decodes
 
 __device__ __forceinline__ bool use_dense(const IndexArgs& ix, bool has_bm, uint32_t nblk_b,
                                           uint32_t nblk_driver) {
   return has_bm && static_cast<float>(nblk_b) >= ix.dense_ratio * static_cast<float>(nblk_driver);
+}
+
+// Bit of doc a in a prefetched bitmap entry; on a hit *idx = posting index.
+__device__ __forceinline__ bool dense_hit(const IndexArgs& ix, uint32_t a, const uint2 v,
+                                          uint32_t* idx) {
+  const uint32_t rel = a - ix.doc_lo;
+  if (rel >= ix.dense_span) return false;
+  const uint32_t sh = rel % kDenseDocs;
+  if (!((v.y >> sh) & 1u)) return false;
+  *idx = v.x + __popc(v.y & ((1u << sh) - 1u));
+  return true;
 }
 
 // tf of posting `idx` of B read from the tf blob (tf >= 255): pack value, or
@@ -281,18 +295,19 @@ __device__ __forceinline__ uint32_t dense_tf_slow(const IndexArgs& ix, const Lis
   return val;
 }
 
-// Is doc a in B?  One 16-byte load; on a hit the posting's rank gives its tf.
-__device__ __forceinline__ bool dense_probe(const IndexArgs& ix, const ListDev& B, uint32_t a,
-                                            uint32_t* tf) {
+// Is doc a in B?  One 8-byte load (dense_load, issued early) and, on a hit,
+// the posting's rank gives its tf (dense_resolve).
+__device__ __forceinline__ uint2 dense_load(const IndexArgs& ix, const ListDev& B, uint32_t a,
+                                            bool act) {
   const uint32_t rel = a - ix.doc_lo;
-  if (rel >= ix.dense_span) return false;
-  const uint32_t e = rel / kDenseDocs, bit = rel - e * kDenseDocs;
-  const uint4 v = reinterpret_cast<const uint4*>(ix.dense + B.bm)[e];
-  const uint32_t w = bit >> 5, sh = bit & 31;
-  const uint32_t word = w == 0 ? v.y : (w == 1 ? v.z : v.w);
-  if (!((word >> sh) & 1u)) return false;
-  const uint32_t idx = v.x + (w > 0 ? __popc(v.y) : 0u) + (w > 1 ? __popc(v.z) : 0u) +
-                       __popc(word & ((1u << sh) - 1u));
+  const bool in = act && rel < ix.dense_span;
+  return reinterpret_cast<const uint2*>(ix.dense + B.bm)[in ? rel / kDenseDocs : 0u];
+}
+
+__device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev& B, uint32_t a,
+                                              const uint2 v, uint32_t* tf) {
+  uint32_t idx;
+  if (!dense_hit(ix, a, v, &idx)) return false;
   uint32_t t = ix.tf8[B.tf8 + idx];
   if (t == kTf8Escape) t = dense_tf_slow(ix, B, idx);
   *tf = t;
@@ -305,7 +320,7 @@ __device__ __forceinline__ bool dense_probe(const IndexArgs& ix, const ListDev& 
 // decodes) and the item count.  item_base / ev_base are filled by pass 2.
 __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                          int nq, QueryPlan* __restrict__ plan,
-                                                         uint32_t* __restrict__ counters) {
+                                                         uint32_t* __restrict__ counters, FusedReplay fr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
   const QueryIn q = qs[i];
@@ -345,6 +360,10 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     p.n_items = (nd + seg - 1) / seg;
   }
   plan[i] = p;
+  if (fr.q_done) {
+    fr.q_done[i] = 0;
+    if (p.n_items == 0) fr.n_hits[i] = 0;   // no item will replay an empty query
+  }
 }
 
 // Pass 2, one workgroup: exclusive scans of item counts and event capacities.
@@ -395,11 +414,33 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     counters[kCtrHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
 }
 
+// Pass 3, one thread per query: the item -> query map of the segment kernel
+// and the zeroed per-item thresholds (skipped when the plan did not fit).
+__global__ __launch_bounds__(256) void item_map_kernel(const QueryPlan* __restrict__ plan, int nq,
+                                                       const uint32_t* __restrict__ counters,
+                                                       uint32_t* __restrict__ item_q,
+                                                       uint64_t* __restrict__ pub) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq || (counters[kCtrError] & kErrCapacity)) return;
+  const QueryPlan p = plan[i];
+  for (uint32_t j = 0; j < p.n_items; ++j) {
+    item_q[p.item_base + j] = static_cast<uint32_t>(i);
+    if (pub) pub[p.item_base + j] = 0;
+  }
+}
+
 // -------------------------------------------------------------- segment --
 constexpr uint32_t kWin = 64;  // directory window: one entry per lane
 
 struct WaveLds {
   uint32_t mb[8][128];   // doc ids of up to 8 other-list blocks decoded side by side
+  uint32_t dtd[128];     // the driver's VInts tail block: doc ids
+  uint32_t dtt[128];     //   and tfs
+  Event evs[64];         // events buffered for one coalesced store
+  uint32_t cur[kMaxTerms];  // per other slot: cursor into its block directory
+  uint32_t roff[64];     // fused replay: segment offsets of the event stream
+  uint4 dblk[64];        // the driver's directory entries of the current segment
+  uint32_t dmeta[64];
   uint32_t tf[128];      // cooperative decode of a VInts tf tail
   uint32_t dl[128];      // distinct other-list blocks probed by the driver block
   BlockDev wblk[kWin];   // directory window of the current other list: entries cur..cur+63
@@ -504,13 +545,280 @@ __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm
   return idf * tfn;
 }
 
-__global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+// --------------------------------------------------------------- replay --
+// Events handed from one workgroup to another inside the segment kernel
+// (fused replay) travel with agent-scope relaxed atomics, which gfx950 issues
+// as sc1 (coherent across the XCDs' L2s) loads and stores; the hand-off itself
+// is a per-query counter.  No buffer_wbl2 / buffer_inv of whole L2s needed.
+__device__ __forceinline__ void store_event_coherent(Event* dst, const Event& e) {
+  uint64_t* w = reinterpret_cast<uint64_t*>(dst);
+  __hip_atomic_store(w, static_cast<uint64_t>(__double_as_longlong(e.score)), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 1, static_cast<uint64_t>(static_cast<uint32_t>(e.doc)), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool kCoherent>
+__device__ __forceinline__ void load_event(const Event* src, double* sc, int32_t* dc) {
+  if (kCoherent) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(src);
+    *sc = __longlong_as_double(static_cast<long long>(
+        __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    *dc = static_cast<int32_t>(__hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  } else {
+    *sc = src->score;
+    *dc = src->doc;
+  }
+}
+
+template <bool kCoherent>
+__device__ __forceinline__ uint32_t load_count(const uint32_t* p) {
+  if (kCoherent) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+__device__ __forceinline__ double shfl_f64(double v, uint32_t src) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __shfl(static_cast<uint32_t>(u), static_cast<int>(src), 64);
+  const uint32_t hi = __shfl(static_cast<uint32_t>(u >> 32), static_cast<int>(src), 64);
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+}
+
+// libstdc++ std::priority_queue<unique_ptr<ResultDocEntry>, vector, EntryGreater>
+// (query_processing.h:510-524): push = push_back + __push_heap, pop = __pop_heap
+// (+ __adjust_heap) + pop_back, with comp(a, b) = a.score > b.score.
+// The heap lives in the wave's registers, lane i = heap[i] (k <= 64); the
+// library's sift loops run as a scalar walk that reads single lanes
+// (v_readlane) and writes one lane by a compare-select: a few cycles per
+// step, no LDS round trips.
+struct WaveHeap {
+  double hs = 0.0;
+  int32_t hd = 0;
+  uint32_t n = 0;
+
+  __device__ __forceinline__ double at(uint32_t i) const { return readlane_f64(hs, static_cast<int>(i)); }
+  __device__ __forceinline__ int32_t doc(uint32_t i) const {
+    return static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(hd), static_cast<int>(i)));
+  }
+  __device__ __forceinline__ void set(uint32_t i, double vs, int32_t vd) {
+    if ((threadIdx.x & 63) == i) { hs = vs; hd = vd; }
+  }
+  // __push_heap(first, hole, 0, value)
+  __device__ __forceinline__ void push_hole(uint32_t hole, double vs, int32_t vd) {
+    while (hole > 0) {
+      const uint32_t parent = (hole - 1) >> 1;
+      const double ps = at(parent);
+      if (!(ps > vs)) break;
+      set(hole, ps, doc(parent));
+      hole = parent;
+    }
+    set(hole, vs, vd);
+  }
+  __device__ __forceinline__ void push(double vs, int32_t vd) { push_hole(n, vs, vd); ++n; }
+  __device__ __forceinline__ void pop() {
+    if (n > 1) {
+      const uint32_t len = n - 1;
+      const double vs = at(len);
+      const int32_t vd = doc(len);
+      // __adjust_heap(first, 0, len, value)
+      uint32_t hole = 0, child = 0;
+      while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (at(child) > at(child - 1)) --child;
+        set(hole, at(child), doc(child));
+        hole = child;
+      }
+      if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        set(hole, at(child - 1), doc(child - 1));
+        hole = child - 1;
+      }
+      push_hole(hole, vs, vd);
+    }
+    --n;
+  }
+};
+
+// Running filter over a query's event stream, in doc-id order: an event is
+// one the reference heap inserts iff fewer than k earlier events have a score
+// >= its score (the top-k multiset of any prefix is carried by its events).
+// `emit(score, doc)` is called, wave-uniformly, for exactly those events.
+struct EventFilter {
+  double pt = 0.0;    // running top-k of events, lane t = rank t
+  uint32_t pt_n = 0;
+  uint32_t k = 0;
+  // one chunk of up to 64 events, lane i = event i of the chunk
+  template <class Emit>
+  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&& emit) {
+    const uint32_t l = threadIdx.x & 63;
+    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    uint64_t cm = __ballot(valid && (pt_n < k || sc > kth));
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const double sv = readlane_f64(sc, fl);
+      const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
+      const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
+      if (pos < k) {
+        emit(sv, dv);
+        const double up = wave_shr1_f64(pt);
+        if (l > pos) pt = up;
+        else if (l == pos) pt = sv;
+        pt_n = pt_n + 1 > k ? k : pt_n + 1;
+      }
+    }
+  }
+};
+
+// The events of `nseg` segments (doc-id order), consumed as one stream in
+// chunks of 64: the segment counts are loaded 64 at a time and scanned into
+// s_off (LDS); each lane finds its event's segment by binary search there, and
+// the next chunk's loads are issued before the current chunk is filtered.
+// count_of(r) and base_of(r) give segment r's event count and first event.
+template <bool kCoherent = false, class CountOf, class BaseOf, class Emit>
+__device__ __forceinline__ void consume_stream(EventFilter& F, uint32_t nseg, CountOf count_of,
+                                               BaseOf base_of, uint32_t* s_off, Emit&& emit) {
+  const uint32_t l = threadIdx.x & 63;
+  for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
+    const uint32_t nj = min(64u, nseg - r0);
+    const uint32_t c = l < nj ? count_of(r0 + l) : 0u;
+    const uint32_t inc = wave_incl_scan(c);
+    const uint32_t total = uni(__builtin_amdgcn_readlane(inc, 63));
+    __builtin_amdgcn_wave_barrier();
+    s_off[l] = inc - c;
+    __builtin_amdgcn_wave_barrier();
+    auto load = [&](uint32_t g, double* sc, int32_t* dc) {
+      *sc = 0.0;
+      *dc = 0;
+      if (g < total) {
+        uint32_t lo = 0, len = nj;   // last j with s_off[j] <= g
+        while (len > 1) {
+          const uint32_t h = len >> 1;
+          if (s_off[lo + h] <= g) { lo += h; len -= h; } else { len = h; }
+        }
+        const Event* e = base_of(r0 + lo) + (g - s_off[lo]);
+        load_event<kCoherent>(e, sc, dc);
+      }
+    };
+    double sc, nsc;
+    int32_t dc, ndc;
+    load(l, &sc, &dc);
+    for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+      load(c0 + 64 + l, &nsc, &ndc);
+      F.step(sc, dc, c0 + l < total, emit);
+      sc = nsc;
+      dc = ndc;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// RankDoc (query_processing.h:595-602) on the restated heap, then SortHeap
+// (query_processing.h:551-562): results leave with one coalesced store.
+struct HeapSink {
+  WaveHeap H;
+  uint32_t k = 0;
+  __device__ __forceinline__ void insert(double sv, int32_t dv) {
+    if (H.n < k) H.push(sv, dv);
+    else if (sv > H.at(0)) { H.pop(); H.push(sv, dv); }
+  }
+  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t m = H.n;
+    double os = 0.0;
+    int32_t od = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+      const double ts = H.at(0);
+      const int32_t td = __builtin_amdgcn_readlane(H.hd, 0);
+      if (l == m - 1 - i) { os = ts; od = td; }
+      H.pop();
+    }
+    if (l < m) {
+      HitDev h;
+      h.doc = od;
+      h.pad = 0;
+      h.score = os;
+      out[l] = h;
+    }
+    if (l == 0) *n_out = static_cast<int32_t>(m);
+  }
+};
+
+// One wave per query: filter the events of its segments (doc-id order) and
+// apply the survivors of the filter to the heap.
+template <bool kCoherent>
+__device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
+                                             const QueryPlan* __restrict__ plan, int qi,
+                                             const Event* events, const uint32_t* ev_cnt,
+                                             HitDev* __restrict__ hits, int hit_stride,
+                                             int32_t* __restrict__ n_hits, uint32_t* s_off) {
+  const QueryPlan P = plan[qi];
+  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  EventFilter F;
+  F.k = k;
+  HeapSink sink;
+  sink.k = k;
+  consume_stream<kCoherent>(
+      F, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
+      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
+      s_off, [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+  sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
+}
+
+// out-of-line copy for the segment kernel (keeps its register allocation
+// independent of the replay code; called once per query)
+__device__ __noinline__ void replay_query_call(const QueryIn* qs, const QueryPlan* plan, int qi,
+                                               const Event* events, const uint32_t* ev_cnt,
+                                               HitDev* hits, int hit_stride, int32_t* n_hits,
+                                               uint32_t* s_off) {
+  replay_query<true>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
+}
+
+__global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
+                                                    const QueryPlan* __restrict__ plan, int nq,
+                                                    const Event* __restrict__ events,
+                                                    const uint32_t* __restrict__ ev_cnt,
+                                                    HitDev* __restrict__ hits, int hit_stride,
+                                                    int32_t* __restrict__ n_hits) {
+  __shared__ uint32_t s_off[64];
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
+}
+
+// waves per SIMD the segment kernel is compiled for (register budget)
+#ifndef WSR_SEG_WAVES
+#define WSR_SEG_WAVES 3
+#endif
+
+// Section timers of the diagnostics build (-DWSR_PROFILE): core-clock cycles
+// per workgroup, charged to the section that ends at each WSR_T.
+#ifdef WSR_PROFILE
+#define WSR_T0()                                        \
+  uint64_t prof_t = __builtin_amdgcn_s_memtime();       \
+  const uint64_t prof_start = prof_t;                   \
+  uint32_t prof_acc[5] = {0, 0, 0, 0, 0};
+#define WSR_T(i)                                                        \
+  {                                                                     \
+    const uint64_t now = __builtin_amdgcn_s_memtime();                  \
+    prof_acc[i] += static_cast<uint32_t>(now - prof_t);                 \
+    prof_t = now;                                                       \
+  }
+#else
+#define WSR_T0()
+#define WSR_T(i)
+#endif
+
+__global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
                                                      Event* __restrict__ events,
                                                      uint32_t* __restrict__ ev_cnt,
-                                                     uint32_t* __restrict__ stats) {
+                                                     uint32_t* __restrict__ stats, FusedReplay fr,
+                                                     const uint32_t* __restrict__ item_q,
+                                                     uint64_t* __restrict__ pub) {
   __shared__ WaveLds S;
+  WSR_T0()
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
@@ -536,24 +844,7 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
       ++tried;
     }
     if (item >= total) break;
-    // query of this item: last q with plan[q].item_base <= item (bases are
-    // non-decreasing), found with two wave-wide probes instead of a binary search
-    uint32_t qi;
-    {
-      const uint32_t stride = (static_cast<uint32_t>(nq) + 63) / 64;
-      const uint32_t q1 = l * stride;
-      const uint64_t m1 = __ballot(q1 < static_cast<uint32_t>(nq) && plan[q1].item_base <= item);
-      const uint32_t lo = (63 - __clzll(m1)) * stride;
-      const uint32_t hi = min(lo + stride, static_cast<uint32_t>(nq));
-      uint32_t best = lo;
-      for (uint32_t c = lo; c < hi; c += 64) {
-        const uint32_t q2 = c + l;
-        const uint64_t m2 = __ballot(q2 < hi && plan[q2].item_base <= item);
-        if (m2) best = c + 63 - __clzll(m2);
-        if (m2 != ~0ull) break;
-      }
-      qi = uni(best);
-    }
+    const uint32_t qi = uni(item_q[item]);   // written by plan_scan_kernel
     const QueryPlan P = plan[qi];
     const int32_t* qlist = qs[qi].list;
     const uint32_t r = item - P.item_base;
@@ -566,114 +857,199 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
     const uint32_t b1 = min(b0 + seg, A.nblk);
     Event* ev_out = events + P.ev_base + static_cast<uint64_t>(r) * seg * 128;
     uint32_t ev_n = 0;
+    // Score floor from the earlier segments of the query: pub[item] holds the
+    // largest k-th best score known from survivors at or before this segment
+    // (max of this segment's running k-th best and its predecessor's floor).
+    // k survivors before this segment score >= the floor, so nothing at or
+    // below it can be a heap insertion of the reference run.
+    uint64_t* my_pub = pub ? pub + item : nullptr;
+    const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
+    double last_pub = 0.0;
 
-    // per other slot: cursor into its block directory, seeded at the segment's first doc
-    uint32_t cur[kMaxTerms];
-    BlockDev blk = ix.blocks[A.blk0 + b0];
-    uint32_t meta = ix.blk_meta[A.blk0 + b0];
-    const uint32_t first_doc = b0 == 0 ? 0u : blk.prev + 1u;
+    // the driver's directory entries of this segment, one per lane (seg <= kSegCost < 64)
+    __syncthreads();
+    if (b0 + l < b1) {
+      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[A.blk0 + b0 + l];
+      S.dmeta[l] = ix.blk_meta[A.blk0 + b0 + l];
+    }
+    __syncthreads();
+    const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     bool done = false;   // some other list has no doc >= the next driver doc
+    uint32_t fo = kMaxTerms;   // first other slot in query order
 #pragma unroll
     for (uint32_t s = 0; s < kMaxTerms; ++s) {
-      cur[s] = 0;
       if (s < nt && s != d) {
         const ListDev B = ix.lists[qlist[s]];
-        cur[s] = uni(find_block(ix.blk_last + B.blk0, 0, B.nblk, first_doc));
-        if (cur[s] >= B.nblk) done = true;
+        if (fo == kMaxTerms) fo = s;
+        if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
+          // probed through its bitmap: no cursor, only its end matters
+          if (first_doc > ix.blk_last[B.blk0 + B.nblk - 1]) done = true;
+        } else {
+          const uint32_t c0 = uni(find_block(ix.blk_last + B.blk0, 0, B.nblk, first_doc));
+          if (l == 0) S.cur[s] = c0;
+          if (c0 >= B.nblk) done = true;
+        }
+      }
+    }
+    // the first other list's bitmap entries are fetched one block ahead
+    ListDev F = A;
+    bool fo_dense = false;
+    if (fo < kMaxTerms) {
+      F = ix.lists[qlist[fo]];
+      fo_dense = use_dense(ix, F.bm != kNoDense, F.nblk, A.nblk);
+    }
+    const DenseEnt* f_dense = fo_dense ? ix.dense + F.bm : ix.dense;
+    const uint8_t* f_tf8 = ix.tf8 + (fo_dense ? F.tf8 : 0ull);
+    const uint32_t f_last = fo_dense ? uni(ix.blk_last[F.blk0 + F.nblk - 1]) : 0u;
+
+    // The driver's VInts tail block (docs and tfs) is decoded into LDS once,
+    // so that the per-block loads below have the same count on every path
+    // (the compiler's vmcnt accounting then lets the next block's loads stay
+    // in flight while this block is scored).
+    bool dtail = false;
+    if (b0 < b1) {
+      const uint32_t mt = uni(S.dmeta[b1 - 1 - b0]);
+      dtail = (mt & 0xFF) == 0;
+      if (dtail) {
+        const int bi = static_cast<int>(b1 - 1 - b0);
+        const uint32_t cnt = A.tail_cnt;
+        decode_block(ix.blob + A.base + uni(S.dblk[bi].z), 0, cnt, true,
+                     uni(S.dblk[bi].x), S.dtd);
+        __syncthreads();
+        decode_block(ix.blob + A.base + uni(S.dblk[bi].w), mt >> 8, cnt,
+                     false, 0, S.dtt);
+        __syncthreads();
       }
     }
 
     double pt = 0.0;     // running top-k scores, lane t holds rank t (descending)
     uint32_t pt_n = 0;   // valid entries (uniform)
-    // raw pack words of the next driver block, fetched one block ahead
-    uint32_t nx0 = 0, nx1 = 0;
-    if ((meta & 0xFF) && b0 < b1) {
-      nx0 = pack_value(ix.blob + A.base + blk.doc_rel + 2, meta & 0xFF, 2 * l);
-      nx1 = pack_value(ix.blob + A.base + blk.doc_rel + 2, meta & 0xFF, 2 * l + 1);
-    }
+    uint32_t evb = 0;    // events buffered in S.evs (flushed 64 at a time)
 
-    for (uint32_t b = b0; b < b1 && !done; ++b) {
-      const uint32_t bn = b + 1 < b1 ? b + 1 : b;
-      const BlockDev blk_next = ix.blocks[A.blk0 + bn];
-      const uint32_t meta_next = ix.blk_meta[A.blk0 + bn];
-      const BlockDev blk_cur = blk;
-      const uint32_t meta_cur = meta;
-      blk = blk_next;
-      meta = meta_next;
+    // Stage of one driver block: doc ids, in-range flags and the loads scoring
+    // needs (doc lengths, the driver's tf, the first other list's bitmap
+    // entries), issued one block before the block is scored.  Every load is
+    // unconditional (masked lanes read index 0) so the count is static.
+    // (Loaded values are kept raw; selects on them happen where they are
+    // consumed, so the fetch itself never waits for its own loads.)
+    struct Stage {
+      uint32_t a0, a1, c0, c1, ta0, ta1;
+      bool al0, al1, ok0, ok1;
+      uint2 p0, p1;
+    };
+    // raw pack words of the driver block to decode next (issued a block ahead)
+    uint32_t nx0 = 0, nx1 = 0;
+    auto issue_words = [&](uint32_t b) __attribute__((always_inline)) {
+      const int bi = static_cast<int>(b - b0);
+      const uint32_t m = uni(S.dmeta[bi]);
+      const uint32_t rel = uni(S.dblk[bi].z);
+      const uint32_t bits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
+      nx0 = pack_value(ix.blob + A.base + rel + 2, bits, 2 * l);
+      nx1 = pack_value(ix.blob + A.base + rel + 2, bits, 2 * l + 1);
+    };
+    auto fetch = [&](uint32_t b, Stage& g) __attribute__((always_inline)) {
+      const int bi = static_cast<int>(b - b0);
+      const uint32_t prev = uni(S.dblk[bi].x);
+      const uint32_t tf_rel = uni(S.dblk[bi].w);
+      const uint32_t m = uni(S.dmeta[bi]);
       const uint32_t cnt = (b == A.nblk - 1) ? A.tail_cnt : 128u;
-      __syncthreads();
-      uint32_t a0, a1;
-      if (meta_cur & 0xFF) {
+      const bool is_tail = dtail && b == b1 - 1;
+      {
         const uint32_t x0 = nx0, x1 = nx1;
         const uint32_t sm = x0 + x1;
         const uint32_t inc = wave_incl_scan(sm);
-        a0 = blk_cur.prev + (inc - sm) + x0;
-        a1 = a0 + x1;
-      } else {
-        decode_block(ix.blob + A.base + blk_cur.doc_rel, 0, cnt, true, blk_cur.prev, S.mb[0]);
-        a0 = S.mb[0][2 * l];
-        a1 = S.mb[0][2 * l + 1];
+        const uint32_t p0 = prev + (inc - sm) + x0;
+        g.a0 = is_tail ? S.dtd[2 * l] : p0;
+        g.a1 = is_tail ? S.dtd[2 * l + 1] : p0 + x1;
       }
-      // prefetch the next driver block's pack words
-      if (b + 1 < b1 && (meta_next & 0xFF)) {
-        nx0 = pack_value(ix.blob + A.base + blk_next.doc_rel + 2, meta_next & 0xFF, 2 * l);
-        nx1 = pack_value(ix.blob + A.base + blk_next.doc_rel + 2, meta_next & 0xFF, 2 * l + 1);
+      issue_words(b + 1 < b1 ? b + 1 : b);
+      g.al0 = 2 * l < cnt && g.a0 >= ix.doc_lo && g.a0 < ix.doc_hi;
+      g.al1 = 2 * l + 1 < cnt && g.a1 >= ix.doc_lo && g.a1 < ix.doc_hi;
+      g.ok0 = g.al0 && g.a0 < ix.n_c4;
+      g.ok1 = g.al1 && g.a1 < ix.n_c4;
+      g.c0 = ix.c4[g.ok0 ? g.a0 : 0u];
+      g.c1 = ix.c4[g.ok1 ? g.a1 : 0u];
+      const uint32_t tbits = (m >> 8) ? (m >> 8) : 1u;
+      const uint8_t* tp = ix.blob + A.base + tf_rel;
+      g.ta0 = pack_tf(tp, tbits, 2 * l);
+      g.ta1 = pack_tf(tp, tbits, 2 * l + 1);
+      const uint32_t r0 = g.a0 - ix.doc_lo, r1 = g.a1 - ix.doc_lo;
+      const bool d0 = fo_dense && g.al0 && r0 < ix.dense_span;
+      const bool d1 = fo_dense && g.al1 && r1 < ix.dense_span;
+      g.p0 = reinterpret_cast<const uint2*>(f_dense)[d0 ? r0 / kDenseDocs : 0u];
+      g.p1 = reinterpret_cast<const uint2*>(f_dense)[d1 ? r1 / kDenseDocs : 0u];
+    };
+    auto flush_events = [&](uint32_t n) __attribute__((always_inline)) {
+      __builtin_amdgcn_wave_barrier();
+      if (l < n) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
+      __builtin_amdgcn_wave_barrier();
+    };
+
+    // Score driver block b (stage cs) while the loads of block b+1 (stage ns) fly.
+    auto step = [&](Stage& cs, Stage& ns, uint32_t b) __attribute__((always_inline)) {
+      // first other list through its bitmap: hits, and their tf bytes, issued
+      // before the next block's loads so that waiting for them does not wait
+      // for those
+      bool fh0 = false, fh1 = false;
+      uint32_t fi0 = 0, fi1 = 0;
+      if (fo_dense) {
+        fh0 = cs.al0 && dense_hit(ix, cs.a0, cs.p0, &fi0);
+        fh1 = cs.al1 && dense_hit(ix, cs.a1, cs.p1, &fi1);
       }
+      const uint32_t ft0 = f_tf8[fh0 ? fi0 : 0u], ft1 = f_tf8[fh1 ? fi1 : 0u];
+      const uint64_t floor_bits =
+          prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      fetch(b + 1 < b1 ? b + 1 : b, ns);
       ++n_dblk;
-      bool al0 = 2 * l < cnt && a0 >= ix.doc_lo && a0 < ix.doc_hi;
-      bool al1 = 2 * l + 1 < cnt && a1 >= ix.doc_lo && a1 < ix.doc_hi;
-      // issued now, consumed at scoring time: doc lengths and the driver's tf
-      const uint32_t c0 = al0 && a0 < ix.n_c4 ? ix.c4[a0] : 0u;
-      const uint32_t c1 = al1 && a1 < ix.n_c4 ? ix.c4[a1] : 0u;
-      uint32_t ta0 = 0, ta1 = 0;
-      {
-        const uint32_t tbits = meta_cur >> 8;
-        const uint8_t* tp = ix.blob + A.base + blk_cur.tf_rel;
-        if (tbits) {
-          ta0 = pack_tf(tp, tbits, 2 * l);
-          ta1 = pack_tf(tp, tbits, 2 * l + 1);
-        } else {
-          __syncthreads();
-          decode_block(tp, 0, cnt, false, 0, S.tf);
-          ta0 = S.tf[2 * l];
-          ta1 = S.tf[2 * l + 1];
-        }
-      }
+      const uint32_t a0 = cs.a0, a1 = cs.a1;
+      bool al0 = cs.al0, al1 = cs.al1;
+      WSR_T(1)
       double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
-      bool scored_norm = false;
-      double nrm0 = 0.0, nrm1 = 0.0;
+      const double nrm0 = length_norm(cs.ok0 ? cs.c0 : 0u, ix.avg);
+      const double nrm1 = length_norm(cs.ok1 ? cs.c1 : 0u, ix.avg);
+      const bool is_tail = dtail && b == b1 - 1;
+      const uint32_t ta0 = is_tail ? S.dtt[2 * l] : cs.ta0;
+      const uint32_t ta1 = is_tail ? S.dtt[2 * l + 1] : cs.ta1;
 
       for (uint32_t s = 0; s < nt; ++s) {
         if (__ballot(al0 || al1) == 0) break;
         const ListDev L = ix.lists[qlist[s]];
-        if (!scored_norm) {
-          nrm0 = length_norm(c0, ix.avg);
-          nrm1 = length_norm(c1, ix.avg);
-          scored_norm = true;
-        }
         if (s == d) {  // the driver's own tf
           if (al0) s0 += bm25_term(L.idf, ta0, nrm0);
           if (al1) s1 += bm25_term(L.idf, ta1, nrm1);
           continue;
         }
         const ListDev& B = L;
+        if (s == fo && fo_dense) {
+          // past B's last doc nothing later in the segment can match
+          if (__ballot((al0 && a0 > f_last) || (al1 && a1 > f_last))) done = true;
+          uint32_t t0 = ft0, t1 = ft1;
+          if (fh0 && t0 == kTf8Escape) t0 = dense_tf_slow(ix, B, fi0);
+          if (fh1 && t1 == kTf8Escape) t1 = dense_tf_slow(ix, B, fi1);
+          al0 = al0 && fh0;
+          al1 = al1 && fh1;
+          if (al0) s0 += bm25_term(B.idf, t0, nrm0);
+          if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+          WSR_T(2)
+          continue;
+        }
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
           uint32_t t0 = 0, t1 = 0;
-          const bool h0 = al0 && dense_probe(ix, B, a0, &t0);
-          const bool h1 = al1 && dense_probe(ix, B, a1, &t1);
-          // past B's last doc nothing later in the segment can match
+          const uint2 v0 = dense_load(ix, B, a0, al0);
+          const uint2 v1 = dense_load(ix, B, a1, al1);
+          const bool h0 = al0 && dense_resolve(ix, B, a0, v0, &t0);
+          const bool h1 = al1 && dense_resolve(ix, B, a1, v1, &t1);
           const uint32_t blast = ix.blk_last[B.blk0 + B.nblk - 1];
           if (__ballot((al0 && a0 > blast) || (al1 && a1 > blast))) done = true;
           al0 = h0;
           al1 = h1;
           if (al0) s0 += bm25_term(B.idf, t0, nrm0);
           if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+          WSR_T(2)
           continue;
         }
         const uint32_t* last = ix.blk_last + B.blk0;
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kMaxTerms; ++u) if (u == s) c = cur[u];
+        const uint32_t c = uni(S.cur[s]);
         // directory window cur..cur+63 into LDS (one coalesced round)
         const uint32_t wn = min(kWin, B.nblk - c);
         uint32_t wl = 0;
@@ -779,17 +1155,20 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
         if (al0) s0 += bm25_term(B.idf, t0, nrm0);
         if (al1) s1 += bm25_term(B.idf, t1, nrm1);
         // advance the cursor to the furthest block queried (docs only increase)
-#pragma unroll
-        for (uint32_t u = 0; u < kMaxTerms; ++u)
-          if (u == s && nd && jlast > cur[u]) cur[u] = jlast;
+        if (l == 0 && nd && jlast > c) S.cur[s] = jlast;
+        WSR_T(3)
       }
-      if (__ballot(al0 || al1) == 0) continue;
+      if (__ballot(al0 || al1) == 0) return;
       n_surv += __popcll(__ballot(al0)) + __popcll(__ballot(al1));
 
-      // running top-k: candidates beat the k-th best at block start
+      // running top-k: candidates beat the k-th best at block start and the
+      // floor of the earlier segments (scores are > 0, so bits order as values)
+      const double flo = __longlong_as_double(static_cast<long long>(
+          (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
+          uni(static_cast<uint32_t>(floor_bits))));
       const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-      uint64_t cm0 = __ballot(al0 && (pt_n < k || s0 > kth));
-      uint64_t cm1 = __ballot(al1 && (pt_n < k || s1 > kth));
+      uint64_t cm0 = __ballot(al0 && s0 > flo && (pt_n < k || s0 > kth));
+      uint64_t cm1 = __ballot(al1 && s1 > flo && (pt_n < k || s1 > kth));
       while (cm0 | cm1) {
         const int fl = __builtin_ctzll(cm0 | cm1);
         const bool second = !((cm0 >> fl) & 1);
@@ -803,158 +1182,95 @@ __global__ __launch_bounds__(64, 5) void segment_kernel(IndexArgs ix, const Quer
             e.score = sv;
             e.doc = static_cast<int32_t>(dv);
             e.pad = 0;
-            ev_out[ev_n] = e;
+            S.evs[evb] = e;
           }
           ++ev_n;
+          if (++evb == 64) { flush_events(64); evb = 0; }
           const double up = wave_shr1_f64(pt);
           if (l > pos) pt = up;
           else if (l == pos) pt = sv;
           pt_n = pt_n + 1 > k ? k : pt_n + 1;
         }
       }
+      if (my_pub) {
+        const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+        const double pv = kn > flo ? kn : flo;
+        if (pv > last_pub) {
+          if (l == 0)
+            __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pv)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last_pub = pv;
+        }
+      }
+      WSR_T(4)
+    };
+
+    Stage sa, sb;
+    if (b0 < b1) {
+      issue_words(b0);
+      fetch(b0, sa);
     }
-    if (l == 0) ev_cnt[item] = ev_n;
+    WSR_T(0)
+    for (uint32_t b = b0; b < b1 && !done; b += 2) {
+      step(sa, sb, b);
+      if (b + 1 >= b1 || done) break;
+      step(sb, sa, b + 1);
+    }
+    if (evb) flush_events(evb);
+    // Re-filter this segment's events against the earlier segments' floor as
+    // it stands now (it only grows, and every value it takes is backed by k
+    // survivors before this segment), keeping the doc order.
+    if (prev_pub && ev_n > 0) {
+      const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double fl_end = __longlong_as_double(static_cast<long long>(
+          (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
+          uni(static_cast<uint32_t>(fb))));
+      uint32_t kept = 0;
+      for (uint32_t c = 0; c < ev_n; c += 64) {
+        double sc = 0.0;
+        int32_t dc = 0;
+        const bool in = c + l < ev_n;
+        if (in) load_event<true>(&ev_out[c + l], &sc, &dc);
+        const bool keep = in && sc > fl_end;
+        const uint64_t km = __ballot(keep);
+        if (keep) {
+          Event e;
+          e.score = sc;
+          e.doc = dc;
+          e.pad = 0;
+          store_event_coherent(&ev_out[kept + __popcll(km & lt)], e);
+        }
+        kept += __popcll(km);
+      }
+      ev_n = kept;
+    }
+    if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fr.q_done) {
+      // the workgroup that finishes a query's last item replays the query:
+      // its coherent event stores complete before the counter moves, and the
+      // replay reads the other items' events with coherent loads
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      uint32_t old = 0;
+      if (l == 0)
+        old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = uni(old);
+      if (old + 1 == P.n_items)
+        replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
+                          fr.n_hits, S.roff);
+    }
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
     stats[blockIdx.x * kStatStride + 0] = n_surv;
     stats[blockIdx.x * kStatStride + 1] = n_dblk;
     stats[blockIdx.x * kStatStride + 2] = n_oblk;
+#ifdef WSR_PROFILE
+    for (int i = 0; i < 5; ++i) stats[blockIdx.x * kStatStride + 4 + i] = prof_acc[i];
+    stats[blockIdx.x * kStatStride + 9] =
+        static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - prof_start);
+#endif
   }
-}
-
-// --------------------------------------------------------------- replay --
-// libstdc++ std::priority_queue<unique_ptr<ResultDocEntry>, vector, EntryGreater>
-// (query_processing.h:510-524): push = push_back + __push_heap, pop = __pop_heap
-// (+ __adjust_heap) + pop_back, with comp(a, b) = a.score > b.score.
-struct HeapView {
-  double* sc;
-  int32_t* dc;
-  uint32_t stride;
-  __device__ double& s(uint32_t i) { return sc[i * stride]; }
-  __device__ int32_t& d(uint32_t i) { return dc[i * stride]; }
-  __device__ void push_hole(uint32_t hole, uint32_t top, double vs, int32_t vd) {
-    uint32_t parent = hole ? (hole - 1) / 2 : 0;
-    while (hole > top && s(parent) > vs) {
-      s(hole) = s(parent); d(hole) = d(parent);
-      hole = parent;
-      parent = hole ? (hole - 1) / 2 : 0;
-    }
-    s(hole) = vs; d(hole) = vd;
-  }
-  __device__ void push(uint32_t& n, double vs, int32_t vd) { push_hole(n, 0, vs, vd); ++n; }
-  __device__ void pop(uint32_t& n) {
-    if (n > 1) {
-      const uint32_t len = n - 1;
-      const double vs = s(len); const int32_t vd = d(len);
-      s(len) = s(0); d(len) = d(0);
-      // __adjust_heap(first, 0, len, value)
-      uint32_t hole = 0, child = 0;
-      while (child < (len - 1) / 2) {
-        child = 2 * (child + 1);
-        if (s(child) > s(child - 1)) --child;
-        s(hole) = s(child); d(hole) = d(child);
-        hole = child;
-      }
-      if ((len & 1) == 0 && child == (len - 2) / 2) {
-        child = 2 * (child + 1);
-        s(hole) = s(child - 1); d(hole) = d(child - 1);
-        hole = child - 1;
-      }
-      push_hole(hole, 0, vs, vd);
-    }
-    --n;
-  }
-};
-
-// Running filter over a query's event stream, in doc-id order: an event is
-// one the reference heap inserts iff fewer than k earlier events have a score
-// >= its score (the top-k multiset of any prefix is carried by its events).
-// `emit(score, doc)` is called, wave-uniformly, for exactly those events.
-struct EventFilter {
-  double pt = 0.0;    // running top-k of events, lane t = rank t
-  uint32_t pt_n = 0;
-  uint32_t k = 0;
-  template <class Emit>
-  __device__ __forceinline__ void consume(const Event* ev, uint32_t ne, Emit&& emit) {
-    const uint32_t l = threadIdx.x & 63;
-    for (uint32_t c = 0; c < ne; c += 64) {
-      const uint32_t i = c + l;
-      const bool valid = i < ne;
-      double sc = 0.0;
-      int32_t dc = 0;
-      if (valid) { sc = ev[i].score; dc = ev[i].doc; }
-      const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-      uint64_t cm = __ballot(valid && (pt_n < k || sc > kth));
-      while (cm) {
-        const int fl = __builtin_ctzll(cm);
-        cm &= cm - 1;
-        const double sv = readlane_f64(sc, fl);
-        const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
-        const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
-        if (pos < k) {
-          emit(sv, dv);
-          const double up = wave_shr1_f64(pt);
-          if (l > pos) pt = up;
-          else if (l == pos) pt = sv;
-          pt_n = pt_n + 1 > k ? k : pt_n + 1;
-        }
-      }
-    }
-  }
-};
-
-// RankDoc (query_processing.h:595-602) on the restated heap, then SortHeap
-// (query_processing.h:551-562).  Lane 0 owns the heap.
-struct HeapSink {
-  HeapView H;
-  uint32_t n = 0, k = 0;
-  __device__ __forceinline__ void insert(double sv, int32_t dv) {
-    if ((threadIdx.x & 63) == 0) {
-      uint32_t m = n;
-      if (m < k) H.push(m, sv, dv);
-      else if (sv > H.s(0)) { H.pop(m); H.push(m, sv, dv); }
-    }
-    n = n < k ? n + 1 : n;
-  }
-  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
-    if ((threadIdx.x & 63) == 0) {
-      const uint32_t m = n;
-      for (uint32_t i = 0; i < m; ++i) {
-        HitDev h;
-        h.doc = H.d(0);
-        h.pad = 0;
-        h.score = H.s(0);
-        out[m - 1 - i] = h;
-        H.pop(n);
-      }
-      *n_out = static_cast<int32_t>(m);
-    }
-  }
-};
-
-// One wave per query: filter the events of its segments (doc-id order) and
-// apply the survivors of the filter to the heap.
-__global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
-                                                    const QueryPlan* __restrict__ plan, int nq,
-                                                    const Event* __restrict__ events,
-                                                    const uint32_t* __restrict__ ev_cnt,
-                                                    HitDev* __restrict__ hits, int hit_stride,
-                                                    int32_t* __restrict__ n_hits) {
-  __shared__ double s_sc[kMaxK];
-  __shared__ int32_t s_dc[kMaxK];
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const QueryPlan P = plan[qi];
-  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
-  EventFilter F;
-  F.k = k;
-  HeapSink sink{HeapView{s_sc, s_dc, 1}, 0, k};
-  for (uint32_t r = 0; r < P.n_items; ++r) {
-    const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
-    F.consume(ev, uni(ev_cnt[P.item_base + r]), [&](double sv, int32_t dv) { sink.insert(sv, dv); });
-  }
-  sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
 }
 
 // ------------------------------------------------------ doc-range shards --
@@ -969,18 +1285,20 @@ __global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restr
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const QueryPlan P = plan[qi];
+  __shared__ uint32_t s_off[64];
   EventFilter F;
   F.k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
   Event* out = events + P.ev_base;
   uint32_t n = 0;
-  for (uint32_t r = 0; r < P.n_items; ++r) {
-    const Event* ev = events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128;
-    // writes land at index n <= index being read: a chunk is read before any write
-    F.consume(ev, uni(ev_cnt[P.item_base + r]), [&](double sv, int32_t dv) {
-      if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
-      ++n;
-    });
-  }
+  // writes land at out[n], below the address of every event not yet read
+  // (event g of the stream sits at or above out + g, and n <= g)
+  consume_stream(
+      F, P.n_items, [&](uint32_t r) { return ev_cnt[P.item_base + r]; },
+      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
+      s_off, [&](double sv, int32_t dv) {
+        if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
+        ++n;
+      });
   if ((threadIdx.x & 63) == 0) scount[qi] = static_cast<int32_t>(n);
 }
 
@@ -1038,40 +1356,45 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
                                                           const Event* __restrict__ recv,
                                                           HitDev* __restrict__ hits, int hit_stride,
                                                           int32_t* __restrict__ n_hits) {
-  __shared__ double s_sc[kMaxK];
-  __shared__ int32_t s_dc[kMaxK];
+  __shared__ uint32_t s_off[64];
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const int gq = q0 + qi;
   const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
   EventFilter F;
   F.k = k;
-  HeapSink sink{HeapView{s_sc, s_dc, 1}, 0, k};
-  for (int g = 0; g < n_shards; ++g) {
-    const Event* ev = recv + rbase[g] + roff[static_cast<int64_t>(g) * nq + qi];
-    F.consume(ev, uni(static_cast<uint32_t>(rcount[static_cast<int64_t>(g) * nq + qi])),
-              [&](double sv, int32_t dv) { sink.insert(sv, dv); });
-  }
+  HeapSink sink;
+  sink.k = k;
+  consume_stream(
+      F, static_cast<uint32_t>(n_shards),
+      [&](uint32_t g) { return static_cast<uint32_t>(rcount[static_cast<int64_t>(g) * nq + qi]); },
+      [&](uint32_t g) { return recv + rbase[g] + roff[static_cast<int64_t>(g) * nq + qi]; }, s_off,
+      [&](double sv, int32_t dv) { sink.insert(sv, dv); });
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int seg_grid, hipStream_t st) {
+                       int seg_grid, const FusedReplay& fr, uint32_t* item_q, uint64_t* pub,
+                       hipStream_t st) {
   if (nq > 0)
     hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
-                       counters);
+                       counters, fr);
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
                      item_capacity, static_cast<uint32_t>(seg_grid));
+  if (nq > 0)
+    hipLaunchKernelGGL(item_map_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, plan, nq, counters,
+                       item_q, pub);
   return hipGetLastError();
 }
 
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
-                           int grid, hipStream_t st) {
+                           int grid, const FusedReplay& fr, const uint32_t* item_q,
+                           uint64_t* pub, hipStream_t st) {
   hipLaunchKernelGGL(segment_kernel, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
-                     events, ev_cnt, stats);
+                     events, ev_cnt, stats, fr, item_q, pub);
   return hipGetLastError();
 }
 
