@@ -9,7 +9,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -m pytest tests -x -q -m gpu > "$O/pytest_gpu.log" 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 echo "pytest gpu ok"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1
 echo "smoke ok"
