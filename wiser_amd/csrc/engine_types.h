@@ -58,7 +58,7 @@ struct QueryPlan {
   uint32_t item_base;   // first work item of this query
   uint32_t n_items;     // segments (0 for empty queries)
   uint32_t seg_blocks;  // driver blocks per segment
-  uint32_t driver;      // query slot of the shortest list
+  uint32_t driver;      // query slot of the shortest list (bits 0-7) | item cost bucket << 8
   uint64_t ev_base;     // first event slot (capacity = driver blocks * 128)
 };
 static_assert(sizeof(QueryPlan) == 24, "QueryPlan layout");

@@ -48,6 +48,10 @@ enum { kErrLimit = 1, kErrCapacity = 2 };
 #endif
 constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
+// item cost classes for the longest-first queue order (QueryPlan::driver >> 8);
+// kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
+constexpr int kCostBuckets = 8;
+constexpr float kItemFixedCost = 4.0f;
 
 // Replay fused into the segment kernel: the workgroup that completes a
 // query's last item replays it (q_done: per-query completed items, zeroed by

@@ -355,7 +355,13 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
                                                 : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
     uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
     seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
-    p.driver = d;
+    // cost class of one item (log2 of its block decodes, plus a fixed part
+    // for the per-item setup): the queue hands out heavy items first
+    const float item_cost = static_cast<float>(seg) * cost + kItemFixedCost;
+    const uint32_t ic = static_cast<uint32_t>(item_cost);
+    uint32_t bucket = 31u - __clz(ic > 1u ? ic : 1u);
+    bucket = bucket >= kCostBuckets ? kCostBuckets - 1 : bucket;
+    p.driver = d | (bucket << 8);
     p.seg_blocks = seg;
     p.n_items = (nd + seg - 1) / seg;
   }
@@ -366,46 +372,80 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
   }
 }
 
-// Pass 2, one workgroup: exclusive scans of item counts and event capacities.
+// Pass 2, one workgroup of 1024: event capacities are scanned in query order;
+// items are numbered bucket-major, heaviest cost bucket first (query order
+// inside a bucket, a query's items consecutive), so the persistent waves take
+// the long items first and the short ones fill the tail (longest-first list
+// scheduling).
 __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __restrict__ plan,
                                                          uint32_t* __restrict__ counters,
                                                          uint64_t ev_capacity, uint32_t item_capacity,
                                                          uint32_t seg_grid) {
-  __shared__ uint32_t s_items[1024];
+  constexpr int kWaves = 1024 / 64;
   __shared__ uint64_t s_cap[1024];
+  __shared__ uint32_t s_bt[kCostBuckets][kWaves];   // per bucket, per wave item totals
   const int t = threadIdx.x, T = blockDim.x;
+  const uint32_t wv = t / 64, l = t & 63;
   const int per = (nq + T - 1) / T;
   const int q0 = t * per, q1 = min(nq, q0 + per);
-  uint32_t items = 0;
+  uint32_t cnt[kCostBuckets];
+#pragma unroll
+  for (int bk = 0; bk < kCostBuckets; ++bk) cnt[bk] = 0;
   uint64_t cap = 0;
   for (int i = q0; i < q1; ++i) {
     const QueryPlan p = plan[i];
-    items += p.n_items;
+    const uint32_t bk = p.driver >> 8;
+#pragma unroll
+    for (int b = 0; b < kCostBuckets; ++b) cnt[b] += bk == static_cast<uint32_t>(b) ? p.n_items : 0u;
     cap += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
-  s_items[t] = items;
   s_cap[t] = cap;
+  uint32_t ex[kCostBuckets];   // items of this bucket in lower lanes of the wave
+#pragma unroll
+  for (int b = 0; b < kCostBuckets; ++b) {
+    const uint32_t inc = wave_incl_scan(cnt[b]);
+    ex[b] = inc - cnt[b];
+    if (l == 63) s_bt[b][wv] = inc;
+  }
   __syncthreads();
-  for (int d = 1; d < T; d <<= 1) {  // Hillis-Steele over the thread totals
-    uint32_t a = 0; uint64_t c = 0;
-    if (t >= d) { a = s_items[t - d]; c = s_cap[t - d]; }
+  for (int d = 1; d < T; d <<= 1) {  // Hillis-Steele over the thread capacities
+    uint64_t c = 0;
+    if (t >= d) c = s_cap[t - d];
     __syncthreads();
-    s_items[t] += a; s_cap[t] += c;
+    s_cap[t] += c;
     __syncthreads();
   }
-  uint32_t ib = s_items[t] - items;
+  // base of every bucket (heavier buckets first) and of this wave inside it
+  uint32_t ib[kCostBuckets];
+  uint32_t run = 0;
+#pragma unroll
+  for (int b = kCostBuckets - 1; b >= 0; --b) {
+    uint32_t below = 0, tot = 0;
+    for (uint32_t w = 0; w < static_cast<uint32_t>(kWaves); ++w) {
+      const uint32_t v = s_bt[b][w];
+      below += w < wv ? v : 0u;
+      tot += v;
+    }
+    ib[b] = run + below + ex[b];
+    run += tot;
+  }
+  const uint32_t total_items = run;
   uint64_t cb = s_cap[t] - cap;
   for (int i = q0; i < q1; ++i) {
     QueryPlan& p = plan[i];
-    p.item_base = ib;
+    const uint32_t bk = p.driver >> 8;
+    uint32_t base = 0;
+#pragma unroll
+    for (int b = 0; b < kCostBuckets; ++b)
+      if (bk == static_cast<uint32_t>(b)) { base = ib[b]; ib[b] += p.n_items; }
+    p.item_base = base;
     p.ev_base = cb;
-    ib += p.n_items;
     cb += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
   if (t == T - 1) {
-    const bool fits = s_cap[t] <= ev_capacity && s_items[t] <= item_capacity;
+    const bool fits = s_cap[t] <= ev_capacity && total_items <= item_capacity;
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
-    counters[kCtrItems] = fits ? s_items[t] : 0u;  // never write past the workspace
+    counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
     counters[kCtrEvCap] = static_cast<uint32_t>(s_cap[t] > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap[t]);
   }
   // Work queue: shard s serves items s, s+8, s+16, ...; workgroup w starts on
@@ -436,7 +476,8 @@ struct WaveLds {
   uint32_t mb[8][128];   // doc ids of up to 8 other-list blocks decoded side by side
   uint32_t dtd[128];     // the driver's VInts tail block: doc ids
   uint32_t dtt[128];     //   and tfs
-  Event evs[64];         // events buffered for one coalesced store
+  Event evs[128];        // events buffered for coalesced stores
+  double norm[256];      // Bm25Similarity cache_ (host table, scoring.h:85-90)
   uint32_t cur[kMaxTerms];  // per other slot: cursor into its block directory
   uint32_t roff[64];     // fused replay: segment offsets of the event stream
   uint4 dblk[64];        // the driver's directory entries of the current segment
@@ -809,6 +850,275 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
 #define WSR_T(i)
 #endif
 
+// ------------------------------------------------- lean bitmap segment --
+// Byte loads of the pipeline are whole aligned dwords, kept raw until the
+// consuming stage extracts the byte (an extraction next to the load would make
+// the loop wait for it in the iteration that issued it).
+__device__ __forceinline__ uint32_t byte_word(const uint8_t* p, uint32_t* sh) {
+  *sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3) << 3;
+  return *reinterpret_cast<const uint32_t*>(__builtin_align_down(p, 4));
+}
+
+// Three dwords covering values 2l and 2l+1 of a 128-value pack whose data
+// starts at d (bit width b <= 32): one load per lane for both values.
+__device__ __forceinline__ void pair_words(const uint8_t* d, uint32_t b, uint32_t l, uint32_t& w0,
+                                           uint32_t& w1, uint32_t& w2, uint32_t& sh) {
+  const uint32_t bit = 2 * l * b;
+  const uint8_t* a = d + (bit >> 3);
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a) & 3);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(a, 4));
+  w0 = w[0];
+  w1 = w[1];
+  w2 = w[2];
+  sh = (mis << 3) + (bit & 7);
+}
+
+__device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sh,
+                                            uint32_t b, uint32_t& v0, uint32_t& v1) {
+  const uint32_t mask = b >= 32 ? 0xFFFFFFFFu : ((1u << b) - 1u);
+  v0 = __builtin_amdgcn_alignbit(w1, w0, sh) & mask;   // sh <= 31
+  const uint32_t s2 = sh + b;                           // <= 63
+  const bool up = s2 >= 32;
+  v1 = __builtin_amdgcn_alignbit(up ? w2 : w1, up ? w1 : w0, s2 & 31u) & mask;
+}
+
+// Segment of an item whose other lists all carry rank bitmaps (the common
+// case: a short driver against long lists).  The driver's blocks stream
+// through a software pipeline, one block per stage and iteration j:
+//   C(j-2)  compaction: the survivors of block j-2 (docs present in the most
+//           selective other list O1) are appended, in doc order, to a queue in
+//           LDS with their doc-length code and both tfs; every full 64 are
+//           scored one per lane (all query terms, query order, the further
+//           other lists probed here) and fed to the running top-k;
+//   H(j-1)  O1's bitmap words of block j-1 give hits and posting ranks; the
+//           hits' 1-byte tfs are loaded;
+//   D(j)    block j's doc ids are unpacked and prefix-summed; O1's bitmap
+//           words, the doc-length bytes and the driver's tf words are loaded;
+//   W(j+1)  the doc-id pack words of block j+1 (and the score floor) are loaded.
+// Every load is issued unconditionally (drained stages read index 0) so each
+// stage waits only for loads issued one iteration earlier.  Scoring one
+// survivor per lane instead of two postings per lane keeps the f64 work
+// proportional to the survivors.
+__device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, const int32_t* qlist,
+                                             uint32_t nt, uint32_t d, uint32_t o1, uint32_t k,
+                                             const ListDev& A, uint32_t b0, uint32_t b1, bool dtail,
+                                             uint32_t min_last, const uint64_t* prev_pub,
+                                             uint64_t* my_pub, Event* ev_out, uint32_t& ev_n,
+                                             uint32_t& evb, double& pt, uint32_t& pt_n,
+                                             double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt();
+  const ListDev O = ix.lists[qlist[o1]];
+  const uint2* o_bm = reinterpret_cast<const uint2*>(ix.dense + O.bm);
+  const uint8_t* o_tf8 = ix.tf8 + O.tf8;
+  const uint32_t lo = ix.doc_lo, span = ix.dense_span;
+  const uint32_t hi_rel = ix.doc_hi - ix.doc_lo;   // docs a with a - lo < hi_rel are in the image
+  const double idf_d = A.idf, idf_o = O.idf;
+  uint32_t* qdoc = &S.mb[0][0];     // survivor queue (ring of 256, reuses the decode area)
+  uint32_t* qc4 = qdoc + 256;
+  uint32_t* qtd = qdoc + 512;
+  uint32_t* qto = qdoc + 768;       // tf byte, or 0x80000000 | posting index when escaped
+  uint32_t qhead = 0, qtail = 0;
+  uint32_t bend = b1;
+  uint64_t floor_bits = 0;
+  // the floor is loaded every iteration (a fixed load count per iteration);
+  // without an earlier segment a valid global word is read and ignored
+  const uint64_t* floor_src = prev_pub ? prev_pub : reinterpret_cast<const uint64_t*>(ix.lists);
+  const bool has_floor = prev_pub != nullptr;
+
+  // buffered events (up to 127) to ev_out, after a chunk's top-k loop so the
+  // loop itself holds no stores
+  auto flush = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
+    if (l + 64 < evb) store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[l + 64]);
+    __builtin_amdgcn_wave_barrier();
+    evb = 0;
+  };
+  // score survivors qhead .. qhead+n (n <= 64, lane = doc order) and run the top-k
+  auto score_chunk = [&](uint32_t n) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t e = (qhead + l) & 255u;
+    bool alive = l < n;
+    const uint32_t doc = qdoc[e];
+    const uint32_t c4 = qc4[e];
+    const uint32_t td = qtd[e];
+    uint32_t to = qto[e];
+    __builtin_amdgcn_wave_barrier();
+    qhead += n;
+    if (__ballot(alive && (to & 0x80000000u))) {
+      if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
+    }
+    const double norm = S.norm[c4 & 255u];
+    double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
+    for (uint32_t s = 0; s < nt; ++s) {
+      if (s == d) {
+        sc += bm25_term(idf_d, alive ? td : 0u, norm);
+      } else if (s == o1) {
+        sc += bm25_term(idf_o, alive ? to : 0u, norm);
+      } else {
+        const ListDev B = ix.lists[qlist[s]];
+        uint32_t t = 0;
+        const uint2 v = dense_load(ix, B, doc, alive);
+        alive = alive && dense_resolve(ix, B, doc, v, &t);
+        if (__ballot(alive) == 0) break;
+        sc += bm25_term(B.idf, alive ? t : 0u, norm);
+      }
+    }
+    const uint64_t am = __ballot(alive);
+    if (am == 0) return;
+    n_surv += __popcll(am);
+    // running top-k: candidates beat the k-th best so far and the floor of the
+    // query's earlier segments (scores are > 0, so bits order as values)
+    const uint64_t fb = has_floor ? floor_bits : 0ull;
+    const double flo = __longlong_as_double(static_cast<long long>(
+        (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
+        uni(static_cast<uint32_t>(fb))));
+    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    uint64_t cm = __ballot(alive && sc > flo && (pt_n < k || sc > kth));
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const double sv = readlane_f64(sc, fl);
+      const uint32_t dv = __builtin_amdgcn_readlane(doc, fl);
+      const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
+      if (pos < k) {
+        if (l == 0) {
+          Event ev;
+          ev.score = sv;
+          ev.doc = static_cast<int32_t>(dv);
+          ev.pad = 0;
+          S.evs[evb] = ev;
+        }
+        ++ev_n;
+        ++evb;
+        const double up = wave_shr1_f64(pt);
+        if (l > pos) pt = up;
+        else if (l == pos) pt = sv;
+        pt_n = pt_n + 1 > k ? k : pt_n + 1;
+      }
+    }
+    if (evb >= 64) flush();
+    if (my_pub) {
+      const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+      const double pv = kn > flo ? kn : flo;
+      if (pv > last_pub) {
+        if (l == 0)
+          __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pv)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_pub = pv;
+      }
+    }
+  };
+
+  // Pipeline registers, in two alternating sets: iteration j reads set X
+  // (written by iteration j-1) and writes set Y, then j+1 runs with the roles
+  // swapped.  No register holding an in-flight load is ever copied (a copy
+  // would wait for the load).
+  struct Regs {
+    uint32_t w0 = 0, w1 = 0, w2 = 0, wsh = 0;      // doc-id pack words of the next block
+    uint64_t floor = 0;                            // score floor word
+    // D: a decoded block
+    uint32_t da0 = 0, da1 = 0, dc0 = 0, dc1 = 0, dcs0 = 0, dcs1 = 0;   // docs, length words
+    uint32_t dt0 = 0, dt1 = 0, dt2 = 0, dtsh = 0, dtb = 1;             // driver tf words
+    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);              // O1 bitmap words
+    bool dok0 = false, dok1 = false, dtl = false;
+    // H: O1 hits of the block decoded one iteration earlier
+    uint32_t hf0 = 0, hf1 = 0, hfs0 = 0, hfs1 = 0, hx0 = 0, hx1 = 0;   // tf byte words, ranks
+    bool hh0 = false, hh1 = false;
+  };
+  Regs RA, RB;
+
+  auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
+    const uint32_t bi = b < b1 ? b - b0 : 0u;
+    const uint32_t m = uni(S.dmeta[bi]);
+    const uint32_t bits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
+    pair_words(ix.blob + A.base + uni(S.dblk[bi].z) + 2, bits, l, Y.w0, Y.w1, Y.w2, Y.wsh);
+    Y.floor = __hip_atomic_load(floor_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
+    // W(j+1): issued first, so it has a whole iteration to arrive
+    issue_words(j + 1, Y);
+    // C(j-2): compaction of block j-2: its hits are in X (H of iteration
+    // j-1), its decoded fields still in Y (D of iteration j-2; D(j) below
+    // overwrites them only after this stage)
+    if (j >= b0 + 2) {
+      floor_bits = X.floor;
+      uint32_t td0, td1;
+      pair_values(Y.dt0, Y.dt1, Y.dt2, Y.dtsh, Y.dtb, td0, td1);
+      if (Y.dtl) { td0 = S.dtt[2 * l]; td1 = S.dtt[2 * l + 1]; }
+      const uint32_t f0 = (X.hf0 >> X.hfs0) & 0xFFu, f1 = (X.hf1 >> X.hfs1) & 0xFFu;
+      const uint32_t to0 = f0 == kTf8Escape ? (0x80000000u | X.hx0) : f0;
+      const uint32_t to1 = f1 == kTf8Escape ? (0x80000000u | X.hx1) : f1;
+      const uint32_t c0 = (Y.dc0 >> Y.dcs0) & 0xFFu, c1 = (Y.dc1 >> Y.dcs1) & 0xFFu;
+      const uint64_t m0 = __ballot(X.hh0), m1 = __ballot(X.hh1);
+      const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
+      const uint32_t r1 = r0 + (X.hh0 ? 1u : 0u);
+      // branch-free: misses write the free slot before the queue head (at
+      // most 63 + 128 entries are live, so it is never one of them)
+      const uint32_t spare = (qhead - 1u) & 255u;
+      const uint32_t e0 = X.hh0 ? (r0 & 255u) : spare, e1 = X.hh1 ? (r1 & 255u) : spare;
+      qdoc[e0] = Y.da0; qc4[e0] = c0; qtd[e0] = td0; qto[e0] = to0;
+      qdoc[e1] = Y.da1; qc4[e1] = c1; qtd[e1] = td1; qto[e1] = to1;
+      qtail += __popcll(m0) + __popcll(m1);
+      // (at most two full chunks: fewer than 64 + 128 entries are queued)
+      if (qtail - qhead >= 64) score_chunk(64);
+      if (qtail - qhead >= 64) score_chunk(64);
+    }
+    // H(j-1): O1 hits of block j-1 (decoded into X), written to Y
+    {
+      const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
+      const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
+      const bool h0 = X.dok0 && q0 < span && ((X.de0.y >> s0) & 1u);
+      const bool h1 = X.dok1 && q1 < span && ((X.de1.y >> s1) & 1u);
+      Y.hx0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
+      Y.hx1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
+      Y.hf0 = byte_word(o_tf8 + (h0 ? Y.hx0 : 0u), &Y.hfs0);
+      Y.hf1 = byte_word(o_tf8 + (h1 ? Y.hx1 : 0u), &Y.hfs1);
+      Y.hh0 = h0; Y.hh1 = h1;
+    }
+    // D(j): decode block j from X's words into Y, issue its loads
+    {
+      const bool live = j < bend;
+      const uint32_t bi = live ? j - b0 : 0u;
+      const uint32_t prev = uni(S.dblk[bi].x);
+      const uint32_t m = uni(S.dmeta[bi]);
+      const uint32_t bits = (m & 0xFF) ? (m & 0xFF) : 1u;
+      const uint32_t cnt = live ? ((j == A.nblk - 1) ? A.tail_cnt : 128u) : 0u;
+      uint32_t x0, x1;
+      pair_values(X.w0, X.w1, X.w2, X.wsh, bits, x0, x1);
+      const uint32_t sm = x0 + x1;
+      const uint32_t inc = wave_incl_scan(sm);
+      uint32_t a0 = prev + (inc - sm) + x0;
+      uint32_t a1 = a0 + x1;
+      const bool tl = live && dtail && j == b1 - 1;
+      if (tl) { a0 = S.dtd[2 * l]; a1 = S.dtd[2 * l + 1]; }
+      const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
+      const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
+      const bool in0 = ok0 && a0 - lo < span, in1 = ok1 && a1 - lo < span;
+      Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
+      Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
+      Y.dc0 = byte_word(ix.c4 + ((ok0 && a0 < ix.n_c4) ? a0 : 0u), &Y.dcs0);
+      Y.dc1 = byte_word(ix.c4 + ((ok1 && a1 < ix.n_c4) ? a1 : 0u), &Y.dcs1);
+      Y.dtb = (m >> 8) ? (m >> 8) : 1u;
+      pair_words(ix.blob + A.base + uni(S.dblk[bi].w) + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, Y.dtsh);
+      Y.da0 = a0; Y.da1 = a1; Y.dok0 = ok0; Y.dok1 = ok1; Y.dtl = tl;
+      if (live) ++n_dblk;
+      // past the smallest last doc of the other lists nothing later can match
+      if (live && __ballot((ok0 && a0 > min_last) || (ok1 && a1 > min_last))) bend = j + 1;
+    }
+  };
+  if (b0 < b1) issue_words(b0, RA);
+  for (uint32_t j = b0; j < bend + 2; j += 2) {
+    body(RA, RB, j);
+    if (j + 1 >= bend + 2) break;
+    body(RB, RA, j + 1);
+  }
+  if (qtail != qhead) score_chunk(qtail - qhead);
+  if (evb) flush();
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
@@ -820,6 +1130,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
   __shared__ WaveLds S;
   WSR_T0()
   const uint32_t l = threadIdx.x & 63;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) S.norm[l + 64 * i] = ix.cache[l + 64 * i];
   const uint64_t lt = lanemask_lt();
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
@@ -848,7 +1160,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     const QueryPlan P = plan[qi];
     const int32_t* qlist = qs[qi].list;
     const uint32_t r = item - P.item_base;
-    const uint32_t d = uni(P.driver);
+    const uint32_t d = uni(P.driver & 0xFFu);
     const uint32_t nt = uni(static_cast<uint32_t>(qs[qi].n_terms));
     const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
     const ListDev A = ix.lists[qlist[d]];
@@ -876,6 +1188,9 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     bool done = false;   // some other list has no doc >= the next driver doc
     uint32_t fo = kMaxTerms;   // first other slot in query order
+    bool all_dense = true;     // every other list is probed through its bitmap
+    uint32_t o1 = kMaxTerms, o1_nblk = 0xFFFFFFFFu;   // the most selective of them
+    uint32_t min_last = 0xFFFFFFFFu;                  // smallest last doc of the others
 #pragma unroll
     for (uint32_t s = 0; s < kMaxTerms; ++s) {
       if (s < nt && s != d) {
@@ -883,8 +1198,12 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         if (fo == kMaxTerms) fo = s;
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
           // probed through its bitmap: no cursor, only its end matters
-          if (first_doc > ix.blk_last[B.blk0 + B.nblk - 1]) done = true;
+          const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
+          if (first_doc > bl) done = true;
+          min_last = bl < min_last ? bl : min_last;
+          if (B.nblk < o1_nblk) { o1 = s; o1_nblk = B.nblk; }
         } else {
+          all_dense = false;
           const uint32_t c0 = uni(find_block(ix.blk_last + B.blk0, 0, B.nblk, first_doc));
           if (l == 0) S.cur[s] = c0;
           if (c0 >= B.nblk) done = true;
@@ -1005,8 +1324,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       bool al0 = cs.al0, al1 = cs.al1;
       WSR_T(1)
       double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
-      const double nrm0 = length_norm(cs.ok0 ? cs.c0 : 0u, ix.avg);
-      const double nrm1 = length_norm(cs.ok1 ? cs.c1 : 0u, ix.avg);
+      const double nrm0 = S.norm[cs.ok0 ? cs.c0 : 0u];
+      const double nrm1 = S.norm[cs.ok1 ? cs.c1 : 0u];
       const bool is_tail = dtail && b == b1 - 1;
       const uint32_t ta0 = is_tail ? S.dtt[2 * l] : cs.ta0;
       const uint32_t ta1 = is_tail ? S.dtt[2 * l + 1] : cs.ta1;
@@ -1205,16 +1524,22 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       WSR_T(4)
     };
 
-    Stage sa, sb;
-    if (b0 < b1) {
-      issue_words(b0);
-      fetch(b0, sa);
-    }
-    WSR_T(0)
-    for (uint32_t b = b0; b < b1 && !done; b += 2) {
-      step(sa, sb, b);
-      if (b + 1 >= b1 || done) break;
-      step(sb, sa, b + 1);
+    if (all_dense && o1 < kMaxTerms) {
+      WSR_T(0)
+      if (!done) lean_segment(ix, S, qlist, nt, d, o1, k, A, b0, b1, dtail, min_last, prev_pub,
+                              my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
+    } else {
+      Stage sa, sb;
+      if (b0 < b1) {
+        issue_words(b0);
+        fetch(b0, sa);
+      }
+      WSR_T(0)
+      for (uint32_t b = b0; b < b1 && !done; b += 2) {
+        step(sa, sb, b);
+        if (b + 1 >= b1 || done) break;
+        step(sb, sa, b + 1);
+      }
     }
     if (evb) flush_events(evb);
     // Re-filter this segment's events against the earlier segments' floor as
