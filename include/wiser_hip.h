@@ -84,6 +84,8 @@ typedef struct wsr_batch_stats {
   double plan_ms, segment_ms, replay_ms;  /* HIP-event times on the engine stream */
   uint64_t events;           /* segment heap-insertion events handed to the replay */
   uint64_t max_query_events; /* the largest per-query event count of the batch */
+  double lean_ms;            /* lean_kernel alone (segment_ms spans it and the concurrent
+                                general segment_kernel) */
 } wsr_batch_stats;
 
 const char* wsr_last_error(void);

@@ -41,7 +41,8 @@ class BatchStats(C.Structure):
                 ("driver_blocks", C.c_uint64), ("other_blocks", C.c_uint64),
                 ("algo_bytes", C.c_uint64), ("plan_ms", C.c_double),
                 ("segment_ms", C.c_double), ("replay_ms", C.c_double),
-                ("events", C.c_uint64), ("max_query_events", C.c_uint64)]
+                ("events", C.c_uint64), ("max_query_events", C.c_uint64),
+                ("lean_ms", C.c_double)]
 
 
 class BuildStats(C.Structure):

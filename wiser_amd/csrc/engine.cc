@@ -61,6 +61,8 @@ struct wsr_handle {
   std::mutex mu;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // general segment kernel, concurrent with the lean kernel
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   VacuumIndex idx;
   IndexArgs args{};
   uint8_t* d_blob = nullptr;
@@ -79,7 +81,8 @@ struct wsr_handle {
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
   std::vector<BlockDev> blocks;     // host copy (debug decode)
   std::vector<uint32_t> meta;
-  int grid = 0;
+  int grid = 0;        // general segment kernel: workgroups (one wave each)
+  int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
 };
 
 struct wsr_batch {
@@ -96,8 +99,9 @@ struct wsr_batch {
   uint32_t* d_qdone = nullptr;   // fused replay: completed items per query
   uint32_t* d_itemq = nullptr;   // item -> query (capacity item_cap)
   uint64_t* d_pub = nullptr;     // per item score floor (capacity item_cap)
-  uint32_t* d_stats = nullptr;   // per segment workgroup: survivors, blocks
+  uint32_t* d_stats = nullptr;   // per general workgroup, then per lean wave: survivors, blocks
   int seg_grid = 0;
+  int lean_wgs = 0;
   // doc-range shard exchange
   uint64_t* d_soff = nullptr;     // per query send offset (events)
   int64_t* d_otot = nullptr;      // per owner totals
@@ -106,7 +110,7 @@ struct wsr_batch {
   uint64_t* d_rbase = nullptr;
   size_t roff_cap = 0;
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   bool ran = false;
 };
 
@@ -176,11 +180,17 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.doc_hi = hi;
     h->args.avg = h->idx.avg_length();
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
     int occ = segment_kernel_occupancy();
     if (occ < 1) occ = 1;
     h->grid = prop.multiProcessorCount * std::min(occ, 32);
+    int locc = lean_kernel_occupancy();
+    if (locc < 1) locc = 1;
+    h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -192,6 +202,9 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
 void wsr_close(wsr_handle* h) {
   if (!h) return;
   if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
+  if (h->stream2) { (void)hipStreamSynchronize(h->stream2); (void)hipStreamDestroy(h->stream2); }
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
                   static_cast<void*>(h->d_meta),
@@ -242,7 +255,8 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
-    HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride * std::max(h->grid, 1)));
+    HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
+                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
@@ -324,6 +338,8 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->nq = nq;
   // persistent grid: never more workgroups than work items can exist
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->grid, items_need)));
+  b->lean_wgs = static_cast<int>(std::max<uint64_t>(
+      1, std::min<uint64_t>(h->lean_wgs, (items_need + kLeanWaves - 1) / kLeanWaves)));
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -346,11 +362,22 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       b->seg_grid, fr, b->d_itemq, h->seg_floor ? b->d_pub : nullptr, st));
+                       kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq,
+                       h->seg_floor ? b->d_pub : nullptr, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
+    // general items on the second stream, lean items here; both drain their
+    // own queue, then the streams join
+    HIP_OK(hipEventRecord(h->ev_fork, st));
+    HIP_OK(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, fr, b->d_itemq,
-                           h->seg_floor ? b->d_pub : nullptr, st));
+                           h->seg_floor ? b->d_pub : nullptr, h->stream2));
+    HIP_OK(hipEventRecord(h->ev_join, h->stream2));
+    HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
+                       b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
+                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, st));
+    HIP_OK(hipEventRecord(b->ev[4], st));
+    HIP_OK(hipStreamWaitEvent(st, h->ev_join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
     if (replay && !fused)
       HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
@@ -396,10 +423,11 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     HIP_OK(hipStreamSynchronize(h->stream));
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * b->seg_grid);
+    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
+    std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * rows);
     HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     uint64_t sv = 0, db = 0, ob = 0;
-    for (int i = 0; i < b->seg_grid; ++i) {
+    for (int i = 0; i < rows; ++i) {
       sv += ws[kStatStride * i]; db += ws[kStatStride * i + 1]; ob += ws[kStatStride * i + 2];
     }
     out->work_items = ctr[kCtrItems];
@@ -427,6 +455,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     HIP_OK(hipEventElapsedTime(&ms, b->ev[0], b->ev[1])); out->plan_ms = ms;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[1], b->ev[2])); out->segment_ms = ms;
     HIP_OK(hipEventElapsedTime(&ms, b->ev[2], b->ev[3])); out->replay_ms = ms;
+    HIP_OK(hipEventElapsedTime(&ms, b->ev[1], b->ev[4])); out->lean_ms = ms;
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -577,11 +606,12 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                        int32_t* n_wg, int32_t* stride) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
-  if (n_wg) *n_wg = b->seg_grid;
+  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;   // general workgroups, then lean waves
+  if (n_wg) *n_wg = rows;
   if (stride) *stride = kStatStride;
   if (!out) return WSR_OK;
   const size_t n = std::min<size_t>(static_cast<size_t>(std::max(max_words, 0)),
-                                    static_cast<size_t>(kStatStride) * b->seg_grid);
+                                    static_cast<size_t>(kStatStride) * rows);
   try {
     HIP_OK(hipStreamSynchronize(h->stream));
     HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));

@@ -29,11 +29,16 @@ struct IndexArgs {
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
-// 4 error flags; the work queue has one head per XCD-sized shard, each on its
-// own 64-byte line (kCtrHead0 + 16*s), so the dequeues of the persistent
-// segment waves do not serialise on a single cache line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrHead0 = 16, kQueueShards = 8,
-       kNumCounters = kCtrHead0 + 16 * kQueueShards };
+// 4 error flags, 6 lean items (items [0, lean) run in lean_kernel, the rest in
+// segment_kernel); each work queue has one head per XCD-sized shard, each on
+// its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 + 16*s general), so
+// the dequeues of the persistent workers do not serialise on a single line.
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16, kQueueShards = 8,
+       kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
+       kNumCounters = kCtrGHead0 + 16 * kQueueShards };
+// QueryPlan::driver = driver slot | cost bucket << 8 | kPlanLean
+constexpr uint32_t kPlanLean = 1u << 16;
+constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
 // per-workgroup statistics written by the segment kernel (no atomics):
 // stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
 #ifdef WSR_PROFILE
@@ -50,7 +55,7 @@ constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; b
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
 // item cost classes for the longest-first queue order (QueryPlan::driver >> 8);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
-constexpr int kCostBuckets = 8;
+constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5
 constexpr float kItemFixedCost = 4.0f;
 
 // Replay fused into the segment kernel: the workgroup that completes a
@@ -66,12 +71,18 @@ struct FusedReplay {
 
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int seg_grid, const FusedReplay& fr, uint32_t* item_q, uint64_t* pub,
-                       hipStream_t st);
+                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       uint64_t* pub, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,
                            uint64_t* pub, hipStream_t st);
+// lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride]
+hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
+                       uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                       int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
+                       uint64_t* pub, hipStream_t st);
+int lean_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);

@@ -141,6 +141,15 @@ __device__ __forceinline__ uint32_t load_byte(const uint8_t* p) {
 // are term frequencies.  `bits` is the pack width from the block directory
 // (0 = VInts blob), so no dependent header load precedes the data loads.
 // Ends with the wave's LDS writes visible to every lane.
+// kWave: the caller's waves run independently (lean kernel): LDS ordering
+// inside one wave needs only a compiler barrier, never a workgroup barrier.
+template <bool kWave = false>
+__device__ __forceinline__ void block_sync() {
+  if (kWave) __builtin_amdgcn_wave_barrier();
+  else __syncthreads();
+}
+
+template <bool kWave = false>
 __device__ void decode_block(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
                              uint32_t seed, uint32_t* out) {
   const uint32_t l = threadIdx.x & 63;
@@ -182,10 +191,10 @@ __device__ void decode_block(const uint8_t* p, uint32_t bits, uint32_t cnt, bool
       before += __popcll(m);
       if (m) prev_term = static_cast<int32_t>(c + 63 - __clzll(m));
     }
-    __syncthreads();
+    block_sync<kWave>();
     x0 = 2 * l < cnt ? out[2 * l] : 0;
     x1 = 2 * l + 1 < cnt ? out[2 * l + 1] : 0;
-    __syncthreads();
+    block_sync<kWave>();
   }
   if (delta) {
     const uint32_t s = x0 + x1;
@@ -195,7 +204,7 @@ __device__ void decode_block(const uint8_t* p, uint32_t bits, uint32_t cnt, bool
   }
   out[2 * l] = x0;
   out[2 * l + 1] = x1;
-  __syncthreads();
+  block_sync<kWave>();
 }
 
 // lower_bound over sorted LDS values s[0..n)
@@ -359,9 +368,14 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     // for the per-item setup): the queue hands out heavy items first
     const float item_cost = static_cast<float>(seg) * cost + kItemFixedCost;
     const uint32_t ic = static_cast<uint32_t>(item_cost);
-    uint32_t bucket = 31u - __clz(ic > 1u ? ic : 1u);
-    bucket = bucket >= kCostBuckets ? kCostBuckets - 1 : bucket;
-    p.driver = d | (bucket << 8);
+    const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
+    const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
+    // lean class: every other list is probed through its bitmap (or none)
+    bool lean = true;
+#pragma unroll
+    for (int s = 0; s < kMaxTerms; ++s)
+      if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
+    p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
     p.seg_blocks = seg;
     p.n_items = (nd + seg - 1) / seg;
   }
@@ -373,36 +387,41 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
 }
 
 // Pass 2, one workgroup of 1024: event capacities are scanned in query order;
-// items are numbered bucket-major, heaviest cost bucket first (query order
-// inside a bucket, a query's items consecutive), so the persistent waves take
-// the long items first and the short ones fill the tail (longest-first list
-// scheduling).
+// items are numbered class-major (lean items first, then general ones), then
+// bucket-major, heaviest cost bucket first (query order inside a bucket, a
+// query's items consecutive), so the persistent workers take the long items
+// first and the short ones fill the tail (longest-first list scheduling).
+constexpr int kPlanKeys = 2 * kCostBuckets;
+__device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
+  const uint32_t bucket = (drv >> 8) & 0xFFu;
+  return ((drv & kPlanLean) ? 0u : static_cast<uint32_t>(kCostBuckets)) + (kCostBuckets - 1 - bucket);
+}
 __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __restrict__ plan,
                                                          uint32_t* __restrict__ counters,
                                                          uint64_t ev_capacity, uint32_t item_capacity,
-                                                         uint32_t seg_grid) {
+                                                         uint32_t lean_grid, uint32_t seg_grid) {
   constexpr int kWaves = 1024 / 64;
   __shared__ uint64_t s_cap[1024];
-  __shared__ uint32_t s_bt[kCostBuckets][kWaves];   // per bucket, per wave item totals
+  __shared__ uint32_t s_bt[kPlanKeys][kWaves];   // per key, per wave item totals
   const int t = threadIdx.x, T = blockDim.x;
   const uint32_t wv = t / 64, l = t & 63;
   const int per = (nq + T - 1) / T;
   const int q0 = t * per, q1 = min(nq, q0 + per);
-  uint32_t cnt[kCostBuckets];
+  uint32_t cnt[kPlanKeys];
 #pragma unroll
-  for (int bk = 0; bk < kCostBuckets; ++bk) cnt[bk] = 0;
+  for (int bk = 0; bk < kPlanKeys; ++bk) cnt[bk] = 0;
   uint64_t cap = 0;
   for (int i = q0; i < q1; ++i) {
     const QueryPlan p = plan[i];
-    const uint32_t bk = p.driver >> 8;
+    const uint32_t bk = plan_key(p.driver);
 #pragma unroll
-    for (int b = 0; b < kCostBuckets; ++b) cnt[b] += bk == static_cast<uint32_t>(b) ? p.n_items : 0u;
+    for (int b = 0; b < kPlanKeys; ++b) cnt[b] += bk == static_cast<uint32_t>(b) ? p.n_items : 0u;
     cap += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
   s_cap[t] = cap;
-  uint32_t ex[kCostBuckets];   // items of this bucket in lower lanes of the wave
+  uint32_t ex[kPlanKeys];   // items of this key in lower lanes of the wave
 #pragma unroll
-  for (int b = 0; b < kCostBuckets; ++b) {
+  for (int b = 0; b < kPlanKeys; ++b) {
     const uint32_t inc = wave_incl_scan(cnt[b]);
     ex[b] = inc - cnt[b];
     if (l == 63) s_bt[b][wv] = inc;
@@ -415,11 +434,11 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     s_cap[t] += c;
     __syncthreads();
   }
-  // base of every bucket (heavier buckets first) and of this wave inside it
-  uint32_t ib[kCostBuckets];
-  uint32_t run = 0;
+  // base of every key (ascending) and of this wave inside it
+  uint32_t ib[kPlanKeys];
+  uint32_t run = 0, n_lean = 0;
 #pragma unroll
-  for (int b = kCostBuckets - 1; b >= 0; --b) {
+  for (int b = 0; b < kPlanKeys; ++b) {
     uint32_t below = 0, tot = 0;
     for (uint32_t w = 0; w < static_cast<uint32_t>(kWaves); ++w) {
       const uint32_t v = s_bt[b][w];
@@ -428,15 +447,16 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     }
     ib[b] = run + below + ex[b];
     run += tot;
+    if (b == kCostBuckets - 1) n_lean = run;
   }
   const uint32_t total_items = run;
   uint64_t cb = s_cap[t] - cap;
   for (int i = q0; i < q1; ++i) {
     QueryPlan& p = plan[i];
-    const uint32_t bk = p.driver >> 8;
+    const uint32_t bk = plan_key(p.driver);
     uint32_t base = 0;
 #pragma unroll
-    for (int b = 0; b < kCostBuckets; ++b)
+    for (int b = 0; b < kPlanKeys; ++b)
       if (bk == static_cast<uint32_t>(b)) { base = ib[b]; ib[b] += p.n_items; }
     p.item_base = base;
     p.ev_base = cb;
@@ -446,12 +466,16 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     const bool fits = s_cap[t] <= ev_capacity && total_items <= item_capacity;
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
     counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
+    counters[kCtrLean] = fits ? n_lean : 0u;
     counters[kCtrEvCap] = static_cast<uint32_t>(s_cap[t] > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap[t]);
   }
-  // Work queue: shard s serves items s, s+8, s+16, ...; workgroup w starts on
-  // item w without a dequeue, so shard s's head starts past those first items.
-  if (t < kQueueShards)
-    counters[kCtrHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
+  // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
+  // starts on relative item w without a dequeue, so shard s's head starts past
+  // those first items (lean: one worker per wave; general: per workgroup).
+  if (t < kQueueShards) {
+    counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
+    counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
+  }
 }
 
 // Pass 3, one thread per query: the item -> query map of the segment kernel
@@ -476,7 +500,7 @@ struct WaveLds {
   uint32_t mb[8][128];   // doc ids of up to 8 other-list blocks decoded side by side
   uint32_t dtd[128];     // the driver's VInts tail block: doc ids
   uint32_t dtt[128];     //   and tfs
-  Event evs[128];        // events buffered for coalesced stores
+  Event evs[64];         // events buffered for one coalesced store
   double norm[256];      // Bm25Similarity cache_ (host table, scoring.h:85-90)
   uint32_t cur[kMaxTerms];  // per other slot: cursor into its block directory
   uint32_t roff[64];     // fused replay: segment offsets of the event stream
@@ -827,6 +851,82 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
   replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
 }
 
+// ------------------------------------------------------ item plumbing --
+// Next work item of a persistent worker over items [lo, hi), split into
+// kQueueShards round-robin shards (relative index i in shard i % kQueueShards),
+// each with its own head on its own 64-byte line; a worker starts with its own
+// shard and steals from the others.  Returns hi when the range is drained.
+__device__ __forceinline__ uint32_t next_item(uint32_t* heads, uint32_t lo, uint32_t hi,
+                                              uint32_t& shard, uint32_t& tried) {
+  const uint32_t n = hi - lo;
+  while (tried < kQueueShards) {
+    uint32_t* head = &heads[16 * shard];
+    const uint32_t limit = (n + kQueueShards - 1 - shard) / kQueueShards;
+    uint32_t local = 0;
+    if ((threadIdx.x & 63) == 0) {
+      local = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (local < limit) local = atomicAdd(head, 1u);
+    }
+    local = uni(local);
+    if (local < limit) return lo + shard + kQueueShards * local;
+    shard = (shard + 1) % kQueueShards;
+    ++tried;
+  }
+  return hi;
+}
+
+// End of a work item: re-filter its events against the earlier segments'
+// floor as it stands now (it only grows, and every value it takes is backed by
+// k survivors before this segment), keeping the doc order; publish the count;
+// with fused replay, the worker that completes a query's last item replays the
+// query (its coherent event stores complete before the counter moves, and the
+// replay reads the other items' events with coherent loads).
+template <bool kWave>
+__device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* plan, uint32_t qi,
+                                            const QueryPlan& P, uint32_t item,
+                                            const uint64_t* prev_pub, Event* ev_out, uint32_t ev_n,
+                                            const Event* events, uint32_t* ev_cnt,
+                                            const FusedReplay& fr, uint32_t* s_off) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt();
+  if (prev_pub && ev_n > 0) {
+    const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double fl_end = __longlong_as_double(static_cast<long long>(
+        (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
+        uni(static_cast<uint32_t>(fb))));
+    uint32_t kept = 0;
+    for (uint32_t c = 0; c < ev_n; c += 64) {
+      double sc = 0.0;
+      int32_t dc = 0;
+      const bool in = c + l < ev_n;
+      if (in) load_event<true>(&ev_out[c + l], &sc, &dc);
+      const bool keep = in && sc > fl_end;
+      const uint64_t km = __ballot(keep);
+      if (keep) {
+        Event e;
+        e.score = sc;
+        e.doc = dc;
+        e.pad = 0;
+        store_event_coherent(&ev_out[kept + __popcll(km & lt)], e);
+      }
+      kept += __popcll(km);
+    }
+    ev_n = kept;
+  }
+  if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fr.q_done) {
+    __builtin_amdgcn_s_waitcnt(0);
+    block_sync<kWave>();
+    uint32_t old = 0;
+    if (l == 0)
+      old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = uni(old);
+    if (old + 1 == P.n_items)
+      replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
+                        fr.n_hits, s_off);
+  }
+}
+
 // waves per SIMD the segment kernel is compiled for (register budget)
 #ifndef WSR_SEG_WAVES
 #define WSR_SEG_WAVES 3
@@ -899,22 +999,41 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // stage waits only for loads issued one iteration earlier.  Scoring one
 // survivor per lane instead of two postings per lane keeps the f64 work
 // proportional to the survivors.
-__device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, const int32_t* qlist,
+// LDS of one wave of the lean kernel
+struct LeanLds {
+  uint32_t q[1024];     // survivor queue (4 rings of 256); at item start the driver's VInts
+                        // tail decode, at item end the replay's segment scan
+  Event evs[64];        // events of one scoring chunk, stored together
+  uint4 dblk[64];       // the driver's directory entries of the segment
+  uint32_t dmeta[64];
+};
+
+// o1 == kMaxTerms: single-term query, every posting of the driver survives.
+// tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
+// dtail, used for block b1 - 1.
+__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, const double* norm_tab,
+                                             const int32_t* qlist,
                                              uint32_t nt, uint32_t d, uint32_t o1, uint32_t k,
                                              const ListDev& A, uint32_t b0, uint32_t b1, bool dtail,
+                                             uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
                                              uint32_t min_last, const uint64_t* prev_pub,
                                              uint64_t* my_pub, Event* ev_out, uint32_t& ev_n,
-                                             uint32_t& evb, double& pt, uint32_t& pt_n,
+                                             double& pt, uint32_t& pt_n,
                                              double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
-  const ListDev O = ix.lists[qlist[o1]];
-  const uint2* o_bm = reinterpret_cast<const uint2*>(ix.dense + O.bm);
-  const uint8_t* o_tf8 = ix.tf8 + O.tf8;
+  const bool single = o1 >= kMaxTerms;
+  const ListDev O = ix.lists[qlist[single ? d : o1]];
+  // (single term: a dummy bitmap read, hits are the driver's postings)
+  // (single term: reads go to a valid dummy word; the image may have no bitmaps)
+  const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
+                             : reinterpret_cast<const uint2*>(ix.dense + O.bm);
+  const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + O.tf8;
+  uint32_t evb = 0;
   const uint32_t lo = ix.doc_lo, span = ix.dense_span;
   const uint32_t hi_rel = ix.doc_hi - ix.doc_lo;   // docs a with a - lo < hi_rel are in the image
   const double idf_d = A.idf, idf_o = O.idf;
-  uint32_t* qdoc = &S.mb[0][0];     // survivor queue (ring of 256, reuses the decode area)
+  uint32_t* qdoc = S.q;             // survivor queue (ring of 256)
   uint32_t* qc4 = qdoc + 256;
   uint32_t* qtd = qdoc + 512;
   uint32_t* qto = qdoc + 768;       // tf byte, or 0x80000000 | posting index when escaped
@@ -926,12 +1045,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
   const uint64_t* floor_src = prev_pub ? prev_pub : reinterpret_cast<const uint64_t*>(ix.lists);
   const bool has_floor = prev_pub != nullptr;
 
-  // buffered events (up to 127) to ev_out, after a chunk's top-k loop so the
-  // loop itself holds no stores
+  // a chunk's events (at most 64) to ev_out, after its top-k loop so the loop
+  // itself holds no stores
   auto flush = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
     if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
-    if (l + 64 < evb) store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[l + 64]);
     __builtin_amdgcn_wave_barrier();
     evb = 0;
   };
@@ -949,11 +1067,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
     if (__ballot(alive && (to & 0x80000000u))) {
       if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
     }
-    const double norm = S.norm[c4 & 255u];
+    const double norm = norm_tab[c4 & 255u];
     double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
     for (uint32_t s = 0; s < nt; ++s) {
       if (s == d) {
         sc += bm25_term(idf_d, alive ? td : 0u, norm);
+        if (single) break;
       } else if (s == o1) {
         sc += bm25_term(idf_o, alive ? to : 0u, norm);
       } else {
@@ -998,7 +1117,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
         pt_n = pt_n + 1 > k ? k : pt_n + 1;
       }
     }
-    if (evb >= 64) flush();
+    if (evb) flush();
     if (my_pub) {
       const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
       const double pv = kn > flo ? kn : flo;
@@ -1016,41 +1135,50 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
   // swapped.  No register holding an in-flight load is ever copied (a copy
   // would wait for the load).
   struct Regs {
-    uint32_t w0 = 0, w1 = 0, w2 = 0, wsh = 0;      // doc-id pack words of the next block
+    uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
+    uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
     uint64_t floor = 0;                            // score floor word
-    // D: a decoded block
-    uint32_t da0 = 0, da1 = 0, dc0 = 0, dc1 = 0, dcs0 = 0, dcs1 = 0;   // docs, length words
-    uint32_t dt0 = 0, dt1 = 0, dt2 = 0, dtsh = 0, dtb = 1;             // driver tf words
-    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);              // O1 bitmap words
+    // D: a decoded block and its loads in flight
+    uint32_t da0 = 0, da1 = 0, dc0 = 0, dc1 = 0;   // docs, doc-length words
+    uint32_t dt0 = 0, dt1 = 0, dt2 = 0;            // driver tf pack words
+    uint32_t dtb = 1, dtrel = 0;                   //   (uniform: width, blob offset)
+    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap words
     bool dok0 = false, dok1 = false, dtl = false;
-    // H: O1 hits of the block decoded one iteration earlier
-    uint32_t hf0 = 0, hf1 = 0, hfs0 = 0, hfs1 = 0, hx0 = 0, hx1 = 0;   // tf byte words, ranks
+    // H: the block decoded one iteration earlier, with its O1 hits
+    uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
+    uint32_t hf0 = 0, hf1 = 0, hx0 = 0, hx1 = 0;   // O1 tf byte words (in flight), posting ranks
     bool hh0 = false, hh1 = false;
   };
   Regs RA, RB;
+  // byte shift of a pair's first value inside its aligned dword (pair_words)
+  auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
+    const uint32_t bit = 2 * l * bits;
+    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ix.blob + A.base)) + rel + 2 +
+                       (bit >> 3);
+    return ((a & 3u) << 3) + (bit & 7u);
+  };
+  const uint32_t tf8_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u);
 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
     const uint32_t m = uni(S.dmeta[bi]);
-    const uint32_t bits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
-    pair_words(ix.blob + A.base + uni(S.dblk[bi].z) + 2, bits, l, Y.w0, Y.w1, Y.w2, Y.wsh);
+    Y.wbits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
+    Y.wrel = uni(S.dblk[bi].z);
+    uint32_t sh;
+    pair_words(ix.blob + A.base + Y.wrel + 2, Y.wbits, l, Y.w0, Y.w1, Y.w2, sh);
     Y.floor = __hip_atomic_load(floor_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // W(j+1): issued first, so it has a whole iteration to arrive
     issue_words(j + 1, Y);
-    // C(j-2): compaction of block j-2: its hits are in X (H of iteration
-    // j-1), its decoded fields still in Y (D of iteration j-2; D(j) below
-    // overwrites them only after this stage)
+    // C(j-2): compaction of block j-2 (its H fields are in X)
     if (j >= b0 + 2) {
       floor_bits = X.floor;
-      uint32_t td0, td1;
-      pair_values(Y.dt0, Y.dt1, Y.dt2, Y.dtsh, Y.dtb, td0, td1);
-      if (Y.dtl) { td0 = S.dtt[2 * l]; td1 = S.dtt[2 * l + 1]; }
-      const uint32_t f0 = (X.hf0 >> X.hfs0) & 0xFFu, f1 = (X.hf1 >> X.hfs1) & 0xFFu;
+      const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
+      const uint32_t f0 = single ? 0u : (X.hf0 >> xs0) & 0xFFu;
+      const uint32_t f1 = single ? 0u : (X.hf1 >> xs1) & 0xFFu;
       const uint32_t to0 = f0 == kTf8Escape ? (0x80000000u | X.hx0) : f0;
       const uint32_t to1 = f1 == kTf8Escape ? (0x80000000u | X.hx1) : f1;
-      const uint32_t c0 = (Y.dc0 >> Y.dcs0) & 0xFFu, c1 = (Y.dc1 >> Y.dcs1) & 0xFFu;
       const uint64_t m0 = __ballot(X.hh0), m1 = __ballot(X.hh1);
       const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
       const uint32_t r1 = r0 + (X.hh0 ? 1u : 0u);
@@ -1058,24 +1186,36 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
       // most 63 + 128 entries are live, so it is never one of them)
       const uint32_t spare = (qhead - 1u) & 255u;
       const uint32_t e0 = X.hh0 ? (r0 & 255u) : spare, e1 = X.hh1 ? (r1 & 255u) : spare;
-      qdoc[e0] = Y.da0; qc4[e0] = c0; qtd[e0] = td0; qto[e0] = to0;
-      qdoc[e1] = Y.da1; qc4[e1] = c1; qtd[e1] = td1; qto[e1] = to1;
+      qdoc[e0] = X.ha0; qc4[e0] = X.hc0; qtd[e0] = X.ht0; qto[e0] = to0;
+      qdoc[e1] = X.ha1; qc4[e1] = X.hc1; qtd[e1] = X.ht1; qto[e1] = to1;
       qtail += __popcll(m0) + __popcll(m1);
-      // (at most two full chunks: fewer than 64 + 128 entries are queued)
-      if (qtail - qhead >= 64) score_chunk(64);
-      if (qtail - qhead >= 64) score_chunk(64);
+      // (at most two full chunks: fewer than 64 + 128 entries are queued;
+      // one call site keeps a single inlined copy of the scoring code)
+#pragma nounroll
+      for (int c = 0; c < 2 && qtail - qhead >= 64; ++c) score_chunk(64);
     }
-    // H(j-1): O1 hits of block j-1 (decoded into X), written to Y
+    // H(j-1): block j-1 (D fields in X): O1 hits, its driver tfs and length
+    // codes extracted, into Y's H fields
     {
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
-      const bool h0 = X.dok0 && q0 < span && ((X.de0.y >> s0) & 1u);
-      const bool h1 = X.dok1 && q1 < span && ((X.de1.y >> s1) & 1u);
+      const bool h0 = X.dok0 && (single || (q0 < span && ((X.de0.y >> s0) & 1u)));
+      const bool h1 = X.dok1 && (single || (q1 < span && ((X.de1.y >> s1) & 1u)));
       Y.hx0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
       Y.hx1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
-      Y.hf0 = byte_word(o_tf8 + (h0 ? Y.hx0 : 0u), &Y.hfs0);
-      Y.hf1 = byte_word(o_tf8 + (h1 ? Y.hx1 : 0u), &Y.hfs1);
+      uint32_t w;
+      Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? Y.hx0 : 0u), &w);
+      Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? Y.hx1 : 0u), &w);
       Y.hh0 = h0; Y.hh1 = h1;
+      Y.ha0 = X.da0; Y.ha1 = X.da1;
+      Y.hc0 = (X.dc0 >> ((X.da0 & 3u) << 3)) & 0xFFu;
+      Y.hc1 = (X.dc1 >> ((X.da1 & 3u) << 3)) & 0xFFu;
+      if (!X.dok0 || X.da0 >= ix.n_c4) Y.hc0 = 0;   // doc beyond the length records
+      if (!X.dok1 || X.da1 >= ix.n_c4) Y.hc1 = 0;
+      uint32_t t0, t1;
+      pair_values(X.dt0, X.dt1, X.dt2, pair_shift(X.dtrel, X.dtb), X.dtb, t0, t1);
+      Y.ht0 = X.dtl ? ttf0 : t0;
+      Y.ht1 = X.dtl ? ttf1 : t1;
     }
     // D(j): decode block j from X's words into Y, issue its loads
     {
@@ -1083,25 +1223,28 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
       const uint32_t bi = live ? j - b0 : 0u;
       const uint32_t prev = uni(S.dblk[bi].x);
       const uint32_t m = uni(S.dmeta[bi]);
-      const uint32_t bits = (m & 0xFF) ? (m & 0xFF) : 1u;
       const uint32_t cnt = live ? ((j == A.nblk - 1) ? A.tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
-      pair_values(X.w0, X.w1, X.w2, X.wsh, bits, x0, x1);
+      pair_values(X.w0, X.w1, X.w2, pair_shift(X.wrel, X.wbits), X.wbits, x0, x1);
       const uint32_t sm = x0 + x1;
       const uint32_t inc = wave_incl_scan(sm);
       uint32_t a0 = prev + (inc - sm) + x0;
       uint32_t a1 = a0 + x1;
       const bool tl = live && dtail && j == b1 - 1;
-      if (tl) { a0 = S.dtd[2 * l]; a1 = S.dtd[2 * l + 1]; }
+      if (tl) { a0 = tdoc0; a1 = tdoc1; }
       const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
       const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
-      const bool in0 = ok0 && a0 - lo < span, in1 = ok1 && a1 - lo < span;
+      const bool in0 = !single && ok0 && a0 - lo < span;
+      const bool in1 = !single && ok1 && a1 - lo < span;
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
-      Y.dc0 = byte_word(ix.c4 + ((ok0 && a0 < ix.n_c4) ? a0 : 0u), &Y.dcs0);
-      Y.dc1 = byte_word(ix.c4 + ((ok1 && a1 < ix.n_c4) ? a1 : 0u), &Y.dcs1);
+      uint32_t w;
+      Y.dc0 = byte_word(ix.c4 + ((ok0 && a0 < ix.n_c4) ? a0 : 0u), &w);
+      Y.dc1 = byte_word(ix.c4 + ((ok1 && a1 < ix.n_c4) ? a1 : 0u), &w);
       Y.dtb = (m >> 8) ? (m >> 8) : 1u;
-      pair_words(ix.blob + A.base + uni(S.dblk[bi].w) + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, Y.dtsh);
+      Y.dtrel = uni(S.dblk[bi].w);
+      uint32_t sh;
+      pair_words(ix.blob + A.base + Y.dtrel + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, sh);
       Y.da0 = a0; Y.da1 = a1; Y.dok0 = ok0; Y.dok1 = ok1; Y.dtl = tl;
       if (live) ++n_dblk;
       // past the smallest last doc of the other lists nothing later can match
@@ -1115,7 +1258,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, WaveLds& S, co
     body(RB, RA, j + 1);
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
-  if (evb) flush();
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1133,28 +1275,18 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) S.norm[l + 64 * i] = ix.cache[l + 64 * i];
   const uint64_t lt = lanemask_lt();
+  // general items are [n_lean, total): the lean kernel takes the others
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0, n_oblk = 0;
-  // first item: this workgroup's own index; then dequeue from the shard heads,
-  // starting with the shard of the workgroup and stealing from the others
+  // first item: this workgroup's own index; then the shard heads
   uint32_t shard = blockIdx.x % kQueueShards;
   uint32_t tried = 0;
-  uint32_t item = blockIdx.x;
+  uint32_t item = n_lean + blockIdx.x;
   for (;;) {
-    while (item >= total && tried < kQueueShards) {
-      uint32_t* head = &counters[kCtrHead0 + 16 * shard];
-      const uint32_t limit = (total + kQueueShards - 1 - shard) / kQueueShards;
-      uint32_t local = 0;
-      if (l == 0) {
-        local = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (local < limit) local = atomicAdd(head, 1u);
-      }
-      local = uni(local);
-      if (local < limit) { item = shard + kQueueShards * local; break; }
-      shard = (shard + 1) % kQueueShards;
-      ++tried;
-    }
+    if (item >= total) item = next_item(&counters[kCtrGHead0], n_lean, total, shard, tried);
     if (item >= total) break;
     const uint32_t qi = uni(item_q[item]);   // written by plan_scan_kernel
     const QueryPlan P = plan[qi];
@@ -1188,9 +1320,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     bool done = false;   // some other list has no doc >= the next driver doc
     uint32_t fo = kMaxTerms;   // first other slot in query order
-    bool all_dense = true;     // every other list is probed through its bitmap
-    uint32_t o1 = kMaxTerms, o1_nblk = 0xFFFFFFFFu;   // the most selective of them
-    uint32_t min_last = 0xFFFFFFFFu;                  // smallest last doc of the others
 #pragma unroll
     for (uint32_t s = 0; s < kMaxTerms; ++s) {
       if (s < nt && s != d) {
@@ -1198,12 +1327,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         if (fo == kMaxTerms) fo = s;
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
           // probed through its bitmap: no cursor, only its end matters
-          const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
-          if (first_doc > bl) done = true;
-          min_last = bl < min_last ? bl : min_last;
-          if (B.nblk < o1_nblk) { o1 = s; o1_nblk = B.nblk; }
+          if (first_doc > ix.blk_last[B.blk0 + B.nblk - 1]) done = true;
         } else {
-          all_dense = false;
           const uint32_t c0 = uni(find_block(ix.blk_last + B.blk0, 0, B.nblk, first_doc));
           if (l == 0) S.cur[s] = c0;
           if (c0 >= B.nblk) done = true;
@@ -1524,66 +1649,19 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       WSR_T(4)
     };
 
-    if (all_dense && o1 < kMaxTerms) {
-      WSR_T(0)
-      if (!done) lean_segment(ix, S, qlist, nt, d, o1, k, A, b0, b1, dtail, min_last, prev_pub,
-                              my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
-    } else {
-      Stage sa, sb;
-      if (b0 < b1) {
-        issue_words(b0);
-        fetch(b0, sa);
-      }
-      WSR_T(0)
-      for (uint32_t b = b0; b < b1 && !done; b += 2) {
-        step(sa, sb, b);
-        if (b + 1 >= b1 || done) break;
-        step(sb, sa, b + 1);
-      }
+    Stage sa, sb;
+    if (b0 < b1) {
+      issue_words(b0);
+      fetch(b0, sa);
+    }
+    WSR_T(0)
+    for (uint32_t b = b0; b < b1 && !done; b += 2) {
+      step(sa, sb, b);
+      if (b + 1 >= b1 || done) break;
+      step(sb, sa, b + 1);
     }
     if (evb) flush_events(evb);
-    // Re-filter this segment's events against the earlier segments' floor as
-    // it stands now (it only grows, and every value it takes is backed by k
-    // survivors before this segment), keeping the doc order.
-    if (prev_pub && ev_n > 0) {
-      const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const double fl_end = __longlong_as_double(static_cast<long long>(
-          (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
-          uni(static_cast<uint32_t>(fb))));
-      uint32_t kept = 0;
-      for (uint32_t c = 0; c < ev_n; c += 64) {
-        double sc = 0.0;
-        int32_t dc = 0;
-        const bool in = c + l < ev_n;
-        if (in) load_event<true>(&ev_out[c + l], &sc, &dc);
-        const bool keep = in && sc > fl_end;
-        const uint64_t km = __ballot(keep);
-        if (keep) {
-          Event e;
-          e.score = sc;
-          e.doc = dc;
-          e.pad = 0;
-          store_event_coherent(&ev_out[kept + __popcll(km & lt)], e);
-        }
-        kept += __popcll(km);
-      }
-      ev_n = kept;
-    }
-    if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (fr.q_done) {
-      // the workgroup that finishes a query's last item replays the query:
-      // its coherent event stores complete before the counter moves, and the
-      // replay reads the other items' events with coherent loads
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      uint32_t old = 0;
-      if (l == 0)
-        old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      old = uni(old);
-      if (old + 1 == P.n_items)
-        replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
-                          fr.n_hits, S.roff);
-    }
+    finish_item<false>(qs, plan, qi, P, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.roff);
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
@@ -1595,6 +1673,103 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     stats[blockIdx.x * kStatStride + 9] =
         static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - prof_start);
 #endif
+  }
+}
+
+
+// ----------------------------------------------------------- lean kernel --
+// Items whose other lists all carry rank bitmaps (and single-term items).
+// Workgroups of kLeanWaves independent waves: each wave dequeues and runs its
+// own items, so the only workgroup barrier is the norm-table fill at start.
+// Small LDS (LeanLds per wave + one shared norm table) and a register budget
+// of WSR_LEAN_WGS workgroups per CU keep several waves per SIMD resident, which
+// is what hides the dependent loads of short items and of the probe chains.
+#ifndef WSR_LEAN_WGS
+#define WSR_LEAN_WGS 4
+#endif
+__global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
+    IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
+    uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
+    uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
+    uint64_t* __restrict__ pub) {
+  __shared__ LeanLds SW[kLeanWaves];
+  __shared__ double norm[256];
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t w = threadIdx.x >> 6;
+  for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
+  __syncthreads();
+  LeanLds& S = SW[w];
+  const uint32_t wid = blockIdx.x * kLeanWaves + w;
+  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+  uint32_t n_surv = 0, n_dblk = 0;
+  uint32_t shard = wid % kQueueShards, tried = 0;
+  uint32_t item = wid;
+  for (;;) {
+    if (item >= n_lean) item = next_item(&counters[kCtrHead0], 0, n_lean, shard, tried);
+    if (item >= n_lean) break;
+    const uint32_t qi = uni(item_q[item]);
+    const QueryPlan P = plan[qi];
+    const int32_t* qlist = qs[qi].list;
+    const uint32_t r = item - P.item_base;
+    const uint32_t d = uni(P.driver & 0xFFu);
+    const uint32_t nt = uni(static_cast<uint32_t>(qs[qi].n_terms));
+    const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
+    const ListDev A = ix.lists[qlist[d]];
+    const uint32_t seg = uni(P.seg_blocks);
+    const uint32_t b0 = r * seg;
+    const uint32_t b1 = min(b0 + seg, A.nblk);
+    Event* ev_out = events + P.ev_base + static_cast<uint64_t>(r) * seg * 128;
+    uint64_t* my_pub = pub ? pub + item : nullptr;
+    const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
+
+    __builtin_amdgcn_wave_barrier();
+    if (b0 + l < b1) {
+      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[A.blk0 + b0 + l];
+      S.dmeta[l] = ix.blk_meta[A.blk0 + b0 + l];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
+    bool done = false;
+    uint32_t o1 = kMaxTerms, o1_nblk = 0xFFFFFFFFu;   // the most selective other list
+    uint32_t min_last = 0xFFFFFFFFu;                  // smallest last doc of the others
+    for (uint32_t s = 0; s < nt; ++s) {
+      if (s == d) continue;
+      const ListDev B = ix.lists[qlist[s]];
+      const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
+      if (first_doc > bl) done = true;
+      min_last = bl < min_last ? bl : min_last;
+      if (B.nblk < o1_nblk) { o1 = s; o1_nblk = B.nblk; }
+    }
+    // the driver's VInts tail block, decoded once into registers (2 per lane)
+    bool dtail = false;
+    uint32_t tdoc0 = 0, tdoc1 = 0, ttf0 = 0, ttf1 = 0;
+    if (b0 < b1) {
+      const uint32_t bi = b1 - 1 - b0;
+      const uint32_t mt = uni(S.dmeta[bi]);
+      dtail = (mt & 0xFF) == 0;
+      if (dtail) {
+        decode_block<true>(ix.blob + A.base + uni(S.dblk[bi].z), 0, A.tail_cnt, true,
+                           uni(S.dblk[bi].x), S.q);
+        decode_block<true>(ix.blob + A.base + uni(S.dblk[bi].w), mt >> 8, A.tail_cnt, false, 0,
+                           S.q + 256);
+        tdoc0 = S.q[2 * l]; tdoc1 = S.q[2 * l + 1];
+        ttf0 = S.q[256 + 2 * l]; ttf1 = S.q[256 + 2 * l + 1];
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    double pt = 0.0, last_pub = 0.0;
+    uint32_t pt_n = 0, ev_n = 0;
+    if (!done)
+      lean_segment(ix, S, norm, qlist, nt, d, o1, k, A, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
+                   min_last, prev_pub, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
+    finish_item<true>(qs, plan, qi, P, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
+    item = 0xFFFFFFFFu;
+  }
+  if (l == 0) {
+    stats[wid * kStatStride + 0] = n_surv;
+    stats[wid * kStatStride + 1] = n_dblk;
+    stats[wid * kStatStride + 2] = 0;
   }
 }
 
@@ -1701,13 +1876,13 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int seg_grid, const FusedReplay& fr, uint32_t* item_q, uint64_t* pub,
-                       hipStream_t st) {
+                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       uint64_t* pub, hipStream_t st) {
   if (nq > 0)
     hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
                        counters, fr);
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
-                     item_capacity, static_cast<uint32_t>(seg_grid));
+                     item_capacity, static_cast<uint32_t>(lean_grid), static_cast<uint32_t>(seg_grid));
   if (nq > 0)
     hipLaunchKernelGGL(item_map_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, plan, nq, counters,
                        item_q, pub);
@@ -1721,6 +1896,22 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
   hipLaunchKernelGGL(segment_kernel, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
                      events, ev_cnt, stats, fr, item_q, pub);
   return hipGetLastError();
+}
+
+hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
+                       uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                       int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
+                       uint64_t* pub, hipStream_t st) {
+  hipLaunchKernelGGL(lean_kernel, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan, nq,
+                     counters, events, ev_cnt, stats, fr, item_q, pub);
+  return hipGetLastError();
+}
+
+int lean_kernel_occupancy() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel, 64 * kLeanWaves, 0) != hipSuccess)
+    return 1;
+  return n;
 }
 
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
