@@ -74,6 +74,7 @@ struct wsr_handle {
   double* d_cache = nullptr;
   DenseEnt* d_dense = nullptr;
   uint8_t* d_tf8 = nullptr;
+  uint8_t* d_plen = nullptr;
   uint32_t dense_lists = 0;
   bool fuse_replay = true;
   bool seg_floor = true;
@@ -156,6 +157,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
     dev_upload(&h->d_blob, img.blob);
+    dev_upload(&h->d_plen, img.plen);
+    h->args.plen = h->d_plen;
     dev_upload(&h->d_lists, img.lists);
     dev_upload(&h->d_blocks, img.blocks);
     dev_upload(&h->d_last, img.blk_last);
@@ -209,7 +212,8 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
-                  static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8)})
+                  static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8),
+                  static_cast<void*>(h->d_plen)})
     if (p) (void)hipFree(p);
   delete h;
 }

@@ -209,7 +209,9 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     uint32_t tail_cnt = 0;
     std::vector<DenseEnt> dense;   // rank bitmap (dense lists only)
     std::vector<uint8_t> tf8;
+    std::vector<uint8_t> plen;     // doc-length code of every posting, 128 per block
   };
+  const std::vector<uint8_t>& c4 = idx.char4_lengths();
   std::vector<Part> parts(L);
   // decode the image's postings of one list and lay down its bitmap + tf bytes
   auto build_dense = [&](Part& pt, const std::vector<SkipRow>& rows, uint64_t r0, uint64_t r1,
@@ -293,6 +295,18 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
           pt.meta.push_back(bd | (bf << 8));
         }
         pt.tail_cnt = (r1 == nrows) ? static_cast<uint32_t>(fcnt) : kPackSize;
+        // doc-length codes in posting order: a block's 128 codes are one
+        // contiguous line for the kernels instead of a gather over the doc ids
+        // (docs past the length records get code 0, as in the kernels)
+        pt.plen.assign((r1 - r0) * kPackSize, 0);
+        for (uint64_t r = r0; r < r1; ++r) {
+          const int cnt = r + 1 == nrows ? fcnt : kPackSize;
+          uint32_t docs[kPackSize];
+          if (!host_decode_block(file + rows[r].doc_off, fend, cnt, true, rows[r].prev_doc, docs))
+            throw std::runtime_error("cannot decode a block of '" + idx.term(id) + "'");
+          uint8_t* o = &pt.plen[(r - r0) * kPackSize];
+          for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
+        }
         const uint64_t n_img = (r1 - r0 - 1) * kPackSize + pt.tail_cnt;
         if (dense_div && span && n_img * dense_div >= span) build_dense(pt, rows, r0, r1, n_img);
       }
@@ -318,6 +332,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.blocks.reserve(nb);
   img.blk_last.reserve(nb);
   img.blk_meta.reserve(nb);
+  img.plen.reserve(nb * kPackSize);
   uint64_t at = 0;
   for (int32_t id = 0; id < L; ++id) {
     Part& p = parts[id];
@@ -345,7 +360,9 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     at += (p.bytes.size() + 15) & ~15ull;
     for (auto& b : p.blocks) { img.blocks.push_back(b); img.blk_last.push_back(b.last); }
     img.blk_meta.insert(img.blk_meta.end(), p.meta.begin(), p.meta.end());
+    img.plen.insert(img.plen.end(), p.plen.begin(), p.plen.end());
     std::vector<uint8_t>().swap(p.bytes);
+    std::vector<uint8_t>().swap(p.plen);
   }
   return img;
 }

@@ -26,6 +26,7 @@ struct IndexArgs {
   const uint8_t* tf8;       // their 1-byte tfs (ListDev::tf8)
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
+  const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,

@@ -1139,7 +1139,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
     uint64_t floor = 0;                            // score floor word
     // D: a decoded block and its loads in flight
-    uint32_t da0 = 0, da1 = 0, dc0 = 0, dc1 = 0;   // docs, doc-length words
+    uint32_t da0 = 0, da1 = 0, dcw = 0;            // docs, doc-length codes (2 bytes of a word)
     uint32_t dt0 = 0, dt1 = 0, dt2 = 0;            // driver tf pack words
     uint32_t dtb = 1, dtrel = 0;                   //   (uniform: width, blob offset)
     uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap words
@@ -1208,10 +1208,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
       Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? Y.hx1 : 0u), &w);
       Y.hh0 = h0; Y.hh1 = h1;
       Y.ha0 = X.da0; Y.ha1 = X.da1;
-      Y.hc0 = (X.dc0 >> ((X.da0 & 3u) << 3)) & 0xFFu;
-      Y.hc1 = (X.dc1 >> ((X.da1 & 3u) << 3)) & 0xFFu;
-      if (!X.dok0 || X.da0 >= ix.n_c4) Y.hc0 = 0;   // doc beyond the length records
-      if (!X.dok1 || X.da1 >= ix.n_c4) Y.hc1 = 0;
+      Y.hc0 = (X.dcw >> ((l & 1u) << 4)) & 0xFFu;
+      Y.hc1 = (X.dcw >> (((l & 1u) << 4) + 8)) & 0xFFu;
       uint32_t t0, t1;
       pair_values(X.dt0, X.dt1, X.dt2, pair_shift(X.dtrel, X.dtb), X.dtb, t0, t1);
       Y.ht0 = X.dtl ? ttf0 : t0;
@@ -1238,9 +1236,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
       const bool in1 = !single && ok1 && a1 - lo < span;
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
-      uint32_t w;
-      Y.dc0 = byte_word(ix.c4 + ((ok0 && a0 < ix.n_c4) ? a0 : 0u), &w);
-      Y.dc1 = byte_word(ix.c4 + ((ok1 && a1 < ix.n_c4) ? a1 : 0u), &w);
+      // doc-length codes of postings 2l, 2l+1: one line per block (plen)
+      Y.dcw = reinterpret_cast<const uint32_t*>(ix.plen)[(A.blk0 + (live ? j : b0)) * 32u + (l >> 1)];
       Y.dtb = (m >> 8) ? (m >> 8) : 1u;
       Y.dtrel = uni(S.dblk[bi].w);
       uint32_t sh;
@@ -1411,8 +1408,9 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       g.al1 = 2 * l + 1 < cnt && g.a1 >= ix.doc_lo && g.a1 < ix.doc_hi;
       g.ok0 = g.al0 && g.a0 < ix.n_c4;
       g.ok1 = g.al1 && g.a1 < ix.n_c4;
-      g.c0 = ix.c4[g.ok0 ? g.a0 : 0u];
-      g.c1 = ix.c4[g.ok1 ? g.a1 : 0u];
+      // doc-length codes of postings 2l, 2l+1 (plen word, bytes picked at use)
+      g.c0 = reinterpret_cast<const uint32_t*>(ix.plen)[(A.blk0 + b) * 32u + (l >> 1)];
+      g.c1 = g.c0;
       const uint32_t tbits = (m >> 8) ? (m >> 8) : 1u;
       const uint8_t* tp = ix.blob + A.base + tf_rel;
       g.ta0 = pack_tf(tp, tbits, 2 * l);
@@ -1449,8 +1447,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       bool al0 = cs.al0, al1 = cs.al1;
       WSR_T(1)
       double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
-      const double nrm0 = S.norm[cs.ok0 ? cs.c0 : 0u];
-      const double nrm1 = S.norm[cs.ok1 ? cs.c1 : 0u];
+      const double nrm0 = S.norm[cs.ok0 ? (cs.c0 >> ((l & 1u) << 4)) & 0xFFu : 0u];
+      const double nrm1 = S.norm[cs.ok1 ? (cs.c1 >> (((l & 1u) << 4) + 8)) & 0xFFu : 0u];
       const bool is_tail = dtail && b == b1 - 1;
       const uint32_t ta0 = is_tail ? S.dtt[2 * l] : cs.ta0;
       const uint32_t ta1 = is_tail ? S.dtt[2 * l + 1] : cs.ta1;
