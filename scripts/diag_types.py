@@ -44,7 +44,8 @@ for name, qs in cls.items():
     for _ in range(args.repeat):
         b.run()
     st = b.stats()
-    print(f"{name:10s} n={len(qs)} plan={st.plan_ms:.3f} seg={st.segment_ms:.3f} replay={st.replay_ms:.3f} "
+    print(f"{name:10s} n={len(qs)} plan={st.plan_ms:.3f} seg={st.segment_ms:.3f} lean={st.lean_ms:.3f} "
+          f"replay={st.replay_ms:.3f} "
           f"items={st.work_items} surv={st.survivors} dblk={st.driver_blocks} oblk={st.other_blocks} "
           f"algoMB={st.algo_bytes/1e6:.1f} events={st.events} maxqev={st.max_query_events}", flush=True)
     n_wg, stride = C.c_int32(), C.c_int32()
@@ -56,12 +57,17 @@ for name, qs in cls.items():
     print(f"   wg={n_wg.value} driver blocks per wg: mean={sum(db)/len(db):.1f} max={db[-1]} "
           f"p50={db[len(db)//2]} p99={db[int(len(db)*0.99)]}")
     if stride.value >= 10:
-        names = ["setup", "driver", "dense", "blocks", "topk"]
+        names = (["setup", "driver", "dense", "blocks", "topk"] if os.environ.get("WSR_DIAG_GENERAL")
+                 else ["setup", "segment", "finish", "dequeue", "-"])
         tot = [sum(r[4 + i] for r in rows) for i in range(5)]
         wall = sorted(r[9] for r in rows)
         allc = sum(tot)
         print("   sections: " + " ".join(f"{n}={100*t/allc:.1f}%" for n, t in zip(names, tot)) +
               f" | wg cycles mean={sum(wall)/len(wall):.0f} p50={wall[len(wall)//2]} max={wall[-1]}"
               f" | cycles/driver block={allc/max(1,sum(db)):.0f}")
+        if not os.environ.get("WSR_DIAG_GENERAL"):
+            st = [sum(r[10 + i] for r in rows) for i in range(4)]
+            print("   lean stages per driver block: " +
+                  " ".join(f"{n}={t/max(1,sum(db)):.0f}" for n, t in zip("WCHD", st)))
     b.close()
 print("class sizes:", {k: len(v) for k, v in cls.items()})

@@ -75,6 +75,7 @@ struct wsr_handle {
   DenseEnt* d_dense = nullptr;
   uint8_t* d_tf8 = nullptr;
   uint8_t* d_plen = nullptr;
+  uint32_t* d_tails = nullptr;
   uint32_t dense_lists = 0;
   bool fuse_replay = true;
   bool seg_floor = true;
@@ -84,12 +85,14 @@ struct wsr_handle {
   std::vector<uint32_t> meta;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
+  int gen_cap = 0;     // general workgroups launched at most
 };
 
 struct wsr_batch {
   int max_q = 0, stride = 0, nq = 0;
   QueryIn* d_q = nullptr;
   QueryPlan* d_plan = nullptr;
+  QueryDesc* d_desc = nullptr;     // lean queries' work records
   uint32_t* d_ctr = nullptr;
   Event* d_events = nullptr;
   uint64_t ev_cap = 0;
@@ -159,6 +162,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     dev_upload(&h->d_blob, img.blob);
     dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
+    dev_upload(&h->d_tails, img.tails);
+    h->args.tails = h->d_tails;
     dev_upload(&h->d_lists, img.lists);
     dev_upload(&h->d_blocks, img.blocks);
     dev_upload(&h->d_last, img.blk_last);
@@ -191,6 +196,9 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     int occ = segment_kernel_occupancy();
     if (occ < 1) occ = 1;
     h->grid = prop.multiProcessorCount * std::min(occ, 32);
+    // general workers hold 12 KB of LDS each: at most 4 per CU, so that the
+    // concurrent lean kernel keeps its occupancy
+    h->gen_cap = prop.multiProcessorCount * std::min(std::min(occ, 32), 4);
     int locc = lean_kernel_occupancy();
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
@@ -213,7 +221,7 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8),
-                  static_cast<void*>(h->d_plen)})
+                  static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails)})
     if (p) (void)hipFree(p);
   delete h;
 }
@@ -255,6 +263,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     b->stride = stride;
     HIP_OK(hipMalloc(&b->d_q, sizeof(QueryIn) * max_q));
     HIP_OK(hipMalloc(&b->d_plan, sizeof(QueryPlan) * max_q));
+    HIP_OK(hipMalloc(&b->d_desc, sizeof(QueryDesc) * max_q));
     HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
@@ -274,6 +283,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (!b) return;
   if (h && h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
+                  static_cast<void*>(b->d_desc),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
                   static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
@@ -292,6 +302,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   std::lock_guard<std::mutex> g(h->mu);
   std::vector<QueryIn> in(nq);
   uint64_t ev_need = 0, items_need = 0, algo = 0;
+  // the device's class rule (plan_query_kernel), restated to size the two
+  // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
+  uint64_t lean_need = 0, gen_need = 0;
+  const float dense_ratio = h->args.dense_ratio;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
     if (s.n_terms > WSR_MAX_TERMS || s.k > WSR_MAX_K || s.k > b->stride)
@@ -312,6 +326,17 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     if (ok && nbmin > 0) {
       ev_need += (static_cast<uint64_t>(nbmin) + kSegCostMax) * 128;
       items_need += nbmin;
+      int drv = 0;
+      for (int t = 1; t < d.n_terms; ++t)
+        if (h->lists[d.list[t]].nblk < h->lists[d.list[drv]].nblk) drv = t;
+      bool lean = true;
+      for (int t = 0; t < d.n_terms; ++t) {
+        const ListDev& L = h->lists[d.list[t]];
+        if (t != drv && !(L.bm != kNoDense &&
+                          static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin)))
+          lean = false;
+      }
+      (lean ? lean_need : gen_need) += nbmin;
       for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[d.list[t]];
       algo += 12ull * d.k;
     }
@@ -341,9 +366,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   }
   b->nq = nq;
   // persistent grid: never more workgroups than work items can exist
-  b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->grid, items_need)));
+  // (at least one worker each: a grid also drains items the estimate missed)
+  b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
-      1, std::min<uint64_t>(h->lean_wgs, (items_need + kLeanWaves - 1) / kLeanWaves)));
+      1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -367,7 +393,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
                        kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq,
-                       h->seg_floor ? b->d_pub : nullptr, st));
+                       h->seg_floor ? b->d_pub : nullptr, b->d_desc, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
     // own queue, then the streams join
@@ -379,7 +405,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipEventRecord(h->ev_join, h->stream2));
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
-                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, st));
+                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, h->ev_join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));

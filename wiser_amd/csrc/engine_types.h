@@ -19,8 +19,12 @@ struct ListDev {
   double idf;         // calc_es_idf(N, df) computed on the host with libm log
   uint64_t bm;        // first DenseEnt of the list's doc bitmap, kNoDense when it has none
   uint64_t tf8;       // byte offset of the list's 1-byte tf array (posting order)
+  uint64_t tail;      // its last block decoded (tail_cnt doc ids, then tail_cnt tfs) in the
+                      // image's tails array when that block is a VInts blob, else kNoTail
+  uint64_t pad;
 };
-static_assert(sizeof(ListDev) == 48, "ListDev layout");
+static_assert(sizeof(ListDev) == 64, "ListDev layout");
+constexpr uint64_t kNoTail = ~0ull;
 
 constexpr uint64_t kNoDense = ~0ull;
 constexpr uint32_t kDenseDocs = 32;   // doc ids per DenseEnt
@@ -62,6 +66,25 @@ struct QueryPlan {
   uint64_t ev_base;     // first event slot (capacity = driver blocks * 128)
 };
 static_assert(sizeof(QueryPlan) == 24, "QueryPlan layout");
+
+// Per-query work description of a lean query (every other list probed by
+// bitmap, or a single term), written by the plan kernels so that a lean item's
+// setup is one load of this record.
+struct QueryDesc {
+  uint64_t a_base;      // driver: blob base of its [docid | tf] span
+  uint64_t a_tail;      //   decoded VInts last block (ListDev::tail)
+  uint64_t o_bm;        // O1 (the other list with the fewest blocks): first bitmap entry
+  uint64_t o_tf8;       //   offset of its 1-byte tfs
+  uint64_t ev_base;     // = QueryPlan::ev_base
+  double a_idf, o_idf;
+  uint32_t a_blk0, a_nblk, a_tail_cnt;
+  uint32_t min_last;    // smallest last doc id over the other lists
+  uint32_t item_base, n_items, seg;
+  uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16 | k << 24
+  uint32_t o_list;      // O1's list id
+  uint32_t pad[9];
+};
+static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
 
 // A heap-insertion event: a survivor that a top-k heap run from empty over its
 // segment inserts (query_processing.h:595-602).

@@ -210,6 +210,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     std::vector<DenseEnt> dense;   // rank bitmap (dense lists only)
     std::vector<uint8_t> tf8;
     std::vector<uint8_t> plen;     // doc-length code of every posting, 128 per block
+    std::vector<uint32_t> tail;    // VInts last block decoded: doc ids, then tfs
   };
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
   std::vector<Part> parts(L);
@@ -306,6 +307,14 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
             throw std::runtime_error("cannot decode a block of '" + idx.term(id) + "'");
           uint8_t* o = &pt.plen[(r - r0) * kPackSize];
           for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
+          if (r + 1 == nrows && (pt.meta.back() & 0xFF) == 0) {
+            // the list's VInts tail, decoded once (the kernels read it as words)
+            uint32_t tfs[kPackSize];
+            if (!host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, tfs))
+              throw std::runtime_error("cannot decode the tf tail of '" + idx.term(id) + "'");
+            pt.tail.assign(docs, docs + cnt);
+            pt.tail.insert(pt.tail.end(), tfs, tfs + cnt);
+          }
         }
         const uint64_t n_img = (r1 - r0 - 1) * kPackSize + pt.tail_cnt;
         if (dense_div && span && n_img * dense_div >= span) build_dense(pt, rows, r0, r1, n_img);
@@ -345,6 +354,13 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     ld.idf = idx.idf(id);
     ld.bm = kNoDense;
     ld.tf8 = 0;
+    ld.tail = kNoTail;
+    ld.pad = 0;
+    if (!p.tail.empty()) {
+      ld.tail = img.tails.size();
+      img.tails.insert(img.tails.end(), p.tail.begin(), p.tail.end());
+      std::vector<uint32_t>().swap(p.tail);
+    }
     if (!p.dense.empty()) {
       ld.bm = img.dense.size();
       ld.tf8 = img.tf8.size();

@@ -82,6 +82,7 @@ struct HostImage {
   std::vector<uint8_t> tf8;     // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
   uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
   uint32_t dense_lists = 0;
+  std::vector<uint32_t> tails;  // decoded VInts last blocks (ListDev::tail)
   std::vector<uint8_t> plen;    // doc-length code (Char4) of every posting: block j of the
                                 // image at [j * 128, j * 128 + 128), 0 past the length records
 };

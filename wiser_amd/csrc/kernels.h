@@ -27,6 +27,7 @@ struct IndexArgs {
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
+  const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
@@ -73,7 +74,7 @@ struct FusedReplay {
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
-                       uint64_t* pub, hipStream_t st);
+                       uint64_t* pub, QueryDesc* desc, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,
@@ -82,7 +83,7 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, hipStream_t st);
+                       uint64_t* pub, const QueryDesc* desc, hipStream_t st);
 int lean_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,

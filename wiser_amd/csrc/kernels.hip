@@ -329,7 +329,8 @@ __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev
 // decodes) and the item count.  item_base / ev_base are filled by pass 2.
 __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                          int nq, QueryPlan* __restrict__ plan,
-                                                         uint32_t* __restrict__ counters, FusedReplay fr) {
+                                                         uint32_t* __restrict__ counters, FusedReplay fr,
+                                                         QueryDesc* __restrict__ desc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
   const QueryIn q = qs[i];
@@ -378,6 +379,41 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
     p.seg_blocks = seg;
     p.n_items = (nd + seg - 1) / seg;
+    if (lean) {
+      // the lean kernel's record: driver, the most selective other list (O1),
+      // the smallest last doc of the others (bases are added by item_map_kernel)
+      const ListDev A = ix.lists[q.list[d]];
+      QueryDesc D;
+      D.a_base = A.base;
+      D.a_tail = A.tail;
+      D.a_idf = A.idf;
+      D.a_blk0 = A.blk0;
+      D.a_nblk = A.nblk;
+      D.a_tail_cnt = A.tail_cnt;
+      uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
+      for (int s = 0; s < q.n_terms; ++s) {
+        if (s == static_cast<int>(d)) continue;
+        const ListDev B = ix.lists[q.list[s]];
+        const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
+        min_last = bl < min_last ? bl : min_last;
+        if (B.nblk < o_nb) { o1 = s; o_nb = B.nblk; }
+      }
+      D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
+      if (o1 < kMaxTerms) {
+        const ListDev O = ix.lists[q.list[o1]];
+        D.o_bm = O.bm; D.o_tf8 = O.tf8; D.o_idf = O.idf;
+        D.o_list = static_cast<uint32_t>(q.list[o1]);
+      }
+      D.min_last = min_last;
+      D.ev_base = 0;
+      D.item_base = 0;
+      D.n_items = p.n_items;
+      D.seg = seg;
+      D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16) |
+                (static_cast<uint32_t>(q.k) << 24);
+      for (int t = 0; t < 9; ++t) D.pad[t] = 0;
+      desc[i] = D;
+    }
   }
   plan[i] = p;
   if (fr.q_done) {
@@ -483,10 +519,15 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
 __global__ __launch_bounds__(256) void item_map_kernel(const QueryPlan* __restrict__ plan, int nq,
                                                        const uint32_t* __restrict__ counters,
                                                        uint32_t* __restrict__ item_q,
-                                                       uint64_t* __restrict__ pub) {
+                                                       uint64_t* __restrict__ pub,
+                                                       QueryDesc* __restrict__ desc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq || (counters[kCtrError] & kErrCapacity)) return;
   const QueryPlan p = plan[i];
+  if (p.driver & kPlanLean) {
+    desc[i].item_base = p.item_base;
+    desc[i].ev_base = p.ev_base;
+  }
   for (uint32_t j = 0; j < p.n_items; ++j) {
     item_q[p.item_base + j] = static_cast<uint32_t>(i);
     if (pub) pub[p.item_base + j] = 0;
@@ -859,19 +900,32 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
 __device__ __forceinline__ uint32_t next_item(uint32_t* heads, uint32_t lo, uint32_t hi,
                                               uint32_t& shard, uint32_t& tried) {
   const uint32_t n = hi - lo;
+  const uint32_t l = threadIdx.x & 63;
   while (tried < kQueueShards) {
-    uint32_t* head = &heads[16 * shard];
+    // the current shard: a load first, so that drained heads see no
+    // read-modify-write from thousands of finishing workers
     const uint32_t limit = (n + kQueueShards - 1 - shard) / kQueueShards;
     uint32_t local = 0;
-    if ((threadIdx.x & 63) == 0) {
-      local = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (local < limit) local = atomicAdd(head, 1u);
+    if (l == 0) {
+      local = __hip_atomic_load(&heads[16 * shard], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (local < limit) local = atomicAdd(&heads[16 * shard], 1u);
     }
     local = uni(local);
     if (local < limit) return lo + shard + kQueueShards * local;
-    shard = (shard + 1) % kQueueShards;
+    // drained (a drained shard stays drained): read all heads in one round
+    // and move to the next shard that still has work
+    uint32_t h = 0, lim = 0;
+    if (l < kQueueShards) {
+      h = __hip_atomic_load(&heads[16 * l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lim = (n + kQueueShards - 1 - l) / kQueueShards;
+    }
+    const uint32_t avail = static_cast<uint32_t>(__ballot(l < kQueueShards && h < lim));
+    if (!avail) break;
+    const uint32_t rot = ((avail >> shard) | (avail << (kQueueShards - shard))) & ((1u << kQueueShards) - 1u);
+    shard = (shard + __builtin_ctz(rot)) % kQueueShards;
     ++tried;
   }
+  tried = kQueueShards;
   return hi;
 }
 
@@ -883,7 +937,7 @@ __device__ __forceinline__ uint32_t next_item(uint32_t* heads, uint32_t lo, uint
 // replay reads the other items' events with coherent loads).
 template <bool kWave>
 __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* plan, uint32_t qi,
-                                            const QueryPlan& P, uint32_t item,
+                                            uint32_t n_items, uint32_t item,
                                             const uint64_t* prev_pub, Event* ev_out, uint32_t ev_n,
                                             const Event* events, uint32_t* ev_cnt,
                                             const FusedReplay& fr, uint32_t* s_off) {
@@ -921,7 +975,7 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     if (l == 0)
       old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = uni(old);
-    if (old + 1 == P.n_items)
+    if (old + 1 == n_items)
       replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
                         fr.n_hits, s_off);
   }
@@ -951,6 +1005,20 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
 #endif
 
 // ------------------------------------------------- lean bitmap segment --
+// Stage timers of the diagnostics build (-DWSR_PROFILE): cycles charged to
+// prof[0..3] = W, C (compaction + scoring), H, D of the lean pipeline.
+#ifdef WSR_PROFILE
+#define LT0() uint64_t lt_t = __builtin_amdgcn_s_memtime();
+#define LT(i)                                                         \
+  {                                                                   \
+    const uint64_t now = __builtin_amdgcn_s_memtime();                \
+    if (prof) prof[i] += static_cast<uint32_t>(now - lt_t);          \
+    lt_t = now;                                                       \
+  }
+#else
+#define LT0()
+#define LT(i)
+#endif
 // Byte loads of the pipeline are whole aligned dwords, kept raw until the
 // consuming stage extracts the byte (an extraction next to the load would make
 // the loop wait for it in the iteration that issued it).
@@ -1003,53 +1071,61 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 struct LeanLds {
   uint32_t q[1024];     // survivor queue (4 rings of 256); at item start the driver's VInts
                         // tail decode, at item end the replay's segment scan
-  Event evs[64];        // events of one scoring chunk, stored together
+  Event evs[128];       // events buffered in LDS, stored when half full and at the end
   uint4 dblk[64];       // the driver's directory entries of the segment
   uint32_t dmeta[64];
+#ifdef WSR_PROFILE
+  uint32_t prof[4];     // lean pipeline stage cycles (diagnostics build)
+#endif
 };
 
 // o1 == kMaxTerms: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
 __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, const double* norm_tab,
-                                             const int32_t* qlist,
-                                             uint32_t nt, uint32_t d, uint32_t o1, uint32_t k,
-                                             const ListDev& A, uint32_t b0, uint32_t b1, bool dtail,
+                                             const QueryDesc& Q, const int32_t* qlist,
+                                             uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
-                                             uint32_t min_last, const uint64_t* prev_pub,
-                                             uint64_t* my_pub, Event* ev_out, uint32_t& ev_n,
+                                             const uint64_t* prev_pub, uint64_t* my_pub,
+                                             Event* ev_out, uint32_t& ev_n,
                                              double& pt, uint32_t& pt_n,
-                                             double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
+                                             double& last_pub, uint32_t& n_surv, uint32_t& n_dblk,
+                                             uint32_t* prof) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
+  const uint32_t d = Q.slots & 0xFFu, o1 = (Q.slots >> 8) & 0xFFu;
+  const uint32_t nt = (Q.slots >> 16) & 0xFFu, k = Q.slots >> 24;
+  const uint32_t min_last = Q.min_last;
   const bool single = o1 >= kMaxTerms;
-  const ListDev O = ix.lists[qlist[single ? d : o1]];
-  // (single term: a dummy bitmap read, hits are the driver's postings)
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
   const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
-                             : reinterpret_cast<const uint2*>(ix.dense + O.bm);
-  const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + O.tf8;
+                             : reinterpret_cast<const uint2*>(ix.dense + Q.o_bm);
+  const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
+  const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
   const uint32_t lo = ix.doc_lo, span = ix.dense_span;
   const uint32_t hi_rel = ix.doc_hi - ix.doc_lo;   // docs a with a - lo < hi_rel are in the image
-  const double idf_d = A.idf, idf_o = O.idf;
+  const double idf_d = Q.a_idf, idf_o = Q.o_idf;
   uint32_t* qdoc = S.q;             // survivor queue (ring of 256)
   uint32_t* qc4 = qdoc + 256;
   uint32_t* qtd = qdoc + 512;
   uint32_t* qto = qdoc + 768;       // tf byte, or 0x80000000 | posting index when escaped
   uint32_t qhead = 0, qtail = 0;
   uint32_t bend = b1;
-  uint64_t floor_bits = 0;
-  // the floor is loaded every iteration (a fixed load count per iteration);
-  // without an earlier segment a valid global word is read and ignored
-  const uint64_t* floor_src = prev_pub ? prev_pub : reinterpret_cast<const uint64_t*>(ix.lists);
-  const bool has_floor = prev_pub != nullptr;
+  // The loop issues only plain loads: coherent (agent-scope) loads, stores
+  // and atomics take longer to complete and, counted in order with the loads,
+  // would hold up every wait behind them.  So the score floor is read once,
+  // here; the segment's own k-th best is published once, at the end; events
+  // stay in LDS until 64 are pending (a chunk adds at most 64).  The final
+  // re-filter in finish_item applies the floor as it stands at the end.
+  const uint64_t floor_bits =
+      prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  double pub_val = 0.0;
 
-  // a chunk's events (at most 64) to ev_out, after its top-k loop so the loop
-  // itself holds no stores
   auto flush = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
     if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
+    if (l + 64 < evb) store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[l + 64]);
     __builtin_amdgcn_wave_barrier();
     evb = 0;
   };
@@ -1065,6 +1141,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     __builtin_amdgcn_wave_barrier();
     qhead += n;
     if (__ballot(alive && (to & 0x80000000u))) {
+      const ListDev O = ix.lists[Q.o_list];
       if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
     }
     const double norm = norm_tab[c4 & 255u];
@@ -1089,7 +1166,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     n_surv += __popcll(am);
     // running top-k: candidates beat the k-th best so far and the floor of the
     // query's earlier segments (scores are > 0, so bits order as values)
-    const uint64_t fb = has_floor ? floor_bits : 0ull;
+    const uint64_t fb = floor_bits;
     const double flo = __longlong_as_double(static_cast<long long>(
         (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
         uni(static_cast<uint32_t>(fb))));
@@ -1117,17 +1194,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
         pt_n = pt_n + 1 > k ? k : pt_n + 1;
       }
     }
-    if (evb) flush();
-    if (my_pub) {
-      const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-      const double pv = kn > flo ? kn : flo;
-      if (pv > last_pub) {
-        if (l == 0)
-          __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pv)),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_pub = pv;
-      }
-    }
+    if (evb >= 64) flush();
+    const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    const double pv = kn > flo ? kn : flo;
+    pub_val = pv > pub_val ? pv : pub_val;
   };
 
   // Pipeline registers, in two alternating sets: iteration j reads set X
@@ -1137,7 +1207,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
   struct Regs {
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
     uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
-    uint64_t floor = 0;                            // score floor word
     // D: a decoded block and its loads in flight
     uint32_t da0 = 0, da1 = 0, dcw = 0;            // docs, doc-length codes (2 bytes of a word)
     uint32_t dt0 = 0, dt1 = 0, dt2 = 0;            // driver tf pack words
@@ -1149,11 +1218,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     uint32_t hf0 = 0, hf1 = 0, hx0 = 0, hx1 = 0;   // O1 tf byte words (in flight), posting ranks
     bool hh0 = false, hh1 = false;
   };
-  Regs RA, RB;
+  Regs R0, R1;
   // byte shift of a pair's first value inside its aligned dword (pair_words)
   auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
     const uint32_t bit = 2 * l * bits;
-    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ix.blob + A.base)) + rel + 2 +
+    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + rel + 2 +
                        (bit >> 3);
     return ((a & 3u) << 3) + (bit & 7u);
   };
@@ -1165,15 +1234,15 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     Y.wbits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
     Y.wrel = uni(S.dblk[bi].z);
     uint32_t sh;
-    pair_words(ix.blob + A.base + Y.wrel + 2, Y.wbits, l, Y.w0, Y.w1, Y.w2, sh);
-    Y.floor = __hip_atomic_load(floor_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pair_words(a_blob + Y.wrel + 2, Y.wbits, l, Y.w0, Y.w1, Y.w2, sh);
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    // W(j+1): issued first, so it has a whole iteration to arrive
+    LT0()
+    // W(j+1): the doc-id words of block j+1
     issue_words(j + 1, Y);
+    LT(0)
     // C(j-2): compaction of block j-2 (its H fields are in X)
     if (j >= b0 + 2) {
-      floor_bits = X.floor;
       const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
       const uint32_t f0 = single ? 0u : (X.hf0 >> xs0) & 0xFFu;
       const uint32_t f1 = single ? 0u : (X.hf1 >> xs1) & 0xFFu;
@@ -1194,6 +1263,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
 #pragma nounroll
       for (int c = 0; c < 2 && qtail - qhead >= 64; ++c) score_chunk(64);
     }
+    LT(1)
     // H(j-1): block j-1 (D fields in X): O1 hits, its driver tfs and length
     // codes extracted, into Y's H fields
     {
@@ -1215,13 +1285,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
       Y.ht0 = X.dtl ? ttf0 : t0;
       Y.ht1 = X.dtl ? ttf1 : t1;
     }
+    LT(2)
     // D(j): decode block j from X's words into Y, issue its loads
     {
       const bool live = j < bend;
       const uint32_t bi = live ? j - b0 : 0u;
       const uint32_t prev = uni(S.dblk[bi].x);
       const uint32_t m = uni(S.dmeta[bi]);
-      const uint32_t cnt = live ? ((j == A.nblk - 1) ? A.tail_cnt : 128u) : 0u;
+      const uint32_t cnt = live ? ((j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
       pair_values(X.w0, X.w1, X.w2, pair_shift(X.wrel, X.wbits), X.wbits, x0, x1);
       const uint32_t sm = x0 + x1;
@@ -1237,24 +1308,30 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
       // doc-length codes of postings 2l, 2l+1: one line per block (plen)
-      Y.dcw = reinterpret_cast<const uint32_t*>(ix.plen)[(A.blk0 + (live ? j : b0)) * 32u + (l >> 1)];
+      Y.dcw = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (live ? j : b0)) * 32u + (l >> 1)];
       Y.dtb = (m >> 8) ? (m >> 8) : 1u;
       Y.dtrel = uni(S.dblk[bi].w);
       uint32_t sh;
-      pair_words(ix.blob + A.base + Y.dtrel + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, sh);
+      pair_words(a_blob + Y.dtrel + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, sh);
       Y.da0 = a0; Y.da1 = a1; Y.dok0 = ok0; Y.dok1 = ok1; Y.dtl = tl;
       if (live) ++n_dblk;
       // past the smallest last doc of the other lists nothing later can match
       if (live && __ballot((ok0 && a0 > min_last) || (ok1 && a1 > min_last))) bend = j + 1;
     }
+    LT(3)
   };
-  if (b0 < b1) issue_words(b0, RA);
+  issue_words(b0, R0);
   for (uint32_t j = b0; j < bend + 2; j += 2) {
-    body(RA, RB, j);
+    body(R0, R1, j);
     if (j + 1 >= bend + 2) break;
-    body(RB, RA, j + 1);
+    body(R1, R0, j + 1);
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
+  if (evb) flush();
+  if (my_pub && pub_val > last_pub && l == 0)
+    __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  last_pub = pub_val;
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1659,7 +1736,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       step(sb, sa, b + 1);
     }
     if (evb) flush_events(evb);
-    finish_item<false>(qs, plan, qi, P, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.roff);
+    finish_item<false>(qs, plan, qi, P.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.roff);
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
@@ -1689,7 +1766,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
-    uint64_t* __restrict__ pub) {
+    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc) {
   __shared__ LeanLds SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
@@ -1703,71 +1780,67 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
   uint32_t n_surv = 0, n_dblk = 0;
   uint32_t shard = wid % kQueueShards, tried = 0;
   uint32_t item = wid;
+#ifdef WSR_PROFILE
+  uint32_t* prof = S.prof;
+  for (int i = 0; i < 4; ++i) prof[i] = 0;
+#else
+  uint32_t* prof = nullptr;
+#endif
+  WSR_T0()
   for (;;) {
     if (item >= n_lean) item = next_item(&counters[kCtrHead0], 0, n_lean, shard, tried);
+    WSR_T(3)
     if (item >= n_lean) break;
     const uint32_t qi = uni(item_q[item]);
-    const QueryPlan P = plan[qi];
-    const int32_t* qlist = qs[qi].list;
-    const uint32_t r = item - P.item_base;
-    const uint32_t d = uni(P.driver & 0xFFu);
-    const uint32_t nt = uni(static_cast<uint32_t>(qs[qi].n_terms));
-    const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
-    const ListDev A = ix.lists[qlist[d]];
-    const uint32_t seg = uni(P.seg_blocks);
+    const QueryDesc Q = desc[qi];   // everything the item's setup needs, one record
+    const uint32_t r = item - Q.item_base;
+    const uint32_t seg = Q.seg;
     const uint32_t b0 = r * seg;
-    const uint32_t b1 = min(b0 + seg, A.nblk);
-    Event* ev_out = events + P.ev_base + static_cast<uint64_t>(r) * seg * 128;
+    const uint32_t b1 = min(b0 + seg, Q.a_nblk);
+    Event* ev_out = events + Q.ev_base + static_cast<uint64_t>(r) * seg * 128;
     uint64_t* my_pub = pub ? pub + item : nullptr;
     const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
 
+    // the segment's directory entries and the driver's decoded VInts tail:
+    // one round of loads
     __builtin_amdgcn_wave_barrier();
     if (b0 + l < b1) {
-      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[A.blk0 + b0 + l];
-      S.dmeta[l] = ix.blk_meta[A.blk0 + b0 + l];
+      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + b0 + l];
+      S.dmeta[l] = ix.blk_meta[Q.a_blk0 + b0 + l];
+    }
+    const bool dtail = b0 < b1 && b1 == Q.a_nblk && Q.a_tail != kNoTail;
+    uint32_t tdoc0 = 0, tdoc1 = 0, ttf0 = 0, ttf1 = 0;
+    if (dtail) {
+      const uint32_t cnt = Q.a_tail_cnt;
+      const uint32_t* t = ix.tails + Q.a_tail;
+      if (2 * l < cnt) { tdoc0 = t[2 * l]; ttf0 = t[cnt + 2 * l]; }
+      if (2 * l + 1 < cnt) { tdoc1 = t[2 * l + 1]; ttf1 = t[cnt + 2 * l + 1]; }
     }
     __builtin_amdgcn_wave_barrier();
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
-    bool done = false;
-    uint32_t o1 = kMaxTerms, o1_nblk = 0xFFFFFFFFu;   // the most selective other list
-    uint32_t min_last = 0xFFFFFFFFu;                  // smallest last doc of the others
-    for (uint32_t s = 0; s < nt; ++s) {
-      if (s == d) continue;
-      const ListDev B = ix.lists[qlist[s]];
-      const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
-      if (first_doc > bl) done = true;
-      min_last = bl < min_last ? bl : min_last;
-      if (B.nblk < o1_nblk) { o1 = s; o1_nblk = B.nblk; }
-    }
-    // the driver's VInts tail block, decoded once into registers (2 per lane)
-    bool dtail = false;
-    uint32_t tdoc0 = 0, tdoc1 = 0, ttf0 = 0, ttf1 = 0;
-    if (b0 < b1) {
-      const uint32_t bi = b1 - 1 - b0;
-      const uint32_t mt = uni(S.dmeta[bi]);
-      dtail = (mt & 0xFF) == 0;
-      if (dtail) {
-        decode_block<true>(ix.blob + A.base + uni(S.dblk[bi].z), 0, A.tail_cnt, true,
-                           uni(S.dblk[bi].x), S.q);
-        decode_block<true>(ix.blob + A.base + uni(S.dblk[bi].w), mt >> 8, A.tail_cnt, false, 0,
-                           S.q + 256);
-        tdoc0 = S.q[2 * l]; tdoc1 = S.q[2 * l + 1];
-        ttf0 = S.q[256 + 2 * l]; ttf1 = S.q[256 + 2 * l + 1];
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
+    // an other list ends before this segment: nothing in it can match
+    const bool done = first_doc > Q.min_last;
+    WSR_T(0)
+    // a query of one item with fused replay: the heap runs here, no events
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
-    if (!done)
-      lean_segment(ix, S, norm, qlist, nt, d, o1, k, A, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
-                   min_last, prev_pub, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
-    finish_item<true>(qs, plan, qi, P, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
+    if (!done && b0 < b1)
+      lean_segment(ix, S, norm, Q, qs[qi].list, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
+                   my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
+    WSR_T(1)
+    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
+    WSR_T(2)
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
     stats[wid * kStatStride + 0] = n_surv;
     stats[wid * kStatStride + 1] = n_dblk;
     stats[wid * kStatStride + 2] = 0;
+#ifdef WSR_PROFILE
+    for (int i = 0; i < 5; ++i) stats[wid * kStatStride + 4 + i] = prof_acc[i];
+    stats[wid * kStatStride + 9] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - prof_start);
+    for (int i = 0; i < 4; ++i) stats[wid * kStatStride + 10 + i] = prof[i];
+#endif
   }
 }
 
@@ -1875,15 +1948,15 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
-                       uint64_t* pub, hipStream_t st) {
+                       uint64_t* pub, QueryDesc* desc, hipStream_t st) {
   if (nq > 0)
     hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
-                       counters, fr);
+                       counters, fr, desc);
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
                      item_capacity, static_cast<uint32_t>(lean_grid), static_cast<uint32_t>(seg_grid));
   if (nq > 0)
     hipLaunchKernelGGL(item_map_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, plan, nq, counters,
-                       item_q, pub);
+                       item_q, pub, desc);
   return hipGetLastError();
 }
 
@@ -1899,9 +1972,9 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, hipStream_t st) {
+                       uint64_t* pub, const QueryDesc* desc, hipStream_t st) {
   hipLaunchKernelGGL(lean_kernel, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan, nq,
-                     counters, events, ev_cnt, stats, fr, item_q, pub);
+                     counters, events, ev_cnt, stats, fr, item_q, pub, desc);
   return hipGetLastError();
 }
 
