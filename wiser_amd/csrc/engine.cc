@@ -61,8 +61,6 @@ struct wsr_handle {
   std::mutex mu;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;   // general segment kernel, concurrent with the lean kernel
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   VacuumIndex idx;
   IndexArgs args{};
   uint8_t* d_blob = nullptr;
@@ -115,6 +113,11 @@ struct wsr_batch {
   size_t roff_cap = 0;
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
+  // Each batch runs on its own streams, so consecutive batches overlap on the
+  // device (one's plan and first items under the other's last items); the
+  // general kernel goes to st2, forked from and joined back into st.
+  hipStream_t st = nullptr, st2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   bool ran = false;
 };
 
@@ -188,9 +191,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.doc_hi = hi;
     h->args.avg = h->idx.avg_length();
     HIP_OK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+
     hipDeviceProp_t prop;
     HIP_OK(hipGetDeviceProperties(&prop, dev));
     int occ = segment_kernel_occupancy();
@@ -213,9 +214,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
 void wsr_close(wsr_handle* h) {
   if (!h) return;
   if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
-  if (h->stream2) { (void)hipStreamSynchronize(h->stream2); (void)hipStreamDestroy(h->stream2); }
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+
   for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
                   static_cast<void*>(h->d_meta),
@@ -271,6 +270,10 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
                                       (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&b->fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&b->join, hipEventDisableTiming));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
     return fail(WSR_E_HIP, e.what());
@@ -281,7 +284,8 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
 
 void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (!b) return;
-  if (h && h->stream) (void)hipStreamSynchronize(h->stream);
+  if (b->st) (void)hipStreamSynchronize(b->st);
+  if (b->st2) (void)hipStreamSynchronize(b->st2);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_desc),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
@@ -293,6 +297,10 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
+  if (b->fork) (void)hipEventDestroy(b->fork);
+  if (b->join) (void)hipEventDestroy(b->join);
+  if (b->st) (void)hipStreamDestroy(b->st);
+  if (b->st2) (void)hipStreamDestroy(b->st2);
   delete b;
 }
 
@@ -343,7 +351,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   }
   try {
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(b->st));
     if (ev_need > b->ev_cap) {
       if (b->d_events) HIP_OK(hipFree(b->d_events));
       b->ev_cap = ev_need + ev_need / 4 + 4096;
@@ -385,7 +393,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = h->stream;
+    hipStream_t st = b->st;
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * kNumCounters, st));
     const bool fused = replay && h->fuse_replay;
     FusedReplay fr{fused ? b->d_qdone : nullptr, b->d_hits, b->stride, b->d_nhits};
@@ -397,17 +405,17 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
     // own queue, then the streams join
-    HIP_OK(hipEventRecord(h->ev_fork, st));
-    HIP_OK(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    HIP_OK(hipEventRecord(b->fork, st));
+    HIP_OK(hipStreamWaitEvent(b->st2, b->fork, 0));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, fr, b->d_itemq,
-                           h->seg_floor ? b->d_pub : nullptr, h->stream2));
-    HIP_OK(hipEventRecord(h->ev_join, h->stream2));
+                           h->seg_floor ? b->d_pub : nullptr, b->st2));
+    HIP_OK(hipEventRecord(b->join, b->st2));
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
                        b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
-    HIP_OK(hipStreamWaitEvent(st, h->ev_join, 0));
+    HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
     if (replay && !fused)
       HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
@@ -422,7 +430,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
 
 int wsr_sync(wsr_handle* h) {
   if (!h) return fail(WSR_E_INVALID, "null argument");
-  hipError_t e = hipStreamSynchronize(h->stream);
+  hipError_t e = hipSetDevice(h->device);
+  if (e == hipSuccess) e = hipDeviceSynchronize();   // every batch's streams
   if (e != hipSuccess) return fail(WSR_E_HIP, hipGetErrorString(e));
   return WSR_OK;
 }
@@ -432,7 +441,7 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(b->st));
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
@@ -450,7 +459,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
   if (!h || !b || !out || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
   std::lock_guard<std::mutex> g(h->mu);
   try {
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(b->st));
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
@@ -521,7 +530,7 @@ int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = h->stream;
+    hipStream_t st = b->st;
     if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
     if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
     if (n_owners > 1024) return fail(WSR_E_LIMIT, "more than 1024 owners");
@@ -543,8 +552,8 @@ int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send) {
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(launch_pack_events(b->d_plan, b->nq, b->d_events, b->d_scount, b->d_soff,
-                              static_cast<Event*>(d_send), h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
+                              static_cast<Event*>(d_send), b->st));
+    HIP_OK(hipStreamSynchronize(b->st));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -559,7 +568,7 @@ int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, 
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = h->stream;
+    hipStream_t st = b->st;
     const size_t n = static_cast<size_t>(n_shards) * nq_owned;
     if (n > b->roff_cap) {
       if (b->d_roff) HIP_OK(hipFree(b->d_roff));
@@ -588,7 +597,7 @@ int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, w
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(b->st));
     if (nq && hits)
       HIP_OK(hipMemcpy(hits, b->d_hits + static_cast<size_t>(q0) * b->stride,
                        sizeof(HitDev) * static_cast<size_t>(nq) * b->stride, hipMemcpyDeviceToHost));
@@ -643,7 +652,7 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
   const size_t n = std::min<size_t>(static_cast<size_t>(std::max(max_words, 0)),
                                     static_cast<size_t>(kStatStride) * rows);
   try {
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(b->st));
     HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
