@@ -26,5 +26,5 @@ for counters in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_s
       python3 "$R/bench.py" --no-cpu --check 0 --steps 5 --warmup 1 > "$O/pmc_pass$i.json" 2> "$O/pmc_pass$i.err"
   echo "pmc pass $i ok"
 done
-python3 "$R/scripts/pmc_traffic.py" "$O/pmc" segment_kernel "$O/pmc_segment.json"
+python3 "$R/scripts/pmc_traffic.py" "$O/pmc" lean_kernel,segment_kernel "$O/pmc_segment.json"
 echo done
