@@ -49,8 +49,10 @@ def parse():
     p.add_argument("--queries", type=int, default=100_000)
     p.add_argument("--batch", type=int, default=4096, help="queries per GPU per step")
     p.add_argument("--k", type=int, default=10)
-    p.add_argument("--mode", choices=["shard", "replica"], default="shard",
-                   help="N>1: doc-range shards with RCCL merge, or full-index replicas")
+    p.add_argument("--mode", choices=["auto", "shard", "replica"], default="auto",
+                   help="N>1: replica = full index per GPU, queries split across ranks (the "
+                        "value when the index fits one GPU: auto); shard = doc-range shards "
+                        "with the RCCL event exchange (auto also measures it, as 'docshard')")
     p.add_argument("--dist-backend", default="nccl",
                    help="shard exchange backend (nccl = RCCL over xGMI; gloo for 1-GPU rehearsals)")
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
@@ -133,127 +135,164 @@ def kernel_accounting(eng, batches):
     return acc
 
 
+def run_shard(a, idx, lines, rank, world, local, dist, threads):
+    """Doc-range shards: every rank runs each global batch (4096*W queries) over
+    its doc range, events are exchanged with RCCL all_to_all, each rank replays
+    the 4096 queries it owns.  Returns (queries, seconds, p50 ms, batches,
+    engine, checked, searcher)."""
+    import torch
+    import wiser_amd as w
+    from wiser_amd.shard import ShardedSearcher
+    t = time.time()
+    S = ShardedSearcher(idx, rank, world, device=local, threads=threads)
+    log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
+    eng = S.engine
+    Q = a.batch * world
+    gb = []
+    for s in range(0, len(lines) - Q + 1, Q):
+        chunk = lines[s:s + Q]
+        b = w.ResidentBatch(eng, Q, a.k)
+        b.upload(resolve(eng, chunk, a.k))
+        gb.append((b, chunk))
+    nb = len(gb)
+
+    def step(i, fetch=False):
+        return S.run(gb[i % nb][0], a.batch, fetch=fetch)
+
+    checked = 0
+    if a.check:   # every rank takes part in the collectives; rank 0 checks
+        hits, nh = step(0, fetch=True)
+        if rank == 0:
+            checked = check_against_oracle(idx, gb[0][1][:a.batch], hits, nh, a.k, a.check)
+    for s in range(a.warmup):
+        step(s)
+    lat = []
+    for i in range(nb):
+        dist.barrier()
+        t0 = time.perf_counter()
+        step(i, fetch=True)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        step(s)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    queries = a.steps * Q  # every rank completes its owned 1/W of each global batch
+    return queries, el, statistics.median(lat), [b for b, _ in gb], eng, checked, S
+
+
+def run_replica(a, idx, lines, rank, world, local, dist, threads):
+    """Full index per GPU; the log is split across ranks, 4096 queries per
+    rank per step, consecutive batches in flight on per-batch streams."""
+    import wiser_amd as w
+    t = time.time()
+    eng = w.VacuumEngine(idx, device=local, threads=threads)
+    eng.Load()
+    log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
+    per_rank = (len(lines) + world - 1) // world
+    mine = lines[rank * per_rank:(rank + 1) * per_rank] or lines[:a.batch]
+    batches, chunks = [], []
+    for s in range(0, len(mine), a.batch):
+        chunk = mine[s:s + a.batch]
+        b = w.ResidentBatch(eng, a.batch, a.k)
+        b.upload(resolve(eng, chunk, a.k))
+        batches.append(b)
+        chunks.append(chunk)
+    nb = len(batches)
+    checked = 0
+    if a.check and rank == 0:
+        batches[0].run()
+        hits, nh = batches[0].fetch()
+        checked = check_against_oracle(idx, chunks[0], hits, nh, a.k, a.check)
+    for s in range(a.warmup):
+        batches[s % nb].run()
+    w.sync(eng)
+    lat = []
+    for b in batches:
+        t0 = time.perf_counter()
+        b.run()
+        b.fetch()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    if dist:
+        dist.barrier()
+    w.sync(eng)
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        batches[s % nb].run()
+    w.sync(eng)
+    el = time.perf_counter() - t0
+    queries = sum(batches[s % nb].nq for s in range(a.steps))
+    return queries, el, statistics.median(lat), batches, eng, checked, None
+
+
+def reduce_timing(dist, el, queries, p50, on_gpu, summed):
+    """Max wall time and p50 over ranks; queries summed (replicas) or as is."""
+    import torch
+    tt = torch.tensor([el, float(queries), p50], dtype=torch.float64)
+    if on_gpu:
+        tt = tt.cuda()
+    mx = tt.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = tt.clone()
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return mx[0].item(), (sm[1].item() if summed else queries), mx[2].item()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    shard = world > 1 and a.mode == "shard"
+    mode = a.mode if world > 1 else "replica"
     if world > 1:
         import torch
         import torch.distributed as dist
         # one GPU per rank; rehearsals with more ranks than GPUs share devices
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group(a.dist_backend if shard else "gloo")
+        dist.init_process_group(a.dist_backend)
+    on_gpu = dist is not None and a.dist_backend == "nccl"
 
-    import wiser_amd as w
     idx, qlog = ensure_index(a, rank, dist)
     lines = [l.split() for l in open(qlog).read().splitlines()]
     threads = min(16, os.cpu_count())
-    checked = 0
 
-    if shard:
-        import torch
-        from wiser_amd.shard import ShardedSearcher
-        t = time.time()
-        S = ShardedSearcher(idx, rank, world, device=local, threads=threads)
-        log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
-        eng = S.engine
-        Q = a.batch * world
-        gb = []
-        for s in range(0, len(lines) - Q + 1, Q):
-            chunk = lines[s:s + Q]
-            b = w.ResidentBatch(eng, Q, a.k)
-            b.upload(resolve(eng, chunk, a.k))
-            gb.append((b, chunk))
-        nb = len(gb)
-
-        def step(i, fetch=False):
-            return S.run(gb[i % nb][0], a.batch, fetch=fetch)
-
-        if a.check:   # every rank takes part in the collectives; rank 0 checks
-            hits, nh = step(0, fetch=True)
-            if rank == 0:
-                checked = check_against_oracle(idx, gb[0][1][:a.batch], hits, nh, a.k, a.check)
-        for s in range(a.warmup):
-            step(s)
-        lat = []
-        for i in range(nb):
-            dist.barrier()
-            t0 = time.perf_counter()
-            step(i, fetch=True)
-            lat.append((time.perf_counter() - t0) * 1e3)
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for s in range(a.steps):
-            step(s)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        queries = a.steps * Q  # every rank completes its owned 1/W of each global batch
-        batches = [b for b, _ in gb]
-        parallelism = f"docshard{world}"
-        global_batch = Q
-    else:
-        t = time.time()
-        eng = w.VacuumEngine(idx, device=local, threads=threads)
-        eng.Load()
-        log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
-        per_rank = (len(lines) + world - 1) // world
-        mine = lines[rank * per_rank:(rank + 1) * per_rank] or lines[:a.batch]
-        batches, chunks = [], []
-        for s in range(0, len(mine), a.batch):
-            chunk = mine[s:s + a.batch]
-            b = w.ResidentBatch(eng, a.batch, a.k)
-            b.upload(resolve(eng, chunk, a.k))
-            batches.append(b)
-            chunks.append(chunk)
-        nb = len(batches)
-        if a.check and rank == 0:
-            batches[0].run()
-            hits, nh = batches[0].fetch()
-            checked = check_against_oracle(idx, chunks[0], hits, nh, a.k, a.check)
-        for s in range(a.warmup):
-            batches[s % nb].run()
-        w.sync(eng)
-        lat = []
-        for b in batches:
-            t0 = time.perf_counter()
-            b.run()
-            b.fetch()
-            lat.append((time.perf_counter() - t0) * 1e3)
-        if dist:
-            dist.barrier()
-        w.sync(eng)
-        t0 = time.perf_counter()
-        for s in range(a.steps):
-            batches[s % nb].run()
-        w.sync(eng)
-        el = time.perf_counter() - t0
-        queries = sum(batches[s % nb].nq for s in range(a.steps))
-        parallelism = f"replicas{world}"
-        global_batch = a.batch * world
-
-    p50 = statistics.median(lat)
+    runner = run_shard if mode == "shard" else run_replica
+    queries, el, p50, batches, eng, checked, S = runner(a, idx, lines, rank, world, local, dist, threads)
+    parallelism = f"docshard{world}" if mode == "shard" else f"replicas{world}"
+    global_batch = a.batch * world
     acc = kernel_accounting(eng, batches)
     nbk = len(batches)
     seg_avg_ms = acc["seg"] / nbk
     achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
-
     if dist:
-        import torch
-        tt = torch.tensor([el, float(queries), p50], dtype=torch.float64)
-        if shard and a.dist_backend == "nccl":
-            tt = tt.cuda()
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        el, p50 = mx[0].item(), mx[2].item()
-        queries = queries if shard else sm[1].item()
+        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=(mode != "shard"))
     qps = queries / el
+    for b in batches:
+        b.close()
+    if S is not None:
+        S.close()
+    else:
+        eng.close()
+
+    # auto at N > 1: the doc-range sharded path, measured the same way, beside
+    # the replica value (the index fits one GPU, so replicas carry the value)
+    docshard = None
+    if dist and a.mode == "auto":
+        sq, sel, sp50, sb, seng, _, SS = run_shard(
+            a, idx, lines, rank, world, local, dist, threads)
+        sel, sq, sp50 = reduce_timing(dist, sel, sq, sp50, on_gpu, summed=False)
+        docshard = {"value": round(sq / sel, 1), "ms_per_step": round(sel / a.steps * 1e3, 4),
+                    "global_batch": a.batch * world, "p50_ms": round(sp50, 3),
+                    "exchange": "all_to_all over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend),
+                    "note": "each rank runs every query over its doc range; events exchanged; "
+                            "each query replayed by its owner"}
+        for b in sb:
+            b.close()
+        SS.close()
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -296,10 +335,9 @@ def main():
                           "other_blocks": int(acc["oblk"] / nbk), "work_items": int(acc["items"] / nbk)},
             "parity_checked_queries": checked,
         }
+        if docshard:
+            out["docshard"] = docshard
         print(json.dumps(out), flush=True)
-    for b in batches:
-        b.close()
-    eng.close()
     if dist:
         dist.destroy_process_group()
 
