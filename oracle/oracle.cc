@@ -157,8 +157,9 @@ struct VIntsIter {
   void skip_to(int i) { while (index() < i) pop(); }
 };
 
-// SkipList::Load (flash_containers.h:354-391); only the docid/tf columns are kept.
-struct SkipEntry { uint32_t prev_doc; uint64_t doc_off, tf_off; };
+// SkipList::Load (flash_containers.h:354-391); the docid / tf / position columns
+// (the offset columns only feed snippets).
+struct SkipEntry { uint32_t prev_doc; uint64_t doc_off, tf_off, pos_off; uint32_t pos_idx; };
 std::vector<SkipEntry> load_skip_list(const uint8_t* buf) {
   if (buf[0] != kSkipMagic) throw std::runtime_error("skip list magic");
   uint64_t n;
@@ -167,14 +168,14 @@ std::vector<SkipEntry> load_skip_list(const uint8_t* buf) {
   std::vector<SkipEntry> rows;
   rows.reserve(n);
   uint32_t pd = 0;
-  uint64_t pdo = 0, pto = 0;
+  uint64_t pdo = 0, pto = 0, ppo = 0;
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t f[7];
     for (int k = 0; k < 7; ++k) p += varint_decode(p, &f[k]);
     uint32_t prev = static_cast<uint32_t>(f[0] + pd);
-    uint64_t dof = f[1] + pdo, tof = f[2] + pto;
-    rows.push_back(SkipEntry{prev, dof, tof});
-    pd = prev; pdo = dof; pto = tof;
+    uint64_t dof = f[1] + pdo, tof = f[2] + pto, pof = f[3] + ppo;
+    rows.push_back(SkipEntry{prev, dof, tof, pof, static_cast<uint32_t>(f[4])});
+    pd = prev; pdo = dof; pto = tof; ppo = pof;
   }
   return rows;
 }
@@ -268,7 +269,174 @@ class TfIter {
   VIntsIter vints_;
 };
 
-// VacuumPostingListIterator (flash_iterators.h:893-1079), no bloom / positions.
+// CozyBoxIterator (flash_iterators.h:280-412): a run of packs then one VInts
+// blob; it does not know where the box ends (the caller counts entries).
+class CozyIter {
+ public:
+  void reset(const uint8_t* file) { file_ = file; type_ = 0; blob_off_ = 0; idx_ = 0; }
+  int type() const { return type_; }
+  // GoToCozyEntry (:294-305)
+  void go(uint64_t blob_off, int in_blob) {
+    if (type_ == 0 || blob_off_ != blob_off) setup(blob_off);
+    if (type_ == 2) vints_.skip_to(in_blob);
+    idx_ = in_blob;
+  }
+  uint32_t value() const {  // :339-348
+    return type_ == 1 ? pack_.cache[idx_] : static_cast<uint32_t>(vints_.peek());
+  }
+  void advance() {  // :309-315
+    go(blob_off_, idx_ + 1);
+    if (at_blob_end()) go(blob_off_ + blob_bytes(), 0);
+  }
+  void advance_by(int n) {  // AdvanceBy (:319-337)
+    while (n > 0) {
+      if (type_ == 1) {
+        const int remain = kPack - idx_;
+        if (n < remain) { idx_ += n; n = 0; }
+        else { go(blob_off_ + blob_bytes(), 0); n -= remain; }
+      } else {
+        advance();
+        --n;
+      }
+    }
+  }
+
+ private:
+  bool at_blob_end() const { return type_ == 1 ? idx_ >= kPack : vints_.is_end(); }
+  // PackedIntsIterator / VIntsIterator::SerializationSize (packed_value.h:426-428
+  // assumes a 1-byte length varint; a VInts blob is always a box's last)
+  uint64_t blob_bytes() const { return type_ == 1 ? 2 + 16ull * pack_.bits : 2 + vints_.end; }
+  void setup(uint64_t blob_off) {  // SetupBlob (:390-403)
+    const uint8_t* p = file_ + blob_off;
+    if (p[0] == kPackMagic) { type_ = 1; pack_.reset(p); pack_.decode(); }
+    else if (p[0] == kVIntsMagic) { type_ = 2; vints_.reset(p); }
+    else throw std::runtime_error("cozy box blob format");
+    blob_off_ = blob_off;
+    idx_ = 0;
+  }
+  const uint8_t* file_ = nullptr;
+  int type_ = 0;  // 0 none, 1 pack, 2 vints
+  uint64_t blob_off_ = 0;
+  int idx_ = 0;
+  PackReader pack_;
+  VIntsIter vints_;
+};
+
+// PositionPostingBagIterator (flash_iterators.h:458-634): the positions of one
+// posting ("bag", tf entries, delta coded from 0 inside the bag).  Bags are
+// found from the skip row of their 128-posting interval plus the tfs before.
+class PosBagIter {
+ public:
+  void reset(const uint8_t* file, const std::vector<SkipEntry>* sl) {
+    cozy_.reset(file); sl_ = sl; tf_.reset(file, sl); cur_bag_ = 0;
+  }
+  void skip_to(int bag) {  // SkipTo (:570-591)
+    if (cozy_.type() == 0 || bag / kPack > cur_bag_ / kPack) {
+      jump(bag);
+    } else {
+      cozy_.advance_by(entries_between(cur_bag_, bag) - n_adv_);
+    }
+    cur_bag_ = bag;
+    prev_ = 0;
+    tf_cur_ = static_cast<int>(tf_.at(bag));
+    n_popped_ = 0;
+    n_adv_ = 0;
+  }
+  uint32_t pop() {  // PopInBag (:593-604)
+    const uint32_t pos = prev_ + cozy_.value();
+    prev_ = pos;
+    ++n_popped_;
+    if (n_popped_ < tf_cur_) { cozy_.advance(); ++n_adv_; }
+    return pos;
+  }
+  bool is_end() const { return n_popped_ >= tf_cur_; }  // IsEndInBag (:606-608)
+
+ private:
+  int entries_between(int a, int b) {  // NumCozyEntriesBetween (:619-628)
+    int n = 0;
+    for (int i = a; i < b; ++i) n += static_cast<int>(tf_.at(i));
+    return n;
+  }
+  void jump(int bag) {  // JumpToPostingBag / FindSkipInterval / GoToSkipPostingBag (:504-536)
+    int i = cur_bag_ / kPack;
+    while (i + 1 < static_cast<int>(sl_->size()) && (i + 1) * kPack <= bag) ++i;
+    const SkipEntry& e = (*sl_)[i];
+    cozy_.go(e.pos_off, static_cast<int>(e.pos_idx));
+    cur_bag_ = i * kPack;
+    cozy_.advance_by(entries_between(i * kPack, bag));
+  }
+  CozyIter cozy_;
+  const std::vector<SkipEntry>* sl_ = nullptr;
+  TfIter tf_;
+  int cur_bag_ = 0, n_popped_ = 0, n_adv_ = 0, tf_cur_ = 0;
+  uint32_t prev_ = 0;
+};
+
+// PhraseQueryProcessor2 (query_processing.h:170-382) over pop-iterators
+// (IsEnd / Pop); returns NumOfMatches and, when `table` is given, the matched
+// positions per term (PositionInfoTable2 rows).
+template <class PosIt>
+int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* table) {
+  const int n = static_cast<int>(its.size());
+  int matches = 0;
+  auto append = [&](int row, int pos) { if (table) (*table)[row].push_back(pos); };
+  if (table) table->assign(n, {});
+  if (n == 2) {  // ProcessTwoTerm (:264-310)
+    PosIt* it0 = its[0];
+    PosIt* it1 = its[1];
+    int pos0 = -100, pos1 = -200;
+    bool tried_pop_end = false;
+    while (!tried_pop_end) {
+      if (pos0 < pos1) {
+        if (!it0->is_end()) pos0 = static_cast<int>(it0->pop());
+        else tried_pop_end = true;
+      } else if (pos0 > pos1) {
+        if (!it1->is_end()) pos1 = static_cast<int>(it1->pop()) - 1;
+        else tried_pop_end = true;
+      } else {
+        append(0, pos0);
+        append(1, pos1 + 1);
+        ++matches;
+        if (!it0->is_end()) pos0 = static_cast<int>(it0->pop());
+        else tried_pop_end = true;
+        if (!it1->is_end()) pos1 = static_cast<int>(it1->pop()) - 1;
+        else tried_pop_end = true;
+      }
+    }
+    return matches;
+  }
+  // ProcessGeneral (:312-336) with InitializeLastPopped / FindMaxAdjustedLastPopped /
+  // MovePoppedBeyond / IsPoppedMatch (:180-252); positions are int (Position)
+  std::vector<int> last(n);
+  for (int i = 0; i < n; ++i) {
+    if (its[i]->is_end()) return 0;
+    last[i] = static_cast<int>(its[i]->pop());
+  }
+  auto move_beyond = [&](int mx) {
+    for (int i = 0; i < n; ++i) {
+      while (!its[i]->is_end() && last[i] - i < mx) last[i] = static_cast<int>(its[i]->pop());
+      if (its[i]->is_end() && last[i] - i < mx) return false;
+    }
+    return true;
+  };
+  for (;;) {
+    int mx = 0;
+    for (int i = 0; i < n; ++i) mx = std::max(mx, last[i] - i);
+    if (!move_beyond(mx)) break;
+    bool match = true;
+    for (int i = 0; i < n; ++i) match = match && last[i] - i == mx;
+    if (match) {
+      for (int i = 0; i < n; ++i) append(i, last[i]);
+      ++matches;
+      if (!move_beyond(mx + 1)) break;
+    }
+  }
+  return matches;
+}
+
+// VacuumPostingListIterator (flash_iterators.h:893-1079).  Bloom filters are
+// not read: with an index written without them the reference's HasTerm answers
+// BLM_MAY_PRESENT (:1039-1058) and every found doc goes to the position check.
 class VacuumIter {
  public:
   VacuumIter(const uint8_t* file, uint64_t off) {
@@ -280,6 +448,8 @@ class VacuumIter {
     skip_ = std::make_shared<std::vector<SkipEntry>>(load_skip_list(buf + 1 + l + 8));
     doc_.reset(file, skip_.get(), n_);
     tf_.reset(file, skip_.get());
+    pos_ = std::make_shared<PosBagIter>();
+    pos_->reset(file, skip_.get());
   }
   int size() const { return n_; }
   bool is_end() const { return doc_.is_end(); }
@@ -287,12 +457,15 @@ class VacuumIter {
   int term_freq() { return static_cast<int>(tf_.at(doc_.posting_index())); }
   void advance() { doc_.advance(); }
   void skip_forward(uint32_t d) { doc_.skip_forward(d); }
+  // AssignPositionBegin (:1002-1005)
+  PosBagIter* position_begin() { pos_->skip_to(doc_.posting_index()); return pos_.get(); }
 
  private:
   int n_ = 0;
   std::shared_ptr<std::vector<SkipEntry>> skip_;
   DocIdIter doc_;
   TfIter tf_;
+  std::shared_ptr<PosBagIter> pos_;
 };
 
 // In-memory posting list iterator for the QqMem restatement (posting_list_delta.h:161-394:
@@ -306,6 +479,7 @@ class MemIter {
   int term_freq() const { return static_cast<int>((*t_)[i_]); }
   void advance() { ++i_; }
   void skip_forward(uint32_t v) { while (i_ < d_->size() && (*d_)[i_] < v) ++i_; }
+  PosBagIter* position_begin() { throw std::runtime_error("phrase queries need a Vacuum index"); }
 
  private:
   const std::vector<uint32_t>* d_;
@@ -371,16 +545,22 @@ class MinHeap {
 template <class It>
 class Processor {
  public:
-  Processor(const Bm25& sim, std::vector<It>* its, const std::vector<uint8_t>& lens, int n_docs, int k)
-      : sim_(sim), its_(*its), lens_(lens), k_(k) {
+  Processor(const Bm25& sim, std::vector<It>* its, const std::vector<uint8_t>& lens, int n_docs, int k,
+            bool phrase = false)
+      : sim_(sim), its_(*its), lens_(lens), k_(k), phrase_(phrase) {
     for (auto& it : its_) idf_.push_back(es_idf(n_docs, it.size()));   // :544-547
   }
-  std::vector<Entry> run() {  // qq_search::ProcessQueryDelta dispatch (:966-978)
+  // qq_search::ProcessQueryDelta dispatch (:966-978): one term ->
+  // SingleTermQueryProcessor; two terms, not a phrase -> TwoTermNonPhrase; else
+  // QueryProcessor (ProcessTwoTerm / ProcessMultipleTerms, same intersection
+  // loops, HandleTheFoundDoc :886-895 on every doc found)
+  std::vector<Entry> run() {
     if (its_.size() == 1) single();
     else if (its_.size() == 2) two();
     else multi();
     return sort_heap();
   }
+  int64_t phrase_checks() const { return n_phrase_checks_; }
 
  private:
   // CalcDocScoreLossy (scoring.h:124-145), terms in query order
@@ -401,6 +581,19 @@ class Processor {
     if (heap_.size() < static_cast<size_t>(k_)) heap_.push(Entry{doc, s});
     else if (s > heap_.top().score) { heap_.pop(); heap_.push(Entry{doc, s}); }
   }
+  // HandleTheFoundDoc (:886-895): a phrase query ranks the doc only when the
+  // positions hold the phrase (FindPhrase :854-867; RankDocForPhrase scores and
+  // inserts exactly as RankDoc, :897-912)
+  void found(int doc) {
+    if (phrase_ && its_.size() > 1) {
+      ++n_phrase_checks_;
+      std::vector<PosBagIter*> ps;
+      for (auto& it : its_) ps.push_back(it.position_begin());
+      if (phrase_process(ps, nullptr) > 0) rank(doc);
+    } else {
+      rank(doc);
+    }
+  }
   void single() {  // :632-641
     auto& it = its_[0];
     while (!it.is_end()) { rank(it.doc_id()); it.advance(); }
@@ -412,7 +605,7 @@ class Processor {
       const int d0 = a.doc_id(), d1 = b.doc_id();
       if (d0 > d1) b.skip_forward(d0);
       else if (d0 < d1) a.skip_forward(d1);
-      else { rank(d0); a.advance(); b.advance(); }
+      else { found(d0); a.advance(); b.advance(); }
     }
   }
   void multi() {  // ProcessMultipleTerms / FindMax / FindMatch :710-728,810-852
@@ -430,7 +623,7 @@ class Processor {
         if (it.is_end()) { fin = true; break; }
         if (it.doc_id() != mx) break;
         if (i == its_.size() - 1) {
-          rank(mx);
+          found(mx);
           for (auto& x : its_) x.advance();
         }
       }
@@ -448,6 +641,8 @@ class Processor {
   std::vector<It>& its_;
   const std::vector<uint8_t>& lens_;
   int k_;
+  bool phrase_;
+  int64_t n_phrase_checks_ = 0;
   std::vector<double> idf_;
   MinHeap heap_;
 };
@@ -634,9 +829,9 @@ int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* t
   }
 }
 
-// VacuumEngine::Search (vacuum_engine.h:201-258), non-phrase, no snippets
-int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k, int32_t* docs,
-                      double* scores, int32_t* doc_freqs) {
+// VacuumEngine::Search (vacuum_engine.h:201-258), no snippets
+int orc_vacuum_search_phrase(orc_vacuum* h, const char* const* terms, int n_terms, int k,
+                             int is_phrase, int32_t* docs, double* scores, int32_t* doc_freqs) {
   if (k == 0) return 0;
   try {
     std::vector<VacuumIter> its;
@@ -646,12 +841,60 @@ int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int 
     }
     if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
     if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
-    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k);
+    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k, is_phrase != 0);
     return emit(p.run(), docs, scores);
   } catch (const std::exception& e) {
     g_err = e.what();
     return -1;
   }
+}
+
+int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k, int32_t* docs,
+                      double* scores, int32_t* doc_freqs) {
+  return orc_vacuum_search_phrase(h, terms, n_terms, k, 0, docs, scores, doc_freqs);
+}
+
+// The positions of one posting through PositionPostingBagIterator (test hook).
+int orc_vacuum_positions(orc_vacuum* h, const char* term, int posting, uint32_t* out, int cap) {
+  auto f = h->tip.find(term);
+  if (f == h->tip.end()) return 0;
+  try {
+    VacuumIter it(h->map, f->second);
+    if (posting < 0 || posting >= it.size()) return 0;
+    it.skip_forward(0);
+    for (int i = 0; i < posting; ++i) it.advance();
+    PosBagIter* p = it.position_begin();
+    int n = 0;
+    while (!p->is_end()) {
+      const uint32_t v = p->pop();
+      if (n < cap) out[n] = v;
+      ++n;
+    }
+    return n;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// PhraseQueryProcessor2 over plain position lists (tests_5.cc:447-581 shape):
+// returns NumOfMatches; table (n_lists x cap) receives the matched positions.
+int orc_phrase_lists(const uint32_t* const* lists, const int* sizes, int n_lists, int32_t* table,
+                     int cap) {
+  struct ListIt {
+    const uint32_t* v; int n; int i;
+    bool is_end() const { return i >= n; }
+    uint32_t pop() { return v[i++]; }
+  };
+  std::vector<ListIt> its(n_lists);
+  std::vector<ListIt*> ps;
+  for (int i = 0; i < n_lists; ++i) { its[i] = ListIt{lists[i], sizes[i], 0}; ps.push_back(&its[i]); }
+  std::vector<std::vector<int>> t;
+  const int m = phrase_process(ps, &t);
+  if (table)
+    for (int i = 0; i < n_lists; ++i)
+      for (int j = 0; j < m && j < cap; ++j) table[i * cap + j] = t[i][j];
+  return m;
 }
 
 int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads, int32_t* docs,
@@ -661,12 +904,16 @@ int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads,
   std::atomic<int> next{0};
   auto work = [&] {
     for (int q; (q = next++) < nq;) {
-      std::vector<std::string> t = explode(lines[q], ' ');
+      // a line in double quotes is a phrase query (gen_synthetic_log.py:262)
+      std::string line = lines[q];
+      const bool phrase = line.size() >= 2 && line.front() == '"' && line.back() == '"';
+      if (phrase) line = line.substr(1, line.size() - 2);
+      std::vector<std::string> t = explode(line, ' ');
       std::vector<const char*> tp;
       for (auto& s : t) tp.push_back(s.c_str());
-      n_out[q] = orc_vacuum_search(h, tp.data(), static_cast<int>(tp.size()), k,
-                                   docs + static_cast<int64_t>(q) * k,
-                                   scores + static_cast<int64_t>(q) * k, nullptr);
+      n_out[q] = orc_vacuum_search_phrase(h, tp.data(), static_cast<int>(tp.size()), k, phrase,
+                                          docs + static_cast<int64_t>(q) * k,
+                                          scores + static_cast<int64_t>(q) * k, nullptr);
     }
   };
   if (threads <= 1) work();

@@ -52,7 +52,17 @@ int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* t
  * (doc_freqs filled only when every term exists, as the reference). */
 int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k,
                       int32_t* docs, double* scores, int32_t* doc_freqs);
-/* Many queries: queries are '\n'-separated lines of ' '-separated terms.
+/* The same with SearchQuery::is_phrase (QueryProcessor's position check). */
+int orc_vacuum_search_phrase(orc_vacuum* h, const char* const* terms, int n_terms, int k,
+                             int is_phrase, int32_t* docs, double* scores, int32_t* doc_freqs);
+/* positions of posting `posting` of a term (PositionPostingBagIterator); returns tf */
+int orc_vacuum_positions(orc_vacuum* h, const char* term, int posting, uint32_t* out, int cap);
+/* PhraseQueryProcessor2 over plain sorted position lists: NumOfMatches, and the
+ * matched positions per list in table[list * cap + match] */
+int orc_phrase_lists(const uint32_t* const* lists, const int* sizes, int n_lists, int32_t* table,
+                     int cap);
+/* Many queries: queries are '\n'-separated lines of ' '-separated terms (a line
+ * in double quotes is a phrase query).
  * Outputs are nq*k arrays plus n per query.  threads >= 1.  Returns nq. */
 int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads,
                             int32_t* docs, double* scores, int32_t* n_out, int max_q);

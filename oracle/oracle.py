@@ -43,6 +43,11 @@ for name, res, args in [
                                   C.c_int]),
     ("orc_vacuum_search", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, _I32P, _F64P,
                                     _I32P]),
+    ("orc_vacuum_search_phrase", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int,
+                                           _I32P, _F64P, _I32P]),
+    ("orc_vacuum_positions", C.c_int, [_P, C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.c_int]),
+    ("orc_phrase_lists", C.c_int, [C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(C.c_int), C.c_int,
+                                   _I32P, C.c_int]),
     ("orc_vacuum_search_lines", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, _I32P, _F64P, _I32P,
                                           C.c_int]),
     ("orc_qqmem_load", _P, [C.c_char_p, C.c_int64, C.c_char_p]),
@@ -61,13 +66,13 @@ def _err():
     return lib.orc_last_error().decode(errors="replace")
 
 
-def _search(fn, h, terms, k):
+def _search(fn, h, terms, k, *extra):
     arr = (C.c_char_p * max(len(terms), 1))(*[t.encode() for t in terms])
     kk = max(k, 1)
     docs = (C.c_int32 * kk)()
     scores = (C.c_double * kk)()
     freqs = (C.c_int32 * max(len(terms), 1))(*([-1] * max(len(terms), 1)))
-    n = fn(h, arr, len(terms), k, docs, scores, freqs)
+    n = fn(h, arr, len(terms), k, *extra, docs, scores, freqs)
     if n < 0:
         raise RuntimeError(_err())
     dfs = [freqs[i] for i in range(len(terms))] if n > 0 or (len(terms) and freqs[0] >= 0) else []
@@ -110,13 +115,26 @@ class OracleVacuum:
             raise RuntimeError(_err())
         return list(d[:m]), list(t[:m])
 
-    def search(self, terms, k):
-        """-> ([(doc, score)], doc_freqs)"""
-        return _search(lib.orc_vacuum_search, self.h, terms, k)
+    def search(self, terms, k, phrase=False):
+        """-> ([(doc, score)], doc_freqs); phrase = SearchQuery::is_phrase"""
+        return _search(lib.orc_vacuum_search_phrase, self.h, terms, k, int(bool(phrase)))
 
-    def search_lines(self, lines, k, threads=1):
-        """Many queries; returns list of [(doc, score)]."""
-        text = "\n".join(" ".join(t) for t in lines).encode()
+    def positions(self, term, posting):
+        """positions of one posting (PositionPostingBagIterator)"""
+        cap = 1 << 16
+        out = (C.c_uint32 * cap)()
+        n = lib.orc_vacuum_positions(self.h, term.encode(), posting, out, cap)
+        if n < 0:
+            raise RuntimeError(_err())
+        return list(out[:min(n, cap)])
+
+    def search_lines(self, lines, k, threads=1, phrases=None):
+        """Many queries; returns list of [(doc, score)].  phrases[i] true: query
+        i is a phrase query (written in double quotes, as the reference's log)."""
+        def fmt(i, t):
+            q = " ".join(t)
+            return f'"{q}"' if phrases is not None and phrases[i] else q
+        text = "\n".join(fmt(i, t) for i, t in enumerate(lines)).encode()
         nq = len(lines)
         docs = (C.c_int32 * (nq * k))()
         scores = (C.c_double * (nq * k))()
@@ -175,3 +193,13 @@ def varint_decode(data: bytes):
     v = C.c_uint64()
     n = lib.orc_varint_decode(buf, C.byref(v))
     return v.value, n
+
+
+def phrase_lists(lists, cap=64):
+    """PhraseQueryProcessor2 over plain position lists -> (n_matches, table)"""
+    arrs = [(C.c_uint32 * max(len(l), 1))(*l) for l in lists]
+    ptrs = (C.POINTER(C.c_uint32) * len(lists))(*[C.cast(a, C.POINTER(C.c_uint32)) for a in arrs])
+    sizes = (C.c_int * len(lists))(*[len(l) for l in lists])
+    table = (C.c_int32 * (len(lists) * cap))()
+    m = lib.orc_phrase_lists(ptrs, sizes, len(lists), table, cap)
+    return m, [[table[i * cap + j] for j in range(min(m, cap))] for i in range(len(lists))]
