@@ -144,7 +144,7 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     import wiser_amd as w
     from wiser_amd.shard import ShardedSearcher
     t = time.time()
-    S = ShardedSearcher(idx, rank, world, device=local, threads=threads)
+    S = ShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
     log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
     eng = S.engine
     Q = a.batch * world
@@ -188,7 +188,8 @@ def run_replica(a, idx, lines, rank, world, local, dist, threads):
     rank per step, consecutive batches in flight on per-batch streams."""
     import wiser_amd as w
     t = time.time()
-    eng = w.VacuumEngine(idx, device=local, threads=threads)
+    # the conjunctive workload never reads positions: the image leaves them out
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
     eng.Load()
     log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
     per_rank = (len(lines) + world - 1) // world

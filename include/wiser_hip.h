@@ -57,6 +57,7 @@ typedef struct wsr_open_opts {
   uint32_t doc_lo;    /* doc-id shard [doc_lo, doc_hi); doc_hi = 0 means all docs */
   uint32_t doc_hi;
   int32_t threads;    /* host threads for the load-time directory build (0 = all) */
+  int32_t positions;  /* 1: also upload the position boxes (phrase queries) */
 } wsr_open_opts;
 
 /* A query with its terms already resolved by wsr_lookup (list id per term, in
@@ -65,7 +66,12 @@ typedef struct wsr_query {
   int32_t n_terms;
   int32_t k;          /* n_results; 0 => empty result */
   int32_t list_ids[WSR_MAX_TERMS];
+  int32_t flags;      /* WSR_QUERY_PHRASE: SearchQuery::is_phrase (types.h:205-256) --
+                         a doc is ranked only if the terms occur at consecutive
+                         positions (QueryProcessor::HandleTheFoundDoc,
+                         query_processing.h:854-912); needs positions at wsr_open */
 } wsr_query;
+#define WSR_QUERY_PHRASE 1
 
 typedef struct wsr_hit {
   int32_t doc_id;
@@ -182,6 +188,10 @@ int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, doub
                         wsr_build_stats* st);
 int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                          const char* out_path, int64_t* n_written);
+/* phrase log (tools/gen_synthetic_log.py:254-265) from a synthetic index's
+ * phrase pool: one "t1 t2" per line, in double quotes */
+int wsr_gen_phrase_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                       const char* out_path, int64_t* n_written);
 
 #ifdef __cplusplus
 }

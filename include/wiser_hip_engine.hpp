@@ -28,7 +28,7 @@ struct SearchQuery {  // types.h:205-256
   int n_results = 5;
   bool return_snippets = false;  // snippets are out of scope: entries carry an empty snippet
   int n_snippet_passages = 3;
-  bool is_phrase = false;        // phrase queries of >= 2 terms are not built yet
+  bool is_phrase = false;        // >= 2 terms: consecutive positions required (WSR_QUERY_PHRASE)
 };
 
 struct SearchResultEntry {  // types.h:259-274
@@ -57,7 +57,7 @@ class VacuumHipEngine {
 
   void Load() {
     if (h_) throw std::runtime_error("Engine is already loaded.");
-    wsr_open_opts o{device_, 0, 0, 0};
+    wsr_open_opts o{device_, 0, 0, 0, 1};   // positions: phrase queries served
     check(wsr_open(dir_.c_str(), &o, &h_));
   }
 
@@ -86,11 +86,11 @@ class VacuumHipEngine {
     int stride = 1;
     for (size_t i = 0; i < qs.size(); ++i) {
       const SearchQuery& q = qs[i];
-      if (q.is_phrase && q.terms.size() > 1) throw std::runtime_error("phrase queries not built");
       if (q.terms.size() > WSR_MAX_TERMS || q.n_results > WSR_MAX_K)
         throw std::runtime_error("query over the engine limits");
       wsr_query& w = in[i];
       w.k = q.n_results < 0 ? 0 : q.n_results;
+      w.flags = (q.is_phrase && q.terms.size() > 1) ? WSR_QUERY_PHRASE : 0;
       bool missing = q.terms.empty();
       for (size_t t = 0; t < q.terms.size(); ++t) {
         int32_t id, df;

@@ -1,4 +1,5 @@
 import os
+import random
 import sys
 
 import pytest
@@ -72,3 +73,62 @@ def synth_small(built, tmp_path_factory):
 def all_tokens():
     with open(os.path.join(DATA, "all-tokens.txt")) as f:
         return f.readline().split()
+
+
+# ---- phrase fixtures (positions index with known token sequences) ----
+def _write_positions_linedoc(path, n_docs, vocab, seed):
+    """WITH_POSITIONS linedoc (title, body, tokens, offsets, positions) of random
+    word sequences; returns the token sequence of every doc."""
+    rng = random.Random(seed)
+    words = [f"w{i}" for i in range(vocab)]
+    weights = [1.0 / (i + 1) for i in range(vocab)]
+    seqs = []
+    with open(path, "w") as f:
+        f.write("FIELDS_HEADER_INDICATOR###\tdoctitle\tbody\ttokenized\toffsets\tpositions\n")
+        for _ in range(n_docs):
+            seq = rng.choices(words, weights, k=rng.randint(1, 60))
+            seqs.append(seq)
+            body = " ".join(seq)
+            occ, offs, at = {}, {}, 0
+            for p, w in enumerate(seq):
+                occ.setdefault(w, []).append(p)
+                offs.setdefault(w, []).append((at, at + len(w)))
+                at += len(w) + 1
+            toks = list(occ)
+            off_col = "".join("".join(f"{s},{e};" for s, e in offs[w]) + "." for w in toks)
+            pos_col = "".join("".join(f"{p};" for p in occ[w]) + "." for w in toks)
+            f.write(f"t\t{body}\t{' '.join(toks)}\t{off_col}\t{pos_col}\n")
+    return seqs
+
+
+@pytest.fixture(scope="module")
+def positions_index(built, tmp_path_factory):
+    """3000 docs over 60 Zipf words: lists of hundreds of postings with position
+    boxes of many packs, so that bags straddle packs and skip intervals."""
+    import wiser_amd as w
+    root = str(tmp_path_factory.mktemp("phr"))
+    path = os.path.join(root, "pos.linedoc")
+    seqs = _write_positions_linedoc(path, 3000, 60, seed=11)
+    d = os.path.join(root, "idx")
+    os.makedirs(d)
+    w.build_from_linedoc(path, d, "WITH_POSITIONS")
+    return d, seqs
+
+
+def has_phrase(seq, terms):
+    n = len(terms)
+    return any(seq[i:i + n] == terms for i in range(len(seq) - n + 1))
+
+
+def phrase_cases(seqs, n, seed):
+    rng = random.Random(seed)
+    cases = []
+    for _ in range(n):
+        m = rng.choice([2, 2, 2, 3, 4])
+        s = rng.choice(seqs)
+        if len(s) >= m and rng.random() < 0.7:
+            i = rng.randrange(len(s) - m + 1)
+            cases.append(s[i:i + m])               # a phrase that occurs
+        else:
+            cases.append([f"w{rng.randrange(12)}" for _ in range(m)])   # head words, maybe repeated
+    return cases

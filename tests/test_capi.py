@@ -5,6 +5,8 @@ import os
 
 import pytest
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def test_exports_every_declared_symbol(built):
     from wiser_amd import _capi
@@ -45,8 +47,20 @@ def test_null_arguments_are_errors(built):
     _capi.lib.wsr_close(None)  # no-op
 
 
-def test_struct_layouts(built):
+def test_struct_layouts(built, tmp_path):
+    """ctypes mirrors agree with include/wiser_hip.h as compiled by gcc."""
+    import subprocess
     from wiser_amd import _capi
-    assert C.sizeof(_capi.Query) == 40
-    assert C.sizeof(_capi.Hit) == 16
-    assert C.sizeof(_capi.OpenOpts) == 16
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "wiser_hip.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(wsr_query),'
+                   ' offsetof(wsr_query, flags), sizeof(wsr_hit), sizeof(wsr_open_opts),'
+                   ' offsetof(wsr_open_opts, positions), sizeof(wsr_batch_stats),'
+                   ' sizeof(wsr_build_stats)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(_capi.Query), _capi.Query.flags.offset, C.sizeof(_capi.Hit),
+                   C.sizeof(_capi.OpenOpts), _capi.OpenOpts.positions.offset,
+                   C.sizeof(_capi.BatchStats), C.sizeof(_capi.BuildStats)]
+    assert C.sizeof(_capi.Query) == 44 and C.sizeof(_capi.Hit) == 16

@@ -218,8 +218,6 @@ def test_limits_fail_loudly(gpu_indexes):
     import wiser_amd as w
     eng, _, _ = gpu_indexes["three"]
     with pytest.raises(NotImplementedError):
-        eng.Search(w.SearchQuery(["hello", "world"], is_phrase=True))
-    with pytest.raises(NotImplementedError):
         eng.Search(w.SearchQuery(["hello"], n_results=65))
 
 

@@ -1,0 +1,138 @@
+"""GPU parity of phrase queries (SearchQuery::is_phrase) against the oracle.
+
+The HIP path ranks a conjunctive survivor only when its position bags hold the
+terms at consecutive positions (QueryProcessor::HandleTheFoundDoc,
+query_processing.h:854-912; PhraseQueryProcessor2, :170-382).  Bit-exact: doc
+ids, order (ties included) and f64 scores, over:
+  * the reference's phrase fixtures (tests_15.cc:96-155, tests_18.cc:334-352);
+  * a 3000-doc positions index with known token sequences (bags straddling
+    packs and skip intervals), 2-4 term phrases that occur and ones that do
+    not, repeated terms, k = 1, 10, 64;
+  * the 20k-doc synthetic Zipf index (real token positions), head-term phrases;
+  * every dense-list probe mode and doc-range shards.
+"""
+import os
+import random
+
+import pytest
+
+from conftest import has_phrase, phrase_cases
+from test_gpu_parity import DENSE_MODES, SCORE_RTOL, _engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_phrase(eng, orc, queries, k, phrase=True):
+    import wiser_amd as w
+    res = eng.SearchBatch([w.SearchQuery(list(q), n_results=k, is_phrase=phrase) for q in queries])
+    bad = []
+    for q, r in zip(queries, res):
+        want, dfs = orc.search(list(q), k, phrase=phrase)
+        got = [(e.doc_id, e.doc_score) for e in r.entries]
+        if got != want or (want and r.doc_freqs != dfs):
+            bad.append((q, got[:3], want[:3]))
+        for (gd, gs), (wd, ws) in zip(got, want):
+            assert abs(gs - ws) <= SCORE_RTOL * max(1.0, abs(ws))
+    assert not bad, f"{len(bad)}/{len(queries)} phrase queries differ, first: {bad[:3]}"
+    return res
+
+
+@pytest.fixture(scope="module", params=sorted(DENSE_MODES))
+def mode(request):
+    return request.param
+
+
+def test_phrase_fixture_kat(indexes, mode):
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    d = indexes["iter3"][0]
+    eng = _engine(d, mode)
+    r = eng.Search(w.SearchQuery(["a", "b"], n_results=10, is_phrase=True))
+    assert sorted(e.doc_id for e in r.entries) == [1, 2]
+    r = eng.Search(w.SearchQuery(["a", "b", "c"], n_results=10, is_phrase=True))
+    assert [e.doc_id for e in r.entries] == [2]
+    assert eng.Search(w.SearchQuery(["b", "a"], n_results=10, is_phrase=True)).Size() == 0
+    orc = OracleVacuum(d)
+    _check_phrase(eng, orc, [["a", "b"], ["b", "c"], ["a", "b", "c"], ["a", "c"], ["c", "b"],
+                             ["a", "a"], ["a"], ["a", "b", "x"]], 10)
+    eng.close()
+    d = indexes["wiki5"][0]
+    eng = _engine(d, mode)
+    assert eng.Search(w.SearchQuery(["a", "b"], is_phrase=True)).Size() == 0
+    assert eng.Search(w.SearchQuery(["anarchist", "movement"], is_phrase=True)).Size() == 1
+    # every adjacent token pair and triple of the 5 long docs, and their reversals
+    orc = OracleVacuum(d)
+    qs = []
+    with open(indexes["wiki5"][2]) as f:
+        f.readline()
+        for line in f:
+            body = line.split("\t")[1].split()
+            for i in range(0, len(body) - 2, 7):
+                qs += [body[i:i + 2], body[i:i + 3], body[i:i + 2][::-1]]
+    _check_phrase(eng, orc, qs, 10)
+    eng.close()
+
+
+def test_phrase_positions_index(positions_index, mode):
+    from oracle.oracle import OracleVacuum
+    d, seqs = positions_index
+    eng = _engine(d, mode)
+    orc = OracleVacuum(d)
+    qs = phrase_cases(seqs, 600, seed=17)
+    for k in (1, 10, 64):
+        res = _check_phrase(eng, orc, qs, k)
+    # the phrase filter is real: result sets are the brute-force phrase docs
+    for q, r in zip(qs, res):
+        docs = {i for i, s in enumerate(seqs) if has_phrase(s, q)}
+        if len(docs) <= 64:
+            assert {e.doc_id for e in r.entries} == docs
+    # mixed batch: phrase and conjunctive queries side by side
+    import wiser_amd as w
+    mixed = [w.SearchQuery(q, n_results=10, is_phrase=(i % 2 == 0)) for i, q in enumerate(qs)]
+    for q, r in zip(mixed, eng.SearchBatch(mixed)):
+        want, _ = orc.search(q.terms, 10, phrase=q.is_phrase)
+        assert [(e.doc_id, e.doc_score) for e in r.entries] == want
+    eng.close()
+    orc.close()
+
+
+def test_phrase_synthetic_zipf(synth_small):
+    from oracle.oracle import OracleVacuum
+    d, _ = synth_small
+    eng = _engine(d, "dense")
+    orc = OracleVacuum(d)
+    rng = random.Random(23)
+    head = [f"t{i:07d}" for i in range(40)]
+    qs = [rng.sample(head, 2) for _ in range(300)] + [rng.sample(head, 3) for _ in range(100)]
+    qs += [[h, h] for h in head[:10]]
+    res = _check_phrase(eng, orc, qs, 10)
+    assert sum(r.Size() > 0 for r in res) > 100   # head phrases do occur
+    eng.close()
+    orc.close()
+
+
+def test_phrase_doc_range_shards(positions_index):
+    """Shard images keep the whole position box of a list; phrase results of a
+    W-way doc-range split replayed in order equal the unsharded oracle."""
+    from oracle.oracle import OracleVacuum
+    from test_shard_gpu import _run_sharded
+    d, seqs = positions_index
+    orc = OracleVacuum(d)
+    qs = phrase_cases(seqs, 240, seed=29)
+    for world in (2, 3):
+        qs2, got = _run_sharded(d, qs, 10, world, phrase=True)
+        for q, g in zip(qs2, got):
+            assert g == orc.search(q, 10, phrase=True)[0], (world, q)
+    orc.close()
+
+
+def test_phrase_needs_positions(indexes):
+    import wiser_amd as w
+    from wiser_amd._capi import WiserError
+    e = w.VacuumEngine(indexes["iter3"][0], positions=False)
+    e.Load()
+    with pytest.raises(WiserError):
+        e.Search(w.SearchQuery(["a", "b"], is_phrase=True))
+    # a one-term phrase is an ordinary single-term query
+    assert e.Search(w.SearchQuery(["a"], is_phrase=True)).Size() == 3
+    e.close()

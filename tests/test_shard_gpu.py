@@ -13,7 +13,7 @@ from conftest import DATA
 pytestmark = pytest.mark.gpu
 
 
-def _run_sharded(index_dir, queries, k, world):
+def _run_sharded(index_dir, queries, k, world, phrase=False):
     import torch
     import wiser_amd as w
     from wiser_amd import _capi
@@ -28,7 +28,7 @@ def _run_sharded(index_dir, queries, k, world):
         e.Load()
         arr = (_capi.Query * len(queries))()
         for i, q in enumerate(queries):
-            arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
+            arr[i] = e.resolve(w.SearchQuery(q, n_results=k, is_phrase=phrase))[0]
         b = w.ResidentBatch(e, len(queries), k)
         b.upload(arr)
         check(lib.wsr_batch_run_events(e._h, b._b))

@@ -23,13 +23,17 @@ ERRORS = {-1: "WSR_E_INVALID", -2: "WSR_E_IO", -3: "WSR_E_HIP", -4: "WSR_E_LIMIT
           -5: "WSR_E_INTERNAL"}
 
 
+QUERY_PHRASE = 1
+
+
 class OpenOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("doc_lo", C.c_uint32), ("doc_hi", C.c_uint32),
-                ("threads", C.c_int32)]
+                ("threads", C.c_int32), ("positions", C.c_int32)]
 
 
 class Query(C.Structure):
-    _fields_ = [("n_terms", C.c_int32), ("k", C.c_int32), ("list_ids", C.c_int32 * MAX_TERMS)]
+    _fields_ = [("n_terms", C.c_int32), ("k", C.c_int32), ("list_ids", C.c_int32 * MAX_TERMS),
+                ("flags", C.c_int32)]
 
 
 class Hit(C.Structure):
@@ -104,6 +108,8 @@ _sigs = {
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
+    "wsr_gen_phrase_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
+                                     C.POINTER(C.c_int64)]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

@@ -74,6 +74,12 @@ struct wsr_handle {
   uint8_t* d_tf8 = nullptr;
   uint8_t* d_plen = nullptr;
   uint32_t* d_tails = nullptr;
+  uint8_t* d_pos_blob = nullptr;    // positions (opened with wsr_open_opts::positions)
+  PosDev* d_pos_lists = nullptr;
+  uint32_t* d_pos_pk = nullptr;
+  uint32_t* d_pos_tail = nullptr;
+  uint32_t* d_pos_start = nullptr;
+  bool positions = false;
   uint32_t dense_lists = 0;
   bool fuse_replay = true;
   bool seg_floor = true;
@@ -102,6 +108,8 @@ struct wsr_batch {
   uint32_t* d_itemq = nullptr;   // item -> query (capacity item_cap)
   uint64_t* d_pub = nullptr;     // per item score floor (capacity item_cap)
   uint32_t* d_stats = nullptr;   // per general workgroup, then per lean wave: survivors, blocks
+  uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
+  bool has_phrase = false;       // the uploaded queries include a phrase query
   int seg_grid = 0;
   int lean_wgs = 0;
   // doc-range shard exchange
@@ -154,7 +162,22 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // segments start from the score floor of the query's earlier segments
     // (WSR_SEG_FLOOR=0: every segment from an empty top-k)
     h->seg_floor = env_number("WSR_SEG_FLOOR", 1) != 0;
-    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div);
+    h->positions = opts && opts->positions;
+    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions);
+    if (h->positions) {
+      dev_upload(&h->d_pos_blob, img.pos_blob);
+      dev_upload(&h->d_pos_lists, img.pos_lists);
+      dev_upload(&h->d_pos_pk, img.pos_pk);
+      dev_upload(&h->d_pos_tail, img.pos_tail);
+      dev_upload(&h->d_pos_start, img.pos_start);
+      h->args.pos_blob = h->d_pos_blob;
+      h->args.pos_lists = h->d_pos_lists;
+      h->args.pos_pk = reinterpret_cast<const uint2*>(h->d_pos_pk);
+      h->args.pos_tail = h->d_pos_tail;
+      h->args.pos_start = h->d_pos_start;
+      std::vector<uint8_t>().swap(img.pos_blob);
+      std::vector<uint32_t>().swap(img.pos_start);
+    }
     dev_upload(&h->d_dense, img.dense);
     dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
@@ -220,7 +243,10 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8),
-                  static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails)})
+                  static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
+                  static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
+                  static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
+                  static_cast<void*>(h->d_pos_start)})
     if (p) (void)hipFree(p);
   delete h;
 }
@@ -292,7 +318,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
                   static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
                   static_cast<void*>(b->d_qdone), static_cast<void*>(b->d_itemq),
-                  static_cast<void*>(b->d_pub),
+                  static_cast<void*>(b->d_pub), static_cast<void*>(b->d_ph),
                   static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase)})
     if (p) (void)hipFree(p);
@@ -314,13 +340,22 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
+  bool has_phrase = false;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
     if (s.n_terms > WSR_MAX_TERMS || s.k > WSR_MAX_K || s.k > b->stride)
       return fail(WSR_E_LIMIT, "query " + std::to_string(i) + ": n_terms or k over the limit");
+    if (s.flags & ~WSR_QUERY_PHRASE)
+      return fail(WSR_E_INVALID, "query " + std::to_string(i) + ": unknown flags");
+    const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
+    if (phrase && !h->positions)
+      return fail(WSR_E_INVALID, "query " + std::to_string(i) +
+                                     ": phrase query on an engine opened without positions");
+    has_phrase = has_phrase || phrase;
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
+    d.flags = phrase ? kQueryPhrase : 0;
     uint32_t nbmin = 0xFFFFFFFFu;
     bool ok = d.n_terms > 0 && d.k > 0;
     for (int t = 0; t < WSR_MAX_TERMS; ++t) {
@@ -337,7 +372,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       int drv = 0;
       for (int t = 1; t < d.n_terms; ++t)
         if (h->lists[d.list[t]].nblk < h->lists[d.list[drv]].nblk) drv = t;
-      bool lean = true;
+      bool lean = !phrase;
       for (int t = 0; t < d.n_terms; ++t) {
         const ListDev& L = h->lists[d.list[t]];
         if (t != drv && !(L.bm != kNoDense &&
@@ -368,11 +403,14 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       HIP_OK(hipMalloc(&b->d_itemq, sizeof(uint32_t) * b->item_cap));
       HIP_OK(hipMalloc(&b->d_pub, sizeof(uint64_t) * b->item_cap));
     }
+    if (has_phrase && !b->d_ph)
+      HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch * std::max(h->gen_cap, 1)));
     if (nq) HIP_OK(hipMemcpy(b->d_q, in.data(), sizeof(QueryIn) * nq, hipMemcpyHostToDevice));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   b->nq = nq;
+  b->has_phrase = has_phrase;
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
@@ -409,7 +447,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipStreamWaitEvent(b->st2, b->fork, 0));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, fr, b->d_itemq,
-                           h->seg_floor ? b->d_pub : nullptr, b->st2));
+                           h->seg_floor ? b->d_pub : nullptr,
+                           b->has_phrase ? b->d_ph : nullptr, b->st2));
     HIP_OK(hipEventRecord(b->join, b->st2));
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
@@ -725,6 +764,18 @@ int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed
   if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
   try {
     int64_t n = gen_two_term_log(index_dir, n_queries, seed, out_path);
+    if (n_written) *n_written = n;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_gen_phrase_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                       const char* out_path, int64_t* n_written) {
+  if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
+  try {
+    int64_t n = gen_phrase_log(index_dir, n_queries, seed, out_path);
     if (n_written) *n_written = n;
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());

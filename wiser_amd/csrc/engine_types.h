@@ -54,8 +54,26 @@ struct QueryIn {
   int32_t n_terms;          // 0 => empty result
   int32_t k;                // n_results (0 => empty result)
   int32_t list[kMaxTerms];  // list ids in query order; -1 => term missing => empty
+  int32_t flags;            // kQueryPhrase: SearchQuery::is_phrase (types.h:205-256)
 };
-static_assert(sizeof(QueryIn) == 40, "QueryIn layout");
+static_assert(sizeof(QueryIn) == 44, "QueryIn layout");
+constexpr int32_t kQueryPhrase = 1;
+
+// Positions of one posting list in the image (phrase queries).  The list's
+// position cozy box (flash_engine_dumper.h:78-104: full packs of 128 entries,
+// then one VInts blob) is copied byte-identical to pos_blob at `base`; pack i
+// starts at base + pos_pk[pk0 + i].x and has bit width pos_pk[pk0 + i].y; the
+// VInts remainder is decoded at load (pos_tail[tail ..]).  Entry e of the box
+// is in pack e / 128 when e < 128 * npk.  The bag of posting p (tf entries,
+// delta coded from 0, flash_iterators.h:593-604) starts at entry
+// pos_start[image slot of p] (slots as plen: 128 per image block).
+struct PosDev {
+  uint64_t base;
+  uint64_t tail;
+  uint32_t pk0;
+  uint32_t npk;
+};
+static_assert(sizeof(PosDev) == 24, "PosDev layout");
 
 // Written by the plan kernel for every query of a batch.
 struct QueryPlan {

@@ -138,7 +138,7 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
   p += 1 + l;
   std::vector<SkipRow> out(n);
   // fields: d prev_doc, d docid off, d tf off, d pos off, pos idx, d off off, off idx
-  uint64_t pd = 0, pdo = 0, pto = 0;
+  uint64_t pd = 0, pdo = 0, pto = 0, ppo = 0;
   for (uint64_t r = 0; r < n; ++r) {
     uint64_t f[7];
     for (int k = 0; k < 7; ++k) {
@@ -147,8 +147,8 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
       p += l;
     }
     pd = static_cast<uint32_t>(pd + f[0]);
-    pdo += f[1]; pto += f[2];
-    out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto};
+    pdo += f[1]; pto += f[2]; ppo += f[3];
+    out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto, ppo, static_cast<uint32_t>(f[4])};
   }
   return out;
 }
@@ -194,7 +194,7 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
 }
 
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div) {
+                      uint32_t dense_div, bool positions) {
   const int32_t L = idx.n_lists();
   const uint8_t* file = idx.file();
   const uint8_t* fend = file + idx.file_bytes();
@@ -211,6 +211,11 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     std::vector<uint8_t> tf8;
     std::vector<uint8_t> plen;     // doc-length code of every posting, 128 per block
     std::vector<uint32_t> tail;    // VInts last block decoded: doc ids, then tfs
+    // positions: the whole box, its pack directory, VInts remainder, bag starts
+    std::vector<uint8_t> pos_bytes;
+    std::vector<uint32_t> pos_pk;
+    std::vector<uint32_t> pos_tail;
+    std::vector<uint32_t> pos_start;
   };
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
   std::vector<Part> parts(L);
@@ -242,6 +247,58 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     }
     pt.tf8.resize(n_img);
     for (uint64_t j = 0; j < n_img; ++j) pt.tf8[j] = static_cast<uint8_t>(tfs[j] < kTf8Escape ? tfs[j] : kTf8Escape);
+  };
+  // The list's position cozy box (flash_engine_dumper.h:78-104): the bag of
+  // posting p holds tf(p) entries starting at entry sum(tf before p).  Walked
+  // from row 0's blob; every skip row's (blob, in-blob index) must agree with
+  // the walk (PositionPostingBagIterator::GoToSkipPostingBag, flash_iterators.h:504-513).
+  auto build_positions = [&](Part& pt, const std::vector<SkipRow>& rows, uint64_t r0, uint64_t r1,
+                             int fcnt, const std::string& term) {
+    const uint64_t nrows = rows.size();
+    std::vector<uint64_t> cum(nrows * kPackSize + 1, 0);
+    uint64_t n = 0;
+    for (uint64_t r = 0; r < nrows; ++r) {
+      const int cnt = r + 1 == nrows ? fcnt : kPackSize;
+      uint32_t tfs[kPackSize];
+      if (!host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, tfs))
+        throw std::runtime_error("cannot decode the tfs of '" + term + "'");
+      for (int i = 0; i < cnt; ++i) { cum[n + 1] = cum[n] + tfs[i]; ++n; }
+    }
+    const uint64_t total = cum[n];
+    if (total >= (1ull << 32)) throw std::runtime_error("position box of '" + term + "' over 2^32 entries");
+    const uint64_t p0 = rows[0].pos_off;
+    const uint64_t npk = total / kPackSize, rem = total % kPackSize;
+    std::vector<uint64_t> blob_at(npk + (rem ? 1 : 0));
+    uint64_t at = p0;
+    for (uint64_t k = 0; k < npk; ++k) {
+      const uint8_t* b = file + at;
+      if (b + 2 > fend || b[0] != kPackMagic || b[1] < 1 || b[1] > 32)
+        throw std::runtime_error("bad position pack in '" + term + "'");
+      blob_at[k] = at;
+      pt.pos_pk.push_back(static_cast<uint32_t>(at - p0));
+      pt.pos_pk.push_back(b[1]);
+      at += 2 + 16ull * b[1];
+    }
+    if (rem) {
+      blob_at[npk] = at;
+      pt.pos_tail.resize(rem);
+      if (file[at] != kVIntsMagic ||
+          !host_decode_block(file + at, fend, static_cast<int>(rem), false, 0, pt.pos_tail.data()))
+        throw std::runtime_error("bad position VInts blob in '" + term + "'");
+      at += blob_bytes(file + at, fend);
+    }
+    if (at > idx.file_bytes() || at - p0 >= (1ull << 32))
+      throw std::runtime_error("position box of '" + term + "' out of range");
+    for (uint64_t r = 0; r < nrows; ++r) {
+      const uint64_t e = cum[r * kPackSize];
+      if (rows[r].pos_off != blob_at[e / kPackSize] || rows[r].pos_idx != e % kPackSize)
+        throw std::runtime_error("skip row position pointer disagrees with the box of '" + term + "'");
+    }
+    pt.pos_bytes.assign(file + p0, file + at);
+    pt.pos_start.assign((r1 - r0) * kPackSize, 0);
+    for (uint64_t r = r0; r < r1; ++r)
+      for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
+        pt.pos_start[(r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i]);
   };
   std::atomic<int32_t> next{0};
   std::atomic<bool> failed{false};
@@ -318,6 +375,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         }
         const uint64_t n_img = (r1 - r0 - 1) * kPackSize + pt.tail_cnt;
         if (dense_div && span && n_img * dense_div >= span) build_dense(pt, rows, r0, r1, n_img);
+        if (positions) build_positions(pt, rows, r0, r1, fcnt, idx.term(id));
       }
     } catch (const std::exception& ex) {
       if (!failed.exchange(true)) err = ex.what();
@@ -342,6 +400,32 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.blk_last.reserve(nb);
   img.blk_meta.reserve(nb);
   img.plen.reserve(nb * kPackSize);
+  img.has_positions = positions;
+  if (positions) {
+    uint64_t pb = 0;
+    for (auto& p : parts) pb += (p.pos_bytes.size() + 15) & ~15ull;
+    img.pos_blob.resize(pb + 64, 0);   // tail pad: lanes read whole dwords
+    img.pos_lists.resize(L, PosDev{0, 0, 0, 0});
+    img.pos_start.reserve(nb * kPackSize);
+    uint64_t pat = 0;
+    for (int32_t id = 0; id < L; ++id) {
+      Part& p = parts[id];
+      PosDev& pd = img.pos_lists[id];
+      pd.base = pat;
+      pd.pk0 = static_cast<uint32_t>(img.pos_pk.size() / 2);
+      pd.npk = static_cast<uint32_t>(p.pos_pk.size() / 2);
+      pd.tail = img.pos_tail.size();
+      if (!p.pos_bytes.empty()) std::memcpy(&img.pos_blob[pat], p.pos_bytes.data(), p.pos_bytes.size());
+      pat += (p.pos_bytes.size() + 15) & ~15ull;
+      img.pos_pk.insert(img.pos_pk.end(), p.pos_pk.begin(), p.pos_pk.end());
+      img.pos_tail.insert(img.pos_tail.end(), p.pos_tail.begin(), p.pos_tail.end());
+      img.pos_start.insert(img.pos_start.end(), p.pos_start.begin(), p.pos_start.end());
+      std::vector<uint8_t>().swap(p.pos_bytes);
+      std::vector<uint32_t>().swap(p.pos_pk);
+      std::vector<uint32_t>().swap(p.pos_tail);
+      std::vector<uint32_t>().swap(p.pos_start);
+    }
+  }
   uint64_t at = 0;
   for (int32_t id = 0; id < L; ++id) {
     Part& p = parts[id];

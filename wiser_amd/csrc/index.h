@@ -26,6 +26,8 @@ struct SkipRow {
   uint32_t prev_doc;
   uint64_t doc_off;  // absolute file offsets of the docid / tf blobs of this row
   uint64_t tf_off;
+  uint64_t pos_off;  // position blob holding the row's first bag, and the bag's
+  uint32_t pos_idx;  // entry index inside that blob (flash_containers.h:312-350)
 };
 
 class VacuumIndex {
@@ -85,6 +87,13 @@ struct HostImage {
   std::vector<uint32_t> tails;  // decoded VInts last blocks (ListDev::tail)
   std::vector<uint8_t> plen;    // doc-length code (Char4) of every posting: block j of the
                                 // image at [j * 128, j * 128 + 128), 0 past the length records
+  // positions (build_image(..., positions = true)): see PosDev
+  bool has_positions = false;
+  std::vector<uint8_t> pos_blob;
+  std::vector<PosDev> pos_lists;            // indexed by list id
+  std::vector<uint32_t> pos_pk;             // per full pack: byte offset, bit width (pairs)
+  std::vector<uint32_t> pos_tail;
+  std::vector<uint32_t> pos_start;          // bag start entry per posting slot (as plen)
 };
 
 // Decode one block (pack or VInts) at p into out[0..cnt); delta-coded blocks
@@ -95,7 +104,7 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
 // dense_div > 0: lists with at least span / dense_div postings in the image get
 // a rank bitmap + 1-byte tf array (0 disables them).
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div = 0);
+                      uint32_t dense_div = 0, bool positions = false);
 
 // Host restatement of the device's dense probe (segment kernel): tf of doc in
 // list L of the image, -1 when absent or when L has no bitmap.

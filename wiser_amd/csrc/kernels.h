@@ -28,6 +28,12 @@ struct IndexArgs {
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
+  // positions (phrase queries; null unless the engine was opened with them)
+  const uint8_t* pos_blob;  // every list's position cozy box, byte-exact from my.vacuum
+  const PosDev* pos_lists;  // indexed by list id
+  const uint2* pos_pk;      // per full pack: byte offset from PosDev::base, bit width
+  const uint32_t* pos_tail; // decoded VInts remainders
+  const uint32_t* pos_start;// bag start entry of every posting, 128 slots per image block
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
@@ -78,7 +84,10 @@ hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan*
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,
-                           uint64_t* pub, hipStream_t st);
+                           uint64_t* pub, uint32_t* ph, hipStream_t st);
+// phrase scratch words per general workgroup (ph: grid * kPhraseScratch u32;
+// null when the batch has no phrase query)
+constexpr int kPhraseScratch = kMaxTerms * 256;
 // lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride]
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,

@@ -314,9 +314,10 @@ __device__ __forceinline__ uint2 dense_load(const IndexArgs& ix, const ListDev& 
 }
 
 __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev& B, uint32_t a,
-                                              const uint2 v, uint32_t* tf) {
+                                              const uint2 v, uint32_t* tf, uint32_t* pidx = nullptr) {
   uint32_t idx;
   if (!dense_hit(ix, a, v, &idx)) return false;
+  if (pidx) *pidx = idx;
   uint32_t t = ix.tf8[B.tf8 + idx];
   if (t == kTf8Escape) t = dense_tf_slow(ix, B, idx);
   *tf = t;
@@ -372,7 +373,9 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
     const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
     // lean class: every other list is probed through its bitmap (or none)
-    bool lean = true;
+    // (a phrase query of 2+ terms needs every term's posting index for its
+    // position check: general class)
+    bool lean = !((q.flags & kQueryPhrase) && q.n_terms > 1);
 #pragma unroll
     for (int s = 0; s < kMaxTerms; ++s)
       if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
@@ -1335,6 +1338,72 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
   __builtin_amdgcn_wave_barrier();
 }
 
+// ---------------------------------------------------------- phrase check --
+// Entry e of a list's position cozy box: pack e / 128 (its offset and width
+// from the pack directory) or the decoded VInts remainder.
+__device__ __forceinline__ uint32_t pos_entry(const IndexArgs& ix, const PosDev& P, uint32_t e) {
+  const uint32_t pk = e >> 7;
+  if (pk < P.npk) {
+    const uint2 w = ix.pos_pk[P.pk0 + pk];
+    return pack_value(ix.pos_blob + P.base + w.x + 2, w.y, e & 127u);
+  }
+  return ix.pos_tail[P.tail + (e - (P.npk << 7))];
+}
+
+// Per general workgroup (kPhraseScratch words), per query term s: the image
+// posting slot of value v (= 2l or 2l+1 of the driver block) at [s*256 + v],
+// its tf at [s*256 + 128 + v] (phrase queries only).
+
+// Does the doc hold the query's terms at consecutive positions?  Term i's bag
+// (query order) = tf_i positions delta coded from 0 starting at entry
+// pos_start[slot_i] of its box.  True iff some a has a + i in bag i for every
+// i, which is PhraseQueryProcessor2::NumOfMatches() > 0 (query_processing.h:
+// 264-336: the 2-term merge and the general max-adjusted walk both find every
+// such a).  One lane per survivor; term state stays in registers (the term
+// loop is unrolled, so every index is static).
+__device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
+                                          const uint32_t* ph, uint32_t v) {
+  int32_t cur[kMaxTerms];
+  uint32_t used[kMaxTerms];
+#pragma unroll
+  for (uint32_t i = 0; i < kMaxTerms; ++i) {
+    cur[i] = 0;
+    used[i] = 0;
+    if (i < nt) {
+      const PosDev P = ix.pos_lists[qlist[i]];
+      cur[i] = static_cast<int32_t>(pos_entry(ix, P, ix.pos_start[ph[i * 256 + v]]));
+      used[i] = 1;
+    }
+  }
+  int32_t a = 0;
+  for (;;) {
+    bool moved = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxTerms; ++i) {
+      if (i < nt) {
+        if (cur[i] - static_cast<int32_t>(i) < a) {
+          const PosDev P = ix.pos_lists[qlist[i]];
+          const uint32_t st = ix.pos_start[ph[i * 256 + v]];
+          const uint32_t tf = ph[i * 256 + 128 + v];
+          do {
+            if (used[i] >= tf) return false;
+            cur[i] += static_cast<int32_t>(pos_entry(ix, P, st + used[i]));
+            ++used[i];
+          } while (cur[i] - static_cast<int32_t>(i) < a);
+        }
+        if (cur[i] - static_cast<int32_t>(i) > a) {
+          a = cur[i] - static_cast<int32_t>(i);
+          moved = true;
+        }
+      }
+    }
+    if (!moved) return true;
+  }
+}
+
+// kPhrase: the batch holds phrase queries (their position check is compiled
+// only into this instance, so the conjunctive kernel keeps its registers).
+template <bool kPhrase>
 __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
@@ -1342,7 +1411,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
                                                      uint32_t* __restrict__ ev_cnt,
                                                      uint32_t* __restrict__ stats, FusedReplay fr,
                                                      const uint32_t* __restrict__ item_q,
-                                                     uint64_t* __restrict__ pub) {
+                                                     uint64_t* __restrict__ pub,
+                                                     uint32_t* __restrict__ ph_all) {
   __shared__ WaveLds S;
   WSR_T0()
   const uint32_t l = threadIdx.x & 63;
@@ -1371,6 +1441,10 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
     const ListDev A = ix.lists[qlist[d]];
     const uint32_t seg = uni(P.seg_blocks);
+    // phrase query: every term's posting of each candidate is recorded in this
+    // workgroup's slice of ph_all, then the positions are checked
+    const bool phrase = kPhrase && nt > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
+    uint32_t* ph = kPhrase ? ph_all + static_cast<uint64_t>(blockIdx.x) * kPhraseScratch : nullptr;
     const uint32_t b0 = r * seg;
     const uint32_t b1 = min(b0 + seg, A.nblk);
     Event* ev_out = events + P.ev_base + static_cast<uint64_t>(r) * seg * 128;
@@ -1530,12 +1604,21 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       const uint32_t ta0 = is_tail ? S.dtt[2 * l] : cs.ta0;
       const uint32_t ta1 = is_tail ? S.dtt[2 * l + 1] : cs.ta1;
 
+      // phrase: image posting slot and tf of term s for values 2l, 2l+1
+      auto rec = [&](uint32_t s, uint32_t sl0, uint32_t sl1, uint32_t tf0, uint32_t tf1)
+          __attribute__((always_inline)) {
+        if (phrase) {
+          if (al0) { ph[s * 256 + 2 * l] = sl0; ph[s * 256 + 128 + 2 * l] = tf0; }
+          if (al1) { ph[s * 256 + 2 * l + 1] = sl1; ph[s * 256 + 128 + 2 * l + 1] = tf1; }
+        }
+      };
       for (uint32_t s = 0; s < nt; ++s) {
         if (__ballot(al0 || al1) == 0) break;
         const ListDev L = ix.lists[qlist[s]];
         if (s == d) {  // the driver's own tf
           if (al0) s0 += bm25_term(L.idf, ta0, nrm0);
           if (al1) s1 += bm25_term(L.idf, ta1, nrm1);
+          rec(s, (A.blk0 + b) * 128u + 2 * l, (A.blk0 + b) * 128u + 2 * l + 1, ta0, ta1);
           continue;
         }
         const ListDev& B = L;
@@ -1549,21 +1632,23 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           al1 = al1 && fh1;
           if (al0) s0 += bm25_term(B.idf, t0, nrm0);
           if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+          rec(s, B.blk0 * 128u + fi0, B.blk0 * 128u + fi1, t0, t1);
           WSR_T(2)
           continue;
         }
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
-          uint32_t t0 = 0, t1 = 0;
+          uint32_t t0 = 0, t1 = 0, x0 = 0, x1 = 0;
           const uint2 v0 = dense_load(ix, B, a0, al0);
           const uint2 v1 = dense_load(ix, B, a1, al1);
-          const bool h0 = al0 && dense_resolve(ix, B, a0, v0, &t0);
-          const bool h1 = al1 && dense_resolve(ix, B, a1, v1, &t1);
+          const bool h0 = al0 && dense_resolve(ix, B, a0, v0, &t0, &x0);
+          const bool h1 = al1 && dense_resolve(ix, B, a1, v1, &t1, &x1);
           const uint32_t blast = ix.blk_last[B.blk0 + B.nblk - 1];
           if (__ballot((al0 && a0 > blast) || (al1 && a1 > blast))) done = true;
           al0 = h0;
           al1 = h1;
           if (al0) s0 += bm25_term(B.idf, t0, nrm0);
           if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+          rec(s, B.blk0 * 128u + x0, B.blk0 * 128u + x1, t0, t1);
           WSR_T(2)
           continue;
         }
@@ -1673,11 +1758,17 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         al1 = h1;
         if (al0) s0 += bm25_term(B.idf, t0, nrm0);
         if (al1) s1 += bm25_term(B.idf, t1, nrm1);
+        rec(s, (B.blk0 + j0) * 128u + p0, (B.blk0 + j1) * 128u + p1, t0, t1);
         // advance the cursor to the furthest block queried (docs only increase)
         if (l == 0 && nd && jlast > c) S.cur[s] = jlast;
         WSR_T(3)
       }
       if (__ballot(al0 || al1) == 0) return;
+      if (phrase) {   // HandleTheFoundDoc: rank only docs that hold the phrase
+        if (al0) al0 = phrase_match(ix, qlist, nt, ph, 2 * l);
+        if (al1) al1 = phrase_match(ix, qlist, nt, ph, 2 * l + 1);
+        if (__ballot(al0 || al1) == 0) return;
+      }
       n_surv += __popcll(__ballot(al0)) + __popcll(__ballot(al1));
 
       // running top-k: candidates beat the k-th best at block start and the
@@ -1963,9 +2054,13 @@ hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan*
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,
-                           uint64_t* pub, hipStream_t st) {
-  hipLaunchKernelGGL(segment_kernel, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
-                     events, ev_cnt, stats, fr, item_q, pub);
+                           uint64_t* pub, uint32_t* ph, hipStream_t st) {
+  if (ph)
+    hipLaunchKernelGGL(segment_kernel<true>, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
+                       events, ev_cnt, stats, fr, item_q, pub, ph);
+  else
+    hipLaunchKernelGGL(segment_kernel<false>, dim3(grid), dim3(64), 0, st, ix, q, plan, nq, counters,
+                       events, ev_cnt, stats, fr, item_q, pub, ph);
   return hipGetLastError();
 }
 
@@ -1996,7 +2091,7 @@ hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const 
 
 int segment_kernel_occupancy() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, segment_kernel, 64, 0) != hipSuccess) return 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, segment_kernel<false>, 64, 0) != hipSuccess) return 1;
   return n;
 }
 

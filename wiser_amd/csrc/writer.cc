@@ -467,6 +467,29 @@ BuildStats build_synthetic(const SyntheticSpec& sp, const std::string& out_dir) 
         occ_pos[at] = static_cast<uint32_t>(i - doc_start[d]);
       }
   }
+  // 3b) phrase pool (tools/gen_synthetic_log.py:216-240 find_all_unique_phrases
+  // over the corpus's own bigrams instead of an English phrase list): bigrams
+  // at uniformly drawn token positions, first come first kept, no term in two
+  // phrases, no "a a"; written to <out_dir>/phrases.txt for gen_phrase_log
+  if (sp.with_positions) {
+    std::mt19937_64 g(sp.seed ^ 0x0000000000000007ull);
+    std::vector<uint8_t> used(V, 0);
+    ::mkdir(out_dir.c_str(), 0777);
+    std::ofstream pf(out_dir + "/phrases.txt", std::ios::trunc);
+    if (!pf) throw std::runtime_error("cannot write " + out_dir + "/phrases.txt");
+    const int64_t want = std::min<int64_t>(50000, V / 2);
+    int64_t got = 0;
+    for (int64_t tries = 0; got < want && tries < 100 * want && T > 1; ++tries) {
+      const int64_t d = static_cast<int64_t>(g() % static_cast<uint64_t>(N));
+      if (len[d] < 2) continue;
+      const uint64_t i = doc_start[d] + g() % (len[d] - 1);
+      const uint32_t a = tok[i], b = tok[i + 1];
+      if (a == b || used[a] || used[b]) continue;
+      used[a] = used[b] = 1;
+      pf << synth_term(a) << ' ' << synth_term(b) << '\n';
+      ++got;
+    }
+  }
   std::vector<uint32_t>().swap(tok);
 
   // 4) encode lists in parallel batches, append in term-id order
@@ -575,6 +598,24 @@ int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t see
   std::ofstream f(out_path, std::ios::trunc);
   for (auto& q : out) f << q << "\n";
   return static_cast<int64_t>(out.size());
+}
+
+int64_t gen_phrase_log(const std::string& dir, int64_t n_queries, uint64_t seed,
+                       const std::string& out_path) {
+  std::ifstream in(dir + "/phrases.txt");
+  if (!in) throw std::runtime_error("no phrase pool " + dir + "/phrases.txt (a synthetic index "
+                                    "built with positions writes one)");
+  std::vector<std::string> pool;
+  for (std::string line; std::getline(in, line);)
+    if (!line.empty()) pool.push_back(line);
+  // rand_items_from_set: n distinct phrases (partial Fisher-Yates)
+  std::mt19937_64 g(seed);
+  const int64_t n = std::min<int64_t>(n_queries, static_cast<int64_t>(pool.size()));
+  for (int64_t i = 0; i < n; ++i)
+    std::swap(pool[i], pool[i + static_cast<int64_t>(g() % (pool.size() - i))]);
+  std::ofstream f(out_path, std::ios::trunc);
+  for (int64_t i = 0; i < n; ++i) f << '"' << pool[i] << "\"\n";   // gen_synthetic_log.py:262
+  return n;
 }
 
 }  // namespace wiser

@@ -47,4 +47,10 @@ BuildStats build_synthetic(const SyntheticSpec& spec, const std::string& out_dir
 int64_t gen_two_term_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
                          const std::string& out_path);
 
+// Phrase query log restating tools/gen_synthetic_log.py:254-265: n phrases
+// drawn without replacement from the index's phrase pool (phrases.txt, written
+// by build_synthetic), one per line in double quotes.
+int64_t gen_phrase_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
+                       const std::string& out_path);
+
 }  // namespace wiser

@@ -14,9 +14,12 @@ Behaviour kept from the reference:
   * ``n_results == 0`` -> empty result (vacuum_engine.h:206-208);
   * any term missing from the dictionary -> empty result, ``doc_freqs`` left
     empty (vacuum_engine.h:210-215);
-  * entries ordered as the reference heap pops them (SortHeap), f64 scores.
-Not built in this round (raise ``NotImplementedError`` rather than answer
-differently): phrase queries of two or more terms, snippets.
+  * entries ordered as the reference heap pops them (SortHeap), f64 scores;
+  * ``is_phrase`` with two or more terms ranks only docs holding the terms at
+    consecutive positions (QueryProcessor, query_processing.h:854-912); the
+    engine must be loaded with ``positions=True`` (the default).
+Not built: snippets (the doc store and highlighter are out of scope; entries
+carry an empty snippet).
 """
 from __future__ import annotations
 
@@ -79,8 +82,10 @@ class VacuumEngine:
     """SearchEngineServiceNew over the HIP engine (vacuum_engine.h:119-258)."""
 
     def __init__(self, engine_dir_path: str, bloom_factor: int = 1, device: int = 0,
-                 doc_range: Optional[Sequence[int]] = None, threads: int = 0):
+                 doc_range: Optional[Sequence[int]] = None, threads: int = 0,
+                 positions: bool = True):
         self.engine_dir_path = engine_dir_path
+        self.positions = positions
         self.bloom_factor = bloom_factor
         self.device = device
         self.doc_range = doc_range
@@ -95,6 +100,7 @@ class VacuumEngine:
         opts.device = self.device
         opts.doc_lo, opts.doc_hi = (self.doc_range if self.doc_range else (0, 0))
         opts.threads = self.threads
+        opts.positions = 1 if self.positions else 0
         h = C.c_void_p()
         check(lib.wsr_open(self.engine_dir_path.encode(), C.byref(opts), C.byref(h)))
         self._h = h
@@ -139,14 +145,13 @@ class VacuumEngine:
 
     def resolve(self, query: SearchQuery):
         """-> (wsr_query, doc_freqs or None) with the reference's empty-result rules."""
-        if query.is_phrase and len(query.terms) > 1:
-            raise NotImplementedError("phrase queries (position intersect + bloom) are not built yet")
         if len(query.terms) > _capi.MAX_TERMS:
             raise NotImplementedError(f"more than {_capi.MAX_TERMS} terms per query")
         if query.n_results > _capi.MAX_K:
             raise NotImplementedError(f"n_results above {_capi.MAX_K}")
         q = _capi.Query()
         q.k = max(0, int(query.n_results))
+        q.flags = _capi.QUERY_PHRASE if (query.is_phrase and len(query.terms) > 1) else 0
         ids, dfs = [], []
         for t in query.terms:
             lid, df = self.lookup(t)
@@ -255,3 +260,23 @@ def gen_two_term_log(index_dir: str, out_path: str, n_queries: int = 100_000, se
     check(lib.wsr_gen_two_term_log(index_dir.encode(), n_queries, seed, out_path.encode(),
                                    C.byref(n)))
     return n.value
+
+
+def gen_phrase_log(index_dir: str, out_path: str, n_queries: int = 10_000, seed: int = 7) -> int:
+    """tools/gen_synthetic_log.py:254-265 over a synthetic index's phrase pool."""
+    n = C.c_int64()
+    check(lib.wsr_gen_phrase_log(index_dir.encode(), n_queries, seed, out_path.encode(),
+                                 C.byref(n)))
+    return n.value
+
+
+def read_query_log(path: str):
+    """-> [(terms, is_phrase)]: one query per line, a phrase in double quotes"""
+    out = []
+    for line in open(path).read().splitlines():
+        line = line.strip()
+        if not line:
+            continue
+        ph = len(line) >= 2 and line[0] == '"' and line[-1] == '"'
+        out.append(((line[1:-1] if ph else line).split(), ph))
+    return out

@@ -70,13 +70,14 @@ class ShardedSearcher:
     """One rank of a doc-range sharded engine (device = local GPU)."""
 
     def __init__(self, index_dir: str, rank: int, world: int, device: int = 0,
-                 threads: int = 0, group=None):
+                 threads: int = 0, group=None, positions: bool = True):
         from .engine import VacuumEngine
         self.rank, self.world, self.group = rank, world, group
         self.n_docs = index_doc_count(index_dir)
         self.doc_range = shard_range(self.n_docs, rank, world)
         self.engine = VacuumEngine(index_dir, device=device, threads=threads,
-                                   doc_range=self.doc_range if world > 1 else None)
+                                   doc_range=self.doc_range if world > 1 else None,
+                                   positions=positions)
         self.engine.Load()
         self._batches = {}
 
