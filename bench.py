@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "queries/sec + p50 lat, 2-term AND BM25 top-10 on Wikipedia, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CPU_SHARE = min(16, os.cpu_count() or 1)   # host threads per GPU on the box (its CPU share)
 
 
 def log(msg):
@@ -56,9 +57,11 @@ def parse():
     p.add_argument("--dist-backend", default="nccl",
                    help="shard exchange backend (nccl = RCCL over xGMI; gloo for 1-GPU rehearsals)")
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
-    p.add_argument("--cpu-seconds", type=float, default=12.0,
+    p.add_argument("--cpu-seconds", type=float, default=16.0,
                    help="bounded CPU-baseline sample (oracle, 1 thread), rank 0 at N=1")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the mixed 1-5 term and phrase legs (N=1 only)")
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
     return p.parse_args()
 
@@ -89,11 +92,11 @@ def resolve(eng, chunk, k):
     return arr
 
 
-def check_against_oracle(idx, chunk, hits, nh, k, n):
+def check_against_oracle(idx, chunk, hits, nh, k, n, phrase=False):
     from oracle.oracle import OracleVacuum
     orc = OracleVacuum(idx)
     for i, terms in enumerate(chunk[:n]):
-        want, _ = orc.search(terms, k)
+        want, _ = orc.search(terms, k, phrase=phrase)
         got = [(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])]
         if got != want:
             raise SystemExit(f"parity failure on {terms}: {got[:3]} vs {want[:3]}")
@@ -101,18 +104,132 @@ def check_against_oracle(idx, chunk, hits, nh, k, n):
     return min(n, len(chunk))
 
 
-def cpu_baseline(idx, lines, k, seconds):
+def cpu_rate(idx, lines, k, seconds, threads, phrases=None):
+    """(queries, seconds) of the oracle over the head of a log, bounded in time."""
     from oracle.oracle import OracleVacuum
     orc = OracleVacuum(idx)
+    step = 64 * threads
     done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and done < len(lines):
-        orc.search_lines(lines[done:done + 64], k, threads=1)
-        done += 64
+    while time.perf_counter() - t0 < seconds:   # the log is cycled when it runs out
+        at = done % len(lines)
+        orc.search_lines(lines[at:at + step], k, threads=threads,
+                         phrases=phrases[at:at + step] if phrases else None)
+        done += len(lines[at:at + step])
     cel = time.perf_counter() - t0
     orc.close()
-    return {"value": round(done / cel, 1), "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} queries of the same log, oracle restatement of "
-                      f"VacuumEngine::Search, 1 thread, {cel:.1f}s"}
+    return done, cel
+
+
+def cpu_baseline(idx, lines, k, seconds):
+    """the CPU restatement on the box's host cores, 1 thread and the
+    box's CPU share (std::thread workers over the shared read-only index, as the
+    reference's gRPC threads share one engine, grpc_server_impl.h:260-263)."""
+    threads = CPU_SHARE
+    d1, c1 = cpu_rate(idx, lines, k, seconds / 2, 1)
+    dn, cn = cpu_rate(idx, lines, k, seconds / 2, threads)
+    return {"value": round(dn / cn, 1), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{dn} queries of the same log (cycled from its start), oracle "
+                      f"restatement of VacuumEngine::Search, {threads} threads, {cn:.1f}s; "
+                      f"1 thread: {d1} queries in {c1:.1f}s",
+            "single_thread": round(d1 / c1, 1), "cpu_model": cpu_model()}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
+    """A secondary workload on one GPU: items = [(terms, is_phrase)] in
+    batches of `batch` resident queries; the timed region runs every batch
+    `passes` times (consecutive batches in flight, as the main leg)."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    batches, chunks = [], []
+    for s in range(0, len(items), batch):
+        chunk = items[s:s + batch]
+        arr = (_capi.Query * len(chunk))()
+        for i, (terms, ph) in enumerate(chunk):
+            arr[i] = eng.resolve(w.SearchQuery(terms, n_results=k, is_phrase=ph))[0]
+        b = w.ResidentBatch(eng, batch, k)
+        b.upload(arr)
+        batches.append(b)
+        chunks.append(chunk)
+    checked = 0
+    if check:
+        batches[0].run()
+        hits, nh = batches[0].fetch()
+        ph = bool(chunks[0][0][1])
+        checked = check_against_oracle(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=ph)
+    for b in batches:
+        b.run()
+    w.sync(eng)
+    lat = []
+    for b in batches:
+        t0 = time.perf_counter()
+        b.run()
+        b.fetch()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    acc = kernel_accounting(eng, batches)
+    w.sync(eng)
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        for b in batches:
+            b.run()
+    w.sync(eng)
+    el = time.perf_counter() - t0
+    nq = len(items) * passes
+    for b in batches:
+        b.close()
+    out = {"value": round(nq / el, 1), "unit": "queries/s", "queries": len(items),
+           "batch": batch, "passes": passes, "p50_ms": round(statistics.median(lat), 3),
+           "segment_ms_per_batch": round(acc["seg"] / len(batches), 4),
+           "survivors_per_batch": int(acc["surv"] / len(batches)),
+           "parity_checked_queries": checked}
+    if cpu_seconds:
+        lines = [t for t, _ in items]
+        phr = [p for _, p in items]
+        d, c = cpu_rate(idx, lines, k, cpu_seconds, CPU_SHARE, phrases=phr)
+        out["cpu_baseline"] = {"value": round(d / c, 1), "cores": CPU_SHARE, "kind": "port",
+                               "sample": f"{d} queries of the leg's log (cycled), {c:.1f}s"}
+    return out
+
+
+def extra_legs(a, idx, local, threads):
+    """BASELINE configs[3] / [4] analogues on the C2 index, one GPU: mixed
+    1-5 term AND queries (AOL shares) and 2-term phrase queries."""
+    import wiser_amd as w
+    legs = {}
+    mixed = os.path.join(idx, "mixed_20000.log")
+    phr = os.path.join(idx, "phrase_10000.log")
+    if not os.path.exists(mixed):
+        w.gen_mixed_log(idx, mixed, n_queries=20000, seed=7)
+    if not os.path.exists(phr):
+        w.gen_phrase_log(idx, phr, n_queries=10000, seed=7)
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+    eng.Load()
+    items = [(l.split(), False) for l in open(mixed).read().splitlines()]
+    legs["c4_mixed_1to5"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
+                                    0 if a.no_cpu else a.cpu_seconds / 4)
+    legs["c4_mixed_1to5"]["workload"] = ("20000 AND queries of 1-5 terms (AOL term-count shares, "
+                                         "gen_synthetic_log group rule, seed 7), top-10")
+    eng.close()
+    t = time.time()
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
+    eng.Load()
+    log(f"engine with positions loaded in {time.time()-t:.1f}s")
+    items = w.read_query_log(phr)
+    legs["c5_phrase"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
+                                0 if a.no_cpu else a.cpu_seconds / 4)
+    legs["c5_phrase"]["workload"] = ("10000 two-term phrase queries drawn from the corpus's "
+                                     "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
+    eng.close()
+    return legs
 
 
 def kernel_accounting(eng, batches):
@@ -298,6 +415,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds)
+    extra = None
+    if rank == 0 and world == 1 and not a.no_extra:
+        extra = extra_legs(a, idx, local, threads)
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_segment.json")
@@ -338,6 +458,8 @@ def main():
         }
         if docshard:
             out["docshard"] = docshard
+        if extra:
+            out["legs"] = extra
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

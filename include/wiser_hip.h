@@ -188,6 +188,9 @@ int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, doub
                         wsr_build_stats* st);
 int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                          const char* out_path, int64_t* n_written);
+/* mixed 1-5 term AND log (AOL term-count shares; SURVEY 8d "C4") */
+int wsr_gen_mixed_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                      const char* out_path, int64_t* n_written);
 /* phrase log (tools/gen_synthetic_log.py:254-265) from a synthetic index's
  * phrase pool: one "t1 t2" per line, in double quotes */
 int wsr_gen_phrase_log(const char* index_dir, int64_t n_queries, uint64_t seed,

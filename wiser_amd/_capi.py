@@ -108,6 +108,8 @@ _sigs = {
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
+    "wsr_gen_mixed_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
+                                    C.POINTER(C.c_int64)]),
     "wsr_gen_phrase_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                      C.POINTER(C.c_int64)]),
 }

@@ -771,6 +771,18 @@ int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed
   return WSR_OK;
 }
 
+int wsr_gen_mixed_log(const char* index_dir, int64_t n_queries, uint64_t seed,
+                      const char* out_path, int64_t* n_written) {
+  if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
+  try {
+    int64_t n = gen_mixed_log(index_dir, n_queries, seed, out_path);
+    if (n_written) *n_written = n;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
 int wsr_gen_phrase_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                        const char* out_path, int64_t* n_written) {
   if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");

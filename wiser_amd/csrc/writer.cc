@@ -554,12 +554,13 @@ BuildStats build_synthetic(const SyntheticSpec& sp, const std::string& out_dir) 
 }
 
 // --------------------------------------------------------- query log gen --
-int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t seed,
-                         const std::string& out_path) {
+namespace {
+// The df groups of tools/gen_synthetic_log.py:21-28 over an index's df table:
+// "low" = floor(log10 df) in 0..3, "high" = 4..6.
+void df_groups(const std::string& dir, std::vector<std::string>* low, std::vector<std::string>* high) {
   std::ifstream tip(dir + "/my.tip", std::ios::binary);
   std::ifstream vac(dir + "/my.vacuum", std::ios::binary);
   if (!tip || !vac) throw std::runtime_error("cannot open index in " + dir);
-  std::vector<std::string> low, high;
   for (;;) {
     uint32_t len;
     if (!tip.read(reinterpret_cast<char*>(&len), 4)) break;
@@ -573,11 +574,18 @@ int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t see
     uint64_t df = 0;
     if (buf[0] != kPostingListMagic || !get_varint(buf + 1, buf + sizeof buf, &df))
       throw std::runtime_error("bad posting list header for " + term);
-    if (df >= 1 && df < 10000) low.push_back(term);
-    else if (df >= 10000 && df < 10000000) high.push_back(term);
+    if (df >= 1 && df < 10000) low->push_back(term);
+    else if (df >= 10000 && df < 10000000) high->push_back(term);
   }
-  if (low.empty() || high.empty() || low.size() + high.size() < 2)
+  if (low->empty() || high->empty() || low->size() + high->size() < 2)
     throw std::runtime_error("df table has an empty low or high group");
+}
+}  // namespace
+
+int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t seed,
+                         const std::string& out_path) {
+  std::vector<std::string> low, high;
+  df_groups(dir, &low, &high);
   std::mt19937_64 g(seed);
   std::unordered_set<std::string> seen;
   std::vector<std::string> out;
@@ -593,6 +601,42 @@ int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t see
     if (t2 == t1) continue;
     if (t2 < t1) std::swap(t1, t2);
     std::string q = t1 + " " + t2;
+    if (seen.insert(q).second) out.push_back(q);
+  }
+  std::ofstream f(out_path, std::ios::trunc);
+  for (auto& q : out) f << q << "\n";
+  return static_cast<int64_t>(out.size());
+}
+
+int64_t gen_mixed_log(const std::string& dir, int64_t n_queries, uint64_t seed,
+                      const std::string& out_path) {
+  std::vector<std::string> low, high;
+  df_groups(dir, &low, &high);
+  // terms per query: the AOL log's shares of 1..5-term queries
+  // (data/AOL_QueryLog_analysis/stat.txt), renormalised
+  const double share[5] = {36.8, 25.2, 17.3, 10.0, 5.3};
+  double tot = 0;
+  for (double x : share) tot += x;
+  std::mt19937_64 g(seed);
+  std::unordered_set<std::string> seen;
+  std::vector<std::string> out;
+  int64_t guard = 0;
+  while (static_cast<int64_t>(out.size()) < n_queries) {
+    if (++guard > 1000 * n_queries + 1000000) throw std::runtime_error("cannot find enough distinct queries");
+    const double u = (static_cast<double>(g() >> 11) * 0x1.0p-53) * tot;
+    int n = 1;
+    for (double acc = share[0]; n < 5 && u >= acc; acc += share[n], ++n) {}
+    std::vector<std::string> terms;
+    int spins = 0;
+    while (static_cast<int>(terms.size()) < n && spins++ < 10000) {
+      const auto& grp = (g() & 1) ? high : low;   // as two_term_queries: group, then term
+      std::string t = grp[g() % grp.size()];
+      if (std::find(terms.begin(), terms.end(), t) == terms.end()) terms.push_back(t);
+    }
+    if (static_cast<int>(terms.size()) < n) continue;
+    std::sort(terms.begin(), terms.end());
+    std::string q;
+    for (auto& t : terms) q += (q.empty() ? "" : " ") + t;
     if (seen.insert(q).second) out.push_back(q);
   }
   std::ofstream f(out_path, std::ios::trunc);

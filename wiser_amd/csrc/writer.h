@@ -47,6 +47,12 @@ BuildStats build_synthetic(const SyntheticSpec& spec, const std::string& out_dir
 int64_t gen_two_term_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
                          const std::string& out_path);
 
+// Mixed 1-5 term AND log (BASELINE configs[3], SURVEY 8d "C4"): terms per query
+// by the AOL log's shares (36.8/25.2/17.3/10.0/5.3 %, renormalised), each term
+// drawn as in gen_two_term_log, distinct and sorted, distinct queries.
+int64_t gen_mixed_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
+                      const std::string& out_path);
+
 // Phrase query log restating tools/gen_synthetic_log.py:254-265: n phrases
 // drawn without replacement from the index's phrase pool (phrases.txt, written
 // by build_synthetic), one per line in double quotes.

@@ -262,6 +262,14 @@ def gen_two_term_log(index_dir: str, out_path: str, n_queries: int = 100_000, se
     return n.value
 
 
+def gen_mixed_log(index_dir: str, out_path: str, n_queries: int = 20_000, seed: int = 7) -> int:
+    """1-5 term AND queries with the AOL term-count shares."""
+    n = C.c_int64()
+    check(lib.wsr_gen_mixed_log(index_dir.encode(), n_queries, seed, out_path.encode(),
+                                C.byref(n)))
+    return n.value
+
+
 def gen_phrase_log(index_dir: str, out_path: str, n_queries: int = 10_000, seed: int = 7) -> int:
     """tools/gen_synthetic_log.py:254-265 over a synthetic index's phrase pool."""
     n = C.c_int64()
