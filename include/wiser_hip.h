@@ -183,6 +183,12 @@ typedef struct wsr_build_stats {
 /* format: "TOKEN_ONLY" or "WITH_POSITIONS"; n_rows < 0 reads every row */
 int wsr_build_from_linedoc(const char* linedoc, int64_t n_rows, const char* format,
                            const char* out_dir, wsr_build_stats* st);
+/* the same, writing the two-way phrase bloom filters of every posting
+ * (FlashEngineDumper::DumpPostingListWithBloom, flash_engine_dumper.h:412-525):
+ * ratio / expected_entries as BloomDumper's (defaults 0.0009, 5) */
+int wsr_build_from_linedoc_bloom(const char* linedoc, int64_t n_rows, const char* format,
+                                 const char* out_dir, float ratio, int32_t expected_entries,
+                                 wsr_build_stats* st);
 int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, double zipf_s,
                         uint64_t seed, int32_t with_positions, int32_t threads,
                         wsr_build_stats* st);

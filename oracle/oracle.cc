@@ -269,6 +269,121 @@ class TfIter {
   VIntsIter vints_;
 };
 
+// ---------------------------------------------------------------- bloom --
+std::atomic<int64_t> g_bloom_checks{0}, g_bloom_pruned{0};
+
+// MurmurHash2 (libbloom/murmur2/MurmurHash2.c:15-64), little-endian reads
+uint32_t murmur2(const void* key, int len, uint32_t seed) {
+  const uint32_t m = 0x5bd1e995;
+  uint32_t h = seed ^ static_cast<uint32_t>(len);
+  const uint8_t* d = static_cast<const uint8_t*>(key);
+  for (; len >= 4; d += 4, len -= 4) {
+    uint32_t k = static_cast<uint32_t>(d[0]) | static_cast<uint32_t>(d[1]) << 8 |
+                 static_cast<uint32_t>(d[2]) << 16 | static_cast<uint32_t>(d[3]) << 24;
+    k *= m; k ^= k >> 24; k *= m;
+    h *= m; h ^= k;
+  }
+  if (len == 3) h ^= static_cast<uint32_t>(d[2]) << 16;
+  if (len >= 2) h ^= static_cast<uint32_t>(d[1]) << 8;
+  if (len >= 1) { h ^= d[0]; h *= m; }
+  h ^= h >> 13; h *= m; h ^= h >> 15;
+  return h;
+}
+
+// bloom_set (libbloom/bloom.c:84-115) + bloom_check (:48-75): 1 = may be present
+struct BloomParams {
+  int bits = 0, hashes = 0;
+  void set(int entries, double error) {
+    const double bpe = -(std::log(error) / 0.480453013918201);
+    bits = static_cast<int>(static_cast<double>(entries) * bpe);
+    hashes = static_cast<int>(std::ceil(0.693147180559945 * bpe));
+  }
+  int check(const uint8_t* bf, const std::string& s) const {
+    const uint32_t a = murmur2(s.data(), static_cast<int>(s.size()), 0x9747b28c);
+    const uint32_t b = murmur2(s.data(), static_cast<int>(s.size()), a);
+    int hits = 0;
+    for (uint32_t i = 0; i < static_cast<uint32_t>(hashes); ++i) {
+      const uint32_t x = (a + i * b) % static_cast<uint32_t>(bits);
+      if (bf[x >> 3] & (1u << (x % 8))) ++hits;
+    }
+    return hits == hashes ? 1 : 0;
+  }
+};
+
+// VacuumHeader (flash_iterators.h:826-889): the "end" fields are the ones used
+// by both readers
+struct VacHeader {
+  bool has_bloom = false;
+  uint32_t bit_array_bytes = 0, expected_entries = 0;
+  float ratio = 0;
+  void load(const uint8_t* p) {
+    ++p;
+    uint64_t v[3];
+    for (int s = 0; s < 2; ++s) {
+      for (int i = 0; i < 3; ++i) p += varint_decode(p, &v[i]);
+      float r;
+      std::memcpy(&r, p, 4);
+      p += 4;
+      if (s == 1) {
+        has_bloom = v[0] != 0;
+        bit_array_bytes = static_cast<uint32_t>(v[1]);
+        expected_entries = static_cast<uint32_t>(v[2]);
+        ratio = r;
+      }
+    }
+  }
+};
+
+// BloomFilterColumnReader (flash_iterators.h:776-823) over BloomSkipList and
+// BloomBoxIterator (flash_containers.h:560-687): the bit array of a posting,
+// nullptr when its box bitmap marks it absent
+class BloomColumn {
+ public:
+  void reset(const uint8_t* pl, uint64_t section_off, uint32_t item_bytes) {
+    pl_ = pl; sec_ = pl + section_off; item_bytes_ = item_bytes; loaded_ = false; box_ = -1;
+  }
+  const uint8_t* bit_array(int posting) {
+    if (!loaded_) {   // LoadSkipList: 0xA4 | n | delta offsets from the list start
+      if (sec_[0] != 0xA4) throw std::runtime_error("bloom skip list magic");
+      uint64_t n, prev = 0;
+      const uint8_t* p = sec_ + 1;
+      p += varint_decode(p, &n);
+      boxes_.clear();
+      for (uint64_t i = 0; i < n; ++i) { uint64_t d; p += varint_decode(p, &d); prev += d; boxes_.push_back(prev); }
+      loaded_ = true;
+    }
+    const int box = posting / kPack;
+    if (box != box_) {   // BloomBoxIterator::Fill
+      const uint8_t* b = pl_ + boxes_.at(box);
+      if (b[0] != 0xF5) throw std::runtime_error("bloom box magic");
+      uint64_t n;
+      const uint8_t* p = b + 1;
+      p += varint_decode(p, &n);
+      int phys = 0;
+      for (uint64_t i = 0; i < n; ++i) {
+        const bool has = p[i / 8] & (0x80u >> (i % 8));   // DecodeBitmapByte, MSB first
+        map_[i] = has ? phys++ : -1;
+      }
+      items_ = p + (n + 7) / 8;
+      n_ = static_cast<int>(n);
+      box_ = box;
+    }
+    const int i = posting % kPack;
+    if (i >= n_ || map_[i] < 0) return nullptr;
+    return items_ + static_cast<uint64_t>(map_[i]) * item_bytes_;
+  }
+
+ private:
+  const uint8_t* pl_ = nullptr;
+  const uint8_t* sec_ = nullptr;
+  uint32_t item_bytes_ = 0;
+  bool loaded_ = false;
+  std::vector<uint64_t> boxes_;
+  int box_ = -1, n_ = 0;
+  int map_[kPack];
+  const uint8_t* items_ = nullptr;
+};
+
 // CozyBoxIterator (flash_iterators.h:280-412): a run of packs then one VInts
 // blob; it does not know where the box ends (the caller counts entries).
 class CozyIter {
@@ -439,12 +554,24 @@ int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* tabl
 // BLM_MAY_PRESENT (:1039-1058) and every found doc goes to the position check.
 class VacuumIter {
  public:
-  VacuumIter(const uint8_t* file, uint64_t off) {
+  VacuumIter(const uint8_t* file, uint64_t off, const VacHeader* hdr = nullptr,
+             const std::string* term = nullptr)
+      : hdr_(hdr), term_(term) {
     const uint8_t* buf = file + off;
     if (buf[0] != kPostingMagic) throw std::runtime_error("posting list magic");
     uint64_t df;
     int l = varint_decode(buf + 1, &df);
     n_ = static_cast<int>(df);
+    if (hdr_ && hdr_->has_bloom) {   // the 8 reserved bytes: section offsets (:923-944)
+      uint64_t b0, b1;
+      const uint8_t* p = buf + 1 + l;
+      p += varint_decode(p, &b0);
+      varint_decode(p, &b1);
+      blm_ = std::make_shared<std::vector<BloomColumn>>(2);
+      (*blm_)[0].reset(buf, b0, hdr_->bit_array_bytes);
+      (*blm_)[1].reset(buf, b1, hdr_->bit_array_bytes);
+      bparams_.set(static_cast<int>(hdr_->expected_entries), static_cast<double>(hdr_->ratio));
+    }
     skip_ = std::make_shared<std::vector<SkipEntry>>(load_skip_list(buf + 1 + l + 8));
     doc_.reset(file, skip_.get(), n_);
     tf_.reset(file, skip_.get());
@@ -459,8 +586,25 @@ class VacuumIter {
   void skip_forward(uint32_t d) { doc_.skip_forward(d); }
   // AssignPositionBegin (:1002-1005)
   PosBagIter* position_begin() { pos_->skip_to(doc_.posting_index()); return pos_.get(); }
+  const std::string& term() const { return *term_; }
+  // HasPriorTerm / HasNextTerm / HasTerm (:994-1000,1039-1058): 0 = not present,
+  // 1 = may be present (always, without bloom filters)
+  int has_prior_term(const std::string& t) { return has_term(0, t); }
+  int has_next_term(const std::string& t) { return has_term(1, t); }
 
  private:
+  int has_term(int side, const std::string& t) {
+    if (!blm_) return 1;
+    ++g_bloom_checks;
+    const uint8_t* bf = (*blm_)[side].bit_array(doc_.posting_index());
+    const int r = bf ? bparams_.check(bf, t) : 0;
+    if (!r) ++g_bloom_pruned;
+    return r;
+  }
+  const VacHeader* hdr_ = nullptr;
+  const std::string* term_ = nullptr;
+  std::shared_ptr<std::vector<BloomColumn>> blm_;
+  BloomParams bparams_;
   int n_ = 0;
   std::shared_ptr<std::vector<SkipEntry>> skip_;
   DocIdIter doc_;
@@ -480,6 +624,9 @@ class MemIter {
   void advance() { ++i_; }
   void skip_forward(uint32_t v) { while (i_ < d_->size() && (*d_)[i_] < v) ++i_; }
   PosBagIter* position_begin() { throw std::runtime_error("phrase queries need a Vacuum index"); }
+  const std::string& term() const { throw std::runtime_error("phrase queries need a Vacuum index"); }
+  int has_prior_term(const std::string&) { return 1; }
+  int has_next_term(const std::string&) { return 1; }
 
  private:
   const std::vector<uint32_t>* d_;
@@ -546,8 +693,8 @@ template <class It>
 class Processor {
  public:
   Processor(const Bm25& sim, std::vector<It>* its, const std::vector<uint8_t>& lens, int n_docs, int k,
-            bool phrase = false)
-      : sim_(sim), its_(*its), lens_(lens), k_(k), phrase_(phrase) {
+            bool phrase = false, int bloom_factor = 1)
+      : sim_(sim), its_(*its), lens_(lens), k_(k), phrase_(phrase), bloom_factor_(bloom_factor) {
     for (auto& it : its_) idf_.push_back(es_idf(n_docs, it.size()));   // :544-547
   }
   // qq_search::ProcessQueryDelta dispatch (:966-978): one term ->
@@ -584,9 +731,25 @@ class Processor {
   // HandleTheFoundDoc (:886-895): a phrase query ranks the doc only when the
   // positions hold the phrase (FindPhrase :854-867; RankDocForPhrase scores and
   // inserts exactly as RankDoc, :897-912)
+  // IsPossibleToPresent (:873-884) with CheckBloomWithEnableFactor (:796-807) and
+  // CheckBloomFallBack (:784-794); BLOOM_NEVER_USE = 0 (types.h:54)
+  bool possible() {
+    if (bloom_factor_ == 0) return true;
+    if (its_.size() != 2) {
+      for (size_t i = 0; i + 1 < its_.size(); ++i)
+        if (its_[i].has_next_term(its_[i + 1].term()) == 0) return false;
+      return true;
+    }
+    const size_t s1 = static_cast<size_t>(its_[0].size()), s2 = static_cast<size_t>(its_[1].size());
+    const size_t f = static_cast<size_t>(bloom_factor_);
+    if (f * s1 <= s2) return its_[0].has_next_term(its_[1].term()) != 0;
+    if (f * s2 < s1) return its_[1].has_prior_term(its_[0].term()) != 0;
+    return true;
+  }
   void found(int doc) {
     if (phrase_ && its_.size() > 1) {
       ++n_phrase_checks_;
+      if (!possible()) return;   // FindPhrase returns 0 matches
       std::vector<PosBagIter*> ps;
       for (auto& it : its_) ps.push_back(it.position_begin());
       if (phrase_process(ps, nullptr) > 0) rank(doc);
@@ -642,6 +805,7 @@ class Processor {
   const std::vector<uint8_t>& lens_;
   int k_;
   bool phrase_;
+  int bloom_factor_;
   int64_t n_phrase_checks_ = 0;
   std::vector<double> idf_;
   MinHeap heap_;
@@ -680,6 +844,8 @@ std::vector<std::string> explode_strict(const std::string& s, char c) {  // util
 struct orc_vacuum {
   uint8_t* map = nullptr;
   size_t len = 0;
+  VacHeader hdr;
+  int bloom_factor = 1;   // CreateSearchEngine's bloom_enable_factor default (engine_factory.h:33-34)
   std::unordered_map<std::string, uint64_t> tip;  // term -> posting list offset
   std::vector<uint8_t> lens;                      // DocLengthCharStore
   int n_docs = 0;
@@ -788,6 +954,7 @@ orc_vacuum* orc_vacuum_open(const char* dir) {
       if (p == MAP_FAILED) throw std::runtime_error("mmap");
       h->map = static_cast<uint8_t*>(p);
       if (h->map[0] != kVacuumMagic) throw std::runtime_error("Vacuum's first byte is wrong");
+      h->hdr.load(h->map);
     }
   } catch (const std::exception& e) {
     g_err = e.what();
@@ -803,6 +970,26 @@ void orc_vacuum_close(orc_vacuum* h) {
 }
 
 int orc_vacuum_term_count(orc_vacuum* h) { return static_cast<int>(h->tip.size()); }
+void orc_vacuum_set_bloom_factor(orc_vacuum* h, int f) { h->bloom_factor = f; }
+int orc_vacuum_has_bloom(orc_vacuum* h) { return h->hdr.has_bloom ? 1 : 0; }
+void orc_bloom_stats(int64_t* checks, int64_t* pruned) {
+  *checks = g_bloom_checks.load();
+  *pruned = g_bloom_pruned.load();
+}
+// the bloom bit array of one posting (0 = prior / begin, 1 = next / end) checked
+// for `elem`: 1 may be present, 0 not present (also: no filter), -1 no bloom
+int orc_vacuum_bloom_check(orc_vacuum* h, const char* term, int posting, int side, const char* elem) {
+  auto f = h->tip.find(term);
+  if (f == h->tip.end() || !h->hdr.has_bloom) return -1;
+  try {
+    VacuumIter it(h->map, f->second, &h->hdr, &f->first);
+    for (int i = 0; i < posting; ++i) it.advance();
+    return side ? it.has_next_term(elem) : it.has_prior_term(elem);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -2;
+  }
+}
 int orc_vacuum_n_docs(orc_vacuum* h) { return h->n_docs; }
 
 int orc_vacuum_df(orc_vacuum* h, const char* term) {
@@ -837,11 +1024,11 @@ int orc_vacuum_search_phrase(orc_vacuum* h, const char* const* terms, int n_term
     std::vector<VacuumIter> its;
     for (int i = 0; i < n_terms; ++i) {  // FindIteratorsSolid (vacuum_engine.h:89-99)
       auto f = h->tip.find(terms[i]);
-      if (f != h->tip.end()) its.emplace_back(h->map, f->second);
+      if (f != h->tip.end()) its.emplace_back(h->map, f->second, &h->hdr, &f->first);
     }
     if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
     if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
-    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k, is_phrase != 0);
+    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k, is_phrase != 0, h->bloom_factor);
     return emit(p.run(), docs, scores);
   } catch (const std::exception& e) {
     g_err = e.what();

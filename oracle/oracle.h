@@ -55,6 +55,13 @@ int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int 
 /* The same with SearchQuery::is_phrase (QueryProcessor's position check). */
 int orc_vacuum_search_phrase(orc_vacuum* h, const char* const* terms, int n_terms, int k,
                              int is_phrase, int32_t* docs, double* scores, int32_t* doc_freqs);
+/* bloom: QueryProcessor's bloom_enable_factor (1 by default, 0 = never use);
+ * whether the index carries bloom filters; checks / prunes counted so far;
+ * one posting's filter checked for an element (1 may be present, 0 not) */
+void orc_vacuum_set_bloom_factor(orc_vacuum* h, int factor);
+int orc_vacuum_has_bloom(orc_vacuum* h);
+void orc_bloom_stats(int64_t* checks, int64_t* pruned);
+int orc_vacuum_bloom_check(orc_vacuum* h, const char* term, int posting, int side, const char* elem);
 /* positions of posting `posting` of a term (PositionPostingBagIterator); returns tf */
 int orc_vacuum_positions(orc_vacuum* h, const char* term, int posting, uint32_t* out, int cap);
 /* PhraseQueryProcessor2 over plain sorted position lists: NumOfMatches, and the

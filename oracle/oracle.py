@@ -56,6 +56,10 @@ for name, res, args in [
     ("orc_qqmem_search", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, _I32P, _F64P,
                                    _I32P]),
     ("orc_ub_negative_char_index", C.c_int64, []),
+    ("orc_vacuum_set_bloom_factor", None, [_P, C.c_int]),
+    ("orc_vacuum_has_bloom", C.c_int, [_P]),
+    ("orc_bloom_stats", None, [C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    ("orc_vacuum_bloom_check", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, C.c_char_p]),
 ]:
     f = getattr(lib, name)
     f.restype = res
@@ -84,10 +88,21 @@ def _search(fn, h, terms, k, *extra):
 class OracleVacuum:
     """VacuumEngine restatement reading my.vacuum / my.tip / my.doc_length."""
 
-    def __init__(self, index_dir: str):
+    def __init__(self, index_dir: str, bloom_factor: int = 1):
         self.h = lib.orc_vacuum_open(index_dir.encode())
         if not self.h:
             raise RuntimeError(_err())
+        lib.orc_vacuum_set_bloom_factor(self.h, bloom_factor)
+
+    def has_bloom(self):
+        return bool(lib.orc_vacuum_has_bloom(self.h))
+
+    def bloom_check(self, term, posting, side, elem):
+        """side 0 = prior (begin) filter, 1 = next (end) filter -> 1 / 0"""
+        r = lib.orc_vacuum_bloom_check(self.h, term.encode(), posting, side, elem.encode())
+        if r < -1:
+            raise RuntimeError(_err())
+        return r
 
     def close(self):
         if self.h:
@@ -203,3 +218,10 @@ def phrase_lists(lists, cap=64):
     table = (C.c_int32 * (len(lists) * cap))()
     m = lib.orc_phrase_lists(ptrs, sizes, len(lists), table, cap)
     return m, [[table[i * cap + j] for j in range(min(m, cap))] for i in range(len(lists))]
+
+
+def bloom_stats():
+    """(bloom checks, docs pruned by a filter) over the process so far"""
+    c, p = C.c_int64(), C.c_int64()
+    lib.orc_bloom_stats(C.byref(c), C.byref(p))
+    return c.value, p.value

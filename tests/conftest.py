@@ -132,3 +132,27 @@ def phrase_cases(seqs, n, seed):
         else:
             cases.append([f"w{rng.randrange(12)}" for _ in range(m)])   # head words, maybe repeated
     return cases
+
+
+# ---- bloom-filter indexes (the same fixtures written with two-way phrase blooms) ----
+BLOOM_RATIO, BLOOM_ENTRIES = 0.0009, 5   # BloomDumper defaults (bloom_filter.h:650-655)
+
+
+def _build_bloom(src, d, fmt="WITH_POSITIONS", bloom=(BLOOM_RATIO, BLOOM_ENTRIES)):
+    import wiser_amd as w
+    os.makedirs(d, exist_ok=True)
+    w.build_from_linedoc(src, d, fmt, bloom=bloom)
+    return d
+
+
+@pytest.fixture(scope="module")
+def bloom_indexes(built, indexes, positions_index, tmp_path_factory):
+    root = str(tmp_path_factory.mktemp("bloom"))
+    out = {}
+    out["bi3"] = (_build_bloom(os.path.join(DATA, "iter_test_3_docs_tf_bi-bloom"), f"{root}/bi3"),
+                  _build_bloom(os.path.join(DATA, "iter_test_3_docs_tf_bi-bloom"), f"{root}/bi3_nb",
+                         bloom=None))
+    out["wiki5"] = (_build_bloom(indexes["wiki5"][2], f"{root}/wiki5"), indexes["wiki5"][0])
+    pos_ld = os.path.join(os.path.dirname(positions_index[0]), "pos.linedoc")
+    out["pos"] = (_build_bloom(pos_ld, f"{root}/pos"), positions_index[0])
+    return out

@@ -136,3 +136,30 @@ def test_phrase_needs_positions(indexes):
     # a one-term phrase is an ordinary single-term query
     assert e.Search(w.SearchQuery(["a"], is_phrase=True)).Size() == 3
     e.close()
+
+
+@pytest.mark.parametrize("name", ["bi3", "wiki5", "pos"])
+def test_bloom_index_loads_and_matches(bloom_indexes, name):
+    """An index written with two-way bloom filters (reference layout) loads; the
+    GPU's exact position check gives the results of the reference's bloom-pruned
+    path (oracle with bloom_enable_factor 1), for phrase and plain queries."""
+    from conftest import all_tokens
+    from oracle.oracle import OracleVacuum
+    d, plain = bloom_indexes[name]
+    eng = _engine(d, "dense")
+    orc = OracleVacuum(d)
+    assert orc.has_bloom()
+    orc_plain = OracleVacuum(plain)
+    rng = random.Random(len(name))
+    if name == "pos":
+        src = os.path.join(os.path.dirname(plain), "pos.linedoc")
+        seqs = [l.rstrip("\n").split("\t")[1].split() for l in open(src).readlines()[1:]]
+        qs = phrase_cases(seqs, 300, seed=43)
+    else:
+        words = ["a", "b", "c", "x"] if name == "bi3" else all_tokens()[:80]
+        qs = [rng.sample(words, 2) for _ in range(150)] + [rng.sample(words, 3) for _ in range(50)]
+    _check_phrase(eng, orc, qs, 10)
+    _check_phrase(eng, orc, qs, 10, phrase=False)
+    for q in qs[:100]:
+        assert orc.search(q, 10, phrase=True) == orc_plain.search(q, 10, phrase=True)
+    eng.close()

@@ -104,6 +104,8 @@ _sigs = {
                                          C.POINTER(C.c_int32)]),
     "wsr_build_from_linedoc": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_char_p,
                                          C.POINTER(BuildStats)]),
+    "wsr_build_from_linedoc_bloom": (C.c_int, [C.c_char_p, C.c_int64, C.c_char_p, C.c_char_p,
+                                               C.c_float, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_build_synthetic": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_double, C.c_uint64,
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,

@@ -740,6 +740,24 @@ int wsr_build_from_linedoc(const char* linedoc, int64_t n_rows, const char* form
   return WSR_OK;
 }
 
+int wsr_build_from_linedoc_bloom(const char* linedoc, int64_t n_rows, const char* format,
+                                 const char* out_dir, float ratio, int32_t expected_entries,
+                                 wsr_build_stats* st) {
+  if (!linedoc || !format || !out_dir) return fail(WSR_E_INVALID, "null argument");
+  if (!(ratio > 0.0f && ratio < 1.0f) || expected_entries < 1)
+    return fail(WSR_E_INVALID, "bloom ratio must be in (0, 1) and expected entries >= 1");
+  try {
+    BloomSpec b;
+    b.on = true;
+    b.ratio = ratio;
+    b.entries = expected_entries;
+    fill_stats(build_from_linedoc(linedoc, n_rows, format, out_dir, b), st);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
 int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, double zipf_s,
                         uint64_t seed, int32_t with_positions, int32_t threads,
                         wsr_build_stats* st) {

@@ -29,6 +29,8 @@ constexpr uint8_t kPostingListMagic = 0xF4;
 constexpr uint8_t kPackMagic = 0xD6;
 constexpr uint8_t kVIntsMagic = 0x9B;
 constexpr uint8_t kVacuumMagic = 0x88;
+constexpr uint8_t kBloomSkipListMagic = 0xA4;   // types.h:44
+constexpr uint8_t kBloomBoxMagic = 0xF5;        // types.h:48
 constexpr int kPackSize = 128;          // values per pack == postings per skip row
 constexpr int kVacuumHeaderBytes = 100; // first posting list starts here
 

@@ -79,8 +79,11 @@ void VacuumIndex::open(const std::string& dir) {
       q += 4;
       if (q > e) throw std::runtime_error("my.vacuum: truncated header");
     }
-    if (has_bloom[1])
-      throw std::runtime_error("my.vacuum carries bloom filters: the phrase/bloom path is not built yet");
+    // Bloom filters (has_bloom) only add sections between the tf and the
+    // position boxes of each list; every box is located through the skip
+    // rows, so the image is built the same way.  The position check of
+    // phrase queries is exact, so the filters (pruning only) are not uploaded.
+    has_bloom_ = has_bloom[1] != 0;
   }
   // --- my.tip (term_index.h:147-159)
   {

@@ -55,6 +55,7 @@ class VacuumIndex {
   // Skip rows of one list (decoded on demand).
   std::vector<SkipRow> rows(int32_t id) const;
   const uint8_t* file() const { return map_; }
+  bool has_bloom() const { return has_bloom_; }
   uint64_t file_bytes() const { return map_len_; }
 
  private:
@@ -69,6 +70,7 @@ class VacuumIndex {
   double cache_[256] = {0};
   uint8_t* map_ = nullptr;
   uint64_t map_len_ = 0;
+  bool has_bloom_ = false;
 };
 
 struct HostImage {

@@ -33,6 +33,7 @@
 #include <unordered_map>
 #include <unordered_set>
 
+#include "bloom.h"
 #include "format.h"
 
 namespace wiser {
@@ -46,6 +47,7 @@ struct TermPostings {
   std::vector<uint32_t> pos_sizes;
   std::vector<uint32_t> off_vals;   // per-bag delta coded [s0,e0,s1,e1..]
   std::vector<uint32_t> off_sizes;
+  std::vector<std::string> blm_begin, blm_end;   // per posting bloom bit arrays (bloom on)
 };
 
 // One encoded box: the bytes plus, for every skip row, where the row's first
@@ -97,11 +99,52 @@ struct EncodedList {
   uint32_t df = 0;
   std::vector<uint32_t> prev_doc;  // per row
   Box doc, tf, pos, off;
+  const std::vector<std::string>* blm[2] = {nullptr, nullptr};   // begin, end (bloom on)
 };
+
+// One bloom section (flash_engine_dumper.h:620-646): the bloom skip list
+// (0xA4 | varint n_boxes | delta varints of box offsets relative to the list
+// start, flash_containers.h:640-660), then the boxes of 128 postings each
+// (0xF5 | varint n | MSB-first presence bitmap | the non-empty bit arrays,
+// flash_containers.h:499-558).  `at` = offset of the section from the list
+// start; the skip list is sized with offsets 512 KB further out, as the
+// reference does, and the gap after it is padding.
+std::string bloom_section(const std::vector<std::string>& arrays, uint64_t at) {
+  std::vector<std::string> boxes;
+  for (size_t i = 0; i < arrays.size(); i += kPackSize) {
+    const size_t n = std::min<size_t>(kPackSize, arrays.size() - i);
+    std::string b;
+    b.push_back(static_cast<char>(kBloomBoxMagic));
+    put_varint(&b, n);
+    for (size_t c = 0; c < n; c += 8) {
+      uint8_t bits = 0;
+      for (size_t o = 0; o < 8 && c + o < n; ++o)
+        if (!arrays[i + c + o].empty()) bits |= static_cast<uint8_t>(1u << (7 - o));
+      b.push_back(static_cast<char>(bits));
+    }
+    for (size_t j = 0; j < n; ++j) b += arrays[i + j];
+    boxes.push_back(std::move(b));
+  }
+  auto skip = [&](uint64_t first) {
+    std::string sl;
+    sl.push_back(static_cast<char>(kBloomSkipListMagic));
+    put_varint(&sl, boxes.size());
+    uint64_t prev = 0, o = first;
+    for (auto& b : boxes) { put_varint(&sl, o - prev); prev = o; o += b.size(); }
+    return sl;
+  };
+  const size_t est = skip(at + 512 * 1024).size();
+  std::string sec = skip(at + est);
+  if (sec.size() > est) throw std::runtime_error("bloom skip list estimate too small");
+  sec.append(est - sec.size(), '\0');
+  for (auto& b : boxes) sec += b;
+  return sec;
+}
 
 void encode_list(const TermPostings& t, EncodedList* e) {
   const size_t n = t.docs.size();
   e->df = static_cast<uint32_t>(n);
+  if (!t.blm_end.empty()) { e->blm[0] = &t.blm_begin; e->blm[1] = &t.blm_end; }
   for (size_t r = 0; r * kPackSize < n; ++r)
     e->prev_doc.push_back(r == 0 ? 0 : t.docs[r * kPackSize - 1]);
   encode_box(t.docs, nullptr, n, true, &e->doc);
@@ -110,11 +153,12 @@ void encode_list(const TermPostings& t, EncodedList* e) {
   encode_box(t.off_vals, &t.off_sizes, n, false, &e->off);
 }
 
-// Skip list with the data sections starting at absolute file offset `data0`.
-std::string encode_skip_list(const EncodedList& e, uint64_t data0) {
+// Skip list with the data sections starting at absolute file offset `data0`
+// (`bloom_bytes` of bloom sections sit between the tf and position boxes).
+std::string encode_skip_list(const EncodedList& e, uint64_t data0, uint64_t bloom_bytes = 0) {
   const uint64_t d0 = data0;
   const uint64_t t0 = d0 + e.doc.bytes.size();
-  const uint64_t p0 = t0 + e.tf.bytes.size();
+  const uint64_t p0 = t0 + e.tf.bytes.size() + bloom_bytes;
   const uint64_t o0 = p0 + e.pos.bytes.size();
   std::string s;
   s.push_back(static_cast<char>(kSkipListMagic));
@@ -139,18 +183,26 @@ std::string encode_skip_list(const EncodedList& e, uint64_t data0) {
 
 class VacuumFileWriter {
  public:
-  explicit VacuumFileWriter(const std::string& dir) : dir_(dir) {
+  explicit VacuumFileWriter(const std::string& dir, const BloomSpec& bloom = BloomSpec())
+      : dir_(dir), bloom_(bloom.on) {
     ::mkdir(dir.c_str(), 0777);
     vac_.open(dir + "/my.vacuum", std::ios::binary | std::ios::trunc);
     tip_.open(dir + "/my.tip", std::ios::binary | std::ios::trunc);
     if (!vac_ || !tip_) throw std::runtime_error("cannot create index files in " + dir);
-    // No bloom filters: has_bloom, bit bytes, expected entries = 0, ratio 0.0f,
-    // for the "begin" and the "end" filter (flash_engine_dumper.h:288-316).
+    // has_bloom, bit array bytes, expected entries, f32 ratio, for the "begin"
+    // and the "end" filter (flash_engine_dumper.h:288-316); zeros without bloom
     std::string h;
     h.push_back(static_cast<char>(kVacuumMagic));
     for (int i = 0; i < 2; ++i) {
-      put_varint(&h, 0); put_varint(&h, 0); put_varint(&h, 0);
-      h.append(4, '\0');
+      if (bloom.on) {
+        put_varint(&h, 1);
+        put_varint(&h, static_cast<uint64_t>(BloomShape(bloom.entries, bloom.ratio).bytes));
+        put_varint(&h, static_cast<uint64_t>(bloom.entries));
+        h.append(reinterpret_cast<const char*>(&bloom.ratio), 4);
+      } else {
+        put_varint(&h, 0); put_varint(&h, 0); put_varint(&h, 0);
+        h.append(4, '\0');
+      }
     }
     h.resize(kVacuumHeaderBytes, '\0');
     vac_.write(h.data(), h.size());
@@ -167,19 +219,47 @@ class VacuumFileWriter {
     put_varint(&head, 0);
     head.resize(resv + 8, '\0');
     const uint64_t skip_start = start + head.size();
-    const size_t est = encode_skip_list(e, skip_start + 512 * 1024).size();
-    const std::string skip = encode_skip_list(e, skip_start + est);
-    if (skip.size() > est) throw std::runtime_error("skip list estimate too small");
-    head += skip;
-    head.append(est - skip.size(), '\0');
+    if (bloom_ && !e.blm[0]) throw std::runtime_error("bloom index: list of '" + term + "' has no filters");
+    // bloom sections are sized from their offsets, which follow the skip list:
+    // size the skip list for bloom sections 512 KB larger than any real one
+    std::string blm[2];
+    if (bloom_) {
+      // upper bound of both sections: every posting's array + box / skip overheads
+      uint64_t ub = 0;
+      for (int i = 0; i < 2; ++i)
+        for (auto& a : *e.blm[i]) ub += a.size();
+      ub += 2 * (e.df / kPackSize + 1) * (kPackSize / 8 + 2 * 10 + 4) + 64;
+      const uint64_t est0 = encode_skip_list(e, skip_start + 512 * 1024, ub + 1024 * 1024).size();
+      uint64_t at = skip_start + est0 + e.doc.bytes.size() + e.tf.bytes.size() - start;
+      for (int i = 0; i < 2; ++i) { blm[i] = bloom_section(*e.blm[i], at); at += blm[i].size(); }
+      const uint64_t bb = blm[0].size() + blm[1].size();
+      // the skip list written below is no larger than est0, so the sections
+      // keep their offsets: pad the skip list gap to est0
+      const std::string skip = encode_skip_list(e, skip_start + est0, bb);
+      if (skip.size() > est0) throw std::runtime_error("skip list estimate too small");
+      const uint64_t s0 = skip_start + est0 + e.doc.bytes.size() + e.tf.bytes.size() - start;
+      std::string ptr;   // the 8 reserved bytes: section offsets from the list start
+      put_varint(&ptr, s0);
+      put_varint(&ptr, s0 + blm[0].size());
+      if (ptr.size() > 8) throw std::runtime_error("bloom section pointers exceed 8 bytes");
+      head.replace(resv, ptr.size(), ptr);
+      head += skip;
+      head.append(est0 - skip.size(), '\0');
+    } else {
+      const size_t est = encode_skip_list(e, skip_start + 512 * 1024).size();
+      const std::string skip = encode_skip_list(e, skip_start + est);
+      if (skip.size() > est) throw std::runtime_error("skip list estimate too small");
+      head += skip;
+      head.append(est - skip.size(), '\0');
+    }
     vac_.write(head.data(), head.size());
     vac_.write(e.doc.bytes.data(), e.doc.bytes.size());
     vac_.write(e.tf.bytes.data(), e.tf.bytes.size());
+    for (auto& b : blm) vac_.write(b.data(), b.size());
     vac_.write(e.pos.bytes.data(), e.pos.bytes.size());
     vac_.write(e.off.bytes.data(), e.off.bytes.size());
-    const uint64_t tf_end = skip_start + est + e.doc.bytes.size() + e.tf.bytes.size();
-    off_ = skip_start + est + e.doc.bytes.size() + e.tf.bytes.size() + e.pos.bytes.size() +
-           e.off.bytes.size();
+    const uint64_t tf_end = start + head.size() + e.doc.bytes.size() + e.tf.bytes.size();
+    off_ = tf_end + blm[0].size() + blm[1].size() + e.pos.bytes.size() + e.off.bytes.size();
     const uint32_t pages = static_cast<uint32_t>((tf_end - start) / 4096);
     const int64_t v = encode_tip_value(pages, start);
     const uint32_t len = static_cast<uint32_t>(term.size());
@@ -195,6 +275,7 @@ class VacuumFileWriter {
 
  private:
   std::string dir_;
+  bool bloom_ = false;
   std::ofstream vac_, tip_;
   uint64_t off_ = 0;
   int64_t n_terms_ = 0;
@@ -285,8 +366,34 @@ void add_bag_delta(std::vector<uint32_t>* vals, std::vector<uint32_t>* sizes,
 
 }  // namespace
 
+namespace {
+// "begin" / "end" neighbour lists of every token of a doc from its positions
+// (the fixture columns bloom_before / bloom: '!'-terminated groups of the
+// terms before / after each occurrence, testdata/iter_test_3_docs_tf_bi-bloom)
+void add_doc_blooms(const std::vector<std::string>& toks,
+                    const std::vector<std::vector<uint32_t>>& pos, const BloomShape& shape,
+                    std::map<std::string, TermPostings>* index) {
+  std::map<uint32_t, const std::string*> at;
+  for (size_t t = 0; t < toks.size(); ++t)
+    for (uint32_t p : pos[t]) at[p] = &toks[t];
+  for (size_t t = 0; t < toks.size(); ++t) {
+    std::vector<std::string> before, after;
+    for (uint32_t p : pos[t]) {
+      if (p > 0) { auto it = at.find(p - 1); if (it != at.end()) before.push_back(*it->second); }
+      auto it = at.find(p + 1);
+      if (it != at.end()) after.push_back(*it->second);
+    }
+    TermPostings& tp = (*index)[toks[t]];
+    tp.blm_begin.push_back(make_bloom(shape, before));
+    tp.blm_end.push_back(make_bloom(shape, after));
+  }
+}
+}  // namespace
+
 BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
-                              const std::string& format, const std::string& out_dir) {
+                              const std::string& format, const std::string& out_dir,
+                              const BloomSpec& bloom) {
+  const BloomShape shape(bloom.entries, bloom.ratio);
   const bool token_only = format == "TOKEN_ONLY";
   if (!token_only && format != "WITH_POSITIONS")
     throw std::runtime_error("unsupported linedoc format " + format);
@@ -319,13 +426,17 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
         offs[t].push_back(static_cast<uint32_t>(j - 1));
         i = j;
       }
+      std::vector<std::string> dtoks;
+      std::vector<std::vector<uint32_t>> dpos;
       for (auto& kv : occ) {
         TermPostings& tp = index[kv.first];
         tp.docs.push_back(doc);
         tp.tfs.push_back(static_cast<uint32_t>(kv.second.size()));
         add_bag_delta(&tp.pos_vals, &tp.pos_sizes, kv.second);
         add_bag_delta(&tp.off_vals, &tp.off_sizes, offs[kv.first]);
+        if (bloom.on) { dtoks.push_back(kv.first); dpos.push_back(kv.second); }
       }
+      if (bloom.on) add_doc_blooms(dtoks, dpos, shape, &index);
       lens.add(ordinal);
     } else {
       std::vector<std::string> toks = explode(items[2], ' ');
@@ -335,6 +446,7 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
         throw std::runtime_error("linedoc row " + std::to_string(doc) +
                                  ": token/offset/position column mismatch");
       std::unordered_set<std::string> seen;
+      std::vector<std::vector<uint32_t>> dpos;
       for (size_t t = 0; t < toks.size(); ++t) {
         if (!seen.insert(toks[t]).second)
           throw std::runtime_error("duplicate token '" + toks[t] + "' in row " + std::to_string(doc));
@@ -347,12 +459,14 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
         tp.tfs.push_back(static_cast<uint32_t>(offsets[t].size()));
         add_bag_delta(&tp.pos_vals, &tp.pos_sizes, pos);
         add_bag_delta(&tp.off_vals, &tp.off_sizes, flat);
+        if (bloom.on) dpos.push_back(pos);
       }
+      if (bloom.on) add_doc_blooms(toks, dpos, shape, &index);
       lens.add(static_cast<uint32_t>(explode(items[1], ' ').size()));
     }
     ++doc;
   }
-  VacuumFileWriter w(out_dir);
+  VacuumFileWriter w(out_dir, bloom);
   BuildStats st;
   for (auto& kv : index) {
     EncodedList e;

@@ -22,6 +22,14 @@ struct SyntheticSpec {
   int threads = 0;             // 0 = hardware concurrency
 };
 
+// Two-way phrase bloom filters (bloom.h): off by default; the reference's
+// BloomDumper defaults are ratio 0.0009, 5 expected entries (bloom_filter.h:650-655).
+struct BloomSpec {
+  bool on = false;
+  float ratio = 0.0009f;
+  int entries = 5;
+};
+
 struct BuildStats {
   int64_t n_docs = 0;
   int64_t n_terms = 0;
@@ -34,8 +42,11 @@ struct BuildStats {
 
 // format: "TOKEN_ONLY" or "WITH_POSITIONS" (engine_loader.h:53-96).
 // Throws std::runtime_error on malformed input.
+// bloom.on: every posting also gets its "begin" / "end" bloom filter over the
+// terms before / after each occurrence of the term in the doc (from positions).
 BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
-                              const std::string& format, const std::string& out_dir);
+                              const std::string& format, const std::string& out_dir,
+                              const BloomSpec& bloom = BloomSpec());
 
 BuildStats build_synthetic(const SyntheticSpec& spec, const std::string& out_dir);
 

@@ -239,10 +239,17 @@ def sync(engine: VacuumEngine) -> None:
 
 # ---- index building (host only) -------------------------------------------
 def build_from_linedoc(linedoc: str, out_dir: str, fmt: str = "WITH_POSITIONS",
-                       n_rows: int = -1) -> _capi.BuildStats:
+                       n_rows: int = -1, bloom: Optional[Sequence] = None) -> _capi.BuildStats:
+    """bloom = (ratio, expected_entries), e.g. (0.0009, 5): also write the
+    two-way phrase bloom filters (flash_engine_dumper.h:412-525)."""
     st = _capi.BuildStats()
-    check(lib.wsr_build_from_linedoc(linedoc.encode(), n_rows, fmt.encode(), out_dir.encode(),
-                                     C.byref(st)))
+    if bloom:
+        check(lib.wsr_build_from_linedoc_bloom(linedoc.encode(), n_rows, fmt.encode(),
+                                               out_dir.encode(), float(bloom[0]), int(bloom[1]),
+                                               C.byref(st)))
+    else:
+        check(lib.wsr_build_from_linedoc(linedoc.encode(), n_rows, fmt.encode(), out_dir.encode(),
+                                         C.byref(st)))
     return st
 
 
