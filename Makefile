@@ -7,7 +7,7 @@ JOBS    ?= 8
 LIB     := wiser_amd/_lib/libwiser_hip.so
 ORACLE  := oracle/_build/liboracle.so
 SRCS    := wiser_amd/csrc/writer.cc wiser_amd/csrc/index.cc wiser_amd/csrc/engine.cc \
-           wiser_amd/csrc/kernels.hip
+           wiser_amd/csrc/server.cc wiser_amd/csrc/kernels.hip
 HDRS    := $(wildcard wiser_amd/csrc/*.h) include/wiser_hip.h
 OBJDIR  := wiser_amd/_lib/obj
 OBJS    := $(patsubst wiser_amd/csrc/%,$(OBJDIR)/%.o,$(SRCS))

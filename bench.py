@@ -229,7 +229,33 @@ def extra_legs(a, idx, local, threads):
     legs["c5_phrase"]["workload"] = ("10000 two-term phrase queries drawn from the corpus's "
                                      "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
     eng.close()
+    legs["serving"] = serving_leg(a, idx, local, threads)
     return legs
+
+
+def serving_leg(a, idx, local, threads):
+    """Single-query serving through the micro-batcher (wsr_server_*): 16 client
+    threads keep 256 queries each in flight (the reference client's threads,
+    grpc_client_impl.h:557-620) over the C2 log; latency = submit -> result."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+    eng.Load()
+    lines = [l.split() for l in open(os.path.join(idx, f"two_term_{a.queries}.log")).read().splitlines()]
+    arr = (_capi.Query * len(lines))()
+    for i, t in enumerate(lines):
+        arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
+    out = {}
+    for clients, depth, window in ((16, 256, 200), (16, 16, 50)):
+        srv = w.Server(eng, max_batch=a.batch, window_us=window)
+        st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
+        srv.close()
+        out[f"in_flight_{clients * depth}"] = {
+            "value": round(st.qps, 1), "unit": "queries/s", "p50_ms": round(st.p50_ms, 3),
+            "p99_ms": round(st.p99_ms, 3), "mean_batch": round(st.mean_batch, 1),
+            "window_us": window, "clients": clients, "depth": depth}
+    eng.close()
+    return out
 
 
 def kernel_accounting(eng, batches):

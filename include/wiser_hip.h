@@ -129,6 +129,30 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
 /* device pointers of the batch's results (for collectives on the caller's side) */
 int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits);
 
+/* ---- serving: micro-batcher over one handle --------------------------
+ * The reference serves single queries from N gRPC worker threads sharing one
+ * engine (grpc_server_impl.h:260-263,382-389).  wsr_server_search() may be
+ * called from any number of threads; a dispatcher thread coalesces the calls
+ * that arrive within window_us (or until max_batch are queued) into one GPU
+ * batch, two batches alternating.  Each call blocks until its own result. */
+typedef struct wsr_server wsr_server;
+typedef struct wsr_serve_stats {
+  uint64_t queries;      /* completed in the run */
+  double seconds, qps;
+  double p50_ms, p99_ms; /* per-query latency, submit -> result on the caller's thread */
+  uint64_t batches;      /* GPU batches the dispatcher ran */
+  double mean_batch;     /* queries per batch */
+} wsr_serve_stats;
+int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_server** out);
+void wsr_server_close(wsr_server* s);
+/* one query (k <= WSR_MAX_K): hits receives n_hits <= k entries */
+int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t* n_hits);
+/* closed-loop load (the reference client's threads, grpc_client_impl.h:557-620):
+ * n_clients threads keep `depth` queries each in flight, drawn round-robin from
+ * q[0..nq), for `seconds`; throughput and latency percentiles in *st */
+int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_clients,
+                     int32_t depth, double seconds, wsr_serve_stats* st);
+
 /* ---- doc-range shards (multi-GPU) ------------------------------------
  * A shard engine (wsr_open_opts.doc_lo/doc_hi) runs every query of a batch over
  * its doc range.  Queries are owned by contiguous slices of q_per_owner queries

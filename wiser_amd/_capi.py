@@ -49,6 +49,12 @@ class BatchStats(C.Structure):
                 ("lean_ms", C.c_double)]
 
 
+class ServeStats(C.Structure):
+    _fields_ = [("queries", C.c_uint64), ("seconds", C.c_double), ("qps", C.c_double),
+                ("p50_ms", C.c_double), ("p99_ms", C.c_double), ("batches", C.c_uint64),
+                ("mean_batch", C.c_double)]
+
+
 class BuildStats(C.Structure):
     _fields_ = [("n_docs", C.c_int64), ("n_terms", C.c_int64), ("n_postings", C.c_int64),
                 ("vacuum_bytes", C.c_int64), ("docs_char4_ge_0x80", C.c_int64),
@@ -110,6 +116,11 @@ _sigs = {
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
+    "wsr_server_open": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    "wsr_server_close": (None, [_P]),
+    "wsr_server_search": (C.c_int, [_P, C.POINTER(Query), C.POINTER(Hit), C.POINTER(C.c_int32)]),
+    "wsr_server_bench": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_double, C.POINTER(ServeStats)]),
     "wsr_gen_mixed_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                     C.POINTER(C.c_int64)]),
     "wsr_gen_phrase_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,

@@ -1,0 +1,276 @@
+// Serving front end over one engine handle: a micro-batcher that coalesces
+// concurrent single-query Search() calls into GPU batches, plus a closed-loop
+// load generator that measures QPS and latency percentiles through it.
+//
+// Reference: the gRPC server shares one read-only engine between N worker
+// threads, each calling engine->Search() for one request at a time
+// (grpc_server_impl.h:104-107,260-263,382-389); the benchmark client keeps
+// several requests in flight per thread (grpc_client_impl.h:448-459,557-620).
+// On the GPU one query is far too little work, so the dispatcher thread here
+// collects requests for a short window (or until a batch is full), runs them
+// as one resident batch (wsr_batch_*), and hands each caller its own entries.
+// Two batches alternate, so the next batch is collected and uploaded while the
+// previous one runs.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/wiser_hip.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Req {
+  wsr_query q;
+  wsr_hit* out = nullptr;
+  int32_t* n_out = nullptr;
+  int rc = WSR_OK;
+  bool done = false;
+};
+
+struct Slot {
+  wsr_batch* b = nullptr;
+  std::vector<Req*> reqs;
+  bool busy = false;
+};
+
+}  // namespace
+
+struct wsr_server {
+  wsr_handle* h = nullptr;
+  int max_batch = 4096;
+  std::chrono::microseconds window{200};
+  std::mutex mu;
+  std::condition_variable cv_work;   // dispatcher: requests arrived / stop
+  std::condition_variable cv_done;   // callers: some request completed
+  std::deque<Req*> queue;
+  bool stop = false;
+  std::thread worker;
+  Slot slots[2];
+  int next = 0;
+  std::vector<wsr_hit> hits;         // fetch buffer of one batch
+  std::vector<int32_t> nh;
+  std::vector<wsr_query> qbuf;
+  std::atomic<uint64_t> batches{0}, queries{0};
+
+  void complete(Slot& s) {
+    int rc = wsr_batch_fetch(h, s.b, hits.data(), nh.data());
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (size_t i = 0; i < s.reqs.size(); ++i) {
+        Req* r = s.reqs[i];
+        r->rc = rc;
+        if (rc == WSR_OK) {
+          const int32_t n = nh[i];
+          std::memcpy(r->out, &hits[i * WSR_MAX_K], sizeof(wsr_hit) * static_cast<size_t>(n));
+          *r->n_out = n;
+        }
+        r->done = true;
+      }
+    }
+    cv_done.notify_all();
+    s.reqs.clear();
+    s.busy = false;
+  }
+
+  void fail_all(std::vector<Req*>& rs, int rc) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (Req* r : rs) { r->rc = rc; r->done = true; }
+    }
+    cv_done.notify_all();
+    rs.clear();
+  }
+
+  void run() {
+    for (;;) {
+      std::vector<Req*> take;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        // nothing waiting: finish what is on the GPU before sleeping
+        while (queue.empty() && !stop) {
+          Slot* oldest = nullptr;
+          for (auto& s : slots)
+            if (s.busy) oldest = &s;   // (at most one is busy here; see below)
+          if (!oldest) { cv_work.wait(lk); continue; }
+          lk.unlock();
+          complete(*oldest);
+          lk.lock();
+        }
+        if (stop && queue.empty()) break;
+        // the batch window starts with its first request
+        const auto deadline = Clock::now() + window;
+        while (static_cast<int>(queue.size()) < max_batch && !stop &&
+               cv_work.wait_until(lk, deadline) != std::cv_status::timeout) {}
+        const size_t n = std::min<size_t>(queue.size(), static_cast<size_t>(max_batch));
+        take.assign(queue.begin(), queue.begin() + static_cast<long>(n));
+        queue.erase(queue.begin(), queue.begin() + static_cast<long>(n));
+      }
+      Slot& s = slots[next];
+      next ^= 1;
+      if (s.busy) complete(s);
+      qbuf.resize(take.size());
+      for (size_t i = 0; i < take.size(); ++i) qbuf[i] = take[i]->q;
+      int rc = wsr_batch_upload(h, s.b, qbuf.data(), static_cast<int32_t>(qbuf.size()));
+      if (rc == WSR_OK) rc = wsr_batch_run(h, s.b);
+      if (rc != WSR_OK) { fail_all(take, rc); continue; }
+      s.reqs = std::move(take);
+      s.busy = true;
+      ++batches;
+      queries += s.reqs.size();
+      // keep at most one batch in flight while the next one is collected:
+      // the other slot, if still busy, completes now
+      Slot& o = slots[next];
+      if (o.busy) complete(o);
+    }
+    for (auto& s : slots)
+      if (s.busy) complete(s);
+  }
+
+  int submit(Req* r) {
+    const wsr_query& q = r->q;
+    if (q.n_terms > WSR_MAX_TERMS || q.k > WSR_MAX_K) return WSR_E_LIMIT;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (stop) return WSR_E_INVALID;
+      queue.push_back(r);
+    }
+    cv_work.notify_one();
+    return WSR_OK;
+  }
+
+  int wait(Req* r) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return r->done; });
+    return r->rc;
+  }
+};
+
+extern "C" {
+
+int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_server** out) {
+  if (!h || !out || max_batch < 1 || window_us < 0) return WSR_E_INVALID;
+  std::unique_ptr<wsr_server> s(new wsr_server());
+  s->h = h;
+  s->max_batch = max_batch;
+  s->window = std::chrono::microseconds(window_us);
+  for (auto& sl : s->slots) {
+    int rc = wsr_batch_create(h, max_batch, WSR_MAX_K, &sl.b);
+    if (rc != WSR_OK) {
+      for (auto& x : s->slots)
+        if (x.b) wsr_batch_destroy(h, x.b);
+      return rc;
+    }
+  }
+  s->hits.resize(static_cast<size_t>(max_batch) * WSR_MAX_K);
+  s->nh.resize(static_cast<size_t>(max_batch));
+  s->worker = std::thread([p = s.get()] { p->run(); });
+  *out = s.release();
+  return WSR_OK;
+}
+
+void wsr_server_close(wsr_server* s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->stop = true;
+  }
+  s->cv_work.notify_all();
+  if (s->worker.joinable()) s->worker.join();
+  for (auto& sl : s->slots)
+    if (sl.b) wsr_batch_destroy(s->h, sl.b);
+  delete s;
+}
+
+int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t* n_hits) {
+  if (!s || !q || !hits || !n_hits) return WSR_E_INVALID;
+  Req r;
+  r.q = *q;
+  r.out = hits;
+  r.n_out = n_hits;
+  int rc = s->submit(&r);
+  if (rc != WSR_OK) return rc;
+  return s->wait(&r);
+}
+
+int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_clients,
+                     int32_t depth, double seconds, wsr_serve_stats* st) {
+  if (!s || !q || nq < 1 || n_clients < 1 || depth < 1 || !st) return WSR_E_INVALID;
+  std::atomic<int> first_rc{WSR_OK};
+  std::vector<std::vector<float>> lat(static_cast<size_t>(n_clients));
+  std::atomic<uint64_t> done{0};
+  const uint64_t b0 = s->batches.load(), q0 = s->queries.load();
+  const auto t_start = Clock::now();
+  const auto t_end = t_start + std::chrono::duration_cast<Clock::duration>(
+                                   std::chrono::duration<double>(seconds));
+  auto client = [&](int c) {
+    std::vector<Req> rq(static_cast<size_t>(depth));
+    std::vector<std::vector<wsr_hit>> out(static_cast<size_t>(depth), std::vector<wsr_hit>(WSR_MAX_K));
+    std::vector<int32_t> nout(static_cast<size_t>(depth));
+    std::vector<Clock::time_point> t0(static_cast<size_t>(depth));
+    uint64_t next_q = static_cast<uint64_t>(c) * 7919u;
+    auto issue = [&](int i) {
+      Req& r = rq[static_cast<size_t>(i)];
+      r = Req();
+      r.q = q[next_q++ % static_cast<uint64_t>(nq)];
+      r.out = out[static_cast<size_t>(i)].data();
+      r.n_out = &nout[static_cast<size_t>(i)];
+      t0[static_cast<size_t>(i)] = Clock::now();
+      const int rc = s->submit(&r);
+      if (rc != WSR_OK) { r.rc = rc; r.done = true; }
+    };
+    for (int i = 0; i < depth; ++i) issue(i);
+    for (uint64_t it = 0;; ++it) {
+      const int i = static_cast<int>(it % static_cast<uint64_t>(depth));
+      const int rc = s->wait(&rq[static_cast<size_t>(i)]);
+      const auto now = Clock::now();
+      if (rc != WSR_OK) { int z = WSR_OK; first_rc.compare_exchange_strong(z, rc); }
+      lat[static_cast<size_t>(c)].push_back(
+          std::chrono::duration<float, std::milli>(now - t0[static_cast<size_t>(i)]).count());
+      ++done;
+      if (now < t_end) issue(i);
+      else {   // drain the rest of this client's window
+        for (int j = 1; j < depth; ++j) {
+          const int k = static_cast<int>((it + static_cast<uint64_t>(j)) % static_cast<uint64_t>(depth));
+          s->wait(&rq[static_cast<size_t>(k)]);
+          lat[static_cast<size_t>(c)].push_back(std::chrono::duration<float, std::milli>(
+              Clock::now() - t0[static_cast<size_t>(k)]).count());
+          ++done;
+        }
+        break;
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int c = 0; c < n_clients; ++c) ts.emplace_back(client, c);
+  for (auto& t : ts) t.join();
+  const double el = std::chrono::duration<double>(Clock::now() - t_start).count();
+  std::vector<float> all;
+  for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double p) {
+    if (all.empty()) return 0.0;
+    size_t i = static_cast<size_t>(p * static_cast<double>(all.size() - 1) + 0.5);
+    return static_cast<double>(all[std::min(i, all.size() - 1)]);
+  };
+  st->queries = done.load();
+  st->seconds = el;
+  st->qps = static_cast<double>(done.load()) / el;
+  st->p50_ms = pct(0.50);
+  st->p99_ms = pct(0.99);
+  st->batches = s->batches.load() - b0;
+  st->mean_batch = st->batches ? static_cast<double>(s->queries.load() - q0) / st->batches : 0.0;
+  return first_rc.load();
+}
+
+}  // extern "C"

@@ -233,6 +233,49 @@ class ResidentBatch:
             self._b = None
 
 
+class Server:
+    """Micro-batching front end (wsr_server_*): Search() may be called from many
+    threads at once; concurrent calls are coalesced into GPU batches.  The
+    analogue of the reference's gRPC workers sharing one engine
+    (grpc_server_impl.h:260-263,382-389)."""
+
+    def __init__(self, engine: VacuumEngine, max_batch: int = 4096, window_us: int = 200):
+        self.engine = engine
+        s = C.c_void_p()
+        check(lib.wsr_server_open(engine._h, max_batch, window_us, C.byref(s)))
+        self._s = s
+
+    def Search(self, query: SearchQuery) -> SearchResult:
+        q, freqs = self.engine.resolve(query)
+        hits = (_capi.Hit * _capi.MAX_K)()
+        n = C.c_int32()
+        check(lib.wsr_server_search(self._s, C.byref(q), hits, C.byref(n)))
+        r = SearchResult()
+        if freqs is not None:
+            r.doc_freqs = list(freqs)
+            r.entries = [SearchResultEntry(hits[j].doc_id, hits[j].score) for j in range(n.value)]
+        return r
+
+    def bench(self, queries, n_clients: int = 16, depth: int = 256,
+              seconds: float = 3.0) -> _capi.ServeStats:
+        """closed-loop load: queries = ctypes array of _capi.Query"""
+        st = _capi.ServeStats()
+        check(lib.wsr_server_bench(self._s, queries, len(queries), n_clients, depth, seconds,
+                                   C.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if self._s is not None:
+            lib.wsr_server_close(self._s)
+            self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def sync(engine: VacuumEngine) -> None:
     check(lib.wsr_sync(engine._h))
 
