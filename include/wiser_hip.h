@@ -126,6 +126,8 @@ int wsr_sync(wsr_handle* h);
 /* copy results to the host (waits for the stream) */
 int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits);
 int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
+/* 1 when the batch's last run has finished on the device, 0 while it runs */
+int wsr_batch_ready(wsr_handle* h, wsr_batch* b);
 /* device pointers of the batch's results (for collectives on the caller's side) */
 int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits);
 

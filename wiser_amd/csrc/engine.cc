@@ -494,6 +494,15 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
   return WSR_OK;
 }
 
+int wsr_batch_ready(wsr_handle* h, wsr_batch* b) {
+  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  if (!b->ran) return 0;
+  const hipError_t e = hipEventQuery(b->ev[3]);   // recorded after the batch's last kernel
+  if (e == hipSuccess) return 1;
+  if (e == hipErrorNotReady) return 0;
+  return fail(WSR_E_HIP, hipGetErrorString(e));
+}
+
 int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
   if (!h || !b || !out || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
   std::lock_guard<std::mutex> g(h->mu);

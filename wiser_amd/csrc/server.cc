@@ -24,6 +24,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/wiser_hip.h"
 
 namespace {
@@ -32,16 +34,19 @@ using Clock = std::chrono::steady_clock;
 
 struct Req {
   wsr_query q;
+  Clock::time_point t_enq;
   wsr_hit* out = nullptr;
   int32_t* n_out = nullptr;
   int rc = WSR_OK;
-  bool done = false;
+  std::atomic<bool> done{false};
+  void reset() { out = nullptr; n_out = nullptr; rc = WSR_OK; done.store(false, std::memory_order_relaxed); }
 };
 
 struct Slot {
   wsr_batch* b = nullptr;
   std::vector<Req*> reqs;
   bool busy = false;
+  uint64_t seq = 0;   // launch order
 };
 
 }  // namespace
@@ -57,68 +62,89 @@ struct wsr_server {
   bool stop = false;
   std::thread worker;
   Slot slots[2];
-  int next = 0;
-  std::vector<wsr_hit> hits;         // fetch buffer of one batch
-  std::vector<int32_t> nh;
+  // fetch buffers of one batch, page-locked so the result copies are DMA'd
+  wsr_hit* hits = nullptr;
+  int32_t* nh = nullptr;
   std::vector<wsr_query> qbuf;
   std::atomic<uint64_t> batches{0}, queries{0};
 
-  void complete(Slot& s) {
-    int rc = wsr_batch_fetch(h, s.b, hits.data(), nh.data());
-    {
-      std::lock_guard<std::mutex> g(mu);
-      for (size_t i = 0; i < s.reqs.size(); ++i) {
-        Req* r = s.reqs[i];
-        r->rc = rc;
-        if (rc == WSR_OK) {
-          const int32_t n = nh[i];
-          std::memcpy(r->out, &hits[i * WSR_MAX_K], sizeof(wsr_hit) * static_cast<size_t>(n));
-          *r->n_out = n;
-        }
-        r->done = true;
-      }
+  // Results are written, then each request's flag is released; callers spin
+  // briefly on their flag and sleep on cv_done only after that, so the
+  // dispatcher takes the lock (to wake sleepers) only when someone sleeps.
+  std::atomic<int> sleepers{0};
+
+  // (done flags are stored seq_cst before `sleepers` is read; a caller bumps
+  // `sleepers` before its last look at its flag, so one of the two sees the other)
+  void finish() {
+    if (sleepers.load(std::memory_order_seq_cst) > 0) {
+      std::lock_guard<std::mutex> g(mu);   // pairs with the sleeper's check under mu
     }
     cv_done.notify_all();
+  }
+
+  void complete(Slot& s) {
+    int rc = wsr_batch_fetch(h, s.b, hits, nh);
+    for (size_t i = 0; i < s.reqs.size(); ++i) {
+      Req* r = s.reqs[i];
+      r->rc = rc;
+      if (rc == WSR_OK) {
+        const int32_t n = nh[i];
+        std::memcpy(r->out, &hits[i * WSR_MAX_K], sizeof(wsr_hit) * static_cast<size_t>(n));
+        *r->n_out = n;
+      }
+      r->done.store(true, std::memory_order_seq_cst);
+    }
+    finish();
     s.reqs.clear();
     s.busy = false;
   }
 
   void fail_all(std::vector<Req*>& rs, int rc) {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      for (Req* r : rs) { r->rc = rc; r->done = true; }
-    }
-    cv_done.notify_all();
+    for (Req* r : rs) { r->rc = rc; r->done.store(true, std::memory_order_seq_cst); }
+    finish();
     rs.clear();
   }
 
+  // Dispatch policy: with the GPU idle, whatever is queued runs at once (the
+  // latency of a lone query is one batch); with one batch running, the next
+  // fills until max_batch or until its oldest request has waited `window`,
+  // then runs beside it; with two running, the older one is completed first.
   void run() {
+    uint64_t seq = 0;
     for (;;) {
+      for (auto& s : slots)   // retire finished batches, oldest first
+        if (s.busy && wsr_batch_ready(h, s.b) == 1) complete(s);
+      Slot* oldest = nullptr;
+      int n_busy = 0;
+      for (auto& s : slots)
+        if (s.busy) { ++n_busy; if (!oldest || s.seq < oldest->seq) oldest = &s; }
       std::vector<Req*> take;
       {
         std::unique_lock<std::mutex> lk(mu);
-        // nothing waiting: finish what is on the GPU before sleeping
-        while (queue.empty() && !stop) {
-          Slot* oldest = nullptr;
-          for (auto& s : slots)
-            if (s.busy) oldest = &s;   // (at most one is busy here; see below)
-          if (!oldest) { cv_work.wait(lk); continue; }
+        if (queue.empty()) {
+          if (stop && !n_busy) break;
+          if (n_busy) cv_work.wait_for(lk, std::chrono::microseconds(20));
+          else if (!stop) cv_work.wait(lk);
+          continue;
+        }
+        if (n_busy == 2) {
           lk.unlock();
           complete(*oldest);
-          lk.lock();
+          continue;
         }
-        if (stop && queue.empty()) break;
-        // the batch window starts with its first request
-        const auto deadline = Clock::now() + window;
-        while (static_cast<int>(queue.size()) < max_batch && !stop &&
-               cv_work.wait_until(lk, deadline) != std::cv_status::timeout) {}
+        if (n_busy == 1 && !stop && static_cast<int>(queue.size()) < max_batch) {
+          const auto due = queue.front()->t_enq + window;
+          const auto now = Clock::now();
+          if (now < due) {
+            cv_work.wait_for(lk, std::min<Clock::duration>(due - now, std::chrono::microseconds(20)));
+            continue;
+          }
+        }
         const size_t n = std::min<size_t>(queue.size(), static_cast<size_t>(max_batch));
         take.assign(queue.begin(), queue.begin() + static_cast<long>(n));
         queue.erase(queue.begin(), queue.begin() + static_cast<long>(n));
       }
-      Slot& s = slots[next];
-      next ^= 1;
-      if (s.busy) complete(s);
+      Slot& s = slots[0].busy ? slots[1] : slots[0];
       qbuf.resize(take.size());
       for (size_t i = 0; i < take.size(); ++i) qbuf[i] = take[i]->q;
       int rc = wsr_batch_upload(h, s.b, qbuf.data(), static_cast<int32_t>(qbuf.size()));
@@ -126,12 +152,9 @@ struct wsr_server {
       if (rc != WSR_OK) { fail_all(take, rc); continue; }
       s.reqs = std::move(take);
       s.busy = true;
+      s.seq = ++seq;
       ++batches;
       queries += s.reqs.size();
-      // keep at most one batch in flight while the next one is collected:
-      // the other slot, if still busy, completes now
-      Slot& o = slots[next];
-      if (o.busy) complete(o);
     }
     for (auto& s : slots)
       if (s.busy) complete(s);
@@ -140,6 +163,7 @@ struct wsr_server {
   int submit(Req* r) {
     const wsr_query& q = r->q;
     if (q.n_terms > WSR_MAX_TERMS || q.k > WSR_MAX_K) return WSR_E_LIMIT;
+    r->t_enq = Clock::now();
     {
       std::lock_guard<std::mutex> g(mu);
       if (stop) return WSR_E_INVALID;
@@ -150,8 +174,15 @@ struct wsr_server {
   }
 
   int wait(Req* r) {
-    std::unique_lock<std::mutex> lk(mu);
-    cv_done.wait(lk, [&] { return r->done; });
+    const auto spin_until = Clock::now() + std::chrono::microseconds(200);
+    while (!r->done.load(std::memory_order_acquire)) {
+      if (Clock::now() < spin_until) { std::this_thread::yield(); continue; }
+      std::unique_lock<std::mutex> lk(mu);
+      ++sleepers;
+      cv_done.wait(lk, [&] { return r->done.load(std::memory_order_seq_cst); });
+      --sleepers;
+      break;
+    }
     return r->rc;
   }
 };
@@ -172,8 +203,14 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
       return rc;
     }
   }
-  s->hits.resize(static_cast<size_t>(max_batch) * WSR_MAX_K);
-  s->nh.resize(static_cast<size_t>(max_batch));
+  if (hipHostMalloc(reinterpret_cast<void**>(&s->hits),
+                    sizeof(wsr_hit) * static_cast<size_t>(max_batch) * WSR_MAX_K) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&s->nh), sizeof(int32_t) * static_cast<size_t>(max_batch)) !=
+          hipSuccess) {
+    for (auto& x : s->slots) wsr_batch_destroy(h, x.b);
+    if (s->hits) (void)hipHostFree(s->hits);
+    return WSR_E_HIP;
+  }
   s->worker = std::thread([p = s.get()] { p->run(); });
   *out = s.release();
   return WSR_OK;
@@ -189,6 +226,8 @@ void wsr_server_close(wsr_server* s) {
   if (s->worker.joinable()) s->worker.join();
   for (auto& sl : s->slots)
     if (sl.b) wsr_batch_destroy(s->h, sl.b);
+  if (s->hits) (void)hipHostFree(s->hits);
+  if (s->nh) (void)hipHostFree(s->nh);
   delete s;
 }
 
@@ -221,13 +260,13 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
     uint64_t next_q = static_cast<uint64_t>(c) * 7919u;
     auto issue = [&](int i) {
       Req& r = rq[static_cast<size_t>(i)];
-      r = Req();
+      r.reset();
       r.q = q[next_q++ % static_cast<uint64_t>(nq)];
       r.out = out[static_cast<size_t>(i)].data();
       r.n_out = &nout[static_cast<size_t>(i)];
       t0[static_cast<size_t>(i)] = Clock::now();
       const int rc = s->submit(&r);
-      if (rc != WSR_OK) { r.rc = rc; r.done = true; }
+      if (rc != WSR_OK) { r.rc = rc; r.done.store(true); }
     };
     for (int i = 0; i < depth; ++i) issue(i);
     for (uint64_t it = 0;; ++it) {
