@@ -372,7 +372,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       int drv = 0;
       for (int t = 1; t < d.n_terms; ++t)
         if (h->lists[d.list[t]].nblk < h->lists[d.list[drv]].nblk) drv = t;
-      bool lean = !phrase;
+      bool lean = true;
       for (int t = 0; t < d.n_terms; ++t) {
         const ListDev& L = h->lists[d.list[t]];
         if (t != drv && !(L.bm != kNoDense &&
@@ -403,8 +403,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       HIP_OK(hipMalloc(&b->d_itemq, sizeof(uint32_t) * b->item_cap));
       HIP_OK(hipMalloc(&b->d_pub, sizeof(uint64_t) * b->item_cap));
     }
-    if (has_phrase && !b->d_ph)
-      HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch * std::max(h->gen_cap, 1)));
+    if (has_phrase && !b->d_ph)   // general workgroups, then lean waves
+      HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch *
+                                     (static_cast<size_t>(std::max(h->gen_cap, 1)) +
+                                      static_cast<size_t>(std::max(h->lean_wgs, 1)) * kLeanWaves)));
     if (nq) HIP_OK(hipMemcpy(b->d_q, in.data(), sizeof(QueryIn) * nq, hipMemcpyHostToDevice));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
@@ -452,7 +454,9 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(hipEventRecord(b->join, b->st2));
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
-                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc, st));
+                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc,
+                       b->has_phrase ? b->d_ph + static_cast<size_t>(kPhraseScratch) * std::max(h->gen_cap, 1)
+                                     : nullptr, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));

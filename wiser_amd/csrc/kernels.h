@@ -77,6 +77,10 @@ struct FusedReplay {
   int32_t* n_hits;
 };
 
+// phrase scratch words per general workgroup / lean wave (null when the batch
+// has no phrase query)
+constexpr int kPhraseScratch = kMaxTerms * 256;
+
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
@@ -85,14 +89,13 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,
                            uint64_t* pub, uint32_t* ph, hipStream_t st);
-// phrase scratch words per general workgroup (ph: grid * kPhraseScratch u32;
-// null when the batch has no phrase query)
-constexpr int kPhraseScratch = kMaxTerms * 256;
-// lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride]
+
+// lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride];
+// ph: phrase scratch (lean_wgs * kLeanWaves * kPhraseScratch u32), null without phrase queries
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, hipStream_t st);
+                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st);
 int lean_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,

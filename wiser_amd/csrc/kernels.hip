@@ -373,9 +373,7 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
     const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
     // lean class: every other list is probed through its bitmap (or none)
-    // (a phrase query of 2+ terms needs every term's posting index for its
-    // position check: general class)
-    bool lean = !((q.flags & kQueryPhrase) && q.n_terms > 1);
+    bool lean = true;
 #pragma unroll
     for (int s = 0; s < kMaxTerms; ++s)
       if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
@@ -1007,6 +1005,108 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
 #define WSR_T(i)
 #endif
 
+// ---------------------------------------------------------- phrase check --
+// Per general workgroup (kPhraseScratch words), per query term s: the image
+// posting slot of value v (= 2l or 2l+1 of the driver block) at [s*256 + v],
+// its tf at [s*256 + 128 + v] (phrase queries only).
+
+// Does the doc hold the query's terms at consecutive positions?  Term i's bag
+// (query order) = tf_i positions delta coded from 0 starting at entry
+// pos_start[slot_i] of its box.  True iff some a has a + i in bag i for every
+// i, which is PhraseQueryProcessor2::NumOfMatches() > 0 (query_processing.h:
+// 264-336: the 2-term merge and the general max-adjusted walk both find every
+// such a).  One lane per survivor; term state stays in registers (the term
+// loop is unrolled, so every index is static).
+// One position bag read as a stream: entry e of the box sits in pack e / 128
+// (offset and width from the pack directory, reloaded only when the pack
+// changes) or in the decoded VInts remainder; positions are prefix sums of
+// the bag's deltas.
+struct PosStream {
+  const uint8_t* data;   // current pack's values
+  uint32_t bits, pk;     // its width and index (pk = ~0: none yet)
+  uint32_t e, end;       // next entry, one past the bag
+  int32_t cur;           // last position popped
+  __device__ __forceinline__ void init(const IndexArgs& ix, uint32_t slot, uint32_t tf) {
+    e = ix.pos_start[slot];
+    end = e + tf;
+    cur = 0;
+    pk = 0xFFFFFFFFu;
+    data = ix.pos_blob;
+    bits = 1;
+  }
+  // pop the next position (false past the bag's end)
+  __device__ __forceinline__ bool next(const IndexArgs& ix, const PosDev& P) {
+    if (e >= end) return false;
+    const uint32_t p = e >> 7;
+    uint32_t v;
+    if (p < P.npk) {
+      if (p != pk) {
+        const uint2 w = ix.pos_pk[P.pk0 + p];
+        data = ix.pos_blob + P.base + w.x + 2;
+        bits = w.y;
+        pk = p;
+      }
+      v = pack_value(data, bits, e & 127u);
+    } else {
+      v = ix.pos_tail[P.tail + (e - (P.npk << 7))];
+    }
+    ++e;
+    cur += static_cast<int32_t>(v);
+    return true;
+  }
+};
+
+// Does the doc hold the query's terms at consecutive positions?  Term i's bag
+// (query order) = tf_i positions delta coded from 0 starting at entry
+// pos_start[slot_i] of its box (slot_i, tf_i in the caller's scratch ph at
+// [i*256 + v], [i*256 + 128 + v]).  True iff some a has a + i in bag i for
+// every i, which is PhraseQueryProcessor2::NumOfMatches() > 0
+// (query_processing.h:264-336: the 2-term merge and the general max-adjusted
+// walk both find every such a).  One lane per survivor.
+__device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
+                                          const uint32_t* ph, uint32_t v) {
+  if (nt == 2) {   // ProcessTwoTerm: a merge of bag 0 against bag 1 shifted by one
+    const PosDev P0 = ix.pos_lists[qlist[0]], P1 = ix.pos_lists[qlist[1]];
+    PosStream s0, s1;
+    s0.init(ix, ph[v], ph[128 + v]);
+    s1.init(ix, ph[256 + v], ph[384 + v]);
+    if (!s0.next(ix, P0) || !s1.next(ix, P1)) return false;
+    for (;;) {
+      const int32_t a = s0.cur + 1, b = s1.cur;
+      if (a == b) return true;
+      if (a < b) { if (!s0.next(ix, P0)) return false; }
+      else if (!s1.next(ix, P1)) return false;
+    }
+  }
+  PosStream st[kMaxTerms];
+#pragma unroll
+  for (uint32_t i = 0; i < kMaxTerms; ++i) {
+    st[i].init(ix, ph[i * 256 + v], i < nt ? ph[i * 256 + 128 + v] : 0u);
+    if (i < nt && !st[i].next(ix, ix.pos_lists[qlist[i]])) return false;
+  }
+  int32_t a = 0;
+  for (;;) {
+    bool moved = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kMaxTerms; ++i) {
+      if (i < nt) {
+        const int32_t ii = static_cast<int32_t>(i);
+        if (st[i].cur - ii < a) {
+          const PosDev P = ix.pos_lists[qlist[i]];
+          do {
+            if (!st[i].next(ix, P)) return false;
+          } while (st[i].cur - ii < a);
+        }
+        if (st[i].cur - ii > a) {
+          a = st[i].cur - ii;
+          moved = true;
+        }
+      }
+    }
+    if (!moved) return true;
+  }
+}
+
 // ------------------------------------------------- lean bitmap segment --
 // Stage timers of the diagnostics build (-DWSR_PROFILE): cycles charged to
 // prof[0..3] = W, C (compaction + scoring), H, D of the lean pipeline.
@@ -1070,10 +1170,12 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // stage waits only for loads issued one iteration earlier.  Scoring one
 // survivor per lane instead of two postings per lane keeps the f64 work
 // proportional to the survivors.
-// LDS of one wave of the lean kernel
-struct LeanLds {
-  uint32_t q[1024];     // survivor queue (4 rings of 256); at item start the driver's VInts
-                        // tail decode, at item end the replay's segment scan
+// LDS of one wave of the lean kernel (kPh: phrase instance, whose queue also
+// carries the driver's posting slot and O1's posting rank of every survivor)
+template <bool kPh>
+struct LeanLdsT {
+  uint32_t q[kPh ? 1536 : 1024];   // survivor queue (4 or 6 rings of 256); at item end the
+                                   // replay's segment scan
   Event evs[128];       // events buffered in LDS, stored when half full and at the end
   uint4 dblk[64];       // the driver's directory entries of the segment
   uint32_t dmeta[64];
@@ -1085,8 +1187,10 @@ struct LeanLds {
 // o1 == kMaxTerms: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
-__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, const double* norm_tab,
+template <bool kPh>
+__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
+                                             bool phrase, uint32_t* ph,
                                              uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
                                              const uint64_t* prev_pub, uint64_t* my_pub,
@@ -1113,6 +1217,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
   uint32_t* qc4 = qdoc + 256;
   uint32_t* qtd = qdoc + 512;
   uint32_t* qto = qdoc + 768;       // tf byte, or 0x80000000 | posting index when escaped
+  uint32_t* qpd = qdoc + (kPh ? 1024 : 0);   // phrase: driver posting slot
+  uint32_t* qpo = qdoc + (kPh ? 1280 : 0);   //         O1 posting rank
+  const uint32_t o_slot0 = (kPh && phrase) ? ix.lists[Q.o_list].blk0 * 128u : 0u;
   uint32_t qhead = 0, qtail = 0;
   uint32_t bend = b1;
   // The loop issues only plain loads: coherent (agent-scope) loads, stores
@@ -1141,28 +1248,40 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
     const uint32_t c4 = qc4[e];
     const uint32_t td = qtd[e];
     uint32_t to = qto[e];
+    const uint32_t pd = kPh ? qpd[e] : 0u, po = kPh ? qpo[e] : 0u;
     __builtin_amdgcn_wave_barrier();
     qhead += n;
     if (__ballot(alive && (to & 0x80000000u))) {
       const ListDev O = ix.lists[Q.o_list];
       if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
     }
+    // phrase: each term's posting slot and tf, for the position check
+    auto rec = [&](uint32_t s, uint32_t slot, uint32_t tf) __attribute__((always_inline)) {
+      if (kPh && phrase && alive) { ph[s * 256 + l] = slot; ph[s * 256 + 128 + l] = tf; }
+    };
     const double norm = norm_tab[c4 & 255u];
     double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
     for (uint32_t s = 0; s < nt; ++s) {
       if (s == d) {
         sc += bm25_term(idf_d, alive ? td : 0u, norm);
+        rec(s, pd, td);
         if (single) break;
       } else if (s == o1) {
         sc += bm25_term(idf_o, alive ? to : 0u, norm);
+        rec(s, o_slot0 + po, to);
       } else {
         const ListDev B = ix.lists[qlist[s]];
-        uint32_t t = 0;
+        uint32_t t = 0, x = 0;
         const uint2 v = dense_load(ix, B, doc, alive);
-        alive = alive && dense_resolve(ix, B, doc, v, &t);
+        alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
         if (__ballot(alive) == 0) break;
         sc += bm25_term(B.idf, alive ? t : 0u, norm);
+        rec(s, B.blk0 * 128u + x, t);
       }
+    }
+    // HandleTheFoundDoc: a phrase query ranks only docs that hold the phrase
+    if (kPh && phrase && __ballot(alive)) {
+      if (alive) alive = phrase_match(ix, qlist, nt, ph, l);
     }
     const uint64_t am = __ballot(alive);
     if (am == 0) return;
@@ -1260,6 +1379,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
       const uint32_t e0 = X.hh0 ? (r0 & 255u) : spare, e1 = X.hh1 ? (r1 & 255u) : spare;
       qdoc[e0] = X.ha0; qc4[e0] = X.hc0; qtd[e0] = X.ht0; qto[e0] = to0;
       qdoc[e1] = X.ha1; qc4[e1] = X.hc1; qtd[e1] = X.ht1; qto[e1] = to1;
+      if (kPh) {   // block j-2's postings 2l, 2l+1 and their O1 ranks
+        const uint32_t pd0 = (Q.a_blk0 + j - 2) * 128u + 2 * l;
+        qpd[e0] = pd0; qpo[e0] = X.hx0;
+        qpd[e1] = pd0 + 1; qpo[e1] = X.hx1;
+      }
       qtail += __popcll(m0) + __popcll(m1);
       // (at most two full chunks: fewer than 64 + 128 entries are queued;
       // one call site keeps a single inlined copy of the scoring code)
@@ -1336,69 +1460,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLds& S, co
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   last_pub = pub_val;
   __builtin_amdgcn_wave_barrier();
-}
-
-// ---------------------------------------------------------- phrase check --
-// Entry e of a list's position cozy box: pack e / 128 (its offset and width
-// from the pack directory) or the decoded VInts remainder.
-__device__ __forceinline__ uint32_t pos_entry(const IndexArgs& ix, const PosDev& P, uint32_t e) {
-  const uint32_t pk = e >> 7;
-  if (pk < P.npk) {
-    const uint2 w = ix.pos_pk[P.pk0 + pk];
-    return pack_value(ix.pos_blob + P.base + w.x + 2, w.y, e & 127u);
-  }
-  return ix.pos_tail[P.tail + (e - (P.npk << 7))];
-}
-
-// Per general workgroup (kPhraseScratch words), per query term s: the image
-// posting slot of value v (= 2l or 2l+1 of the driver block) at [s*256 + v],
-// its tf at [s*256 + 128 + v] (phrase queries only).
-
-// Does the doc hold the query's terms at consecutive positions?  Term i's bag
-// (query order) = tf_i positions delta coded from 0 starting at entry
-// pos_start[slot_i] of its box.  True iff some a has a + i in bag i for every
-// i, which is PhraseQueryProcessor2::NumOfMatches() > 0 (query_processing.h:
-// 264-336: the 2-term merge and the general max-adjusted walk both find every
-// such a).  One lane per survivor; term state stays in registers (the term
-// loop is unrolled, so every index is static).
-__device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
-                                          const uint32_t* ph, uint32_t v) {
-  int32_t cur[kMaxTerms];
-  uint32_t used[kMaxTerms];
-#pragma unroll
-  for (uint32_t i = 0; i < kMaxTerms; ++i) {
-    cur[i] = 0;
-    used[i] = 0;
-    if (i < nt) {
-      const PosDev P = ix.pos_lists[qlist[i]];
-      cur[i] = static_cast<int32_t>(pos_entry(ix, P, ix.pos_start[ph[i * 256 + v]]));
-      used[i] = 1;
-    }
-  }
-  int32_t a = 0;
-  for (;;) {
-    bool moved = false;
-#pragma unroll
-    for (uint32_t i = 0; i < kMaxTerms; ++i) {
-      if (i < nt) {
-        if (cur[i] - static_cast<int32_t>(i) < a) {
-          const PosDev P = ix.pos_lists[qlist[i]];
-          const uint32_t st = ix.pos_start[ph[i * 256 + v]];
-          const uint32_t tf = ph[i * 256 + 128 + v];
-          do {
-            if (used[i] >= tf) return false;
-            cur[i] += static_cast<int32_t>(pos_entry(ix, P, st + used[i]));
-            ++used[i];
-          } while (cur[i] - static_cast<int32_t>(i) < a);
-        }
-        if (cur[i] - static_cast<int32_t>(i) > a) {
-          a = cur[i] - static_cast<int32_t>(i);
-          moved = true;
-        }
-      }
-    }
-    if (!moved) return true;
-  }
 }
 
 // kPhrase: the batch holds phrase queries (their position check is compiled
@@ -1853,19 +1914,21 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #ifndef WSR_LEAN_WGS
 #define WSR_LEAN_WGS 4
 #endif
+template <bool kPh>
 __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
-    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc) {
-  __shared__ LeanLds SW[kLeanWaves];
+    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc, uint32_t* __restrict__ ph_all) {
+  __shared__ LeanLdsT<kPh> SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
   const uint32_t w = threadIdx.x >> 6;
   for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
   __syncthreads();
-  LeanLds& S = SW[w];
+  LeanLdsT<kPh>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
+  uint32_t* ph = kPh ? ph_all + static_cast<uint64_t>(wid) * kPhraseScratch : nullptr;
   const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0;
@@ -1916,7 +1979,9 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
     if (!done && b0 < b1)
-      lean_segment(ix, S, norm, Q, qs[qi].list, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
+      lean_segment<kPh>(ix, S, norm, Q, qs[qi].list,
+                   kPh && ((Q.slots >> 16) & 0xFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
+                   ph, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
     WSR_T(1)
     finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
@@ -2067,15 +2132,19 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, hipStream_t st) {
-  hipLaunchKernelGGL(lean_kernel, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan, nq,
-                     counters, events, ev_cnt, stats, fr, item_q, pub, desc);
+                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st) {
+  if (ph)
+    hipLaunchKernelGGL(lean_kernel<true>, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
+                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+  else
+    hipLaunchKernelGGL(lean_kernel<false>, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
+                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   return hipGetLastError();
 }
 
 int lean_kernel_occupancy() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel, 64 * kLeanWaves, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false>, 64 * kLeanWaves, 0) != hipSuccess)
     return 1;
   return n;
 }
