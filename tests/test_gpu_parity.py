@@ -24,12 +24,14 @@ DENSE_MODES = {
     "blocks": {"WSR_DENSE_DIV": "0"},
     "dense": {},
     "dense_all": {"WSR_DENSE_DIV": "1000000000", "WSR_DENSE_RATIO": "0"},
+    # every lean item whose driver has a bitmap intersects bitmaps word by word
+    "and_all": {"WSR_DENSE_DIV": "1000000000", "WSR_DENSE_RATIO": "0", "WSR_AND_WPB": "1000000000"},
 }
 
 
 def _engine(d, mode="dense"):
     import wiser_amd as w
-    saved = {k: os.environ.get(k) for k in ("WSR_DENSE_DIV", "WSR_DENSE_RATIO")}
+    saved = {k: os.environ.get(k) for k in ("WSR_DENSE_DIV", "WSR_DENSE_RATIO", "WSR_AND_WPB")}
     try:
         for k in saved:
             os.environ.pop(k, None)

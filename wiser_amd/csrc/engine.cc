@@ -185,6 +185,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.tf8 = h->d_tf8;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
+    h->args.and_wpb = static_cast<float>(env_number("WSR_AND_WPB", 0.0));
     dev_upload(&h->d_blob, img.blob);
     dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;

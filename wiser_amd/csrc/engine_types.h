@@ -94,13 +94,15 @@ struct QueryDesc {
   uint64_t o_bm;        // O1 (the other list with the fewest blocks): first bitmap entry
   uint64_t o_tf8;       //   offset of its 1-byte tfs
   uint64_t ev_base;     // = QueryPlan::ev_base
+  uint64_t a_bm;        // driver's bitmap / 1-byte tfs (kNoDense: none), for the
+  uint64_t a_tf8;       //   bitmap-intersection path of dense drivers
   double a_idf, o_idf;
   uint32_t a_blk0, a_nblk, a_tail_cnt;
   uint32_t min_last;    // smallest last doc id over the other lists
   uint32_t item_base, n_items, seg;
   uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16 | k << 24
   uint32_t o_list;      // O1's list id
-  uint32_t pad[9];
+  uint32_t pad[5];
 };
 static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
 

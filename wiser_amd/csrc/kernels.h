@@ -28,6 +28,9 @@ struct IndexArgs {
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
+  float and_wpb;            // lean items of a driver with a bitmap intersect bitmaps word by
+                            // word when their doc span is <= and_wpb 32-doc words per driver
+                            // block (0 = never)
   // positions (phrase queries; null unless the engine was opened with them)
   const uint8_t* pos_blob;  // every list's position cozy box, byte-exact from my.vacuum
   const PosDev* pos_lists;  // indexed by list id

@@ -406,13 +406,15 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
         D.o_list = static_cast<uint32_t>(q.list[o1]);
       }
       D.min_last = min_last;
+      D.a_bm = A.bm;
+      D.a_tf8 = A.tf8;
       D.ev_base = 0;
       D.item_base = 0;
       D.n_items = p.n_items;
       D.seg = seg;
       D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16) |
                 (static_cast<uint32_t>(q.k) << 24);
-      for (int t = 0; t < 9; ++t) D.pad[t] = 0;
+      for (int t = 0; t < 5; ++t) D.pad[t] = 0;
       desc[i] = D;
     }
   }
@@ -1177,6 +1179,8 @@ struct LeanLdsT {
   uint32_t q[kPh ? 1536 : 1024];   // survivor queue (4 or 6 rings of 256); at item end the
                                    // replay's segment scan
   Event evs[128];       // events buffered in LDS, stored when half full and at the end
+  uint32_t bx[6][64];   // bitmap-intersection step: per lane its word's survivors (exclusive
+                        // prefix), intersected word, driver and O1 (rank, word)
   uint4 dblk[64];       // the driver's directory entries of the segment
   uint32_t dmeta[64];
 #ifdef WSR_PROFILE
@@ -1191,6 +1195,7 @@ template <bool kPh>
 __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t* ph,
+                                             bool and_path, uint32_t first_doc,
                                              uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
                                              const uint64_t* prev_pub, uint64_t* my_pub,
@@ -1246,7 +1251,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     bool alive = l < n;
     const uint32_t doc = qdoc[e];
     const uint32_t c4 = qc4[e];
-    const uint32_t td = qtd[e];
+    uint32_t td = qtd[e];
     uint32_t to = qto[e];
     const uint32_t pd = kPh ? qpd[e] : 0u, po = kPh ? qpo[e] : 0u;
     __builtin_amdgcn_wave_barrier();
@@ -1254,6 +1259,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     if (__ballot(alive && (to & 0x80000000u))) {
       const ListDev O = ix.lists[Q.o_list];
       if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
+    }
+    if (and_path && __ballot(alive && (td & 0x80000000u))) {   // (bitmap path: driver tf >= 255)
+      const ListDev A = ix.lists[qlist[d]];
+      if (alive && (td & 0x80000000u)) td = dense_tf_slow(ix, A, td & 0x7FFFFFFFu);
     }
     // phrase: each term's posting slot and tf, for the position check
     auto rec = [&](uint32_t s, uint32_t slot, uint32_t tf) __attribute__((always_inline)) {
@@ -1447,11 +1456,86 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     }
     LT(3)
   };
-  issue_words(b0, R0);
-  for (uint32_t j = b0; j < bend + 2; j += 2) {
-    body(R0, R1, j);
-    if (j + 1 >= bend + 2) break;
-    body(R1, R0, j + 1);
+  if (and_path) {
+    // Bitmap intersection: the segment's doc span, 32 docs per word, one word
+    // per lane and step; the words of every list are ANDed, so a step costs a
+    // few loads per list whatever the driver's density.  Survivors are taken
+    // in rank order (= doc order) 64 at a time: lane l finds the word holding
+    // survivor c*64 + l by a search over the step's prefix counts and the bit
+    // by a popcount select, and appends it to the queue.
+    const uint32_t last_doc = min(uni(S.dblk[b1 - 1 - b0].y), min_last);
+    const uint32_t a_lo = first_doc > lo ? first_doc - lo : 0u;
+    uint32_t a_hi = last_doc - lo;                      // inclusive, relative
+    if (a_hi >= span) a_hi = span - 1;
+    const uint2* a_bm = reinterpret_cast<const uint2*>(ix.dense + Q.a_bm);
+    const uint8_t* a_tf8 = ix.tf8 + Q.a_tf8;
+    if (span && last_doc >= lo && a_lo <= a_hi) {
+      const uint32_t w0 = a_lo >> 5, w1 = a_hi >> 5;   // inclusive word range
+      for (uint32_t base = w0; base <= w1; base += 64) {
+        const uint32_t wi = base + l;
+        const bool live = wi <= w1;
+        const uint2 va = a_bm[live ? wi : w0];
+        const uint2 vo = single ? make_uint2(0u, 0xFFFFFFFFu) : o_bm[live ? wi : w0];
+        uint32_t m = live ? (va.y & vo.y) : 0u;
+        if (wi == w0) m &= ~0u << (a_lo & 31u);
+        if (wi == w1 && (a_hi & 31u) != 31u) m &= (2u << (a_hi & 31u)) - 1u;
+        for (uint32_t s = 0; s < nt; ++s) {   // the further other lists
+          if (s == d || s == o1 || !__ballot(m)) continue;
+          const ListDev B = ix.lists[qlist[s]];
+          m &= reinterpret_cast<const uint2*>(ix.dense + B.bm)[live ? wi : w0].y;
+        }
+        const uint32_t c = __popc(m);
+        const uint32_t inc = wave_incl_scan(c);
+        const uint32_t total = uni(__builtin_amdgcn_readlane(inc, 63));
+        if (total == 0) continue;
+        __builtin_amdgcn_wave_barrier();
+        S.bx[0][l] = inc - c;
+        S.bx[1][l] = m;
+        S.bx[2][l] = va.x; S.bx[3][l] = va.y;
+        S.bx[4][l] = vo.x; S.bx[5][l] = vo.y;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+          const uint32_t g = c0 + l;
+          const bool has = g < total;
+          // owner lane: the last lane whose exclusive prefix is <= g
+          uint32_t ow = 0;
+#pragma unroll
+          for (uint32_t st = 32; st; st >>= 1)
+            if (S.bx[0][ow + st] <= g) ow += st;
+          uint32_t k = g - S.bx[0][ow], mw = S.bx[1][ow], bit = 0;
+#pragma unroll
+          for (uint32_t st = 16; st; st >>= 1) {   // k-th set bit of mw
+            const uint32_t lowc = __popc(mw & ((1u << st) - 1u));
+            if (k >= lowc) { k -= lowc; bit += st; mw >>= st; }
+          }
+          const uint32_t below = (1u << bit) - 1u;
+          const uint32_t doc = lo + ((base + ow) << 5) + bit;
+          const uint32_t ra = S.bx[2][ow] + __popc(S.bx[3][ow] & below);
+          const uint32_t ro = S.bx[4][ow] + __popc(S.bx[5][ow] & below);
+          const uint32_t ta = load_byte(a_tf8 + (has ? ra : 0u));
+          const uint32_t tb = single ? 0u : load_byte(o_tf8 + (has ? ro : 0u));
+          const uint32_t cc = (has && doc < ix.n_c4) ? load_byte(ix.c4 + doc) : 0u;
+          const uint32_t e = (qtail + l) & 255u;
+          if (has) {
+            qdoc[e] = doc; qc4[e] = cc;
+            qtd[e] = ta == kTf8Escape ? (0x80000000u | ra) : ta;
+            qto[e] = tb == kTf8Escape ? (0x80000000u | ro) : tb;
+            if (kPh) { qpd[e] = Q.a_blk0 * 128u + ra; qpo[e] = ro; }
+          }
+          qtail += min(64u, total - c0);
+          __builtin_amdgcn_wave_barrier();
+          if (qtail - qhead >= 64) score_chunk(64);
+        }
+      }
+    }
+    n_dblk += b1 - b0;
+  } else {
+    issue_words(b0, R0);
+    for (uint32_t j = b0; j < bend + 2; j += 2) {
+      body(R0, R1, j);
+      if (j + 1 >= bend + 2) break;
+      body(R1, R0, j + 1);
+    }
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
   if (evb) flush();
@@ -1974,6 +2058,10 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     // an other list ends before this segment: nothing in it can match
     const bool done = first_doc > Q.min_last;
+    // a driver with a bitmap and a dense segment: intersect bitmaps word by word
+    const bool and_path = ix.and_wpb > 0.0f && Q.a_bm != kNoDense && b0 < b1 &&
+                          static_cast<float>((uni(S.dblk[b1 - 1 - b0].y) - first_doc) >> 5) <
+                              ix.and_wpb * static_cast<float>(b1 - b0);
     WSR_T(0)
     // a query of one item with fused replay: the heap runs here, no events
     double pt = 0.0, last_pub = 0.0;
@@ -1981,7 +2069,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     if (!done && b0 < b1)
       lean_segment<kPh>(ix, S, norm, Q, qs[qi].list,
                    kPh && ((Q.slots >> 16) & 0xFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
-                   ph, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
+                   ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
     WSR_T(1)
     finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
