@@ -23,7 +23,7 @@ kernels = kernel.split(",")
 vals = {k: defaultdict(list) for k in kernels}
 for f in glob.glob(f"{pmc_dir}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0].strip().split("::")[-1]
+        name = r["Kernel_Name"].split("(")[0].strip().split("<")[0].split("::")[-1]
         if name in vals:
             vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 avg, n = defaultdict(float), defaultdict(int)
