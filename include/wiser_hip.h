@@ -126,6 +126,9 @@ int wsr_sync(wsr_handle* h);
 /* copy results to the host (waits for the stream) */
 int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits);
 int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
+/* as wsr_batch_fetch, but only the first `cols` (<= hit stride) entries of each
+ * query: hits is nq x cols (a pitched copy; cols >= every query's k) */
+int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols);
 /* 1 when the batch's last run has finished on the device, 0 while it runs */
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b);
 /* device pointers of the batch's results (for collectives on the caller's side) */

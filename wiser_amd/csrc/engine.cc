@@ -499,6 +499,29 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
   return WSR_OK;
 }
 
+int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols) {
+  if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
+  if (cols < 1 || cols > b->stride) return fail(WSR_E_INVALID, "cols must be in [1, hit stride]");
+  std::lock_guard<std::mutex> g(h->mu);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(b->st));
+    uint32_t ctr[kNumCounters];
+    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
+    if (b->nq) {
+      // the first `cols` entries of every query's row: a pitched copy
+      if (hits)
+        HIP_OK(hipMemcpy2D(hits, sizeof(HitDev) * cols, b->d_hits, sizeof(HitDev) * b->stride,
+                           sizeof(HitDev) * cols, b->nq, hipMemcpyDeviceToHost));
+      if (n_hits) HIP_OK(hipMemcpy(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost));
+    }
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   if (!b->ran) return 0;

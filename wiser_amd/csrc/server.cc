@@ -25,6 +25,9 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/wiser_hip.h"
 
@@ -32,21 +35,44 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// Completion flag of one request: 0 pending, 1 done, 2 pending with its
+// caller asleep on the flag (a futex), so the dispatcher wakes exactly the
+// callers that sleep and never takes a lock to do it.
+constexpr int kPending = 0, kDone = 1, kSleeping = 2;
+
 struct Req {
   wsr_query q;
   Clock::time_point t_enq;
   wsr_hit* out = nullptr;
   int32_t* n_out = nullptr;
   int rc = WSR_OK;
-  std::atomic<bool> done{false};
-  void reset() { out = nullptr; n_out = nullptr; rc = WSR_OK; done.store(false, std::memory_order_relaxed); }
+  std::atomic<int> done{kPending};
+  void reset() { out = nullptr; n_out = nullptr; rc = WSR_OK; done.store(kPending, std::memory_order_relaxed); }
+  void signal() {
+    if (done.exchange(kDone, std::memory_order_acq_rel) == kSleeping)
+      syscall(SYS_futex, reinterpret_cast<int*>(&done), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+  }
+  void wait() {
+    const auto spin_until = Clock::now() + std::chrono::microseconds(10);
+    while (done.load(std::memory_order_acquire) != kDone && Clock::now() < spin_until) {}
+    int v = kPending;
+    while (done.load(std::memory_order_acquire) != kDone) {
+      if (v == kPending && !done.compare_exchange_strong(v, kSleeping, std::memory_order_acq_rel)) {
+        if (v == kDone) break;
+      }
+      syscall(SYS_futex, reinterpret_cast<int*>(&done), FUTEX_WAIT_PRIVATE, kSleeping, nullptr, nullptr, 0);
+      v = kSleeping;
+    }
+  }
 };
+static_assert(sizeof(std::atomic<int>) == sizeof(int), "futex word");
 
 struct Slot {
   wsr_batch* b = nullptr;
   std::vector<Req*> reqs;
   bool busy = false;
   uint64_t seq = 0;   // launch order
+  int32_t kmax = 1;   // the largest k of its queries (result columns to copy)
 };
 
 }  // namespace
@@ -57,9 +83,9 @@ struct wsr_server {
   std::chrono::microseconds window{200};
   std::mutex mu;
   std::condition_variable cv_work;   // dispatcher: requests arrived / stop
-  std::condition_variable cv_done;   // callers: some request completed
   std::deque<Req*> queue;
   bool stop = false;
+  bool idle = false;                 // dispatcher asleep on cv_work (no batch in flight)
   std::thread worker;
   Slot slots[2];
   // fetch buffers of one batch, page-locked so the result copies are DMA'd
@@ -68,40 +94,24 @@ struct wsr_server {
   std::vector<wsr_query> qbuf;
   std::atomic<uint64_t> batches{0}, queries{0};
 
-  // Results are written, then each request's flag is released; callers spin
-  // briefly on their flag and sleep on cv_done only after that, so the
-  // dispatcher takes the lock (to wake sleepers) only when someone sleeps.
-  std::atomic<int> sleepers{0};
-
-  // (done flags are stored seq_cst before `sleepers` is read; a caller bumps
-  // `sleepers` before its last look at its flag, so one of the two sees the other)
-  void finish() {
-    if (sleepers.load(std::memory_order_seq_cst) > 0) {
-      std::lock_guard<std::mutex> g(mu);   // pairs with the sleeper's check under mu
-    }
-    cv_done.notify_all();
-  }
-
   void complete(Slot& s) {
-    int rc = wsr_batch_fetch(h, s.b, hits, nh);
+    int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
       r->rc = rc;
       if (rc == WSR_OK) {
         const int32_t n = nh[i];
-        std::memcpy(r->out, &hits[i * WSR_MAX_K], sizeof(wsr_hit) * static_cast<size_t>(n));
+        std::memcpy(r->out, &hits[i * static_cast<size_t>(s.kmax)], sizeof(wsr_hit) * static_cast<size_t>(n));
         *r->n_out = n;
       }
-      r->done.store(true, std::memory_order_seq_cst);
+      r->signal();
     }
-    finish();
     s.reqs.clear();
     s.busy = false;
   }
 
   void fail_all(std::vector<Req*>& rs, int rc) {
-    for (Req* r : rs) { r->rc = rc; r->done.store(true, std::memory_order_seq_cst); }
-    finish();
+    for (Req* r : rs) { r->rc = rc; r->signal(); }
     rs.clear();
   }
 
@@ -123,8 +133,14 @@ struct wsr_server {
         std::unique_lock<std::mutex> lk(mu);
         if (queue.empty()) {
           if (stop && !n_busy) break;
-          if (n_busy) cv_work.wait_for(lk, std::chrono::microseconds(20));
-          else if (!stop) cv_work.wait(lk);
+          if (n_busy) {
+            lk.unlock();
+            std::this_thread::sleep_for(std::chrono::microseconds(10));
+          } else if (!stop) {
+            idle = true;
+            cv_work.wait(lk);
+            idle = false;
+          }
           continue;
         }
         if (n_busy == 2) {
@@ -136,7 +152,8 @@ struct wsr_server {
           const auto due = queue.front()->t_enq + window;
           const auto now = Clock::now();
           if (now < due) {
-            cv_work.wait_for(lk, std::min<Clock::duration>(due - now, std::chrono::microseconds(20)));
+            lk.unlock();
+            std::this_thread::sleep_for(std::min<Clock::duration>(due - now, std::chrono::microseconds(10)));
             continue;
           }
         }
@@ -146,7 +163,11 @@ struct wsr_server {
       }
       Slot& s = slots[0].busy ? slots[1] : slots[0];
       qbuf.resize(take.size());
-      for (size_t i = 0; i < take.size(); ++i) qbuf[i] = take[i]->q;
+      s.kmax = 1;
+      for (size_t i = 0; i < take.size(); ++i) {
+        qbuf[i] = take[i]->q;
+        s.kmax = std::max(s.kmax, qbuf[i].k);
+      }
       int rc = wsr_batch_upload(h, s.b, qbuf.data(), static_cast<int32_t>(qbuf.size()));
       if (rc == WSR_OK) rc = wsr_batch_run(h, s.b);
       if (rc != WSR_OK) { fail_all(take, rc); continue; }
@@ -164,25 +185,21 @@ struct wsr_server {
     const wsr_query& q = r->q;
     if (q.n_terms > WSR_MAX_TERMS || q.k > WSR_MAX_K) return WSR_E_LIMIT;
     r->t_enq = Clock::now();
+    bool wake;
     {
       std::lock_guard<std::mutex> g(mu);
       if (stop) return WSR_E_INVALID;
       queue.push_back(r);
+      wake = idle;   // the dispatcher sleeps only with no batch in flight
     }
-    cv_work.notify_one();
+    if (wake) cv_work.notify_one();
     return WSR_OK;
   }
 
+  // a short spin (results of a batch arrive together), then sleep on the
+  // request's own flag: spinning callers would take the dispatcher's cores
   int wait(Req* r) {
-    const auto spin_until = Clock::now() + std::chrono::microseconds(200);
-    while (!r->done.load(std::memory_order_acquire)) {
-      if (Clock::now() < spin_until) { std::this_thread::yield(); continue; }
-      std::unique_lock<std::mutex> lk(mu);
-      ++sleepers;
-      cv_done.wait(lk, [&] { return r->done.load(std::memory_order_seq_cst); });
-      --sleepers;
-      break;
-    }
+    r->wait();
     return r->rc;
   }
 };
@@ -266,7 +283,7 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
       r.n_out = &nout[static_cast<size_t>(i)];
       t0[static_cast<size_t>(i)] = Clock::now();
       const int rc = s->submit(&r);
-      if (rc != WSR_OK) { r.rc = rc; r.done.store(true); }
+      if (rc != WSR_OK) { r.rc = rc; r.done.store(kDone); }
     };
     for (int i = 0; i < depth; ++i) issue(i);
     for (uint64_t it = 0;; ++it) {
