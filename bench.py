@@ -57,6 +57,12 @@ def parse():
     p.add_argument("--dist-backend", default="nccl",
                    help="shard exchange backend (nccl = RCCL over xGMI; gloo for 1-GPU rehearsals)")
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
+    p.add_argument("--vacuum-dir", default=None,
+                   help="configs[2]: an existing Vacuum dump (my.vacuum, my.tip, my.doc_length), "
+                        "e.g. the reference's en-Wikipedia index, instead of the C2 corpus")
+    p.add_argument("--linedoc", default=None,
+                   help="configs[2]: build the index from this linedoc first (--format)")
+    p.add_argument("--format", default="WITH_POSITIONS", choices=["WITH_POSITIONS", "TOKEN_ONLY"])
     p.add_argument("--cpu-seconds", type=float, default=16.0,
                    help="bounded CPU-baseline sample (oracle, 1 thread), rank 0 at N=1")
     p.add_argument("--no-cpu", action="store_true")
@@ -67,7 +73,28 @@ def parse():
 
 
 def ensure_index(a, rank, dist):
+    """The C2 synthetic index (default), or -- configs[2] -- an existing Vacuum
+    dump (--vacuum-dir, e.g. the reference's en-Wikipedia dump) or one built here
+    from a linedoc (--linedoc); the two-term log is generated over its df table
+    by the gen_synthetic_log.py:191-214 rule, in --index-dir."""
     import wiser_amd as w
+    if a.vacuum_dir or a.linedoc:
+        idx = a.vacuum_dir
+        if a.linedoc:
+            idx = os.path.join(a.index_dir, "linedoc_" + os.path.basename(a.linedoc))
+        qlog = os.path.join(a.index_dir, f"log_{os.path.basename(idx.rstrip('/'))}_{a.queries}.log")
+        if rank == 0 and not os.path.exists(qlog):
+            os.makedirs(a.index_dir, exist_ok=True)
+            if a.linedoc and not os.path.exists(os.path.join(idx, "READY")):
+                t = time.time()
+                st = w.build_from_linedoc(a.linedoc, idx, a.format)
+                open(os.path.join(idx, "READY"), "w").write("ok")
+                log(f"built index {st.n_docs} docs {st.n_terms} terms from {a.linedoc} "
+                    f"in {time.time()-t:.1f}s")
+            w.gen_two_term_log(idx, qlog, n_queries=a.queries, seed=7)
+        if dist:
+            dist.barrier()
+        return idx, qlog
     idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
     qlog = os.path.join(idx, f"two_term_{a.queries}.log")
     if rank == 0 and not os.path.exists(os.path.join(idx, "READY")):
@@ -205,11 +232,13 @@ def extra_legs(a, idx, local, threads):
     1-5 term AND queries (AOL shares) and 2-term phrase queries."""
     import wiser_amd as w
     legs = {}
-    mixed = os.path.join(idx, "mixed_20000.log")
-    phr = os.path.join(idx, "phrase_10000.log")
+    tag = os.path.basename(idx.rstrip("/"))
+    mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
+    phr = os.path.join(a.index_dir, f"phrase_{tag}_10000.log")
     if not os.path.exists(mixed):
         w.gen_mixed_log(idx, mixed, n_queries=20000, seed=7)
-    if not os.path.exists(phr):
+    has_pool = os.path.exists(os.path.join(idx, "phrases.txt"))
+    if has_pool and not os.path.exists(phr):
         w.gen_phrase_log(idx, phr, n_queries=10000, seed=7)
     eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
     eng.Load()
@@ -219,6 +248,9 @@ def extra_legs(a, idx, local, threads):
     legs["c4_mixed_1to5"]["workload"] = ("20000 AND queries of 1-5 terms (AOL term-count shares, "
                                          "gen_synthetic_log group rule, seed 7), top-10")
     eng.close()
+    if not has_pool:   # phrase pool: synthetic indexes only
+        legs["serving"] = serving_leg(a, idx, local, threads)
+        return legs
     t = time.time()
     eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
     eng.Load()
@@ -243,7 +275,7 @@ def serving_leg(a, idx, local, threads):
     from wiser_amd import _capi
     eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
     eng.Load()
-    lines = [l.split() for l in open(os.path.join(idx, f"two_term_{a.queries}.log")).read().splitlines()]
+    lines = [l.split() for l in open(a.qlog).read().splitlines()]
     arr = (_capi.Query * len(lines))()
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
@@ -403,6 +435,7 @@ def main():
     on_gpu = dist is not None and a.dist_backend == "nccl"
 
     idx, qlog = ensure_index(a, rank, dist)
+    a.qlog = qlog
     lines = [l.split() for l in open(qlog).read().splitlines()]
     threads = min(16, os.cpu_count())
 
@@ -461,7 +494,9 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32/f64",
             "data": "synthetic",
-            "config": {"workload": f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), "
+            "config": {"workload": (f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), "
+                                    if not (a.vacuum_dir or a.linedoc) else
+                                    f"C3: Vacuum index {idx}, ") +
                                    f"{len(lines)} two-term AND queries (gen_synthetic_log rule, "
                                    f"seed 7), {a.batch} queries per GPU per step, top-{a.k}",
                        "global_batch": global_batch, "parallelism": parallelism, "k": a.k},
