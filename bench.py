@@ -482,7 +482,8 @@ def main():
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_segment.json")
-    if os.path.exists(pmc):
+    # (measured on the C2 workload: attached to C2 lines only)
+    if os.path.exists(pmc) and not (a.vacuum_dir or a.linedoc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
