@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     p.n_items = (nd + seg - 1) / seg;
     if (lean) {
       // the lean kernel's record: driver, the most selective other list (O1),
-      // the smallest last doc of the others (bases are added by item_map_kernel)
+      // the smallest last doc of the others (bases are added by plan_scan_kernel)
       const ListDev A = ix.lists[q.list[d]];
       QueryDesc D;
       D.a_base = A.base;
@@ -438,7 +438,10 @@ __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
 __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __restrict__ plan,
                                                          uint32_t* __restrict__ counters,
                                                          uint64_t ev_capacity, uint32_t item_capacity,
-                                                         uint32_t lean_grid, uint32_t seg_grid) {
+                                                         uint32_t lean_grid, uint32_t seg_grid,
+                                                         uint32_t* __restrict__ item_q,
+                                                         uint64_t* __restrict__ pub,
+                                                         QueryDesc* __restrict__ desc) {
   constexpr int kWaves = 1024 / 64;
   __shared__ uint64_t s_cap[1024];
   __shared__ uint32_t s_bt[kPlanKeys][kWaves];   // per key, per wave item totals
@@ -489,6 +492,7 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     if (b == kCostBuckets - 1) n_lean = run;
   }
   const uint32_t total_items = run;
+  const bool fits = s_cap[T - 1] <= ev_capacity && total_items <= item_capacity;
   uint64_t cb = s_cap[t] - cap;
   for (int i = q0; i < q1; ++i) {
     QueryPlan& p = plan[i];
@@ -499,10 +503,21 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
       if (bk == static_cast<uint32_t>(b)) { base = ib[b]; ib[b] += p.n_items; }
     p.item_base = base;
     p.ev_base = cb;
+    // the item -> query map, the zeroed per-item floors and the lean
+    // record's bases (skipped when the plan does not fit the workspace)
+    if (fits) {
+      if (p.driver & kPlanLean) {
+        desc[i].item_base = base;
+        desc[i].ev_base = cb;
+      }
+      for (uint32_t j = 0; j < p.n_items; ++j) {
+        item_q[base + j] = static_cast<uint32_t>(i);
+        if (pub) pub[base + j] = 0;
+      }
+    }
     cb += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
   if (t == T - 1) {
-    const bool fits = s_cap[t] <= ev_capacity && total_items <= item_capacity;
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
     counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
     counters[kCtrLean] = fits ? n_lean : 0u;
@@ -514,26 +529,6 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
   if (t < kQueueShards) {
     counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
     counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
-  }
-}
-
-// Pass 3, one thread per query: the item -> query map of the segment kernel
-// and the zeroed per-item thresholds (skipped when the plan did not fit).
-__global__ __launch_bounds__(256) void item_map_kernel(const QueryPlan* __restrict__ plan, int nq,
-                                                       const uint32_t* __restrict__ counters,
-                                                       uint32_t* __restrict__ item_q,
-                                                       uint64_t* __restrict__ pub,
-                                                       QueryDesc* __restrict__ desc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq || (counters[kCtrError] & kErrCapacity)) return;
-  const QueryPlan p = plan[i];
-  if (p.driver & kPlanLean) {
-    desc[i].item_base = p.item_base;
-    desc[i].ev_base = p.ev_base;
-  }
-  for (uint32_t j = 0; j < p.n_items; ++j) {
-    item_q[p.item_base + j] = static_cast<uint32_t>(i);
-    if (pub) pub[p.item_base + j] = 0;
   }
 }
 
@@ -2197,10 +2192,8 @@ hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan*
     hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
                        counters, fr, desc);
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
-                     item_capacity, static_cast<uint32_t>(lean_grid), static_cast<uint32_t>(seg_grid));
-  if (nq > 0)
-    hipLaunchKernelGGL(item_map_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, plan, nq, counters,
-                       item_q, pub, desc);
+                     item_capacity, static_cast<uint32_t>(lean_grid), static_cast<uint32_t>(seg_grid),
+                     item_q, pub, desc);
   return hipGetLastError();
 }
 
