@@ -129,6 +129,9 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
 /* as wsr_batch_fetch, but only the first `cols` (<= hit stride) entries of each
  * query: hits is nq x cols (a pitched copy; cols >= every query's k) */
 int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols);
+/* page-locked host memory for result arrays (their copies are then DMA'd) */
+int wsr_pinned_alloc(uint64_t bytes, void** out);
+void wsr_pinned_free(void* p);
 /* 1 when the batch's last run has finished on the device, 0 while it runs */
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b);
 /* device pointers of the batch's results (for collectives on the caller's side) */

@@ -117,6 +117,8 @@ _sigs = {
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
     "wsr_batch_ready": (C.c_int, [_P, _P]),
+    "wsr_pinned_alloc": (C.c_int, [C.c_uint64, C.POINTER(_P)]),
+    "wsr_pinned_free": (None, [_P]),
     "wsr_batch_fetch_cols": (C.c_int, [_P, _P, C.POINTER(Hit), C.POINTER(C.c_int32), C.c_int32]),
     "wsr_server_open": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_server_close": (None, [_P]),

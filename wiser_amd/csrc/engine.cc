@@ -522,6 +522,18 @@ int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_
   return WSR_OK;
 }
 
+int wsr_pinned_alloc(uint64_t bytes, void** out) {
+  if (!out) return fail(WSR_E_INVALID, "null argument");
+  *out = nullptr;
+  const hipError_t e = hipHostMalloc(out, bytes ? bytes : 1);
+  if (e != hipSuccess) return fail(WSR_E_HIP, hipGetErrorString(e));
+  return WSR_OK;
+}
+
+void wsr_pinned_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   if (!b->ran) return 0;

@@ -207,6 +207,13 @@ class ResidentBatch:
         check(lib.wsr_batch_create(engine._h, max_queries, hit_stride, C.byref(b)))
         self._b = b
         self.nq = 0
+        # page-locked result arrays, reused by every fetch
+        ph, pn = C.c_void_p(), C.c_void_p()
+        check(lib.wsr_pinned_alloc(C.sizeof(_capi.Hit) * max(max_queries, 1) * hit_stride, C.byref(ph)))
+        check(lib.wsr_pinned_alloc(4 * max(max_queries, 1), C.byref(pn)))
+        self._pin = (ph, pn)
+        self._hits = C.cast(ph, C.POINTER(_capi.Hit * (max(max_queries, 1) * hit_stride))).contents
+        self._nh = C.cast(pn, C.POINTER(C.c_int32 * max(max_queries, 1))).contents
 
     def upload(self, queries) -> None:
         """queries: ctypes array of _capi.Query."""
@@ -217,10 +224,10 @@ class ResidentBatch:
         check(lib.wsr_batch_run(self.engine._h, self._b))
 
     def fetch(self):
-        hits = (_capi.Hit * (max(self.nq, 1) * self.stride))()
-        nh = (C.c_int32 * max(self.nq, 1))()
-        check(lib.wsr_batch_fetch(self.engine._h, self._b, hits, nh))
-        return hits, nh
+        """-> (hits, n_hits): views of the batch's page-locked arrays, valid until
+        the next fetch"""
+        check(lib.wsr_batch_fetch(self.engine._h, self._b, self._hits, self._nh))
+        return self._hits, self._nh
 
     def stats(self) -> _capi.BatchStats:
         st = _capi.BatchStats()
@@ -231,6 +238,9 @@ class ResidentBatch:
         if self._b is not None:
             lib.wsr_batch_destroy(self.engine._h, self._b)
             self._b = None
+            for p in self._pin:
+                lib.wsr_pinned_free(p)
+            self._pin = ()
 
 
 class Server:
