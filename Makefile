@@ -7,7 +7,8 @@ JOBS    ?= 8
 LIB     := wiser_amd/_lib/libwiser_hip.so
 ORACLE  := oracle/_build/liboracle.so
 SRCS    := wiser_amd/csrc/writer.cc wiser_amd/csrc/index.cc wiser_amd/csrc/engine.cc \
-           wiser_amd/csrc/server.cc wiser_amd/csrc/kernels.hip
+           wiser_amd/csrc/server.cc wiser_amd/csrc/docstore.cc wiser_amd/csrc/snippet.cc \
+           wiser_amd/csrc/kernels.hip
 HDRS    := $(wildcard wiser_amd/csrc/*.h) include/wiser_hip.h
 OBJDIR  := wiser_amd/_lib/obj
 OBJS    := $(patsubst wiser_amd/csrc/%,$(OBJDIR)/%.o,$(SRCS))
@@ -29,23 +30,23 @@ $(OBJDIR)/%.o: wiser_amd/csrc/% $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread -l:liblz4.so.1
 
 $(ORACLE): oracle/oracle.cc oracle/oracle.h
 	@mkdir -p oracle/_build
-	$(CXX) $(ORAFLAGS) -o $@ oracle/oracle.cc -lpthread
+	$(CXX) $(ORAFLAGS) -o $@ oracle/oracle.cc -lpthread -l:liblz4.so.1
 
 # diagnostics only: segment-kernel section timers (scripts/diag_types.py --prof)
 PROFLIB := wiser_amd/_lib/prof/libwiser_hip.so
 prof: $(PROFLIB)
 $(PROFLIB): $(SRCS) $(HDRS)
 	@mkdir -p wiser_amd/_lib/prof
-	$(HIPCC) $(HIPFLAGS) -DWSR_PROFILE -shared -o $@ $(SRCS) -lpthread
+	$(HIPCC) $(HIPFLAGS) -DWSR_PROFILE -shared -o $@ $(SRCS) -lpthread -l:liblz4.so.1
 
 # tuning variants (diagnostics only): make variant V=name F="-DFLAG=..."
 variant: $(SRCS) $(HDRS)
 	@mkdir -p wiser_amd/_lib/var_$(V)
-	$(HIPCC) $(HIPFLAGS) $(F) -shared -o wiser_amd/_lib/var_$(V)/libwiser_hip.so $(SRCS) -lpthread
+	$(HIPCC) $(HIPFLAGS) $(F) -shared -o wiser_amd/_lib/var_$(V)/libwiser_hip.so $(SRCS) -lpthread -l:liblz4.so.1
 
 clean:
 	rm -rf wiser_amd/_lib oracle/_build

@@ -20,6 +20,9 @@
  *                               serving loop (grpc_server_impl.h:382-389) or a bench
  *                               (engine_bench.cc:255-279) can keep query batches
  *                               resident in HBM and overlap them
+ *   wsr_snippet / wsr_docs_* .. VacuumEngine::GenerateSnippet (vacuum_engine.h:286-296),
+ *                               ChunkedDocStoreReader (doc_store.h:365-455),
+ *                               SimpleHighlighter (highlighter.h:297-456); host stage
  *   wsr_build_* / wsr_gen_* ... index writer FlashEngineDumper::{LoadLocalDocuments,Dump}
  *                               (flash_engine_dumper.h:674-744) and the query generator
  *                               tools/gen_synthetic_log.py:191-214 (host only, no GPU)
@@ -78,6 +81,33 @@ typedef struct wsr_hit {
   int32_t pad;
   double score;       /* f64 BM25, bit-identical to the reference engine */
 } wsr_hit;
+
+/* ---- snippets (SearchQuery::return_snippets) ---------------------------
+ * The snippet of result entry `doc_id` of query q: VacuumEngine::GenerateSnippet
+ * (vacuum_engine.h:243-253,286-296) over ResultDocEntry::OffsetsForHighliting
+ * (query_processing.h:446-492) and SimpleHighlighter::highlightOffsetsEnums
+ * (highlighter.h:303-441).  A host stage after the GPU top-k, as in the
+ * reference: the doc's offset (and, for a phrase, position) bags are read from
+ * the mapped index, the text from the doc store (my.fdx / my.fdt,
+ * ChunkedDocStoreReader, doc_store.h:365-455; WSR_E_INVALID if the index has
+ * none).  Writes min(len, cap) bytes to out (no terminator) and the full
+ * length to *len. */
+int wsr_snippet(wsr_handle* h, const wsr_query* q, int32_t doc_id, int32_t n_passages,
+                char* out, int32_t cap, int32_t* len);
+/* ChunkedDocStoreReader::Get: the doc's body text */
+int wsr_doc_get(wsr_handle* h, int32_t doc_id, char* out, int32_t cap, int32_t* len);
+/* The same host stage without a device: index dictionary + doc store only. */
+typedef struct wsr_docs wsr_docs;
+int wsr_docs_open(const char* dir, wsr_docs** out);
+void wsr_docs_close(wsr_docs* d);
+int wsr_docs_lookup(wsr_docs* d, const char* term, int32_t* list_id, int32_t* doc_freq);
+int wsr_docs_snippet(wsr_docs* d, const wsr_query* q, int32_t doc_id, int32_t n_passages, char* out,
+                     int32_t cap, int32_t* len);
+int wsr_docs_get(wsr_docs* d, int32_t doc_id, char* out, int32_t cap, int32_t* len);
+/* SimpleHighlighter::highlightOffsetsEnums over explicit offsets: term i has
+ * counts[i] (start, end) pairs, consecutive in pairs[] (tests_2.cc:15-90). */
+int wsr_highlight(const int32_t* pairs, const int32_t* counts, int32_t n_terms, int32_t n_passages,
+                  const char* text, char* out, int32_t cap, int32_t* len);
 
 /* Per-batch counters of the last run (for the roofline / profiles). */
 typedef struct wsr_batch_stats {

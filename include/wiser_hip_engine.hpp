@@ -26,7 +26,7 @@ struct SearchQuery {  // types.h:205-256
   SearchQuery(const TermList& t, bool snippets) : terms(t), return_snippets(snippets) {}
   TermList terms;
   int n_results = 5;
-  bool return_snippets = false;  // snippets are out of scope: entries carry an empty snippet
+  bool return_snippets = false;  // entries get snippets (host stage, wsr_snippet)
   int n_snippet_passages = 3;
   bool is_phrase = false;        // >= 2 terms: consecutive positions required (WSR_QUERY_PHRASE)
 };
@@ -79,6 +79,19 @@ class VacuumHipEngine {
 
   SearchResult Search(const SearchQuery& q) { return SearchBatch({q})[0]; }
 
+  // VacuumEngine::GenerateSnippet (vacuum_engine.h:286-296) for a result entry
+  std::string Snippet(const wsr_query& q, int doc_id, int n_passages) const {
+    std::string s(4096, '\0');
+    int32_t n = 0;
+    check(wsr_snippet(h_, &q, doc_id, n_passages, &s[0], static_cast<int32_t>(s.size()), &n));
+    if (n > static_cast<int32_t>(s.size())) {
+      s.assign(n, '\0');
+      check(wsr_snippet(h_, &q, doc_id, n_passages, &s[0], n, &n));
+    }
+    s.resize(n);
+    return s;
+  }
+
   std::vector<SearchResult> SearchBatch(const std::vector<SearchQuery>& qs) {
     std::vector<wsr_query> in(qs.size());
     std::vector<std::vector<int>> freqs(qs.size());
@@ -116,6 +129,8 @@ class VacuumHipEngine {
         SearchResultEntry e;
         e.doc_id = hits[i * stride + j].doc_id;
         e.doc_score = hits[i * stride + j].score;
+        if (qs[i].return_snippets)   // vacuum_engine.h:248-252
+          e.snippet = Snippet(in[i], e.doc_id, qs[i].n_snippet_passages);
         out[i].entries.push_back(e);
       }
     }

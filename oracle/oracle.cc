@@ -12,12 +12,14 @@
 #include <cstring>
 #include <fcntl.h>
 #include <fstream>
+#include <iterator>
 #include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <queue>
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
@@ -157,9 +159,15 @@ struct VIntsIter {
   void skip_to(int i) { while (index() < i) pop(); }
 };
 
-// SkipList::Load (flash_containers.h:354-391); the docid / tf / position columns
-// (the offset columns only feed snippets).
-struct SkipEntry { uint32_t prev_doc; uint64_t doc_off, tf_off, pos_off; uint32_t pos_idx; };
+// SkipList::Load (flash_containers.h:354-391): docid / tf / position / offset
+// columns (the offset columns feed snippets, vacuum_engine.h:248-252).
+struct SkipEntry {
+  uint32_t prev_doc;
+  uint64_t doc_off, tf_off, pos_off;
+  uint32_t pos_idx;
+  uint64_t off_off;
+  uint32_t off_idx;
+};
 std::vector<SkipEntry> load_skip_list(const uint8_t* buf) {
   if (buf[0] != kSkipMagic) throw std::runtime_error("skip list magic");
   uint64_t n;
@@ -168,14 +176,15 @@ std::vector<SkipEntry> load_skip_list(const uint8_t* buf) {
   std::vector<SkipEntry> rows;
   rows.reserve(n);
   uint32_t pd = 0;
-  uint64_t pdo = 0, pto = 0, ppo = 0;
+  uint64_t pdo = 0, pto = 0, ppo = 0, poo = 0;
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t f[7];
     for (int k = 0; k < 7; ++k) p += varint_decode(p, &f[k]);
     uint32_t prev = static_cast<uint32_t>(f[0] + pd);
-    uint64_t dof = f[1] + pdo, tof = f[2] + pto, pof = f[3] + ppo;
-    rows.push_back(SkipEntry{prev, dof, tof, pof, static_cast<uint32_t>(f[4])});
-    pd = prev; pdo = dof; pto = tof; ppo = pof;
+    uint64_t dof = f[1] + pdo, tof = f[2] + pto, pof = f[3] + ppo, oof = f[5] + poo;
+    rows.push_back(SkipEntry{prev, dof, tof, pof, static_cast<uint32_t>(f[4]), oof,
+                             static_cast<uint32_t>(f[6])});
+    pd = prev; pdo = dof; pto = tof; ppo = pof; poo = oof;
   }
   return rows;
 }
@@ -440,10 +449,14 @@ class CozyIter {
 // PositionPostingBagIterator (flash_iterators.h:458-634): the positions of one
 // posting ("bag", tf entries, delta coded from 0 inside the bag).  Bags are
 // found from the skip row of their 128-posting interval plus the tfs before.
+// offsets = true: OffsetPostingBagIterator (:667-704) -- 2 x tf entries per bag
+// (start, end pairs), the skip rows' offset columns -- popped as
+// LazyBoundedOffsetPairIterator::SinglePop (:748-760), whose running value also
+// starts from 0 at the bag.
 class PosBagIter {
  public:
-  void reset(const uint8_t* file, const std::vector<SkipEntry>* sl) {
-    cozy_.reset(file); sl_ = sl; tf_.reset(file, sl); cur_bag_ = 0;
+  void reset(const uint8_t* file, const std::vector<SkipEntry>* sl, bool offsets = false) {
+    cozy_.reset(file); sl_ = sl; tf_.reset(file, sl); cur_bag_ = 0; mult_ = offsets ? 2 : 1;
   }
   void skip_to(int bag) {  // SkipTo (:570-591)
     if (cozy_.type() == 0 || bag / kPack > cur_bag_ / kPack) {
@@ -453,7 +466,7 @@ class PosBagIter {
     }
     cur_bag_ = bag;
     prev_ = 0;
-    tf_cur_ = static_cast<int>(tf_.at(bag));
+    tf_cur_ = static_cast<int>(tf_.at(bag)) * mult_;
     n_popped_ = 0;
     n_adv_ = 0;
   }
@@ -469,21 +482,22 @@ class PosBagIter {
  private:
   int entries_between(int a, int b) {  // NumCozyEntriesBetween (:619-628)
     int n = 0;
-    for (int i = a; i < b; ++i) n += static_cast<int>(tf_.at(i));
+    for (int i = a; i < b; ++i) n += static_cast<int>(tf_.at(i)) * mult_;
     return n;
   }
   void jump(int bag) {  // JumpToPostingBag / FindSkipInterval / GoToSkipPostingBag (:504-536)
     int i = cur_bag_ / kPack;
     while (i + 1 < static_cast<int>(sl_->size()) && (i + 1) * kPack <= bag) ++i;
     const SkipEntry& e = (*sl_)[i];
-    cozy_.go(e.pos_off, static_cast<int>(e.pos_idx));
+    if (mult_ == 2) cozy_.go(e.off_off, static_cast<int>(e.off_idx));
+    else cozy_.go(e.pos_off, static_cast<int>(e.pos_idx));
     cur_bag_ = i * kPack;
     cozy_.advance_by(entries_between(i * kPack, bag));
   }
   CozyIter cozy_;
   const std::vector<SkipEntry>* sl_ = nullptr;
   TfIter tf_;
-  int cur_bag_ = 0, n_popped_ = 0, n_adv_ = 0, tf_cur_ = 0;
+  int cur_bag_ = 0, n_popped_ = 0, n_adv_ = 0, tf_cur_ = 0, mult_ = 1;
   uint32_t prev_ = 0;
 };
 
@@ -491,30 +505,37 @@ class PosBagIter {
 // (IsEnd / Pop); returns NumOfMatches and, when `table` is given, the matched
 // positions per term (PositionInfoTable2 rows).
 template <class PosIt>
-int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* table) {
+int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* table,
+                   std::vector<std::vector<int>>* apr = nullptr) {
   const int n = static_cast<int>(its.size());
   int matches = 0;
-  auto append = [&](int row, int pos) { if (table) (*table)[row].push_back(pos); };
+  // AppendPositionCol / pos_table_.Append: PositionInfo{pos, term_appearance}
+  auto append = [&](int row, int pos, int ap) {
+    if (table) (*table)[row].push_back(pos);
+    if (apr) (*apr)[row].push_back(ap);
+  };
   if (table) table->assign(n, {});
+  if (apr) apr->assign(n, {});
   if (n == 2) {  // ProcessTwoTerm (:264-310)
     PosIt* it0 = its[0];
     PosIt* it1 = its[1];
     int pos0 = -100, pos1 = -200;
+    int apr0 = -1, apr1 = -1;
     bool tried_pop_end = false;
     while (!tried_pop_end) {
       if (pos0 < pos1) {
-        if (!it0->is_end()) pos0 = static_cast<int>(it0->pop());
+        if (!it0->is_end()) { pos0 = static_cast<int>(it0->pop()); ++apr0; }
         else tried_pop_end = true;
       } else if (pos0 > pos1) {
-        if (!it1->is_end()) pos1 = static_cast<int>(it1->pop()) - 1;
+        if (!it1->is_end()) { pos1 = static_cast<int>(it1->pop()) - 1; ++apr1; }
         else tried_pop_end = true;
       } else {
-        append(0, pos0);
-        append(1, pos1 + 1);
+        append(0, pos0, apr0);
+        append(1, pos1 + 1, apr1);
         ++matches;
-        if (!it0->is_end()) pos0 = static_cast<int>(it0->pop());
+        if (!it0->is_end()) { pos0 = static_cast<int>(it0->pop()); ++apr0; }
         else tried_pop_end = true;
-        if (!it1->is_end()) pos1 = static_cast<int>(it1->pop()) - 1;
+        if (!it1->is_end()) { pos1 = static_cast<int>(it1->pop()) - 1; ++apr1; }
         else tried_pop_end = true;
       }
     }
@@ -522,14 +543,15 @@ int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* tabl
   }
   // ProcessGeneral (:312-336) with InitializeLastPopped / FindMaxAdjustedLastPopped /
   // MovePoppedBeyond / IsPoppedMatch (:180-252); positions are int (Position)
-  std::vector<int> last(n);
+  std::vector<int> last(n), ap(n, 0);
   for (int i = 0; i < n; ++i) {
     if (its[i]->is_end()) return 0;
     last[i] = static_cast<int>(its[i]->pop());
+    ap[i] = 0;
   }
   auto move_beyond = [&](int mx) {
     for (int i = 0; i < n; ++i) {
-      while (!its[i]->is_end() && last[i] - i < mx) last[i] = static_cast<int>(its[i]->pop());
+      while (!its[i]->is_end() && last[i] - i < mx) { last[i] = static_cast<int>(its[i]->pop()); ++ap[i]; }
       if (its[i]->is_end() && last[i] - i < mx) return false;
     }
     return true;
@@ -541,7 +563,7 @@ int phrase_process(std::vector<PosIt*>& its, std::vector<std::vector<int>>* tabl
     bool match = true;
     for (int i = 0; i < n; ++i) match = match && last[i] - i == mx;
     if (match) {
-      for (int i = 0; i < n; ++i) append(i, last[i]);
+      for (int i = 0; i < n; ++i) append(i, last[i], ap[i]);
       ++matches;
       if (!move_beyond(mx + 1)) break;
     }
@@ -573,6 +595,7 @@ class VacuumIter {
       bparams_.set(static_cast<int>(hdr_->expected_entries), static_cast<double>(hdr_->ratio));
     }
     skip_ = std::make_shared<std::vector<SkipEntry>>(load_skip_list(buf + 1 + l + 8));
+    file_ = file;
     doc_.reset(file, skip_.get(), n_);
     tf_.reset(file, skip_.get());
     pos_ = std::make_shared<PosBagIter>();
@@ -586,6 +609,22 @@ class VacuumIter {
   void skip_forward(uint32_t d) { doc_.skip_forward(d); }
   // AssignPositionBegin (:1002-1005)
   PosBagIter* position_begin() { pos_->skip_to(doc_.posting_index()); return pos_.get(); }
+  int posting_index() const { return doc_.posting_index(); }
+  // OffsetPairsBegin (:1007-1012) -> LazyBoundedOffsetPairIterator drained by
+  // ResultDocEntry::ExpandOffsets (query_processing.h:454-466): the (start, end)
+  // pairs of posting `posting`
+  std::vector<std::pair<int, int>> offset_pairs(int posting) const {
+    PosBagIter it;
+    it.reset(file_, skip_.get(), true);
+    it.skip_to(posting);
+    std::vector<std::pair<int, int>> v;
+    while (!it.is_end()) {
+      const int a = static_cast<int>(it.pop());
+      const int b = static_cast<int>(it.pop());
+      v.emplace_back(a, b);
+    }
+    return v;
+  }
   const std::string& term() const { return *term_; }
   // HasPriorTerm / HasNextTerm / HasTerm (:994-1000,1039-1058): 0 = not present,
   // 1 = may be present (always, without bloom filters)
@@ -606,6 +645,7 @@ class VacuumIter {
   std::shared_ptr<std::vector<BloomColumn>> blm_;
   BloomParams bparams_;
   int n_ = 0;
+  const uint8_t* file_ = nullptr;
   std::shared_ptr<std::vector<SkipEntry>> skip_;
   DocIdIter doc_;
   TfIter tf_;
@@ -623,6 +663,7 @@ class MemIter {
   int term_freq() const { return static_cast<int>((*t_)[i_]); }
   void advance() { ++i_; }
   void skip_forward(uint32_t v) { while (i_ < d_->size() && (*d_)[i_] < v) ++i_; }
+  int posting_index() const { return static_cast<int>(i_); }
   PosBagIter* position_begin() { throw std::runtime_error("phrase queries need a Vacuum index"); }
   const std::string& term() const { throw std::runtime_error("phrase queries need a Vacuum index"); }
   int has_prior_term(const std::string&) { return 1; }
@@ -638,7 +679,17 @@ class MemIter {
 // std::priority_queue<unique_ptr<ResultDocEntry>, vector, EntryGreater>
 // (query_processing.h:510-524) with libstdc++'s __push_heap / __adjust_heap /
 // __pop_heap restated; comp(a, b) = a.score > b.score.
-struct Entry { int doc; double score; };
+// With snippets on, an entry also keeps what ResultDocEntry keeps for them
+// (query_processing.h:386-445): each list's posting index at the doc (its
+// LazyBoundedOffsetPairIterator), the phrase match table's term appearances
+// (PositionInfoTable2, RankDocForPhrase) and is_phrase.
+struct Entry {
+  int doc;
+  double score;
+  std::vector<int> post;
+  std::vector<std::vector<int>> apr;
+  bool phrase = false;
+};
 class MinHeap {
  public:
   size_t size() const { return v_.size(); }
@@ -708,6 +759,7 @@ class Processor {
     return sort_heap();
   }
   int64_t phrase_checks() const { return n_phrase_checks_; }
+  void capture(bool on) { capture_ = on; }
 
  private:
   // CalcDocScoreLossy (scoring.h:124-145), terms in query order
@@ -722,11 +774,20 @@ class Processor {
     }
     return s;
   }
-  // RankDoc (query_processing.h:588-603)
-  void rank(int doc) {
+  // RankDoc (query_processing.h:588-603) / RankDocForPhrase (:897-912) and
+  // InsertToHeap (:605-616, :914-925)
+  void rank(int doc, std::vector<std::vector<int>>* apr = nullptr) {
     const double s = score(doc);
-    if (heap_.size() < static_cast<size_t>(k_)) heap_.push(Entry{doc, s});
-    else if (s > heap_.top().score) { heap_.pop(); heap_.push(Entry{doc, s}); }
+    if (heap_.size() < static_cast<size_t>(k_)) insert(doc, s, apr);
+    else if (s > heap_.top().score) { heap_.pop(); insert(doc, s, apr); }
+  }
+  void insert(int doc, double s, std::vector<std::vector<int>>* apr) {
+    Entry e{doc, s};
+    if (capture_) {
+      for (auto& it : its_) e.post.push_back(it.posting_index());
+      if (apr) { e.apr = *apr; e.phrase = true; }
+    }
+    heap_.push(e);
   }
   // HandleTheFoundDoc (:886-895): a phrase query ranks the doc only when the
   // positions hold the phrase (FindPhrase :854-867; RankDocForPhrase scores and
@@ -752,7 +813,8 @@ class Processor {
       if (!possible()) return;   // FindPhrase returns 0 matches
       std::vector<PosBagIter*> ps;
       for (auto& it : its_) ps.push_back(it.position_begin());
-      if (phrase_process(ps, nullptr) > 0) rank(doc);
+      std::vector<std::vector<int>> apr;
+      if (phrase_process(ps, nullptr, capture_ ? &apr : nullptr) > 0) rank(doc, capture_ ? &apr : nullptr);
     } else {
       rank(doc);
     }
@@ -807,9 +869,240 @@ class Processor {
   bool phrase_;
   int bloom_factor_;
   int64_t n_phrase_checks_ = 0;
+  bool capture_ = false;
   std::vector<double> idf_;
   MinHeap heap_;
 };
+
+// ----------------------------------------------------------- snippets ----
+// LZ4 is the reference's own third-party codec for the doc store
+// (doc_store.h:15,26-128); the system liblz4 1.9.3 is linked.
+extern "C" int LZ4_decompress_safe(const char* src, char* dst, int compressed_size, int dst_capacity);
+
+// ChunkedDocStoreReader (doc_store.h:365-455) with DecompressText /
+// DecodeHeader (:50-128): my.fdx = varint n_doc_ids | varint buffer size |
+// n x int64 (offset << 1 | aligned); my.fdt chunks = 0x33 | varint n_chunks |
+// varint chunk sizes | LZ4 blocks.
+class DocStoreReader {
+ public:
+  ~DocStoreReader() { if (fdt_) munmap(fdt_, fdt_len_); }
+  void load(const std::string& dir) {
+    std::ifstream f(dir + "/my.fdx", std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open my.fdx");
+    std::string raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(raw.data());
+    uint64_t n, bs;
+    size_t at = varint_decode(a, &n);
+    at += varint_decode(a + at, &bs);
+    n_ = static_cast<int>(n);
+    buf_size_ = static_cast<int>(bs);
+    for (int i = 0; i < n_; ++i) {
+      int64_t v;
+      std::memcpy(&v, a + at, 8);
+      at += 8;
+      offsets_.push_back(v);
+    }
+    int fd = ::open((dir + "/my.fdt").c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open my.fdt");
+    struct stat sb;
+    fstat(fd, &sb);
+    fdt_len_ = sb.st_size;
+    if (fdt_len_) {
+      void* p = mmap(nullptr, fdt_len_, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (p == MAP_FAILED) { ::close(fd); throw std::runtime_error("mmap my.fdt"); }
+      fdt_ = static_cast<uint8_t*>(p);
+    }
+    ::close(fd);
+  }
+  std::string get(int id) const {  // Get (:426-443)
+    if (id < 0 || id >= n_) throw std::runtime_error("doc id outside the doc store");
+    int64_t start = offsets_[id];
+    if (start & 1) { start >>= 1; start = start + 4096 - start % 4096; }
+    else start >>= 1;
+    const uint8_t* c = fdt_ + start;
+    if (c[0] != 0x33) throw std::runtime_error("Compressed doc has the wrong magic number");
+    VIntsHeaderless hdr{c + 1};
+    const uint64_t nch = hdr.pop();
+    std::vector<uint64_t> sizes;
+    for (uint64_t i = 0; i < nch; ++i) sizes.push_back(hdr.pop());
+    const char* chunk = reinterpret_cast<const char*>(c + 1 + hdr.off);
+    std::vector<char> buf(buf_size_);
+    std::string text;
+    for (uint64_t i = 0; i < nch; ++i) {
+      const int got = LZ4_decompress_safe(chunk, buf.data(), static_cast<int>(sizes[i]), buf_size_);
+      if (got < 0) throw std::runtime_error("Failed to decompresse.");
+      chunk += sizes[i];
+      text.append(buf.data(), got);
+    }
+    return text;
+  }
+
+ private:
+  struct VIntsHeaderless {   // VarintIteratorUnbounded
+    const uint8_t* p;
+    size_t off = 0;
+    uint64_t pop() { uint64_t v; off += varint_decode(p + off, &v); return v; }
+  };
+  int n_ = 0, buf_size_ = 0;
+  std::vector<int64_t> offsets_;
+  uint8_t* fdt_ = nullptr;
+  size_t fdt_len_ = 0;
+};
+
+// SimpleHighlighter::highlightOffsetsEnums (highlighter.h:297-456) with
+// SentenceBreakIteratorNew (:118-197), Passage (:79-116), Offset_Iterator
+// (:46-73).  float arithmetic as the reference (pivot 87, k1 1.2, b 0.75).
+using OffPair = std::pair<int, int>;
+struct HlOffsetIt {
+  const std::vector<OffPair>* offs;
+  size_t i = 0;
+  int start, end, weight = 1;
+  explicit HlOffsetIt(const std::vector<OffPair>* o) : offs(o) {
+    start = (*o)[0].first;   // (the reference dereferences begin() unchecked)
+    end = (*o)[0].second;
+  }
+  void next() {
+    ++i;
+    if (i == offs->size()) { start = end = -1; return; }
+    start = (*offs)[i].first;
+    end = (*offs)[i].second;
+  }
+};
+struct HlPassage {
+  int start = -1, end = -1;
+  float score = 0;
+  std::vector<OffPair> matches;
+  void reset() { start = end = -1; score = 0; matches.clear(); }
+  std::string to_string(const std::string& doc) {   // :97-115
+    std::string res = doc.substr(start, end - start + 1) + "\n";
+    std::sort(matches.begin(), matches.end(),
+              [](const OffPair& a, const OffPair& b) { return a.first > b.first; });
+    for (auto& m : matches) {
+      res.insert(m.second - start + 1, "<\\b>");
+      res.insert(std::max(0, m.first - start), "<b>");
+    }
+    return res;
+  }
+};
+struct HlSentences {   // SentenceBreakIteratorNew::next(int offset) (:176-192)
+  const std::string* text;
+  int start = -1, end = -1, last;
+  explicit HlSentences(const std::string& t) : text(&t), last(static_cast<int>(t.size()) - 1) {}
+  int next(int offset) {
+    if (offset > last) return 0;
+    for (end = offset; end < last; ++end)
+      if ((*text)[end] == '.') break;
+    for (start = std::max(0, offset - 1); start > 0; --start) {
+      if ((*text)[start] == '.') { ++start; break; }
+    }
+    return 1;
+  }
+};
+float hl_passage_norm(int start) {
+  const float pivot = 87;
+  return 1 + 1 / static_cast<float>(std::log(static_cast<float>(pivot + start)));
+}
+float hl_tf_norm(int freq, int len) {
+  const float pivot = 87, k1 = 1.2f, b = 0.75f;
+  const float norm = k1 * ((1 - b) + b * (len / pivot));
+  return freq / (freq + norm);
+}
+std::string highlight(const std::vector<std::vector<OffPair>>& table, int max_passages,
+                      const std::string& doc) {
+  if (table.empty()) return "";
+  HlSentences sent(doc);
+  auto cmp_off = [](const HlOffsetIt& a, const HlOffsetIt& b) { return a.start > b.start; };
+  std::priority_queue<HlOffsetIt, std::vector<HlOffsetIt>, decltype(cmp_off)> offq(cmp_off);
+  for (auto& row : table) offq.push(HlOffsetIt(&row));
+  auto cmp_pass = [](HlPassage* const& a, HlPassage* const& b) { return a->score > b->score; };
+  std::priority_queue<HlPassage*, std::vector<HlPassage*>, decltype(cmp_pass)> pq(cmp_pass);
+  std::vector<std::unique_ptr<HlPassage>> pool;
+  auto fresh = [&]() { pool.emplace_back(new HlPassage()); return pool.back().get(); };
+  float min_score = -1;
+  HlPassage* cur = fresh();
+  while (!offq.empty()) {
+    HlOffsetIt it = offq.top();
+    offq.pop();
+    int s = it.start;
+    if (s == -1) continue;
+    int e = it.end;
+    if (e > cur->end) {
+      if (cur->start >= 0) {
+        cur->score = cur->score * hl_passage_norm(cur->start);
+        if (pq.size() == static_cast<size_t>(max_passages) && cur->score <= min_score) {
+          cur->reset();
+        } else {
+          pq.push(cur);
+          if (pq.size() > static_cast<size_t>(max_passages)) {
+            cur = pq.top();
+            pq.pop();
+            cur->reset();
+          } else {
+            cur = fresh();
+          }
+          min_score = pq.top()->score;
+        }
+      }
+      if (sent.next(e) <= 0) break;
+      cur->start = sent.start;
+      cur->end = sent.end;
+    }
+    int tf = 0;
+    for (;;) {
+      ++tf;
+      cur->matches.emplace_back(s, e);
+      it.next();
+      if (it.start == -1) break;
+      s = it.start;
+      e = it.end;
+      if (e > cur->end) { offq.push(it); break; }
+    }
+    cur->score = cur->score + it.weight * hl_tf_norm(tf, cur->end - cur->start + 1);
+  }
+  cur->score = cur->score * hl_passage_norm(cur->start);
+  if (cur->score > 0) {
+    if (pq.size() < static_cast<size_t>(max_passages)) {
+      pq.push(cur);
+    } else if (cur->score > min_score) {
+      pq.pop();
+      pq.push(cur);
+    }
+  }
+  std::vector<HlPassage*> out;
+  while (!pq.empty()) { out.push_back(pq.top()); pq.pop(); }
+  std::sort(out.begin(), out.end(), [](HlPassage* const& a, HlPassage* const& b) { return a->start < b->start; });
+  std::string res;
+  for (auto* p : out) res += p->to_string(doc);
+  return res;
+}
+
+// ResultDocEntry::OffsetsForHighliting (query_processing.h:446-492) then
+// VacuumEngine::GenerateSnippet (vacuum_engine.h:286-296)
+std::string entry_snippet(const std::vector<VacuumIter>& its, const Entry& e, const DocStoreReader& ds,
+                          int n_passages) {
+  std::vector<std::vector<OffPair>> table;
+  if (e.phrase) {   // FilterOffsetByPosition: the pair of each matched appearance
+    for (size_t r = 0; r < e.apr.size() && !e.apr[r].empty(); ++r) {
+      const auto pairs = its[r].offset_pairs(e.post[r]);
+      std::vector<OffPair> row;
+      int cur = -1;
+      OffPair pr{0, 0};
+      for (int ap : e.apr[r]) {
+        while (cur < ap) {
+          if (cur + 1 >= static_cast<int>(pairs.size()))
+            throw std::runtime_error("offset_iter does not suppose to reach the end.");
+          pr = pairs[cur + 1];
+          ++cur;
+        }
+        row.push_back(pr);
+      }
+      table.push_back(row);
+    }
+  } else {          // ExpandOffsets
+    for (size_t i = 0; i < its.size(); ++i) table.push_back(its[i].offset_pairs(e.post[i]));
+  }
+  return highlight(table, n_passages, ds.get(e.doc));
+}
 
 int emit(const std::vector<Entry>& r, int32_t* docs, double* scores) {
   for (size_t i = 0; i < r.size(); ++i) { docs[i] = r[i].doc; scores[i] = r[i].score; }
@@ -850,6 +1143,12 @@ struct orc_vacuum {
   std::vector<uint8_t> lens;                      // DocLengthCharStore
   int n_docs = 0;
   Bm25 sim;
+  std::string dir;
+  std::unique_ptr<DocStoreReader> docs;   // loaded on first use (snippets)
+  const DocStoreReader& doc_store() {
+    if (!docs) { docs.reset(new DocStoreReader()); docs->load(dir); }
+    return *docs;
+  }
 };
 
 struct orc_qqmem {
@@ -910,6 +1209,7 @@ orc_vacuum* orc_vacuum_open(const char* dir) {
   std::unique_ptr<orc_vacuum> h(new orc_vacuum());
   try {
     const std::string d(dir);
+    h->dir = d;
     {  // DocLengthCharStore::Deserialize (doc_length_store.h:163-190)
       std::ifstream f(d + "/my.doc_length", std::ios::binary);
       if (!f) throw std::runtime_error("cannot open my.doc_length");
@@ -1030,6 +1330,90 @@ int orc_vacuum_search_phrase(orc_vacuum* h, const char* const* terms, int n_term
     if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
     Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k, is_phrase != 0, h->bloom_factor);
     return emit(p.run(), docs, scores);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// VacuumEngine::Search with SearchQuery::return_snippets (vacuum_engine.h:243-253)
+int orc_vacuum_search_snippets(orc_vacuum* h, const char* const* terms, int n_terms, int k,
+                               int is_phrase, int n_passages, int32_t* docs, double* scores,
+                               char* buf, int64_t cap, int64_t* snip_end) {
+  if (k == 0) return 0;
+  try {
+    std::vector<VacuumIter> its;
+    for (int i = 0; i < n_terms; ++i) {
+      auto f = h->tip.find(terms[i]);
+      if (f != h->tip.end()) its.emplace_back(h->map, f->second, &h->hdr, &f->first);
+    }
+    if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
+    Processor<VacuumIter> p(h->sim, &its, h->lens, h->n_docs, k, is_phrase != 0, h->bloom_factor);
+    p.capture(true);
+    const std::vector<Entry> r = p.run();
+    const DocStoreReader& ds = h->doc_store();
+    int64_t at = 0;
+    for (size_t i = 0; i < r.size(); ++i) {
+      docs[i] = r[i].doc;
+      scores[i] = r[i].score;
+      const std::string sn = entry_snippet(its, r[i], ds, n_passages);
+      if (at + static_cast<int64_t>(sn.size()) > cap) throw std::runtime_error("snippet buffer too small");
+      std::memcpy(buf + at, sn.data(), sn.size());
+      at += static_cast<int64_t>(sn.size());
+      snip_end[i] = at;
+    }
+    return static_cast<int>(r.size());
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// SimpleHighlighter::highlightOffsetsEnums on explicit offset pairs (tests_2.cc:15-90):
+// pairs holds sum(counts) (start, end) pairs, term by term.  Returns the length.
+int orc_highlight(const int32_t* pairs, const int32_t* counts, int n_terms, int n_passages,
+                  const char* doc, char* out, int cap) {
+  try {
+    std::vector<std::vector<OffPair>> table(n_terms);
+    for (int t = 0; t < n_terms; ++t) {
+      for (int j = 0; j < counts[t]; ++j) table[t].emplace_back(pairs[0], pairs[1]), pairs += 2;
+    }
+    const std::string s = highlight(table, n_passages, doc);
+    if (static_cast<int>(s.size()) > cap) throw std::runtime_error("highlight buffer too small");
+    std::memcpy(out, s.data(), s.size());
+    return static_cast<int>(s.size());
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// ChunkedDocStoreReader::Get (doc_store.h:426-443).  Returns the length.
+int64_t orc_docstore_get(orc_vacuum* h, int doc, char* out, int64_t cap) {
+  try {
+    const std::string s = h->doc_store().get(doc);
+    if (static_cast<int64_t>(s.size()) > cap) throw std::runtime_error("doc buffer too small");
+    std::memcpy(out, s.data(), s.size());
+    return static_cast<int64_t>(s.size());
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// The (start, end) offset pairs of posting `posting` of a term (OffsetPostingBagIterator).
+int orc_vacuum_offsets(orc_vacuum* h, const char* term, int posting, int32_t* out, int cap) {
+  auto f = h->tip.find(term);
+  if (f == h->tip.end()) return 0;
+  try {
+    VacuumIter it(h->map, f->second);
+    if (posting < 0 || posting >= it.size()) return 0;
+    const auto v = it.offset_pairs(posting);
+    for (size_t i = 0; i < v.size() && static_cast<int>(i) < cap; ++i) {
+      out[2 * i] = v[i].first;
+      out[2 * i + 1] = v[i].second;
+    }
+    return static_cast<int>(v.size());
   } catch (const std::exception& e) {
     g_err = e.what();
     return -1;

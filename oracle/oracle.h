@@ -68,6 +68,19 @@ int orc_vacuum_positions(orc_vacuum* h, const char* term, int posting, uint32_t*
  * matched positions per list in table[list * cap + match] */
 int orc_phrase_lists(const uint32_t* const* lists, const int* sizes, int n_lists, int32_t* table,
                      int cap);
+/* SearchQuery::return_snippets: as orc_vacuum_search_phrase, plus each entry's
+ * snippet (n_passages passages) concatenated into buf; snip_end[i] = end of
+ * entry i's snippet.  Needs the doc store (my.fdx / my.fdt). */
+int orc_vacuum_search_snippets(orc_vacuum* h, const char* const* terms, int n_terms, int k,
+                               int is_phrase, int n_passages, int32_t* docs, double* scores,
+                               char* buf, int64_t cap, int64_t* snip_end);
+/* SimpleHighlighter over explicit offsets (pairs: sum(counts) start,end pairs) */
+int orc_highlight(const int32_t* pairs, const int32_t* counts, int n_terms, int n_passages,
+                  const char* doc, char* out, int cap);
+/* ChunkedDocStoreReader::Get; returns the text length */
+int64_t orc_docstore_get(orc_vacuum* h, int doc, char* out, int64_t cap);
+/* offset pairs of one posting (OffsetPostingBagIterator); returns tf */
+int orc_vacuum_offsets(orc_vacuum* h, const char* term, int posting, int32_t* out, int cap);
 /* Many queries: queries are '\n'-separated lines of ' '-separated terms (a line
  * in double quotes is a phrase query).
  * Outputs are nq*k arrays plus n per query.  threads >= 1.  Returns nq. */

@@ -60,6 +60,12 @@ for name, res, args in [
     ("orc_vacuum_has_bloom", C.c_int, [_P]),
     ("orc_bloom_stats", None, [C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("orc_vacuum_bloom_check", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, C.c_char_p]),
+    ("orc_vacuum_search_snippets", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int,
+                                             C.c_int, _I32P, _F64P, C.c_char_p, C.c_int64,
+                                             C.POINTER(C.c_int64)]),
+    ("orc_highlight", C.c_int, [_I32P, _I32P, C.c_int, C.c_int, C.c_char_p, C.c_char_p, C.c_int]),
+    ("orc_docstore_get", C.c_int64, [_P, C.c_int, C.c_char_p, C.c_int64]),
+    ("orc_vacuum_offsets", C.c_int, [_P, C.c_char_p, C.c_int, _I32P, C.c_int]),
 ]:
     f = getattr(lib, name)
     f.restype = res
@@ -133,6 +139,45 @@ class OracleVacuum:
     def search(self, terms, k, phrase=False):
         """-> ([(doc, score)], doc_freqs); phrase = SearchQuery::is_phrase"""
         return _search(lib.orc_vacuum_search_phrase, self.h, terms, k, int(bool(phrase)))
+
+    def search_snippets(self, terms, k, n_passages=3, phrase=False):
+        """VacuumEngine::Search with return_snippets -> [(doc, score, snippet)]"""
+        if k == 0:
+            return []
+        arr = (C.c_char_p * max(len(terms), 1))(*[t.encode() for t in terms])
+        docs = (C.c_int32 * k)()
+        scores = (C.c_double * k)()
+        ends = (C.c_int64 * k)()
+        cap = 1 << 22
+        buf = C.create_string_buffer(cap)
+        n = lib.orc_vacuum_search_snippets(self.h, arr, len(terms), k, int(bool(phrase)), n_passages,
+                                           docs, scores, buf, cap, ends)
+        if n < 0:
+            raise RuntimeError(_err())
+        raw = buf.raw
+        out, at = [], 0
+        for i in range(n):
+            out.append((docs[i], scores[i], raw[at:ends[i]].decode("utf-8", errors="surrogateescape")))
+            at = ends[i]
+        return out
+
+    def document(self, doc):
+        """ChunkedDocStoreReader::Get"""
+        cap = 1 << 24
+        buf = C.create_string_buffer(cap)
+        n = lib.orc_docstore_get(self.h, doc, buf, cap)
+        if n < 0:
+            raise RuntimeError(_err())
+        return buf.raw[:n].decode("utf-8", errors="surrogateescape")
+
+    def offsets(self, term, posting):
+        """(start, end) offset pairs of one posting (OffsetPostingBagIterator)"""
+        cap = 1 << 15
+        out = (C.c_int32 * (2 * cap))()
+        n = lib.orc_vacuum_offsets(self.h, term.encode(), posting, out, cap)
+        if n < 0:
+            raise RuntimeError(_err())
+        return [(out[2 * i], out[2 * i + 1]) for i in range(min(n, cap))]
 
     def positions(self, term, posting):
         """positions of one posting (PositionPostingBagIterator)"""
@@ -218,6 +263,19 @@ def phrase_lists(lists, cap=64):
     table = (C.c_int32 * (len(lists) * cap))()
     m = lib.orc_phrase_lists(ptrs, sizes, len(lists), table, cap)
     return m, [[table[i * cap + j] for j in range(min(m, cap))] for i in range(len(lists))]
+
+
+def highlight(offsets, n_passages, text):
+    """SimpleHighlighter::highlightOffsetsEnums over explicit per-term (start, end) lists"""
+    flat = [v for term in offsets for pr in term for v in pr]
+    pairs = (C.c_int32 * max(1, len(flat)))(*flat)
+    counts = (C.c_int32 * max(1, len(offsets)))(*[len(t) for t in offsets])
+    cap = 1 << 20
+    buf = C.create_string_buffer(cap)
+    n = lib.orc_highlight(pairs, counts, len(offsets), n_passages, text.encode(), buf, cap)
+    if n < 0:
+        raise RuntimeError(_err())
+    return buf.raw[:n].decode("utf-8", errors="surrogateescape")
 
 
 def bloom_stats():

@@ -2,10 +2,10 @@
 Vacuum (WiSER) index.  The compute path is libwiser_hip.so (hand-written HIP
 for gfx950) behind the C ABI in include/wiser_hip.h; this package is the thin
 Python mirror of the reference's SearchEngineServiceNew surface."""
-from .engine import (CreateSearchEngine, ResidentBatch, SearchQuery, SearchResult,  # noqa: F401
+from .engine import (CreateSearchEngine, DocsHost, ResidentBatch, SearchQuery, SearchResult,  # noqa: F401
                      SearchResultEntry, Server, VacuumEngine, build_from_linedoc, build_synthetic,
                      gen_mixed_log, gen_phrase_log, gen_two_term_log, read_query_log, sync)
 
-__all__ = ["CreateSearchEngine", "VacuumEngine", "SearchQuery", "SearchResult",
+__all__ = ["CreateSearchEngine", "DocsHost", "VacuumEngine", "SearchQuery", "SearchResult",
            "SearchResultEntry", "ResidentBatch", "Server", "build_from_linedoc", "build_synthetic",
            "gen_mixed_log", "gen_phrase_log", "gen_two_term_log", "read_query_log", "sync"]

@@ -129,6 +129,17 @@ _sigs = {
                                     C.POINTER(C.c_int64)]),
     "wsr_gen_phrase_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                      C.POINTER(C.c_int64)]),
+    "wsr_snippet": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.c_char_p, C.c_int32,
+                              C.POINTER(C.c_int32)]),
+    "wsr_doc_get": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
+    "wsr_docs_open": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    "wsr_docs_close": (None, [_P]),
+    "wsr_docs_lookup": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "wsr_docs_snippet": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.c_char_p, C.c_int32,
+                                   C.POINTER(C.c_int32)]),
+    "wsr_docs_get": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
+    "wsr_highlight": (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                C.c_char_p, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)
@@ -140,6 +151,26 @@ def check(rc):
     if rc != WSR_OK:
         raise WiserError(rc, lib.wsr_last_error().decode(errors="replace"))
     return rc
+
+
+def text_call(fn, *args, cap: int = 4096) -> str:
+    """Call a (..., char* out, int32 cap, int32* len) entry point, growing the
+    buffer when the text is longer than it."""
+    while True:
+        buf = C.create_string_buffer(cap)
+        n = C.c_int32()
+        check(fn(*args, buf, cap, C.byref(n)))
+        if n.value <= cap:
+            return buf.raw[: n.value].decode("utf-8", errors="surrogateescape")
+        cap = n.value
+
+
+def highlight(offsets, n_passages: int, text: str) -> str:
+    """SimpleHighlighter::highlightOffsetsEnums over explicit per-term (start, end) lists."""
+    flat = [v for term in offsets for pr in term for v in pr]
+    pairs = (C.c_int32 * max(1, len(flat)))(*flat)
+    counts = (C.c_int32 * max(1, len(offsets)))(*[len(t) for t in offsets])
+    return text_call(lib.wsr_highlight, pairs, counts, len(offsets), n_passages, text.encode())
 
 
 def header_symbols(path: str = HEADER):

@@ -16,6 +16,7 @@
 #include "engine_types.h"
 #include "index.h"
 #include "kernels.h"
+#include "snippet.h"
 #include "writer.h"
 
 namespace wiser {
@@ -62,6 +63,7 @@ struct wsr_handle {
   int device = 0;
   hipStream_t stream = nullptr;
   VacuumIndex idx;
+  DocStore docs;                    // my.fdx / my.fdt when the index has them (snippets)
   IndexArgs args{};
   uint8_t* d_blob = nullptr;
   ListDev* d_lists = nullptr;
@@ -140,6 +142,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
   std::unique_ptr<wsr_handle> h(new wsr_handle());
   try {
     h->idx.open(dir);
+    h->docs.open(dir);
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());
   }
@@ -270,6 +273,107 @@ int wsr_lookup(wsr_handle* h, const char* term, int32_t* list_id, int32_t* df) {
   if (list_id) *list_id = id;
   if (df) *df = id < 0 ? 0 : static_cast<int32_t>(h->idx.df(id));
   return WSR_OK;
+}
+
+// ------------------------------------------------------------ snippets ----
+// Host stage after the top-k, as in the reference (vacuum_engine.h:243-253).
+struct wsr_docs {
+  VacuumIndex idx;
+  DocStore docs;
+};
+
+namespace {
+int copy_out(const std::string& s, char* out, int32_t cap, int32_t* len) {
+  if (len) *len = static_cast<int32_t>(s.size());
+  if (out && cap > 0) std::memcpy(out, s.data(), std::min<size_t>(s.size(), static_cast<size_t>(cap)));
+  return WSR_OK;
+}
+
+int snippet_of(const VacuumIndex& idx, const DocStore& docs, const wsr_query* q, int32_t doc,
+               int32_t n_passages, char* out, int32_t cap, int32_t* len) {
+  if (!q || !len || n_passages < 0) return fail(WSR_E_INVALID, "bad snippet arguments");
+  if (q->n_terms < 1 || q->n_terms > WSR_MAX_TERMS) return fail(WSR_E_LIMIT, "bad term count");
+  if (!docs.is_open()) return fail(WSR_E_INVALID, "the index has no doc store (my.fdx / my.fdt)");
+  for (int i = 0; i < q->n_terms; ++i)
+    if (q->list_ids[i] < 0 || q->list_ids[i] >= idx.n_lists())
+      return fail(WSR_E_INVALID, "a query term is not in the index (no result entries)");
+  try {
+    return copy_out(make_snippet(idx, docs, q->list_ids, q->n_terms, (q->flags & WSR_QUERY_PHRASE) != 0,
+                                 doc, n_passages),
+                    out, cap, len);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_INVALID, e.what());
+  }
+}
+
+int doc_text(const DocStore& docs, int32_t doc, char* out, int32_t cap, int32_t* len) {
+  if (!len) return fail(WSR_E_INVALID, "null argument");
+  try {
+    return copy_out(docs.get(doc), out, cap, len);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_INVALID, e.what());
+  }
+}
+}  // namespace
+
+int wsr_snippet(wsr_handle* h, const wsr_query* q, int32_t doc, int32_t n_passages, char* out,
+                int32_t cap, int32_t* len) {
+  if (!h) return fail(WSR_E_INVALID, "null argument");
+  return snippet_of(h->idx, h->docs, q, doc, n_passages, out, cap, len);
+}
+
+int wsr_doc_get(wsr_handle* h, int32_t doc, char* out, int32_t cap, int32_t* len) {
+  if (!h) return fail(WSR_E_INVALID, "null argument");
+  return doc_text(h->docs, doc, out, cap, len);
+}
+
+int wsr_docs_open(const char* dir, wsr_docs** out) {
+  if (!dir || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = nullptr;
+  std::unique_ptr<wsr_docs> d(new wsr_docs());
+  try {
+    d->idx.open(dir);
+    if (!d->docs.open(dir)) return fail(WSR_E_IO, std::string("no doc store in ") + dir);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  *out = d.release();
+  return WSR_OK;
+}
+
+void wsr_docs_close(wsr_docs* d) { delete d; }
+
+int wsr_docs_lookup(wsr_docs* d, const char* term, int32_t* list_id, int32_t* df) {
+  if (!d || !term) return fail(WSR_E_INVALID, "null argument");
+  const int32_t id = d->idx.find(term);
+  if (list_id) *list_id = id;
+  if (df) *df = id < 0 ? 0 : static_cast<int32_t>(d->idx.df(id));
+  return WSR_OK;
+}
+
+int wsr_docs_snippet(wsr_docs* d, const wsr_query* q, int32_t doc, int32_t n_passages, char* out,
+                     int32_t cap, int32_t* len) {
+  if (!d) return fail(WSR_E_INVALID, "null argument");
+  return snippet_of(d->idx, d->docs, q, doc, n_passages, out, cap, len);
+}
+
+int wsr_docs_get(wsr_docs* d, int32_t doc, char* out, int32_t cap, int32_t* len) {
+  if (!d) return fail(WSR_E_INVALID, "null argument");
+  return doc_text(d->docs, doc, out, cap, len);
+}
+
+int wsr_highlight(const int32_t* pairs, const int32_t* counts, int32_t n_terms, int32_t n_passages,
+                  const char* text, char* out, int32_t cap, int32_t* len) {
+  if ((!pairs && n_terms > 0) || (!counts && n_terms > 0) || !text || !len || n_terms < 0)
+    return fail(WSR_E_INVALID, "null argument");
+  try {
+    std::vector<std::vector<OffsetPair>> t(n_terms);
+    for (int32_t i = 0; i < n_terms; ++i)
+      for (int32_t j = 0; j < counts[i]; ++j, pairs += 2) t[i].emplace_back(pairs[0], pairs[1]);
+    return copy_out(highlight_offsets(t, n_passages, text), out, cap, len);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_INVALID, e.what());
+  }
 }
 
 int wsr_list_bytes(wsr_handle* h, int32_t id, uint64_t* out) {

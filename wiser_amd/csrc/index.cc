@@ -141,7 +141,7 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
   p += 1 + l;
   std::vector<SkipRow> out(n);
   // fields: d prev_doc, d docid off, d tf off, d pos off, pos idx, d off off, off idx
-  uint64_t pd = 0, pdo = 0, pto = 0, ppo = 0;
+  uint64_t pd = 0, pdo = 0, pto = 0, ppo = 0, poo = 0;
   for (uint64_t r = 0; r < n; ++r) {
     uint64_t f[7];
     for (int k = 0; k < 7; ++k) {
@@ -150,8 +150,9 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
       p += l;
     }
     pd = static_cast<uint32_t>(pd + f[0]);
-    pdo += f[1]; pto += f[2]; ppo += f[3];
-    out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto, ppo, static_cast<uint32_t>(f[4])};
+    pdo += f[1]; pto += f[2]; ppo += f[3]; poo += f[5];
+    out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto, ppo, static_cast<uint32_t>(f[4]), poo,
+                     static_cast<uint32_t>(f[6])};
   }
   return out;
 }

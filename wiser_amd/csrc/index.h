@@ -28,6 +28,8 @@ struct SkipRow {
   uint64_t tf_off;
   uint64_t pos_off;  // position blob holding the row's first bag, and the bag's
   uint32_t pos_idx;  // entry index inside that blob (flash_containers.h:312-350)
+  uint64_t off_off;  // the same for the offset box (snippets)
+  uint32_t off_idx;
 };
 
 class VacuumIndex {

@@ -34,6 +34,7 @@
 #include <unordered_set>
 
 #include "bloom.h"
+#include "docstore.h"
 #include "format.h"
 
 namespace wiser {
@@ -403,11 +404,16 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
   std::getline(in, line);  // header row
   std::map<std::string, TermPostings> index;  // sorted term order in my.tip / my.vacuum
   DocLengths lens;
+  // doc store: DocInfo::Body() = column 2 for TOKEN_ONLY, column 1 otherwise
+  // (engine_loader.h:63-65,91-93), added by FlashEngineDumper (flash_engine_dumper.h:717)
+  DocStoreWriter store;
+  store.open(out_dir);
   uint32_t doc = 0;
   while ((n_rows < 0 || doc < n_rows) && std::getline(in, line)) {
     std::vector<std::string> items = explode_strict(line, '\t');
     if (items.size() < (token_only ? 3u : 5u))
       throw std::runtime_error("linedoc row " + std::to_string(doc) + " has too few columns");
+    store.add(token_only ? items[2] : items[1]);
     if (token_only) {
       // Body = tokens = column 2; tf = token count; positions = token ordinals;
       // offsets = char span (end inclusive) of each occurrence in column 2.
@@ -466,6 +472,7 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
     }
     ++doc;
   }
+  store.close();
   VacuumFileWriter w(out_dir, bloom);
   BuildStats st;
   for (auto& kv : index) {

@@ -18,8 +18,9 @@ Behaviour kept from the reference:
   * ``is_phrase`` with two or more terms ranks only docs holding the terms at
     consecutive positions (QueryProcessor, query_processing.h:854-912); the
     engine must be loaded with ``positions=True`` (the default).
-Not built: snippets (the doc store and highlighter are out of scope; entries
-carry an empty snippet).
+Snippets (SearchQuery.return_snippets): a host stage after the GPU top-k, as
+in the reference (vacuum_engine.h:243-253): offsets from the index, text from the
+doc store (my.fdx / my.fdt), SimpleHighlighter -- wsr_snippet in the C ABI.
 """
 from __future__ import annotations
 
@@ -43,7 +44,7 @@ class SearchQuery:
 
 @dataclass
 class SearchResultEntry:
-    """types.h:259-274 (snippet stays empty: the doc store is out of scope)"""
+    """types.h:259-274 (snippet filled when the query asks for snippets)"""
     doc_id: int
     doc_score: float
     snippet: str = ""
@@ -185,9 +186,21 @@ class VacuumEngine:
                 r.doc_freqs = list(freqs[i])
                 for j in range(nh[i]):
                     h = hits[i * stride + j]
-                    r.entries.append(SearchResultEntry(h.doc_id, h.score))
+                    e = SearchResultEntry(h.doc_id, h.score)
+                    if queries[i].return_snippets:   # vacuum_engine.h:248-252
+                        e.snippet = self.snippet(arr[i], h.doc_id, queries[i].n_snippet_passages)
+                    r.entries.append(e)
             out.append(r)
         return out
+
+    def snippet(self, q, doc_id: int, n_passages: int) -> str:
+        """VacuumEngine::GenerateSnippet for result entry doc_id of resolved query q."""
+        # (a 1-term phrase query is a plain query in the reference's dispatch)
+        return _capi.text_call(lib.wsr_snippet, self._h, C.byref(q), doc_id, n_passages)
+
+    def GetDocument(self, doc_id: int) -> str:
+        """The doc store's body text (ChunkedDocStoreReader::Get)."""
+        return _capi.text_call(lib.wsr_doc_get, self._h, doc_id)
 
     def decode_block(self, list_id: int, block: int, which: int = 0):
         """Device decode of one block (test hook) -> list of values."""
@@ -195,6 +208,46 @@ class VacuumEngine:
         cnt = C.c_int32()
         check(lib.wsr_debug_decode_block(self._h, list_id, block, which, buf, C.byref(cnt)))
         return list(buf[: cnt.value])
+
+
+class DocsHost:
+    """The snippet stage alone, without a device: the index dictionary and the doc
+    store of a Vacuum dump (wsr_docs_*).  Same snippets as VacuumEngine's."""
+
+    def __init__(self, engine_dir_path: str):
+        h = C.c_void_p()
+        check(lib.wsr_docs_open(engine_dir_path.encode(), C.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if self._h is not None:
+            lib.wsr_docs_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def query(self, terms: Sequence[str], is_phrase: bool = False):
+        q = _capi.Query()
+        q.n_terms = len(terms)
+        q.k = 1
+        q.flags = _capi.QUERY_PHRASE if (is_phrase and len(terms) > 1) else 0
+        for i, t in enumerate(terms):
+            lid, df = C.c_int32(), C.c_int32()
+            check(lib.wsr_docs_lookup(self._h, t.encode(), C.byref(lid), C.byref(df)))
+            q.list_ids[i] = lid.value
+        return q
+
+    def snippet(self, terms: Sequence[str], doc_id: int, n_passages: int = 3,
+                is_phrase: bool = False) -> str:
+        q = self.query(terms, is_phrase)
+        return _capi.text_call(lib.wsr_docs_snippet, self._h, C.byref(q), doc_id, n_passages)
+
+    def GetDocument(self, doc_id: int) -> str:
+        return _capi.text_call(lib.wsr_docs_get, self._h, doc_id)
 
 
 class ResidentBatch:
