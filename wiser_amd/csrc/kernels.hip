@@ -71,15 +71,19 @@ __device__ __forceinline__ uint32_t dpp(uint32_t x) {
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143, kWaveShr1 = 0x138;
 
-// inclusive sum inside aligned groups of W lanes (W = 2..64)
+// inclusive sum inside aligned groups of W lanes (W = 2..64).  A row_shr lane
+// whose source lies outside its 16-lane row keeps the 0 it was given, so for
+// W >= 16 no lane test is needed and each step folds into one v_add_u32_dpp;
+// groups narrower than a row must not take sums across their own boundary.
 template <int W>
 __device__ __forceinline__ uint32_t group_incl_scan(uint32_t x) {
   const uint32_t r = threadIdx.x & ((W < 16 ? W : 16) - 1);
+  constexpr bool kRow = W >= 16;
   uint32_t y;
-  y = dpp<kRowShr1>(x); if (r >= 1) x += y;
-  if (W > 2) { y = dpp<kRowShr2>(x); if (r >= 2) x += y; }
-  if (W > 4) { y = dpp<kRowShr4>(x); if (r >= 4) x += y; }
-  if (W > 8) { y = dpp<kRowShr8>(x); if (r >= 8) x += y; }
+  y = dpp<kRowShr1>(x); if (kRow || r >= 1) x += y;
+  if (W > 2) { y = dpp<kRowShr2>(x); if (kRow || r >= 2) x += y; }
+  if (W > 4) { y = dpp<kRowShr4>(x); if (kRow || r >= 4) x += y; }
+  if (W > 8) { y = dpp<kRowShr8>(x); x += y; }
   if (W > 16) { y = dpp<kRowBcast15, 0xA>(x); x += y; }
   if (W > 32) { y = dpp<kRowBcast31, 0xC>(x); x += y; }
   return x;
@@ -91,13 +95,13 @@ __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b 
 
 // max over the lanes below this one (0 for lane 0)
 __device__ __forceinline__ uint32_t wave_excl_max(uint32_t x) {
-  const uint32_t r = threadIdx.x & 15;
+  // (out-of-row lanes read 0, the identity of an unsigned max)
   x = dpp<kWaveShr1>(x);
   uint32_t y;
-  y = dpp<kRowShr1>(x); if (r >= 1) x = umax(x, y);
-  y = dpp<kRowShr2>(x); if (r >= 2) x = umax(x, y);
-  y = dpp<kRowShr4>(x); if (r >= 4) x = umax(x, y);
-  y = dpp<kRowShr8>(x); if (r >= 8) x = umax(x, y);
+  y = dpp<kRowShr1>(x); x = umax(x, y);
+  y = dpp<kRowShr2>(x); x = umax(x, y);
+  y = dpp<kRowShr4>(x); x = umax(x, y);
+  y = dpp<kRowShr8>(x); x = umax(x, y);
   y = dpp<kRowBcast15, 0xA>(x); x = umax(x, y);
   y = dpp<kRowBcast31, 0xC>(x); x = umax(x, y);
   return x;
@@ -1169,13 +1173,15 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // proportional to the survivors.
 // LDS of one wave of the lean kernel (kPh: phrase instance, whose queue also
 // carries the driver's posting slot and O1's posting rank of every survivor)
-template <bool kPh>
+// (kAnd: the instance that may take the bitmap-intersection path; the others
+// leave out its step buffer, so that more workgroups fit a CU's LDS)
+template <bool kPh, bool kAnd>
 struct LeanLdsT {
   uint32_t q[kPh ? 1536 : 1024];   // survivor queue (4 or 6 rings of 256); at item end the
                                    // replay's segment scan
   Event evs[128];       // events buffered in LDS, stored when half full and at the end
-  uint32_t bx[6][64];   // bitmap-intersection step: per lane its word's survivors (exclusive
-                        // prefix), intersected word, driver and O1 (rank, word)
+  uint32_t bx[kAnd ? 6 : 1][kAnd ? 64 : 1];   // bitmap-intersection step: per lane its word's
+                        // survivors (exclusive prefix), intersected word, driver and O1 (rank, word)
   uint4 dblk[64];       // the driver's directory entries of the segment
   uint32_t dmeta[64];
 #ifdef WSR_PROFILE
@@ -1186,8 +1192,8 @@ struct LeanLdsT {
 // o1 == kMaxTerms: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
-template <bool kPh>
-__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
+template <bool kPh, bool kAnd>
+__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, kAnd>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t* ph,
                                              bool and_path, uint32_t first_doc,
@@ -1451,7 +1457,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     }
     LT(3)
   };
-  if (and_path) {
+  if (kAnd && and_path) {
     // Bitmap intersection: the segment's doc span, 32 docs per word, one word
     // per lane and step; the words of every list are ANDed, so a step costs a
     // few loads per list whatever the driver's density.  Survivors are taken
@@ -1993,19 +1999,19 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #ifndef WSR_LEAN_WGS
 #define WSR_LEAN_WGS 4
 #endif
-template <bool kPh>
+template <bool kPh, bool kAnd>
 __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
     uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc, uint32_t* __restrict__ ph_all) {
-  __shared__ LeanLdsT<kPh> SW[kLeanWaves];
+  __shared__ LeanLdsT<kPh, kAnd> SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
   const uint32_t w = threadIdx.x >> 6;
   for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
   __syncthreads();
-  LeanLdsT<kPh>& S = SW[w];
+  LeanLdsT<kPh, kAnd>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
   uint32_t* ph = kPh ? ph_all + static_cast<uint64_t>(wid) * kPhraseScratch : nullptr;
   const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
@@ -2062,7 +2068,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
     if (!done && b0 < b1)
-      lean_segment<kPh>(ix, S, norm, Q, qs[qi].list,
+      lean_segment<kPh, kAnd>(ix, S, norm, Q, qs[qi].list,
                    kPh && ((Q.slots >> 16) & 0xFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
                    ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
@@ -2214,18 +2220,23 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
                        uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st) {
+  // (a persistent grid sized for the conjunctive instance: waves of a larger
+  // instance that find no room start later and find the queue drained)
   if (ph)
-    hipLaunchKernelGGL(lean_kernel<true>, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
+    hipLaunchKernelGGL((lean_kernel<true, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
                        nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+  else if (ix.and_wpb > 0.0f)
+    hipLaunchKernelGGL((lean_kernel<false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
+                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   else
-    hipLaunchKernelGGL(lean_kernel<false>, dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
-                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+    hipLaunchKernelGGL((lean_kernel<false, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
+                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   return hipGetLastError();
 }
 
 int lean_kernel_occupancy() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false>, 64 * kLeanWaves, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false, false>, 64 * kLeanWaves, 0) != hipSuccess)
     return 1;
   return n;
 }
