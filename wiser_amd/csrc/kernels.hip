@@ -2008,7 +2008,9 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
   __shared__ LeanLdsT<kPh, kAnd> SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
-  const uint32_t w = threadIdx.x >> 6;
+  // (wave-uniform; said so, so that the item indices, segment bounds and the
+  // pipeline's loop counter derived from it are scalar, not per-lane values)
+  const uint32_t w = uni(threadIdx.x >> 6);
   for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
   __syncthreads();
   LeanLdsT<kPh, kAnd>& S = SW[w];
