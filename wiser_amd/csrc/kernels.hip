@@ -1340,15 +1340,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
     uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
     // D: a decoded block and its loads in flight
-    uint32_t da0 = 0, da1 = 0, dcw = 0;            // docs, doc-length codes (2 bytes of a word)
+    uint32_t da0 = ~0u, da1 = ~0u, dcw = 0;        // docs, doc-length codes (2 bytes of a word)
     uint32_t dt0 = 0, dt1 = 0, dt2 = 0;            // driver tf pack words
     uint32_t dtb = 1, dtrel = 0;                   //   (uniform: width, blob offset)
     uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap words
-    bool dok0 = false, dok1 = false, dtl = false;
+    // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
+    // block or outside the image, a rank with bit 31 set is an O1 miss -- so
+    // that they take no scalar lane-mask registers across the iteration)
+    uint32_t dtl = 0;                              // uniform: the block is the VInts tail
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
-    uint32_t hf0 = 0, hf1 = 0, hx0 = 0, hx1 = 0;   // O1 tf byte words (in flight), posting ranks
-    bool hh0 = false, hh1 = false;
+    uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (in flight)
+    uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit)
+
   };
   Regs R0, R1;
   // byte shift of a pair's first value inside its aligned dword (pair_words)
@@ -1380,13 +1384,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t f1 = single ? 0u : (X.hf1 >> xs1) & 0xFFu;
       const uint32_t to0 = f0 == kTf8Escape ? (0x80000000u | X.hx0) : f0;
       const uint32_t to1 = f1 == kTf8Escape ? (0x80000000u | X.hx1) : f1;
-      const uint64_t m0 = __ballot(X.hh0), m1 = __ballot(X.hh1);
+      const bool hh0 = !(X.hx0 >> 31), hh1 = !(X.hx1 >> 31);
+      const uint64_t m0 = __ballot(hh0), m1 = __ballot(hh1);
       const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
-      const uint32_t r1 = r0 + (X.hh0 ? 1u : 0u);
+      const uint32_t r1 = r0 + (hh0 ? 1u : 0u);
       // branch-free: misses write the free slot before the queue head (at
       // most 63 + 128 entries are live, so it is never one of them)
       const uint32_t spare = (qhead - 1u) & 255u;
-      const uint32_t e0 = X.hh0 ? (r0 & 255u) : spare, e1 = X.hh1 ? (r1 & 255u) : spare;
+      const uint32_t e0 = hh0 ? (r0 & 255u) : spare, e1 = hh1 ? (r1 & 255u) : spare;
       qdoc[e0] = X.ha0; qc4[e0] = X.hc0; qtd[e0] = X.ht0; qto[e0] = to0;
       qdoc[e1] = X.ha1; qc4[e1] = X.hc1; qtd[e1] = X.ht1; qto[e1] = to1;
       if (kPh) {   // block j-2's postings 2l, 2l+1 and their O1 ranks
@@ -1406,14 +1411,17 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     {
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
-      const bool h0 = X.dok0 && (single || (q0 < span && ((X.de0.y >> s0) & 1u)));
-      const bool h1 = X.dok1 && (single || (q1 < span && ((X.de1.y >> s1) & 1u)));
-      Y.hx0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
-      Y.hx1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
+      const bool h0 = X.da0 != ~0u && (single || (q0 < span && ((X.de0.y >> s0) & 1u)));
+      const bool h1 = X.da1 != ~0u && (single || (q1 < span && ((X.de1.y >> s1) & 1u)));
+      const uint32_t x0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
+      const uint32_t x1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
       uint32_t w;
-      Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? Y.hx0 : 0u), &w);
-      Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? Y.hx1 : 0u), &w);
-      Y.hh0 = h0; Y.hh1 = h1;
+      Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? x0 : 0u), &w);
+      Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? x1 : 0u), &w);
+      // (ranks are < 2^31; a single-term item's are unused)
+      Y.hx0 = h0 ? (x0 & 0x7FFFFFFFu) : 0x80000000u;
+      Y.hx1 = h1 ? (x1 & 0x7FFFFFFFu) : 0x80000000u;
+
       Y.ha0 = X.da0; Y.ha1 = X.da1;
       Y.hc0 = (X.dcw >> ((l & 1u) << 4)) & 0xFFu;
       Y.hc1 = (X.dcw >> (((l & 1u) << 4) + 8)) & 0xFFu;
@@ -1450,7 +1458,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       Y.dtrel = uni(S.dblk[bi].w);
       uint32_t sh;
       pair_words(a_blob + Y.dtrel + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, sh);
-      Y.da0 = a0; Y.da1 = a1; Y.dok0 = ok0; Y.dok1 = ok1; Y.dtl = tl;
+      Y.da0 = ok0 ? a0 : ~0u; Y.da1 = ok1 ? a1 : ~0u; Y.dtl = tl ? 1u : 0u;
       if (live) ++n_dblk;
       // past the smallest last doc of the other lists nothing later can match
       if (live && __ballot((ok0 && a0 > min_last) || (ok1 && a1 > min_last))) bend = j + 1;
