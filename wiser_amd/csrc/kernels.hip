@@ -1175,11 +1175,17 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // carries the driver's posting slot and O1's posting rank of every survivor)
 // (kAnd: the instance that may take the bitmap-intersection path; the others
 // leave out its step buffer, so that more workgroups fit a CU's LDS)
+// (WSR_LEAN_EVS: capacity of the LDS event buffer, 128 or 64; at 64 it is
+// flushed after every chunk that added events)
+#ifndef WSR_LEAN_EVS
+#define WSR_LEAN_EVS 128
+#endif
 template <bool kPh, bool kAnd>
 struct LeanLdsT {
   uint32_t q[kPh ? 1536 : 1024];   // survivor queue (4 or 6 rings of 256); at item end the
                                    // replay's segment scan
-  Event evs[128];       // events buffered in LDS, stored when half full and at the end
+  Event evs[WSR_LEAN_EVS];   // events buffered in LDS, stored when a chunk could overflow them
+                             // and at the end
   uint32_t bx[kAnd ? 6 : 1][kAnd ? 64 : 1];   // bitmap-intersection step: per lane its word's
                         // survivors (exclusive prefix), intersected word, driver and O1 (rank, word)
   uint4 dblk[64];       // the driver's directory entries of the segment
@@ -1241,7 +1247,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   auto flush = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
     if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
-    if (l + 64 < evb) store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[l + 64]);
+    if (WSR_LEAN_EVS > 64 && l + 64 < evb)
+      store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[(l + 64) % WSR_LEAN_EVS]);
     __builtin_amdgcn_wave_barrier();
     evb = 0;
   };
@@ -1326,7 +1333,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         pt_n = pt_n + 1 > k ? k : pt_n + 1;
       }
     }
-    if (evb >= 64) flush();
+    if (evb && evb >= WSR_LEAN_EVS - 64) flush();
     const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     const double pv = kn > flo ? kn : flo;
     pub_val = pv > pub_val ? pv : pub_val;
@@ -2014,13 +2021,20 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
     uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc, uint32_t* __restrict__ ph_all) {
   __shared__ LeanLdsT<kPh, kAnd> SW[kLeanWaves];
+#ifdef WSR_LEAN_GNORM
+  const double* norm = ix.cache;   // (read through the caches: no LDS copy)
+  const uint32_t l = threadIdx.x & 63;
+#else
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
+#endif
   // (wave-uniform; said so, so that the item indices, segment bounds and the
   // pipeline's loop counter derived from it are scalar, not per-lane values)
   const uint32_t w = uni(threadIdx.x >> 6);
+#ifndef WSR_LEAN_GNORM
   for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
   __syncthreads();
+#endif
   LeanLdsT<kPh, kAnd>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
   uint32_t* ph = kPh ? ph_all + static_cast<uint64_t>(wid) * kPhraseScratch : nullptr;
