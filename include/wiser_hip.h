@@ -94,6 +94,15 @@ typedef struct wsr_hit {
  * length to *len. */
 int wsr_snippet(wsr_handle* h, const wsr_query* q, int32_t doc_id, int32_t n_passages,
                 char* out, int32_t cap, int32_t* len);
+/* The snippets of a batch's result entries, built by `threads` host threads
+ * (0 = all cores): entry j of query i is hits[i * stride + j], j < n_hits[i]
+ * (what wsr_search_batch / wsr_batch_fetch return).  The snippets are packed
+ * into buf in entry order; ends[i * stride + j] = end offset of that entry's
+ * snippet (entries past n_hits[i] are empty).  *total = bytes needed; if it
+ * exceeds cap nothing is written and WSR_E_LIMIT is returned. */
+int wsr_snippets_batch(wsr_handle* h, const wsr_query* q, int32_t nq, const wsr_hit* hits,
+                       const int32_t* n_hits, int32_t stride, int32_t n_passages, int32_t threads,
+                       char* buf, uint64_t cap, uint64_t* ends, uint64_t* total);
 /* ChunkedDocStoreReader::Get: the doc's body text */
 int wsr_doc_get(wsr_handle* h, int32_t doc_id, char* out, int32_t cap, int32_t* len);
 /* The same host stage without a device: index dictionary + doc store only. */

@@ -129,10 +129,37 @@ class VacuumHipEngine {
         SearchResultEntry e;
         e.doc_id = hits[i * stride + j].doc_id;
         e.doc_score = hits[i * stride + j].score;
-        if (qs[i].return_snippets)   // vacuum_engine.h:248-252
-          e.snippet = Snippet(in[i], e.doc_id, qs[i].n_snippet_passages);
         out[i].entries.push_back(e);
       }
+    }
+    // vacuum_engine.h:248-252: snippets of every entry, the batch at once on the
+    // host's threads, one call per distinct n_snippet_passages
+    std::map<int, std::vector<int32_t>> groups;   // n_passages -> n_hits masked to that group
+    for (size_t i = 0; i < qs.size(); ++i) {
+      if (!qs[i].return_snippets || empty[i] || nh[i] == 0) continue;
+      auto& g = groups[qs[i].n_snippet_passages];
+      if (g.empty()) g.assign(qs.size(), 0);
+      g[i] = nh[i];
+    }
+    for (auto& kv : groups) {
+      std::vector<uint64_t> ends(qs.size() * stride);
+      uint64_t total = 0;
+      std::string buf(1 << 16, '\0');
+      int rc = wsr_snippets_batch(h_, in.data(), static_cast<int32_t>(qs.size()), hits.data(), kv.second.data(),
+                                  stride, kv.first, 0, &buf[0], buf.size(), ends.data(), &total);
+      if (rc == WSR_E_LIMIT && total > buf.size()) {
+        buf.assign(total, '\0');
+        rc = wsr_snippets_batch(h_, in.data(), static_cast<int32_t>(qs.size()), hits.data(), kv.second.data(),
+                                stride, kv.first, 0, &buf[0], buf.size(), ends.data(), &total);
+      }
+      check(rc);
+      uint64_t at = 0;
+      for (size_t i = 0; i < qs.size(); ++i)
+        for (int j = 0; j < stride; ++j) {
+          const uint64_t e = ends[i * stride + j];
+          if (j < kv.second[i]) out[i].entries[j].snippet.assign(buf, at, e - at);
+          at = e;
+        }
     }
     return out;
   }

@@ -31,3 +31,27 @@ def test_cpp_host_matches_oracle(indexes, tmp_path):
         want, _ = o.search(q, 10)
         got = [(int(x.split(":")[0]), float.fromhex(x.split(":")[1])) for x in line.split()]
         assert got == want, q
+
+
+@pytest.mark.gpu
+def test_cpp_host_snippets_match_oracle(indexes, tmp_path):
+    """VacuumHipEngine (C++ mirror) with return_snippets: the batched host
+    snippet stage (wsr_snippets_batch) after the GPU top-k."""
+    from oracle.oracle import OracleVacuum
+    d = indexes["wiki5"][0]
+    rng = random.Random(6)
+    toks = all_tokens()
+    qs = [[t] for t in rng.sample(toks, 60)] + [rng.sample(toks[:300], 2) for _ in range(60)]
+    log = tmp_path / "q.log"
+    log.write_text("\n".join(" ".join(q) for q in qs) + "\n")
+    out = subprocess.run([CLI, d, str(log), "10", "snippets"], capture_output=True, text=True, check=True)
+    lines = out.stdout.split("\n")
+    o = OracleVacuum(d)
+    n = 0
+    for i, q in enumerate(qs):
+        want = o.search_snippets(q, 10)
+        hits = [(int(x.split(":")[0]), float.fromhex(x.split(":")[1])) for x in lines[2 * i].split()]
+        snips = [bytes.fromhex(x).decode() for x in lines[2 * i + 1].split(",")] if hits else []
+        assert [(d_, s_, sn) for (d_, s_), sn in zip(hits, snips)] == want, q
+        n += len(want)
+    assert n > 100

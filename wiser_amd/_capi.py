@@ -132,6 +132,9 @@ _sigs = {
     "wsr_snippet": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.c_char_p, C.c_int32,
                               C.POINTER(C.c_int32)]),
     "wsr_doc_get": (C.c_int, [_P, C.c_int32, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
+    "wsr_snippets_batch": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.POINTER(Hit),
+                                     C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                     C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "wsr_docs_open": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "wsr_docs_close": (None, [_P]),
     "wsr_docs_lookup": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
@@ -163,6 +166,34 @@ def text_call(fn, *args, cap: int = 4096) -> str:
         if n.value <= cap:
             return buf.raw[: n.value].decode("utf-8", errors="surrogateescape")
         cap = n.value
+
+
+def snippets_batch(h, queries, hits, n_hits, stride: int, n_passages: int, threads: int = 0):
+    """wsr_snippets_batch -> list (per query) of lists of snippet strings."""
+    nq = len(n_hits)
+    ends = (C.c_uint64 * max(1, nq * stride))()
+    total = C.c_uint64()
+    cap = 1 << 16
+    while True:
+        buf = C.create_string_buffer(cap)
+        rc = lib.wsr_snippets_batch(h, queries, nq, hits, n_hits, stride, n_passages, threads, buf, cap,
+                                    ends, C.byref(total))
+        if rc == -4 and total.value > cap:   # WSR_E_LIMIT: grow to the reported size
+            cap = total.value
+            continue
+        check(rc)
+        break
+    raw = buf.raw
+    out, at = [], 0
+    for i in range(nq):
+        row = []
+        for j in range(stride):
+            e = ends[i * stride + j]
+            if j < n_hits[i]:
+                row.append(raw[at:e].decode("utf-8", errors="surrogateescape"))
+            at = e
+        out.append(row)
+    return out
 
 
 def highlight(offsets, n_passages: int, text: str) -> str:

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <cstdlib>
@@ -64,6 +65,7 @@ struct wsr_handle {
   hipStream_t stream = nullptr;
   VacuumIndex idx;
   DocStore docs;                    // my.fdx / my.fdt when the index has them (snippets)
+  std::unique_ptr<SkipRowCache> rows;   // decoded skip rows for the snippet stage
   IndexArgs args{};
   uint8_t* d_blob = nullptr;
   ListDev* d_lists = nullptr;
@@ -143,6 +145,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
   try {
     h->idx.open(dir);
     h->docs.open(dir);
+    h->rows.reset(new SkipRowCache(h->idx));
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());
   }
@@ -280,6 +283,7 @@ int wsr_lookup(wsr_handle* h, const char* term, int32_t* list_id, int32_t* df) {
 struct wsr_docs {
   VacuumIndex idx;
   DocStore docs;
+  std::unique_ptr<SkipRowCache> rows;
 };
 
 namespace {
@@ -289,17 +293,23 @@ int copy_out(const std::string& s, char* out, int32_t cap, int32_t* len) {
   return WSR_OK;
 }
 
-int snippet_of(const VacuumIndex& idx, const DocStore& docs, const wsr_query* q, int32_t doc,
-               int32_t n_passages, char* out, int32_t cap, int32_t* len) {
-  if (!q || !len || n_passages < 0) return fail(WSR_E_INVALID, "bad snippet arguments");
+int check_snippet_query(const VacuumIndex& idx, const DocStore& docs, const wsr_query* q) {
   if (q->n_terms < 1 || q->n_terms > WSR_MAX_TERMS) return fail(WSR_E_LIMIT, "bad term count");
   if (!docs.is_open()) return fail(WSR_E_INVALID, "the index has no doc store (my.fdx / my.fdt)");
   for (int i = 0; i < q->n_terms; ++i)
     if (q->list_ids[i] < 0 || q->list_ids[i] >= idx.n_lists())
       return fail(WSR_E_INVALID, "a query term is not in the index (no result entries)");
+  return WSR_OK;
+}
+
+int snippet_of(const VacuumIndex& idx, const SkipRowCache& rows, const DocStore& docs, const wsr_query* q,
+               int32_t doc, int32_t n_passages, char* out, int32_t cap, int32_t* len) {
+  if (!q || !len || n_passages < 0) return fail(WSR_E_INVALID, "bad snippet arguments");
+  const int rc = check_snippet_query(idx, docs, q);
+  if (rc != WSR_OK) return rc;
   try {
-    return copy_out(make_snippet(idx, docs, q->list_ids, q->n_terms, (q->flags & WSR_QUERY_PHRASE) != 0,
-                                 doc, n_passages),
+    return copy_out(make_snippet(idx, rows, docs, q->list_ids, q->n_terms,
+                                 (q->flags & WSR_QUERY_PHRASE) != 0, doc, n_passages),
                     out, cap, len);
   } catch (const std::exception& e) {
     return fail(WSR_E_INVALID, e.what());
@@ -319,7 +329,59 @@ int doc_text(const DocStore& docs, int32_t doc, char* out, int32_t cap, int32_t*
 int wsr_snippet(wsr_handle* h, const wsr_query* q, int32_t doc, int32_t n_passages, char* out,
                 int32_t cap, int32_t* len) {
   if (!h) return fail(WSR_E_INVALID, "null argument");
-  return snippet_of(h->idx, h->docs, q, doc, n_passages, out, cap, len);
+  return snippet_of(h->idx, *h->rows, h->docs, q, doc, n_passages, out, cap, len);
+}
+
+int wsr_snippets_batch(wsr_handle* h, const wsr_query* q, int32_t nq, const wsr_hit* hits,
+                       const int32_t* n_hits, int32_t stride, int32_t n_passages, int32_t threads,
+                       char* buf, uint64_t cap, uint64_t* ends, uint64_t* total) {
+  if (!h || (nq > 0 && (!q || !hits || !n_hits || !ends)) || !total || nq < 0 || stride <= 0 ||
+      n_passages < 0)
+    return fail(WSR_E_INVALID, "bad snippet batch arguments");
+  std::vector<std::pair<int32_t, int32_t>> work;   // (query, entry)
+  for (int32_t i = 0; i < nq; ++i) {
+    if (n_hits[i] < 0 || n_hits[i] > stride) return fail(WSR_E_INVALID, "bad hit count");
+    if (n_hits[i] == 0) continue;
+    const int rc = check_snippet_query(h->idx, h->docs, &q[i]);
+    if (rc != WSR_OK) return rc;
+    for (int32_t j = 0; j < n_hits[i]; ++j) work.emplace_back(i, j);
+  }
+  std::vector<std::string> out(static_cast<size_t>(nq) * stride);
+  std::atomic<size_t> next{0};
+  std::mutex err_mu;
+  std::string err;
+  auto run = [&]() {
+    for (size_t w; (w = next.fetch_add(1)) < work.size();) {
+      const int32_t i = work[w].first, j = work[w].second;
+      try {
+        out[static_cast<size_t>(i) * stride + j] =
+            make_snippet(h->idx, *h->rows, h->docs, q[i].list_ids, q[i].n_terms,
+                         (q[i].flags & WSR_QUERY_PHRASE) != 0, hits[static_cast<size_t>(i) * stride + j].doc_id,
+                         n_passages);
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (err.empty()) err = e.what();
+      }
+    }
+  };
+  int nt = threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency());
+  nt = std::max(1, std::min<int>(nt, std::min<size_t>(64, work.size())));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(run);
+  run();
+  for (auto& t : pool) t.join();
+  if (!err.empty()) return fail(WSR_E_INVALID, err);
+  uint64_t n = 0;
+  for (const auto& s : out) n += s.size();
+  *total = n;
+  if (n > cap) return fail(WSR_E_LIMIT, "snippet buffer too small (see *total)");
+  uint64_t at = 0;
+  for (size_t e = 0; e < out.size(); ++e) {
+    if (!out[e].empty()) std::memcpy(buf + at, out[e].data(), out[e].size());
+    at += out[e].size();
+    ends[e] = at;
+  }
+  return WSR_OK;
 }
 
 int wsr_doc_get(wsr_handle* h, int32_t doc, char* out, int32_t cap, int32_t* len) {
@@ -334,6 +396,7 @@ int wsr_docs_open(const char* dir, wsr_docs** out) {
   try {
     d->idx.open(dir);
     if (!d->docs.open(dir)) return fail(WSR_E_IO, std::string("no doc store in ") + dir);
+    d->rows.reset(new SkipRowCache(d->idx));
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());
   }
@@ -354,7 +417,7 @@ int wsr_docs_lookup(wsr_docs* d, const char* term, int32_t* list_id, int32_t* df
 int wsr_docs_snippet(wsr_docs* d, const wsr_query* q, int32_t doc, int32_t n_passages, char* out,
                      int32_t cap, int32_t* len) {
   if (!d) return fail(WSR_E_INVALID, "null argument");
-  return snippet_of(d->idx, d->docs, q, doc, n_passages, out, cap, len);
+  return snippet_of(d->idx, *d->rows, d->docs, q, doc, n_passages, out, cap, len);
 }
 
 int wsr_docs_get(wsr_docs* d, int32_t doc, char* out, int32_t cap, int32_t* len) {

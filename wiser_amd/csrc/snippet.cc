@@ -63,8 +63,9 @@ struct Posting {
   uint32_t tf[kPackSize];
 };
 
-Posting locate(const VacuumIndex& idx, int32_t list, int32_t doc) {
-  const std::vector<SkipRow> rows = idx.rows(list);
+Posting locate(const VacuumIndex& idx, const SkipRowCache& cache, int32_t list, int32_t doc) {
+  const std::shared_ptr<const std::vector<SkipRow>> keep = cache.get(list);
+  const std::vector<SkipRow>& rows = *keep;
   const uint32_t df = idx.df(list);
   if (rows.empty()) throw std::runtime_error("empty posting list");
   // block r holds the docs in (prev_doc[r], prev_doc[r + 1]]; row 0 starts at 0
@@ -273,10 +274,21 @@ std::string highlight_offsets(const std::vector<std::vector<OffsetPair>>& terms,
   return out;
 }
 
-std::string make_snippet(const VacuumIndex& idx, const DocStore& docs, const int32_t* lists, int n,
-                         bool phrase, int32_t doc, int n_passages) {
+std::shared_ptr<const std::vector<SkipRow>> SkipRowCache::get(int32_t list) const {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = rows_.find(list);
+    if (it != rows_.end()) return it->second;
+  }
+  auto r = std::make_shared<const std::vector<SkipRow>>(idx_.rows(list));
+  std::lock_guard<std::mutex> g(mu_);
+  return rows_.emplace(list, std::move(r)).first->second;
+}
+
+std::string make_snippet(const VacuumIndex& idx, const SkipRowCache& rows, const DocStore& docs,
+                         const int32_t* lists, int n, bool phrase, int32_t doc, int n_passages) {
   std::vector<Posting> ps;
-  for (int i = 0; i < n; ++i) ps.push_back(locate(idx, lists[i], doc));
+  for (int i = 0; i < n; ++i) ps.push_back(locate(idx, rows, lists[i], doc));
   std::vector<std::vector<OffsetPair>> terms;
   if (phrase && n > 1) {
     // only the matched occurrences (FilterOffsetByPosition); the doc is a

@@ -17,6 +17,9 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
 #include <string>
 #include <utility>
 #include <vector>
@@ -28,10 +31,24 @@ namespace wiser {
 
 using OffsetPair = std::pair<int, int>;
 
+// Decoded skip rows per list, shared by the threads of the snippet stage
+// (the reference re-decodes a list's whole skip list for every iterator,
+// flash_iterators.h:946-948; a snippet needs them for k docs per query).
+class SkipRowCache {
+ public:
+  explicit SkipRowCache(const VacuumIndex& idx) : idx_(idx) {}
+  std::shared_ptr<const std::vector<SkipRow>> get(int32_t list) const;
+
+ private:
+  const VacuumIndex& idx_;
+  mutable std::mutex mu_;
+  mutable std::unordered_map<int32_t, std::shared_ptr<const std::vector<SkipRow>>> rows_;
+};
+
 // The snippet of doc `doc` for a query of n list ids (query order).  The doc
 // must hold every term (it is a result entry); throws std::runtime_error otherwise.
-std::string make_snippet(const VacuumIndex& idx, const DocStore& docs, const int32_t* lists, int n,
-                         bool phrase, int32_t doc, int n_passages);
+std::string make_snippet(const VacuumIndex& idx, const SkipRowCache& rows, const DocStore& docs,
+                         const int32_t* lists, int n, bool phrase, int32_t doc, int n_passages);
 
 // SimpleHighlighter::highlightOffsetsEnums over explicit per-term offset lists
 // (each non-empty).

@@ -91,6 +91,7 @@ class VacuumEngine:
         self.device = device
         self.doc_range = doc_range
         self.threads = threads
+        self.snippet_threads = 0     # host threads of the snippet stage (0 = all cores)
         self._h = None
 
     # ---- SearchEngineServiceNew -------------------------------------
@@ -186,11 +187,26 @@ class VacuumEngine:
                 r.doc_freqs = list(freqs[i])
                 for j in range(nh[i]):
                     h = hits[i * stride + j]
-                    e = SearchResultEntry(h.doc_id, h.score)
-                    if queries[i].return_snippets:   # vacuum_engine.h:248-252
-                        e.snippet = self.snippet(arr[i], h.doc_id, queries[i].n_snippet_passages)
-                    r.entries.append(e)
+                    r.entries.append(SearchResultEntry(h.doc_id, h.score))
             out.append(r)
+        # vacuum_engine.h:248-252: the snippet stage, all entries of the batch at
+        # once on the host's threads (grouped by n_snippet_passages)
+        groups: Dict[int, List[int]] = {}
+        for i, sq in enumerate(queries):
+            if sq.return_snippets and freqs[i] is not None and nh[i] > 0:
+                groups.setdefault(int(sq.n_snippet_passages), []).append(i)
+        for n_passages, idx in groups.items():
+            sub_q = (_capi.Query * len(idx))(*[arr[i] for i in idx])
+            sub_h = (_capi.Hit * (len(idx) * stride))()
+            sub_n = (C.c_int32 * len(idx))(*[nh[i] for i in idx])
+            for a, i in enumerate(idx):
+                C.memmove(C.byref(sub_h, a * stride * C.sizeof(_capi.Hit)),
+                          C.byref(hits, i * stride * C.sizeof(_capi.Hit)), stride * C.sizeof(_capi.Hit))
+            snips = _capi.snippets_batch(self._h, sub_q, sub_h, sub_n, stride, n_passages,
+                                         self.snippet_threads)
+            for a, i in enumerate(idx):
+                for e, sn in zip(out[i].entries, snips[a]):
+                    e.snippet = sn
         return out
 
     def snippet(self, q, doc_id: int, n_passages: int) -> str:
