@@ -250,6 +250,7 @@ def extra_legs(a, idx, local, threads):
     eng.close()
     if not has_pool:   # phrase pool: synthetic indexes only
         legs["serving"] = serving_leg(a, idx, local, threads)
+        legs["c1_snippets"] = snippet_leg(a, local, threads)
         return legs
     t = time.time()
     eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
@@ -262,7 +263,100 @@ def extra_legs(a, idx, local, threads):
                                      "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
     eng.close()
     legs["serving"] = serving_leg(a, idx, local, threads)
+    legs["c1_snippets"] = snippet_leg(a, local, threads)
     return legs
+
+
+def snippet_leg(a, local, threads):
+    """configs[0] ("C1"): the reference's own 10k-doc TOKEN_ONLY linedoc
+    (src/testdata/test_doc_tokenized), single-term BM25 top-10 over every
+    distinct token plus 10k tokens sampled with seed 1, here with
+    SearchQuery::return_snippets (3 passages): GPU top-k, then the host snippet
+    stage over the box's CPU share (wsr_snippets_batch).  Checked against the
+    oracle's VacuumEngine::Search + GenerateSnippet, which is also the CPU
+    baseline (1 thread)."""
+    import random
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    src = os.path.join(ROOT, "tests", "golden", "data", "test_doc_tokenized")
+    d = os.path.join(a.index_dir, "c1_test_doc_tokenized")
+    if not os.path.exists(os.path.join(d, "READY")):
+        os.makedirs(d, exist_ok=True)
+        w.build_from_linedoc(src, d, "TOKEN_ONLY")
+        open(os.path.join(d, "READY"), "w").write("ok")
+    toks = set()
+    with open(src) as f:
+        next(f)
+        for line in f:
+            toks.update(line.rstrip("\n").split("\t")[2].split())
+    distinct = sorted(toks)
+    rng = random.Random(1)
+    terms = distinct + [rng.choice(distinct) for _ in range(10000)]
+    eng = w.VacuumEngine(d, device=local, threads=threads, positions=False)
+    eng.Load()
+    eng.snippet_threads = CPU_SHARE
+    from wiser_amd import _capi
+    # native path timed: the batch's GPU top-k (wsr_search_batch), then the
+    # snippet stage of its entries on CPU_SHARE threads (wsr_snippets_batch)
+    batches = []
+    for i in range(0, len(terms), a.batch):
+        chunk = terms[i:i + a.batch]
+        arr = (_capi.Query * len(chunk))(*[eng.resolve(w.SearchQuery([t], n_results=a.k))[0]
+                                           for t in chunk])
+        batches.append((arr, len(chunk)))
+    cap = 64 << 20
+    sbuf = C.create_string_buffer(cap)
+    ends = (C.c_uint64 * (a.batch * a.k))()
+    total = C.c_uint64()
+    def run(snip):
+        t_topk = t_snip = 0.0
+        n = 0
+        for arr, nq in batches:
+            hits = (_capi.Hit * (nq * a.k))()
+            nh = (C.c_int32 * nq)()
+            t0 = time.perf_counter()
+            _capi.check(_capi.lib.wsr_search_batch(eng._h, arr, nq, a.k, hits, nh))
+            t1 = time.perf_counter()
+            if snip:
+                _capi.check(_capi.lib.wsr_snippets_batch(eng._h, arr, nq, hits, nh, a.k, 3, CPU_SHARE,
+                                                         sbuf, cap, ends, C.byref(total)))
+                n += sum(nh)
+            t_topk += t1 - t0
+            t_snip += time.perf_counter() - t1
+        return t_topk, t_snip, n
+    run(True)   # warm (and fills the skip-row cache)
+    t_topk, t_snip, n_snip = run(True)
+    el = t_topk + t_snip
+    # Python mirror, for parity: SearchBatch with return_snippets
+    res = eng.SearchBatch([w.SearchQuery([t], n_results=a.k, return_snippets=True)
+                           for t in terms[: a.check]])
+    orc = OracleVacuum(d)
+    bad = 0
+    for t, r in zip(terms[: a.check], res):
+        want = orc.search_snippets([t], a.k)
+        bad += [(e.doc_id, e.doc_score, e.snippet) for e in r.entries] != want
+    if bad:
+        raise SystemExit(f"c1 snippet leg: {bad} queries differ from the oracle")
+    out = {"value": round(len(terms) / el, 1), "unit": "queries/s", "queries": len(terms),
+           "snippets": n_snip, "snippets_per_s": round(n_snip / t_snip, 1), "snippet_threads": CPU_SHARE,
+           "topk_ms_per_batch": round(1e3 * t_topk / len(batches), 3),
+           "snippet_ms_per_batch": round(1e3 * t_snip / len(batches), 3),
+           "parity_checked_queries": min(a.check, len(terms)),
+           "workload": ("C1: the reference's 10k-doc TOKEN_ONLY linedoc, single-term top-10 over every "
+                        f"distinct token ({len(distinct)}) + 10000 sampled (seed 1), return_snippets, "
+                        "3 passages; per batch of 4096: GPU top-k (wsr_search_batch, host arrays in and "
+                        "out) then the snippet stage (wsr_snippets_batch)")}
+    if not a.no_cpu:
+        t0, n, i = time.time(), 0, 0
+        while time.time() - t0 < 2.0:
+            orc.search_snippets([terms[i % len(terms)]], a.k)
+            n += 1
+            i += 1
+        out["cpu_baseline"] = {"value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
+                               "sample": f"{n} queries of the leg's list, oracle Search + GenerateSnippet, 2s"}
+    orc.close()
+    eng.close()
+    return out
 
 
 def serving_leg(a, idx, local, threads):

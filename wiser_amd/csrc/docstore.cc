@@ -140,7 +140,8 @@ std::string DocStore::get(int32_t doc) const {
     p += l;
   }
   std::string text;
-  std::vector<char> buf(buf_bytes_);
+  thread_local std::vector<char> buf;   // (one decode buffer per thread, no zero fill per call)
+  if (buf.size() < static_cast<size_t>(buf_bytes_)) buf.resize(buf_bytes_);
   for (uint64_t s : sizes) {
     if (static_cast<uint64_t>(end - p) < s) throw std::runtime_error("doc store record: truncated");
     const int got = LZ4_decompress_safe(reinterpret_cast<const char*>(p), buf.data(),

@@ -64,8 +64,7 @@ struct Posting {
 };
 
 Posting locate(const VacuumIndex& idx, const SkipRowCache& cache, int32_t list, int32_t doc) {
-  const std::shared_ptr<const std::vector<SkipRow>> keep = cache.get(list);
-  const std::vector<SkipRow>& rows = *keep;
+  const std::vector<SkipRow>& rows = cache.get(list);
   const uint32_t df = idx.df(list);
   if (rows.empty()) throw std::runtime_error("empty posting list");
   // block r holds the docs in (prev_doc[r], prev_doc[r + 1]]; row 0 starts at 0
@@ -274,15 +273,15 @@ std::string highlight_offsets(const std::vector<std::vector<OffsetPair>>& terms,
   return out;
 }
 
-std::shared_ptr<const std::vector<SkipRow>> SkipRowCache::get(int32_t list) const {
+const std::vector<SkipRow>& SkipRowCache::get(int32_t list) const {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     auto it = rows_.find(list);
-    if (it != rows_.end()) return it->second;
+    if (it != rows_.end()) return *it->second;
   }
-  auto r = std::make_shared<const std::vector<SkipRow>>(idx_.rows(list));
-  std::lock_guard<std::mutex> g(mu_);
-  return rows_.emplace(list, std::move(r)).first->second;
+  std::unique_ptr<const std::vector<SkipRow>> r(new std::vector<SkipRow>(idx_.rows(list)));
+  std::unique_lock<std::shared_mutex> g(mu_);
+  return *rows_.emplace(list, std::move(r)).first->second;   // (a racing decode is dropped)
 }
 
 std::string make_snippet(const VacuumIndex& idx, const SkipRowCache& rows, const DocStore& docs,

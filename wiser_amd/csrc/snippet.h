@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <unordered_map>
 #include <string>
 #include <utility>
@@ -37,12 +38,14 @@ using OffsetPair = std::pair<int, int>;
 class SkipRowCache {
  public:
   explicit SkipRowCache(const VacuumIndex& idx) : idx_(idx) {}
-  std::shared_ptr<const std::vector<SkipRow>> get(int32_t list) const;
+  // (entries are never dropped, so the reference stays valid; lookups take a
+  // shared lock, a first decode an exclusive one)
+  const std::vector<SkipRow>& get(int32_t list) const;
 
  private:
   const VacuumIndex& idx_;
-  mutable std::mutex mu_;
-  mutable std::unordered_map<int32_t, std::shared_ptr<const std::vector<SkipRow>>> rows_;
+  mutable std::shared_mutex mu_;
+  mutable std::unordered_map<int32_t, std::unique_ptr<const std::vector<SkipRow>>> rows_;
 };
 
 // The snippet of doc `doc` for a query of n list ids (query order).  The doc
