@@ -1423,8 +1423,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t x0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
       const uint32_t x1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
       uint32_t w;
+#ifdef WSR_DIAG_NO_TF8   // timing diagnostic only (wrong tfs): no O1 tf gathers
+      Y.hf0 = 0x01010101u; Y.hf1 = 0x01010101u; (void)w;
+#else
       Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? x0 : 0u), &w);
       Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? x1 : 0u), &w);
+#endif
       // (ranks are < 2^31; a single-term item's are unused)
       Y.hx0 = h0 ? (x0 & 0x7FFFFFFFu) : 0x80000000u;
       Y.hx1 = h1 ? (x1 & 0x7FFFFFFFu) : 0x80000000u;
