@@ -574,14 +574,18 @@ def main():
     if rank == 0 and world == 1 and not a.no_extra:
         extra = extra_legs(a, idx, local, threads)
 
-    traffic = None
+    traffic = traffic_x1 = None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_segment.json")
-    # (measured on the C2 workload: attached to C2 lines only)
+    # (measured on the C2 workload: attached to C2 lines only).  traffic applies
+    # the guide's x2 FETCH_SIZE correction to every read; it is calibrated only
+    # for wide streaming reads, so the uncorrected figure is given beside it.
     if os.path.exists(pmc) and not (a.vacuum_dir or a.linedoc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            pm = json.load(open(pmc))
+            traffic = pm.get("hbm_bytes_per_launch")
+            traffic_x1 = pm["read_bytes_per_launch"] / 2 + pm["write_bytes_per_launch"]
         except Exception:
-            traffic = None
+            traffic = traffic_x1 = None
 
     if rank == 0:
         out = {
@@ -599,6 +603,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_fetch_uncorrected": traffic_x1,
                          # the segment phase: lean_kernel with the general
                          # segment_kernel beside it on a second stream (one batch
                          # at a time, HIP events fork -> join)

@@ -66,6 +66,8 @@ struct wsr_handle {
   VacuumIndex idx;
   DocStore docs;                    // my.fdx / my.fdt when the index has them (snippets)
   std::unique_ptr<SkipRowCache> rows;   // decoded skip rows for the snippet stage
+  std::mutex pool_mu;                   // wsr_search_batch's reusable batches
+  std::vector<wsr_batch*> pool;
   IndexArgs args{};
   uint8_t* d_blob = nullptr;
   ListDev* d_lists = nullptr;
@@ -243,6 +245,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
 
 void wsr_close(wsr_handle* h) {
   if (!h) return;
+  for (wsr_batch* b : h->pool) wsr_batch_destroy(h, b);
+  h->pool.clear();
   if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
 
   for (void* p : {static_cast<void*>(h->d_blob), static_cast<void*>(h->d_lists),
@@ -767,13 +771,32 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stri
                      int32_t* n_hits) {
   if (!h || nq < 0 || (nq && (!q || !hits || !n_hits))) return fail(WSR_E_INVALID, "bad arguments");
   if (nq == 0) return WSR_OK;
+  // batches are kept in a per-handle pool (one per concurrent caller): creating
+  // one allocates its device buffers, which would dominate a small call
   wsr_batch* b = nullptr;
-  int rc = wsr_batch_create(h, nq, stride, &b);
-  if (rc) return rc;
-  rc = wsr_batch_upload(h, b, q, nq);
+  {
+    std::lock_guard<std::mutex> g(h->pool_mu);
+    for (size_t i = 0; i < h->pool.size(); ++i)
+      if (h->pool[i]->max_q >= nq && h->pool[i]->stride == stride) {
+        b = h->pool[i];
+        h->pool.erase(h->pool.begin() + i);
+        break;
+      }
+  }
+  if (!b) {
+    int32_t cap = 64;
+    while (cap < nq) cap *= 2;
+    const int rc = wsr_batch_create(h, cap, stride, &b);
+    if (rc) return rc;
+  }
+  int rc = wsr_batch_upload(h, b, q, nq);
   if (!rc) rc = wsr_batch_run(h, b);
   if (!rc) rc = wsr_batch_fetch(h, b, hits, n_hits);
-  wsr_batch_destroy(h, b);
+  {
+    std::lock_guard<std::mutex> g(h->pool_mu);
+    if (!rc && h->pool.size() < 8) { h->pool.push_back(b); b = nullptr; }
+  }
+  if (b) wsr_batch_destroy(h, b);
   return rc;
 }
 
