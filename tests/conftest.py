@@ -13,6 +13,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first():
+    """torch ships its own HIP runtime; libwiser_hip.so links the system ROCm
+    one.  Both work in one process when torch initialises first (as bench.py's
+    distributed path does); a torch first touched after the engine has opened
+    a device finds no GPU.  So touch it first, whatever subset of tests runs."""
+    try:
+        import torch
+        torch.cuda.is_available()
+    except Exception:
+        pass
+
+
 @pytest.fixture(scope="session")
 def built():
     """Make sure libwiser_hip.so and liboracle.so exist (hipcc cross-compiles on CPU)."""
