@@ -93,6 +93,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) { return group_in
 
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 
+// A wave-uniform value kept in a vector register: for values only ever used as
+// VALU operands, so that they do not compete for the scalar registers of a
+// loop that already needs more than the 106 it can have.
+#ifndef WSR_NO_VPIN
+template <class T>
+__device__ __forceinline__ T in_vgpr(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+#else
+template <class T>
+__device__ __forceinline__ T in_vgpr(T x) { return x; }
+#endif
+
 // max over the lanes below this one (0 for lane 0)
 __device__ __forceinline__ uint32_t wave_excl_max(uint32_t x) {
   // (out-of-row lanes read 0, the identity of an unsigned max)
@@ -1214,7 +1228,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint64_t lt = lanemask_lt();
   const uint32_t d = Q.slots & 0xFFu, o1 = (Q.slots >> 8) & 0xFFu;
   const uint32_t nt = (Q.slots >> 16) & 0xFFu, k = Q.slots >> 24;
-  const uint32_t min_last = Q.min_last;
+  const uint32_t min_last = in_vgpr(Q.min_last);
   const bool single = o1 >= kMaxTerms;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
   const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
@@ -1222,9 +1236,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
-  const uint32_t lo = ix.doc_lo, span = ix.dense_span;
-  const uint32_t hi_rel = ix.doc_hi - ix.doc_lo;   // docs a with a - lo < hi_rel are in the image
-  const double idf_d = Q.a_idf, idf_o = Q.o_idf;
+  const uint32_t lo = in_vgpr(ix.doc_lo), span = in_vgpr(ix.dense_span);
+  const uint32_t hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);   // docs a with a - lo < hi_rel are in the image
+  const double idf_d = in_vgpr(Q.a_idf), idf_o = in_vgpr(Q.o_idf);
   uint32_t* qdoc = S.q;             // survivor queue (ring of 256)
   uint32_t* qc4 = qdoc + 256;
   uint32_t* qtd = qdoc + 512;
@@ -1369,7 +1383,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                        (bit >> 3);
     return ((a & 3u) << 3) + (bit & 7u);
   };
-  const uint32_t tf8_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u);
+  const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
