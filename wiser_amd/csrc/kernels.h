@@ -60,7 +60,7 @@ constexpr int kStatStride = 4;
 enum { kErrLimit = 1, kErrCapacity = 2 };
 
 #ifndef WSR_SEG_COST
-#define WSR_SEG_COST 48
+#define WSR_SEG_COST 63
 #endif
 constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
