@@ -461,7 +461,7 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
                                                          uint64_t* __restrict__ pub,
                                                          QueryDesc* __restrict__ desc) {
   constexpr int kWaves = 1024 / 64;
-  __shared__ uint64_t s_capw[kWaves];            // per wave event-capacity totals
+  __shared__ uint64_t s_cap[1024];
   __shared__ uint32_t s_bt[kPlanKeys][kWaves];   // per key, per wave item totals
   const int t = threadIdx.x, T = blockDim.x;
   const uint32_t wv = t / 64, l = t & 63;
@@ -478,12 +478,7 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     for (int b = 0; b < kPlanKeys; ++b) cnt[b] += bk == static_cast<uint32_t>(b) ? p.n_items : 0u;
     cap += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
-  // event capacity, counted in whole blocks (it is n_items * seg * 128): a
-  // wave's block count stays far below 2^32, so the wave scan runs in 32 bits
-  // and only the per-wave totals are 64-bit
-  const uint32_t cap32 = static_cast<uint32_t>(cap >> 7);
-  const uint32_t cap_inc = wave_incl_scan(cap32);
-  if (l == 63) s_capw[wv] = static_cast<uint64_t>(cap_inc) << 7;
+  s_cap[t] = cap;
   uint32_t ex[kPlanKeys];   // items of this key in lower lanes of the wave
 #pragma unroll
   for (int b = 0; b < kPlanKeys; ++b) {
@@ -492,12 +487,12 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     if (l == 63) s_bt[b][wv] = inc;
   }
   __syncthreads();
-  uint64_t cap_below = static_cast<uint64_t>(cap_inc - cap32) << 7, cap_total = 0;   // events before
-                                                                                     // this thread's queries
-  for (uint32_t w = 0; w < static_cast<uint32_t>(kWaves); ++w) {
-    const uint64_t v = s_capw[w];
-    cap_below += w < wv ? v : 0u;
-    cap_total += v;
+  for (int d = 1; d < T; d <<= 1) {  // Hillis-Steele over the thread capacities
+    uint64_t c = 0;
+    if (t >= d) c = s_cap[t - d];
+    __syncthreads();
+    s_cap[t] += c;
+    __syncthreads();
   }
   // base of every key (ascending) and of this wave inside it
   uint32_t ib[kPlanKeys];
@@ -515,8 +510,8 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     if (b == kCostBuckets - 1) n_lean = run;
   }
   const uint32_t total_items = run;
-  const bool fits = cap_total <= ev_capacity && total_items <= item_capacity;
-  uint64_t cb = cap_below;
+  const bool fits = s_cap[T - 1] <= ev_capacity && total_items <= item_capacity;
+  uint64_t cb = s_cap[t] - cap;
   for (int i = q0; i < q1; ++i) {
     QueryPlan& p = plan[i];
     const uint32_t bk = plan_key(p.driver);
@@ -544,7 +539,7 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
     if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
     counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
     counters[kCtrLean] = fits ? n_lean : 0u;
-    counters[kCtrEvCap] = static_cast<uint32_t>(cap_total > 0xFFFFFFFFull ? 0xFFFFFFFFull : cap_total);
+    counters[kCtrEvCap] = static_cast<uint32_t>(s_cap[t] > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap[t]);
   }
   // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
   // starts on relative item w without a dequeue, so shard s's head starts past
