@@ -64,6 +64,13 @@ enum { kErrLimit = 1, kErrCapacity = 2 };
 #endif
 constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
+// phrase queries: every survivor also runs the position check, so an item of
+// kSegCost blocks is longer; smaller items keep the queue's tail balanced
+#ifndef WSR_SEG_COST_PHRASE
+#define WSR_SEG_COST_PHRASE 8
+#endif
+constexpr int kSegCostPhrase = WSR_SEG_COST_PHRASE;
+static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSegCost");
 // item cost classes for the longest-first queue order (QueryPlan::driver >> 8);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5

@@ -382,7 +382,8 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
       if (s < q.n_terms && s != static_cast<int>(d))
         cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
                                                 : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
-    uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
+    const bool ph = q.n_terms > 1 && (q.flags & kQueryPhrase);
+    uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : kSegCost) / cost);
     seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
     // cost class of one item (log2 of its block decodes, plus a fixed part
     // for the per-item setup): the queue hands out heavy items first
