@@ -5,7 +5,7 @@ set -eu -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 cd "$R"
 run() {
-  timeout -k 10 300 python3 bench.py --no-cpu --steps 10 --warmup 2 2>/dev/null | python3 -c "import json,sys;d=json.loads(sys.stdin.read());c=d['legs']['c5_phrase'];print('value', d['value'], 'phrase', c['value'], 'phrase_seg', c['segment_ms_per_batch'])"
+  timeout -k 10 300 python3 bench.py --no-cpu --steps 10 --warmup 2 2>/dev/null | python3 -c "import json,sys;d=json.loads(sys.stdin.read());c=d['legs']['c5_phrase'];print('value', d['value'], 'mixed', d['legs']['c4_mixed_1to5']['value'], d['legs']['c4_mixed_1to5']['segment_ms_per_batch'], 'phrase', c['value'], 'phrase_seg', c['segment_ms_per_batch'])"
 }
 for round in 1 2; do
   echo "== default ($round)"; run

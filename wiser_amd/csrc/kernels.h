@@ -71,6 +71,12 @@ static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane
 #endif
 constexpr int kSegCostPhrase = WSR_SEG_COST_PHRASE;
 static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSegCost");
+// conjunctive items of the general (non-bitmap) kernel
+#ifndef WSR_SEG_COST_GENERAL
+#define WSR_SEG_COST_GENERAL 63
+#endif
+constexpr int kSegCostGeneral = WSR_SEG_COST_GENERAL;
+static_assert(kSegCostGeneral <= kSegCost, "the event workspace is sized for kSegCost");
 // item cost classes for the longest-first queue order (QueryPlan::driver >> 8);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5

@@ -383,7 +383,12 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
         cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
                                                 : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
     const bool ph = q.n_terms > 1 && (q.flags & kQueryPhrase);
-    uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : kSegCost) / cost);
+    // lean class: every other list is probed through its bitmap (or none)
+    bool lean = true;
+#pragma unroll
+    for (int s = 0; s < kMaxTerms; ++s)
+      if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
+    uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : lean ? kSegCost : kSegCostGeneral) / cost);
     seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
     // cost class of one item (log2 of its block decodes, plus a fixed part
     // for the per-item setup): the queue hands out heavy items first
@@ -391,11 +396,6 @@ __global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const Que
     const uint32_t ic = static_cast<uint32_t>(item_cost);
     const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
     const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-    // lean class: every other list is probed through its bitmap (or none)
-    bool lean = true;
-#pragma unroll
-    for (int s = 0; s < kMaxTerms; ++s)
-      if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
     p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
     p.seg_blocks = seg;
     p.n_items = (nd + seg - 1) / seg;
