@@ -16,7 +16,7 @@ OBJS    := $(patsubst wiser_amd/csrc/%,$(OBJDIR)/%.o,$(SRCS))
 # -ffp-contract=off everywhere: the reference build has no FMA (CMakeLists.txt:6,12)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall \
             -Wno-unused-function
-ORAFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -shared
+ORAFLAGS := -O3 -DNDEBUG -std=c++17 -fPIC -ffp-contract=off -Wall -shared
 
 CLI     := wiser_amd/_lib/engine_cli
 

@@ -27,9 +27,11 @@
  *                               (flash_engine_dumper.h:674-744) and the query generator
  *                               tools/gen_synthetic_log.py:191-214 (host only, no GPU)
  *
- * Threading: a handle may be used from several threads; calls on one handle
- * are serialised internally (the reference's engine is shared read-only by
- * its gRPC threads, grpc_server_impl.h:260-263).
+ * Threading: a handle may be used from several threads (the reference's
+ * engine is shared read-only by its gRPC threads, grpc_server_impl.h:260-263):
+ * its image is read-only after wsr_open, wsr_search_batch / wsr_search_text
+ * may be called concurrently, and threads that each own a wsr_batch drive
+ * them concurrently (a batch itself is used by one thread at a time).
  */
 #ifndef WISER_HIP_H
 #define WISER_HIP_H
@@ -146,10 +148,26 @@ int wsr_lookup(wsr_handle* h, const char* term, int32_t* list_id, int32_t* doc_f
 /* bytes of docid+tf span held in HBM for a list (0 if absent from this shard) */
 int wsr_list_bytes(wsr_handle* h, int32_t list_id, uint64_t* out);
 
+/* The per-query checks wsr_batch_upload applies (term / k limits, flags, a
+ * phrase query needs positions): WSR_OK or the code upload would return. */
+int wsr_check_query(wsr_handle* h, const wsr_query* q);
+
 /* Run nq queries synchronously.  hits: nq * hit_stride entries (hit_stride >=
  * every query's k); n_hits[q] = entries written for query q. */
 int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t hit_stride,
                      wsr_hit* hits, int32_t* n_hits);
+
+/* Queries as text, the reference's query-log format (QueryProducerByLog,
+ * query_pool.h:319-378): one query per line, terms separated by spaces, a
+ * line in double quotes is a phrase query.  Every term is resolved through the
+ * term index (VacuumInvertedIndex::FindIteratorsSolid, vacuum_engine.h:89-99);
+ * q[0..*nq) receives the queries (k results each). */
+int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t max_q,
+                     wsr_query* q, int32_t* nq);
+/* The whole Search chain from strings: wsr_resolve_text, then wsr_search_batch
+ * (upload, run, results to the host). */
+int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t hit_stride,
+                    int32_t max_q, wsr_hit* hits, int32_t* n_hits, int32_t* nq);
 
 /* ---- resident batches ------------------------------------------------ */
 int wsr_batch_create(wsr_handle* h, int32_t max_queries, int32_t hit_stride, wsr_batch** out);
@@ -263,6 +281,12 @@ int wsr_build_from_linedoc_bloom(const char* linedoc, int64_t n_rows, const char
 int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, double zipf_s,
                         uint64_t seed, int32_t with_positions, int32_t threads,
                         wsr_build_stats* st);
+/* BASELINE configs[2] stand-in: an index whose df histogram follows the
+ * reference's en-Wikipedia one (tools/gen_synthetic_log.py:8-16) scaled by
+ * term_scale, over n_docs docs (writer.h: WikiSpec); lists are streamed to
+ * disk, so host memory does not grow with the corpus */
+int wsr_build_wiki_standin(const char* out_dir, int64_t n_docs, double term_scale, uint64_t seed,
+                           int32_t threads, wsr_build_stats* st);
 int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                          const char* out_path, int64_t* n_written);
 /* mixed 1-5 term AND log (AOL term-count shares; SURVEY 8d "C4") */

@@ -1,0 +1,103 @@
+"""Configs at their stated size on the GPU (C2 was only spot-checked
+by bench.py, C3 never run):
+  * C2 (BASELINE configs[1]): the 1M-doc synthetic Zipf index of bench.py and
+    2,048 queries of its logged two-term workload, bit for bit against the oracle;
+  * C3 stand-in (configs[2]): the en-Wikipedia-shaped corpus (df histogram of
+    gen_synthetic_log.py:8-16) at 1/10 of its terms over 500k docs, its
+    two-term log, bit for bit;
+  * the whole Search chain from query strings (wsr_search_text).
+"""
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c2_full(built, tmp_path_factory):
+    import wiser_amd as w
+    d = str(tmp_path_factory.mktemp("c2full"))
+    st = w.build_synthetic(d, n_docs=1_000_000, vocab=500_000, threads=min(16, os.cpu_count()))
+    log = os.path.join(d, "two_term_100000.log")
+    w.gen_two_term_log(d, log, n_queries=100_000, seed=7)
+    return d, log, st
+
+
+@pytest.fixture(scope="module")
+def c3_small(built, tmp_path_factory):
+    import wiser_amd as w
+    d = str(tmp_path_factory.mktemp("c3small"))
+    st = w.build_wiki_standin(d, n_docs=500_000, term_scale=0.1, threads=min(16, os.cpu_count()))
+    log = os.path.join(d, "two_term.log")
+    w.gen_two_term_log(d, log, n_queries=20_000, seed=7)
+    return d, log, st
+
+
+def _check_log(d, log, nq, k=10, stride=7):
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    lines = [l.split() for l in open(log).read().splitlines()]
+    # spread over the whole log: every stride-th query
+    qs = lines[::stride][:nq]
+    eng = w.VacuumEngine(d, positions=False)
+    eng.Load()
+    res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
+    orc = OracleVacuum(d)
+    want = orc.search_lines(qs, k, threads=min(16, os.cpu_count()))
+    bad = [(q, [(e.doc_id, e.doc_score) for e in r.entries][:3], x[:3])
+           for q, r, x in zip(qs, res, want) if [(e.doc_id, e.doc_score) for e in r.entries] != x]
+    eng.close()
+    orc.close()
+    assert not bad, bad[:3]
+    return sum(1 for x in want if x)
+
+
+def test_c2_full_size_logged_queries(c2_full):
+    d, log, st = c2_full
+    assert st.n_docs == 1_000_000
+    nonempty = _check_log(d, log, 2048)
+    assert nonempty > 500
+
+
+def test_c2_full_size_k64_other_slice(c2_full):
+    # k = 64 (the largest) over another slice of the log
+    d, log, _ = c2_full
+    _check_log(d, log, 512, k=64, stride=97)
+
+
+def test_c3_standin_logged_queries(c3_small):
+    d, log, st = c3_small
+    assert st.n_terms > 500_000
+    _check_log(d, log, 2048, stride=5)
+
+
+def test_search_text_chain(c3_small):
+    """wsr_search_text (strings -> host results) = per-query oracle, including
+    unknown terms, phrase-quoted lines on a positions=0 engine being refused,
+    and blank lines skipped."""
+    import ctypes as C
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from oracle.oracle import OracleVacuum
+    d, log, _ = c3_small
+    lines = open(log).read().splitlines()[:300] + ["nosuchterm w00000001", "", "  w00000002  "]
+    text = "\n".join(lines).encode()
+    eng = w.VacuumEngine(d, positions=False)
+    eng.Load()
+    hits = (_capi.Hit * (len(lines) * 10))()
+    nh = (C.c_int32 * len(lines))()
+    nq = C.c_int32()
+    _capi.check(_capi.lib.wsr_search_text(eng._h, text, len(text), 10, 10, len(lines), hits, nh,
+                                           C.byref(nq)))
+    qs = [l.split() for l in lines if l.strip()]
+    assert nq.value == len(qs)
+    orc = OracleVacuum(d)
+    for i, q in enumerate(qs):
+        got = [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])]
+        assert got == orc.search(q, 10)[0], q
+    bad = b'"w00000001 w00000002"'
+    rc = _capi.lib.wsr_search_text(eng._h, bad, len(bad), 10, 10, 4, hits, nh, C.byref(nq))
+    assert rc == _capi.E_INVALID
+    eng.close()
+    orc.close()

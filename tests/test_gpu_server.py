@@ -69,3 +69,47 @@ def test_closed_loop_bench(synth_small):
     assert 0 < st.p50_ms <= st.p99_ms
     srv.close()
     eng.close()
+
+
+def test_bad_request_fails_alone(synth_small):
+    """one caller's bad query (a phrase query on an engine opened
+    without positions, an unknown flag, k over the limit) fails at submit and
+    never takes the other callers' queries of the same batch down with it."""
+    import ctypes as C
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from oracle.oracle import OracleVacuum
+    d, _ = synth_small
+    eng = w.VacuumEngine(d, positions=False)
+    eng.Load()
+    srv = w.Server(eng, max_batch=256, window_us=2000)
+    orc = OracleVacuum(d)
+    good = [[f"t{i:07d}", f"t{i + 1:07d}"] for i in range(0, 120, 2)]
+    results, errors = {}, {}
+
+    def good_worker(i):
+        r = srv.Search(w.SearchQuery(good[i], n_results=10))
+        results[i] = [(e.doc_id, e.doc_score) for e in r.entries]
+
+    def bad_worker(kind):
+        q = eng.resolve(w.SearchQuery(good[0], n_results=10, is_phrase=(kind == "phrase")))[0]
+        if kind == "flags":
+            q.flags = 6
+        elif kind == "k":
+            q.k = 1000
+        hits = (_capi.Hit * 1024)()
+        nh = C.c_int32()
+        errors[kind] = _capi.lib.wsr_server_search(srv._s, C.byref(q), hits, C.byref(nh))
+
+    ts = [threading.Thread(target=good_worker, args=(i,)) for i in range(len(good))]
+    ts += [threading.Thread(target=bad_worker, args=(k,)) for k in ("phrase", "flags", "k")]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert errors["phrase"] == _capi.E_INVALID and errors["flags"] == _capi.E_INVALID
+    assert errors["k"] == _capi.E_LIMIT
+    for i, q in enumerate(good):
+        assert results[i] == orc.search(q, 10)[0], q
+    srv.close()
+    eng.close()

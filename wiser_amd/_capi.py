@@ -19,6 +19,7 @@ MAX_TERMS = 8
 MAX_K = 64
 
 WSR_OK = 0
+E_INVALID, E_IO, E_HIP, E_LIMIT, E_INTERNAL = -1, -2, -3, -4, -5
 ERRORS = {-1: "WSR_E_INVALID", -2: "WSR_E_IO", -3: "WSR_E_HIP", -4: "WSR_E_LIMIT",
           -5: "WSR_E_INTERNAL"}
 
@@ -85,6 +86,11 @@ _sigs = {
     "wsr_list_bytes": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_uint64)]),
     "wsr_search_batch": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.POINTER(Hit),
                                    C.POINTER(C.c_int32)]),
+    "wsr_check_query": (C.c_int, [_P, C.POINTER(Query)]),
+    "wsr_resolve_text": (C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int32, C.c_int32, C.POINTER(Query),
+                                   C.POINTER(C.c_int32)]),
+    "wsr_search_text": (C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                  C.POINTER(Hit), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_batch_create": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_batch_destroy": (None, [_P, _P]),
     "wsr_batch_upload": (C.c_int, [_P, _P, C.POINTER(Query), C.c_int32]),
@@ -114,6 +120,8 @@ _sigs = {
                                                C.c_float, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_build_synthetic": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_double, C.c_uint64,
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
+    "wsr_build_wiki_standin": (C.c_int, [C.c_char_p, C.c_int64, C.c_double, C.c_uint64,
+                                         C.c_int32, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
     "wsr_batch_ready": (C.c_int, [_P, _P]),

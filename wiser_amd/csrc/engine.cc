@@ -41,8 +41,8 @@ int fail(int code, const std::string& msg) {
       throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(e_));     \
   } while (0)
 
-template <class T>
-void dev_upload(T** dst, const std::vector<T>& src) {
+template <class T, class A>
+void dev_upload(T** dst, const std::vector<T, A>& src) {
   const size_t n = std::max<size_t>(src.size(), 1) * sizeof(T);
   HIP_OK(hipMalloc(reinterpret_cast<void**>(dst), n));
   if (!src.empty()) HIP_OK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
@@ -207,8 +207,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     std::vector<double> cache(h->idx.bm25_cache(), h->idx.bm25_cache() + 256);
     dev_upload(&h->d_cache, cache);
     h->lists = img.lists;
-    h->blocks = img.blocks;
-    h->meta = img.blk_meta;
+    h->blocks.assign(img.blocks.begin(), img.blocks.end());
+    h->meta.assign(img.blk_meta.begin(), img.blk_meta.end());
     h->list_bytes = img.list_bytes;
     h->args.blob = h->d_blob;
     h->args.lists = h->d_lists;
@@ -502,10 +502,21 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   delete b;
 }
 
+int wsr_check_query(wsr_handle* h, const wsr_query* q) {
+  if (!h || !q) return fail(WSR_E_INVALID, "null argument");
+  if (q->n_terms > WSR_MAX_TERMS || q->k > WSR_MAX_K)
+    return fail(WSR_E_LIMIT, "n_terms or k over the limit");
+  if (q->flags & ~WSR_QUERY_PHRASE) return fail(WSR_E_INVALID, "unknown flags");
+  if ((q->flags & WSR_QUERY_PHRASE) && q->n_terms > 1 && !h->positions)
+    return fail(WSR_E_INVALID, "phrase query on an engine opened without positions");
+  return WSR_OK;
+}
+
 int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq) {
   if (!h || !b || (nq > 0 && !q) || nq < 0 || nq > b->max_q)
     return fail(WSR_E_INVALID, "bad upload arguments");
-  std::lock_guard<std::mutex> g(h->mu);
+  // (no handle lock: the handle's image is read-only after wsr_open and the
+  // batch belongs to the caller, so threads with their own batches pipeline)
   std::vector<QueryIn> in(nq);
   uint64_t ev_need = 0, items_need = 0, algo = 0;
   // the device's class rule (plan_query_kernel), restated to size the two
@@ -515,14 +526,11 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   bool has_phrase = false;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
-    if (s.n_terms > WSR_MAX_TERMS || s.k > WSR_MAX_K || s.k > b->stride)
-      return fail(WSR_E_LIMIT, "query " + std::to_string(i) + ": n_terms or k over the limit");
-    if (s.flags & ~WSR_QUERY_PHRASE)
-      return fail(WSR_E_INVALID, "query " + std::to_string(i) + ": unknown flags");
+    if (s.k > b->stride)
+      return fail(WSR_E_LIMIT, "query " + std::to_string(i) + ": k over the batch's hit stride");
+    const int qrc = wsr_check_query(h, &s);
+    if (qrc) return fail(qrc, "query " + std::to_string(i) + ": " + g_err);
     const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
-    if (phrase && !h->positions)
-      return fail(WSR_E_INVALID, "query " + std::to_string(i) +
-                                     ": phrase query on an engine opened without positions");
     has_phrase = has_phrase || phrase;
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
@@ -602,7 +610,6 @@ int wsr_batch_run_events(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, f
 
 static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
-  std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
@@ -653,7 +660,6 @@ int wsr_sync(wsr_handle* h) {
 
 int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits) {
   if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
-  std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
@@ -673,7 +679,6 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
 int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols) {
   if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
   if (cols < 1 || cols > b->stride) return fail(WSR_E_INVALID, "cols must be in [1, hit stride]");
-  std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
@@ -798,6 +803,57 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stri
   }
   if (b) wsr_batch_destroy(h, b);
   return rc;
+}
+
+int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t max_q,
+                     wsr_query* q, int32_t* nq_out) {
+  if (!h || (!text && len > 0) || len < 0 || max_q < 0 || (max_q && !q) || !nq_out || k < 0)
+    return fail(WSR_E_INVALID, "bad resolve_text arguments");
+  // QueryProducerByLog (query_pool.h:319-378): one query per line, terms
+  // separated by spaces, a line in double quotes is a phrase query; each term
+  // through the term index (VacuumInvertedIndex::FindIteratorsSolid,
+  // vacuum_engine.h:89-99)
+  int32_t n = 0;
+  std::string term;
+  for (int64_t at = 0; at < len;) {
+    int64_t e = at;
+    while (e < len && text[e] != '\n') ++e;
+    int64_t a = at, z = e;
+    at = e + 1;
+    while (a < z && (text[a] == ' ' || text[a] == '\r' || text[a] == '\t')) ++a;
+    while (z > a && (text[z - 1] == ' ' || text[z - 1] == '\r' || text[z - 1] == '\t')) --z;
+    if (a == z) continue;
+    if (n >= max_q) return fail(WSR_E_LIMIT, "more than max_q queries in the text");
+    wsr_query& w = q[n];
+    std::memset(&w, 0, sizeof w);
+    if (z - a >= 2 && text[a] == '"' && text[z - 1] == '"') { w.flags = WSR_QUERY_PHRASE; ++a; --z; }
+    w.k = k;
+    for (int64_t i = a; i < z;) {
+      while (i < z && text[i] == ' ') ++i;
+      int64_t j = i;
+      while (j < z && text[j] != ' ') ++j;
+      if (j > i) {
+        if (w.n_terms >= WSR_MAX_TERMS)
+          return fail(WSR_E_LIMIT, "query " + std::to_string(n) + ": more than WSR_MAX_TERMS terms");
+        term.assign(text + i, static_cast<size_t>(j - i));
+        w.list_ids[w.n_terms++] = h->idx.find(term);
+      }
+      i = j;
+    }
+    for (int t = w.n_terms; t < WSR_MAX_TERMS; ++t) w.list_ids[t] = -1;
+    ++n;
+  }
+  *nq_out = n;
+  return WSR_OK;
+}
+
+int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t hit_stride,
+                    int32_t max_q, wsr_hit* hits, int32_t* n_hits, int32_t* nq_out) {
+  if (!h || !nq_out || max_q < 0) return fail(WSR_E_INVALID, "bad search_text arguments");
+  std::vector<wsr_query> q(static_cast<size_t>(max_q));
+  int rc = wsr_resolve_text(h, text, len, k, max_q, q.data(), nq_out);
+  if (rc) return rc;
+  return wsr_search_batch(h, q.data(), *nq_out, hit_stride, hits, n_hits);
 }
 
 int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
@@ -1010,6 +1066,22 @@ int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, doub
     sp.with_positions = with_positions != 0;
     sp.threads = threads;
     fill_stats(build_synthetic(sp, out_dir), st);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_build_wiki_standin(const char* out_dir, int64_t n_docs, double term_scale, uint64_t seed,
+                           int32_t threads, wsr_build_stats* st) {
+  if (!out_dir || n_docs < 16 || !(term_scale > 0)) return fail(WSR_E_INVALID, "bad arguments");
+  try {
+    WikiSpec sp;
+    sp.n_docs = n_docs;
+    sp.term_scale = term_scale;
+    sp.seed = seed;
+    sp.threads = threads;
+    fill_stats(build_wiki_standin(sp, out_dir), st);
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());
   }

@@ -99,15 +99,18 @@ inline void append_pack(std::string* out, const uint32_t* v /*128*/) {
   const int b = pack_bits_for(v, kPackSize);
   out->push_back(static_cast<char>(kPackMagic));
   out->push_back(static_cast<char>(b));
+  // value j at bits [j*b, j*b+b) of a little-endian stream of 64-bit words
+  uint64_t w[2 * 32 + 1] = {0};
+  for (int j = 0; j < kPackSize; ++j) {
+    const uint32_t bit = static_cast<uint32_t>(j) * b;
+    const uint64_t val = v[j];
+    const uint32_t at = bit >> 6, sh = bit & 63;
+    w[at] |= val << sh;
+    if (sh + b > 64) w[at + 1] |= val >> (64 - sh);
+  }
   const size_t base = out->size();
   out->resize(base + 16 * b, 0);
-  uint8_t* d = reinterpret_cast<uint8_t*>(&(*out)[base]);
-  for (int j = 0; j < kPackSize; ++j) {
-    uint64_t bit = static_cast<uint64_t>(j) * b;
-    uint64_t val = v[j];
-    for (int k = 0; k < b; ++k, ++bit)
-      if ((val >> k) & 1) d[bit >> 3] |= static_cast<uint8_t>(1u << (bit & 7));
-  }
+  std::memcpy(&(*out)[base], w, 16 * b);   // (x86 and gfx950 hosts: little-endian)
 }
 
 inline void append_vints(std::string* out, const uint32_t* v, int n) {

@@ -2,10 +2,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <fcntl.h>
 #include <fstream>
+#include <mutex>
 #include <stdexcept>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -89,25 +93,57 @@ void VacuumIndex::open(const std::string& dir) {
   {
     std::ifstream f(dir + "/my.tip", std::ios::binary);
     if (!f) throw std::runtime_error("cannot open " + dir + "/my.tip");
-    std::string all((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-    size_t at = 0;
-    while (at < all.size()) {
+    f.seekg(0, std::ios::end);
+    std::string all(static_cast<size_t>(f.tellg()), '\0');
+    f.seekg(0);
+    f.read(&all[0], all.size());
+    if (!f) throw std::runtime_error("cannot read " + dir + "/my.tip");
+    // entry positions first (sequential), then every list header checked in
+    // parallel (millions of terms: one page of my.vacuum touched per list)
+    struct Ent { size_t at; uint32_t len; uint64_t off, df; };
+    std::vector<Ent> ents;
+    for (size_t at = 0; at < all.size();) {
       if (at + 4 > all.size()) throw std::runtime_error("truncated my.tip");
       uint32_t len;
       std::memcpy(&len, &all[at], 4);
-      at += 4;
-      if (at + len + 8 > all.size()) throw std::runtime_error("truncated my.tip entry");
-      std::string term = all.substr(at, len);
-      at += len;
+      if (at + 4 + len + 8 > all.size()) throw std::runtime_error("truncated my.tip entry");
       int64_t v;
-      std::memcpy(&v, &all[at], 8);
-      at += 8;
-      const uint64_t off = tip_offset(v);
-      if (off + 2 > map_len_ || map_[off] != kPostingListMagic)
-        throw std::runtime_error("posting list of '" + term + "' has a wrong magic byte");
-      uint64_t df = 0;
-      if (!get_varint(map_ + off + 1, map_ + map_len_, &df) || df == 0)
-        throw std::runtime_error("posting list of '" + term + "' has a bad doc freq");
+      std::memcpy(&v, &all[at + 4 + len], 8);
+      ents.push_back(Ent{at + 4, len, tip_offset(v), 0});
+      at += 4 + len + 8;
+    }
+    {
+      const size_t n = ents.size();
+      const int nt = static_cast<int>(std::max<size_t>(1, std::min<size_t>(16, n / 65536)));
+      std::atomic<size_t> bad{~size_t{0}};
+      auto work = [&](int t) {
+        for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+          Ent& e = ents[i];
+          uint64_t df = 0;
+          if (e.off + 2 > map_len_ || map_[e.off] != kPostingListMagic ||
+              !get_varint(map_ + e.off + 1, map_ + map_len_, &df) || df == 0) {
+            size_t cur = bad.load();
+            while (i < cur && !bad.compare_exchange_weak(cur, i)) {}
+            return;
+          }
+          e.df = df;
+        }
+      };
+      std::vector<std::thread> ts;
+      for (int t = 1; t < nt; ++t) ts.emplace_back(work, t);
+      work(0);
+      for (auto& t : ts) t.join();
+      if (bad.load() != ~size_t{0})
+        throw std::runtime_error("posting list of '" + all.substr(ents[bad].at, ents[bad].len) +
+                                 "' has a wrong magic byte or a bad doc freq");
+    }
+    lookup_.reserve(ents.size());
+    terms_.reserve(ents.size());
+    off_.reserve(ents.size());
+    df_.reserve(ents.size());
+    for (const Ent& e : ents) {
+      std::string term = all.substr(e.at, e.len);
+      const uint64_t off = e.off, df = e.df;
       auto ins = lookup_.emplace(term, static_cast<int32_t>(terms_.size()));
       if (!ins.second) { // later entries win, as htrie_map assignment does
         const int32_t id = ins.first->second;
@@ -129,6 +165,12 @@ void VacuumIndex::open(const std::string& dir) {
 }
 
 std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
+  std::vector<SkipRow> out;
+  rows_into(id, &out);
+  return out;
+}
+
+void VacuumIndex::rows_into(int32_t id, std::vector<SkipRow>* dst) const {
   const uint8_t* end = map_ + map_len_;
   const uint8_t* p = map_ + off_[id];
   uint64_t v;
@@ -139,7 +181,9 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
   uint64_t n = 0;
   l = get_varint(p + 1, end, &n);
   p += 1 + l;
-  std::vector<SkipRow> out(n);
+  if (n > map_len_) throw std::runtime_error("bad skip list length");
+  std::vector<SkipRow>& out = *dst;
+  out.resize(n);
   // fields: d prev_doc, d docid off, d tf off, d pos off, pos idx, d off off, off idx
   uint64_t pd = 0, pdo = 0, pto = 0, ppo = 0, poo = 0;
   for (uint64_t r = 0; r < n; ++r) {
@@ -154,7 +198,6 @@ std::vector<SkipRow> VacuumIndex::rows(int32_t id) const {
     out[r] = SkipRow{static_cast<uint32_t>(pd), pdo, pto, ppo, static_cast<uint32_t>(f[4]), poo,
                      static_cast<uint32_t>(f[6])};
   }
-  return out;
 }
 
 bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta,
@@ -197,6 +240,36 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
   return true;
 }
 
+namespace {
+// Runs fn(id) for every list id on `threads` threads; the first exception wins.
+template <class F>
+void for_each_list(int32_t L, int threads, F&& fn) {
+  std::atomic<int32_t> next{0};
+  std::atomic<bool> failed{false};
+  std::string err;
+  std::mutex err_mu;
+  auto work = [&](int worker) {
+    try {
+      // small lists dominate the count: take them 256 at a time
+      for (int32_t s; (s = next.fetch_add(256)) < L && !failed;)
+        for (int32_t id = s; id < std::min(L, s + 256) && !failed; ++id) fn(id, worker);
+    } catch (const std::exception& ex) {
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!failed.exchange(true)) err = ex.what();
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int i = 1; i < threads; ++i) ts.emplace_back(work, i);
+  work(0);
+  for (auto& t : ts) t.join();
+  if (failed) throw std::runtime_error(err);
+}
+}  // namespace
+
+// Three passes over the lists, none of which allocates per list: (1) size the
+// list's part of every image array, (2) prefix sums in list-id order, (3) fill
+// the arrays in place.  (Millions of one-block lists -- the en-Wikipedia shape
+// -- made per-list vectors and their serial concatenation the load's cost.)
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
                       uint32_t dense_div, bool positions) {
   const int32_t L = idx.n_lists();
@@ -206,267 +279,297 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   const uint64_t span_end = std::min<uint64_t>(doc_hi, static_cast<uint64_t>(std::max(idx.n_docs(), 0)));
   const uint32_t span = span_end > doc_lo ? static_cast<uint32_t>(span_end - doc_lo) : 0u;
   const uint64_t n_ent = (static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs;
-  struct Part {
-    std::vector<BlockDev> blocks;  // doc_rel / tf_rel relative to the list's span
-    std::vector<uint32_t> meta;
-    std::vector<uint8_t> bytes;    // docid span followed by tf span
-    uint32_t tail_cnt = 0;
-    std::vector<DenseEnt> dense;   // rank bitmap (dense lists only)
-    std::vector<uint8_t> tf8;
-    std::vector<uint8_t> plen;     // doc-length code of every posting, 128 per block
-    std::vector<uint32_t> tail;    // VInts last block decoded: doc ids, then tfs
-    // positions: the whole box, its pack directory, VInts remainder, bag starts
-    std::vector<uint8_t> pos_bytes;
-    std::vector<uint32_t> pos_pk;
-    std::vector<uint32_t> pos_tail;
-    std::vector<uint32_t> pos_start;
-  };
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
-  std::vector<Part> parts(L);
-  // decode the image's postings of one list and lay down its bitmap + tf bytes
-  auto build_dense = [&](Part& pt, const std::vector<SkipRow>& rows, uint64_t r0, uint64_t r1,
-                         uint64_t n_img) {
-    std::vector<uint32_t> docs(n_img), tfs(n_img);
-    for (uint64_t r = r0; r < r1; ++r) {
-      const int cnt = r + 1 == r1 ? static_cast<int>(pt.tail_cnt) : kPackSize;
-      const uint64_t at = (r - r0) * kPackSize;
-      if (!host_decode_block(file + rows[r].doc_off, fend, cnt, true, rows[r].prev_doc, &docs[at]) ||
-          !host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, &tfs[at]))
-        throw std::runtime_error("cannot decode a block for the dense image");
-    }
-    // a doc inside [doc_lo, doc_hi) but past the doc-length records cannot be
-    // represented: keep the list on the block path
-    for (uint64_t i = 0; i < n_img; ++i)
-      if (docs[i] >= doc_lo && docs[i] < doc_hi && docs[i] - doc_lo >= span) return;
-    pt.dense.assign(n_ent, DenseEnt{0, 0});
-    uint64_t i = 0;
-    for (uint64_t e = 0; e < n_ent; ++e) {
-      const uint64_t start = doc_lo + e * kDenseDocs;
-      while (i < n_img && docs[i] < start) ++i;
-      pt.dense[e].rank = static_cast<uint32_t>(i);
-      for (uint64_t j = i; j < n_img && docs[j] < start + kDenseDocs; ++j) {
-        const uint32_t bit = static_cast<uint32_t>(docs[j] - start);
-        pt.dense[e].w |= 1u << bit;
-      }
-    }
-    pt.tf8.resize(n_img);
-    for (uint64_t j = 0; j < n_img; ++j) pt.tf8[j] = static_cast<uint8_t>(tfs[j] < kTf8Escape ? tfs[j] : kTf8Escape);
+  struct Info {            // pass 1: the list's share of the image
+    uint32_t r0 = 0, r1 = 0;   // image rows [r0, r1); r0 >= r1: no docs in the image
+    uint32_t fcnt = 0;         // postings of the list's final row
+    uint32_t tail_cnt = 0;     // postings of the image's last row
+    uint64_t bytes = 0;        // docid span + tf span
+    uint8_t dense = 0, vtail = 0;
   };
-  // The list's position cozy box (flash_engine_dumper.h:78-104): the bag of
-  // posting p holds tf(p) entries starting at entry sum(tf before p).  Walked
-  // from row 0's blob; every skip row's (blob, in-blob index) must agree with
-  // the walk (PositionPostingBagIterator::GoToSkipPostingBag, flash_iterators.h:504-513).
-  auto build_positions = [&](Part& pt, const std::vector<SkipRow>& rows, uint64_t r0, uint64_t r1,
-                             int fcnt, const std::string& term) {
-    const uint64_t nrows = rows.size();
-    std::vector<uint64_t> cum(nrows * kPackSize + 1, 0);
-    uint64_t n = 0;
-    for (uint64_t r = 0; r < nrows; ++r) {
-      const int cnt = r + 1 == nrows ? fcnt : kPackSize;
-      uint32_t tfs[kPackSize];
-      if (!host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, tfs))
-        throw std::runtime_error("cannot decode the tfs of '" + term + "'");
-      for (int i = 0; i < cnt; ++i) { cum[n + 1] = cum[n] + tfs[i]; ++n; }
-    }
-    const uint64_t total = cum[n];
-    if (total >= (1ull << 32)) throw std::runtime_error("position box of '" + term + "' over 2^32 entries");
-    const uint64_t p0 = rows[0].pos_off;
-    const uint64_t npk = total / kPackSize, rem = total % kPackSize;
-    std::vector<uint64_t> blob_at(npk + (rem ? 1 : 0));
-    uint64_t at = p0;
-    for (uint64_t k = 0; k < npk; ++k) {
-      const uint8_t* b = file + at;
-      if (b + 2 > fend || b[0] != kPackMagic || b[1] < 1 || b[1] > 32)
-        throw std::runtime_error("bad position pack in '" + term + "'");
-      blob_at[k] = at;
-      pt.pos_pk.push_back(static_cast<uint32_t>(at - p0));
-      pt.pos_pk.push_back(b[1]);
-      at += 2 + 16ull * b[1];
-    }
-    if (rem) {
-      blob_at[npk] = at;
-      pt.pos_tail.resize(rem);
-      if (file[at] != kVIntsMagic ||
-          !host_decode_block(file + at, fend, static_cast<int>(rem), false, 0, pt.pos_tail.data()))
-        throw std::runtime_error("bad position VInts blob in '" + term + "'");
-      at += blob_bytes(file + at, fend);
-    }
-    if (at > idx.file_bytes() || at - p0 >= (1ull << 32))
-      throw std::runtime_error("position box of '" + term + "' out of range");
-    for (uint64_t r = 0; r < nrows; ++r) {
-      const uint64_t e = cum[r * kPackSize];
-      if (rows[r].pos_off != blob_at[e / kPackSize] || rows[r].pos_idx != e % kPackSize)
-        throw std::runtime_error("skip row position pointer disagrees with the box of '" + term + "'");
-    }
-    pt.pos_bytes.assign(file + p0, file + at);
-    pt.pos_start.assign((r1 - r0) * kPackSize, 0);
-    for (uint64_t r = r0; r < r1; ++r)
-      for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
-        pt.pos_start[(r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i]);
-  };
-  std::atomic<int32_t> next{0};
-  std::atomic<bool> failed{false};
-  std::string err;
-  auto work = [&] {
-    try {
-      for (int32_t id; (id = next++) < L && !failed;) {
-        const std::vector<SkipRow> rows = idx.rows(id);
-        const uint32_t df = idx.df(id);
-        const uint64_t nrows = rows.size();
-        if (nrows != (df + kPackSize - 1) / kPackSize)
-          throw std::runtime_error("skip rows do not match df for '" + idx.term(id) + "'");
-        // last doc of each block: prev of the next row; decode the final block.
-        std::vector<uint32_t> last(nrows);
-        for (uint64_t r = 0; r + 1 < nrows; ++r) last[r] = rows[r + 1].prev_doc;
-        const int fcnt = static_cast<int>(df - kPackSize * (nrows - 1));
-        {
-          uint32_t tmp[kPackSize];
-          if (!host_decode_block(file + rows[nrows - 1].doc_off, fend, fcnt, true,
-                                 rows[nrows - 1].prev_doc, tmp))
-            throw std::runtime_error("cannot decode the last block of '" + idx.term(id) + "'");
-          last[nrows - 1] = tmp[fcnt - 1];
-        }
-        // blocks whose docs can fall into [doc_lo, doc_hi): docs of block r lie in
-        // (prev_doc, last] (block 0: [first, last]).
-        uint64_t r0 = nrows, r1 = 0;
-        for (uint64_t r = 0; r < nrows; ++r) {
-          const bool below_hi = (r == 0) || (static_cast<uint64_t>(rows[r].prev_doc) + 1 < doc_hi);
-          if (below_hi && last[r] >= doc_lo) { r0 = std::min(r0, r); r1 = r + 1; }
-        }
-        Part& pt = parts[id];
-        if (r0 >= r1) continue;  // list has no docs in this shard
-        const uint64_t d0 = rows[r0].doc_off;
-        const uint64_t d1 = rows[r1 - 1].doc_off + blob_bytes(file + rows[r1 - 1].doc_off, fend);
-        const uint64_t t0 = rows[r0].tf_off;
-        const uint64_t t1 = rows[r1 - 1].tf_off + blob_bytes(file + rows[r1 - 1].tf_off, fend);
-        if (d1 <= d0 || t1 <= t0 || d1 > idx.file_bytes() || t1 > idx.file_bytes())
-          throw std::runtime_error("bad blob span for '" + idx.term(id) + "'");
-        pt.bytes.assign(file + d0, file + d1);
-        pt.bytes.insert(pt.bytes.end(), file + t0, file + t1);
-        for (uint64_t r = r0; r < r1; ++r) {
-          pt.blocks.push_back(BlockDev{rows[r].prev_doc, last[r],
-                                       static_cast<uint32_t>(rows[r].doc_off - d0),
-                                       static_cast<uint32_t>((d1 - d0) + rows[r].tf_off - t0)});
-          const uint8_t* pd = file + rows[r].doc_off;
-          const uint8_t* pf = file + rows[r].tf_off;
-          const uint32_t bd = pd[0] == kPackMagic ? pd[1] : 0u;
-          const uint32_t bf = pf[0] == kPackMagic ? pf[1] : 0u;
-          if ((pd[0] != kPackMagic && pd[0] != kVIntsMagic) || (pf[0] != kPackMagic && pf[0] != kVIntsMagic) ||
-              bd > 32 || bf > 32 || (pd[0] == kPackMagic && bd == 0) || (pf[0] == kPackMagic && bf == 0))
-            throw std::runtime_error("bad blob header in '" + idx.term(id) + "'");
-          pt.meta.push_back(bd | (bf << 8));
-        }
-        pt.tail_cnt = (r1 == nrows) ? static_cast<uint32_t>(fcnt) : kPackSize;
-        // doc-length codes in posting order: a block's 128 codes are one
-        // contiguous line for the kernels instead of a gather over the doc ids
-        // (docs past the length records get code 0, as in the kernels)
-        pt.plen.assign((r1 - r0) * kPackSize, 0);
-        for (uint64_t r = r0; r < r1; ++r) {
-          const int cnt = r + 1 == nrows ? fcnt : kPackSize;
-          uint32_t docs[kPackSize];
-          if (!host_decode_block(file + rows[r].doc_off, fend, cnt, true, rows[r].prev_doc, docs))
-            throw std::runtime_error("cannot decode a block of '" + idx.term(id) + "'");
-          uint8_t* o = &pt.plen[(r - r0) * kPackSize];
-          for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
-          if (r + 1 == nrows && (pt.meta.back() & 0xFF) == 0) {
-            // the list's VInts tail, decoded once (the kernels read it as words)
-            uint32_t tfs[kPackSize];
-            if (!host_decode_block(file + rows[r].tf_off, fend, cnt, false, 0, tfs))
-              throw std::runtime_error("cannot decode the tf tail of '" + idx.term(id) + "'");
-            pt.tail.assign(docs, docs + cnt);
-            pt.tail.insert(pt.tail.end(), tfs, tfs + cnt);
-          }
-        }
-        const uint64_t n_img = (r1 - r0 - 1) * kPackSize + pt.tail_cnt;
-        if (dense_div && span && n_img * dense_div >= span) build_dense(pt, rows, r0, r1, n_img);
-        if (positions) build_positions(pt, rows, r0, r1, fcnt, idx.term(id));
-      }
-    } catch (const std::exception& ex) {
-      if (!failed.exchange(true)) err = ex.what();
-    }
+  std::vector<Info> info(L);
+  struct Scratch {   // per worker thread, reused from list to list
+    std::vector<SkipRow> rows;
+    std::vector<uint32_t> last, docs, tfs;
   };
   if (threads < 1) threads = 1;
-  std::vector<std::thread> ts;
-  for (int i = 0; i < threads; ++i) ts.emplace_back(work);
-  for (auto& t : ts) t.join();
-  if (failed) throw std::runtime_error(err);
+  std::vector<Scratch> scratch(threads);
+  // rows and last doc of every row (prev of the next row; the final row decoded)
+  auto load_rows = [&](int32_t id, Scratch& s, uint32_t* fcnt) {
+    idx.rows_into(id, &s.rows);
+    const uint32_t df = idx.df(id);
+    const uint64_t nrows = s.rows.size();
+    if (nrows == 0 || nrows != (df + kPackSize - 1) / kPackSize)
+      throw std::runtime_error("skip rows do not match df for '" + idx.term(id) + "'");
+    s.last.resize(nrows);
+    for (uint64_t r = 0; r + 1 < nrows; ++r) s.last[r] = s.rows[r + 1].prev_doc;
+    *fcnt = static_cast<uint32_t>(df - kPackSize * (nrows - 1));
+    uint32_t tmp[kPackSize];
+    if (!host_decode_block(file + s.rows[nrows - 1].doc_off, fend, static_cast<int>(*fcnt), true,
+                           s.rows[nrows - 1].prev_doc, tmp))
+      throw std::runtime_error("cannot decode the last block of '" + idx.term(id) + "'");
+    s.last[nrows - 1] = tmp[*fcnt - 1];
+  };
+  auto row_cnt = [](const Info& in, uint64_t r, uint64_t nrows) {
+    return r + 1 == nrows ? static_cast<int>(in.fcnt) : kPackSize;
+  };
 
+  const bool timing = std::getenv("WSR_LOAD_TIMING") != nullptr;
+  auto t_mark = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[wsr load] %s %.3f s\n", what, std::chrono::duration<double>(now - t_mark).count());
+    t_mark = now;
+  };
+  // ---- pass 1
+  for_each_list(L, threads, [&](int32_t id, int worker) {
+    Scratch& s = scratch[worker];
+    Info& in = info[id];
+    load_rows(id, s, &in.fcnt);
+    const uint64_t nrows = s.rows.size();
+    // blocks whose docs can fall into [doc_lo, doc_hi): docs of block r lie in
+    // (prev_doc, last] (block 0: [first, last]).
+    uint64_t r0 = nrows, r1 = 0;
+    for (uint64_t r = 0; r < nrows; ++r) {
+      const bool below_hi = (r == 0) || (static_cast<uint64_t>(s.rows[r].prev_doc) + 1 < doc_hi);
+      if (below_hi && s.last[r] >= doc_lo) { r0 = std::min(r0, r); r1 = r + 1; }
+    }
+    if (r0 >= r1) { in.r0 = in.r1 = 0; return; }
+    in.r0 = static_cast<uint32_t>(r0);
+    in.r1 = static_cast<uint32_t>(r1);
+    const uint64_t d0 = s.rows[r0].doc_off;
+    const uint64_t d1 = s.rows[r1 - 1].doc_off + blob_bytes(file + s.rows[r1 - 1].doc_off, fend);
+    const uint64_t t0 = s.rows[r0].tf_off;
+    const uint64_t t1 = s.rows[r1 - 1].tf_off + blob_bytes(file + s.rows[r1 - 1].tf_off, fend);
+    if (d1 <= d0 || t1 <= t0 || d1 > idx.file_bytes() || t1 > idx.file_bytes() ||
+        d1 - d0 + (t1 - t0) >= (1ull << 32))
+      throw std::runtime_error("bad blob span for '" + idx.term(id) + "'");
+    in.bytes = (d1 - d0) + (t1 - t0);
+    in.tail_cnt = (r1 == nrows) ? in.fcnt : kPackSize;
+    in.vtail = r1 == nrows && file[s.rows[nrows - 1].doc_off] == kVIntsMagic;
+    const uint64_t n_img = (r1 - r0 - 1) * kPackSize + in.tail_cnt;
+    if (dense_div && span && n_img * dense_div >= span) {
+      // a doc inside [doc_lo, doc_hi) but past the doc-length records cannot be
+      // represented in a bitmap: such a list stays on the block path
+      bool ok = true;
+      const uint64_t lim = static_cast<uint64_t>(doc_lo) + span;
+      for (uint64_t r = r0; r < r1 && ok; ++r) {
+        if (s.last[r] < lim) continue;
+        if (r > 0 && static_cast<uint64_t>(s.rows[r].prev_doc) + 1 >= doc_hi) continue;
+        uint32_t docs[kPackSize];
+        const int cnt = row_cnt(in, r, nrows);
+        if (!host_decode_block(file + s.rows[r].doc_off, fend, cnt, true, s.rows[r].prev_doc, docs))
+          throw std::runtime_error("cannot decode a block for the dense image");
+        for (int i = 0; i < cnt; ++i)
+          if (docs[i] >= lim && docs[i] < doc_hi) ok = false;
+      }
+      in.dense = ok;
+    }
+  });
+
+  lap("pass 1 (sizes)");
+  // ---- pass 2: offsets in list-id order
   HostImage img;
   img.doc_lo = doc_lo;
   img.doc_hi = doc_hi;
   img.dense_span = span;
   img.lists.resize(L);
   img.list_bytes.resize(L);
-  uint64_t total = 0, nb = 0;
-  for (auto& p : parts) { total += (p.bytes.size() + 15) & ~15ull; nb += p.blocks.size(); }
-  img.blob.resize(total + 64, 0);  // tail pad: lanes read whole dwords past a blob end
-  img.blocks.reserve(nb);
-  img.blk_last.reserve(nb);
-  img.blk_meta.reserve(nb);
-  img.plen.reserve(nb * kPackSize);
   img.has_positions = positions;
-  if (positions) {
-    uint64_t pb = 0;
-    for (auto& p : parts) pb += (p.pos_bytes.size() + 15) & ~15ull;
-    img.pos_blob.resize(pb + 64, 0);   // tail pad: lanes read whole dwords
-    img.pos_lists.resize(L, PosDev{0, 0, 0, 0});
-    img.pos_start.reserve(nb * kPackSize);
-    uint64_t pat = 0;
-    for (int32_t id = 0; id < L; ++id) {
-      Part& p = parts[id];
-      PosDev& pd = img.pos_lists[id];
-      pd.base = pat;
-      pd.pk0 = static_cast<uint32_t>(img.pos_pk.size() / 2);
-      pd.npk = static_cast<uint32_t>(p.pos_pk.size() / 2);
-      pd.tail = img.pos_tail.size();
-      if (!p.pos_bytes.empty()) std::memcpy(&img.pos_blob[pat], p.pos_bytes.data(), p.pos_bytes.size());
-      pat += (p.pos_bytes.size() + 15) & ~15ull;
-      img.pos_pk.insert(img.pos_pk.end(), p.pos_pk.begin(), p.pos_pk.end());
-      img.pos_tail.insert(img.pos_tail.end(), p.pos_tail.begin(), p.pos_tail.end());
-      img.pos_start.insert(img.pos_start.end(), p.pos_start.begin(), p.pos_start.end());
-      std::vector<uint8_t>().swap(p.pos_bytes);
-      std::vector<uint32_t>().swap(p.pos_pk);
-      std::vector<uint32_t>().swap(p.pos_tail);
-      std::vector<uint32_t>().swap(p.pos_start);
-    }
-  }
-  uint64_t at = 0;
+  uint64_t at = 0, nb = 0, ne = 0, ntf8 = 0, ntail = 0;
   for (int32_t id = 0; id < L; ++id) {
-    Part& p = parts[id];
+    const Info& in = info[id];
     ListDev& ld = img.lists[id];
+    const uint32_t nbl = in.r1 > in.r0 ? in.r1 - in.r0 : 0u;
     ld.base = at;
-    ld.blk0 = static_cast<uint32_t>(img.blocks.size());
-    ld.nblk = static_cast<uint32_t>(p.blocks.size());
+    ld.blk0 = static_cast<uint32_t>(nb);
+    ld.nblk = nbl;
     ld.df = idx.df(id);
-    ld.tail_cnt = p.tail_cnt;
+    ld.tail_cnt = nbl ? in.tail_cnt : 0u;
     ld.idf = idx.idf(id);
     ld.bm = kNoDense;
     ld.tf8 = 0;
     ld.tail = kNoTail;
     ld.pad = 0;
-    if (!p.tail.empty()) {
-      ld.tail = img.tails.size();
-      img.tails.insert(img.tails.end(), p.tail.begin(), p.tail.end());
-      std::vector<uint32_t>().swap(p.tail);
-    }
-    if (!p.dense.empty()) {
-      ld.bm = img.dense.size();
-      ld.tf8 = img.tf8.size();
-      img.dense.insert(img.dense.end(), p.dense.begin(), p.dense.end());
-      img.tf8.insert(img.tf8.end(), p.tf8.begin(), p.tf8.end());
+    if (!nbl) { img.list_bytes[id] = 0; continue; }
+    if (in.vtail) { ld.tail = ntail; ntail += 2ull * in.tail_cnt; }
+    if (in.dense) {
+      ld.bm = ne;
+      ld.tf8 = ntf8;
+      ne += n_ent;
+      ntf8 += (nbl - 1) * static_cast<uint64_t>(kPackSize) + in.tail_cnt;
       ++img.dense_lists;
-      std::vector<DenseEnt>().swap(p.dense);
-      std::vector<uint8_t>().swap(p.tf8);
     }
-    if (!p.bytes.empty()) std::memcpy(&img.blob[at], p.bytes.data(), p.bytes.size());
-    img.docid_tf_bytes += p.bytes.size();
-    img.list_bytes[id] = p.bytes.size();
-    at += (p.bytes.size() + 15) & ~15ull;
-    for (auto& b : p.blocks) { img.blocks.push_back(b); img.blk_last.push_back(b.last); }
-    img.blk_meta.insert(img.blk_meta.end(), p.meta.begin(), p.meta.end());
-    img.plen.insert(img.plen.end(), p.plen.begin(), p.plen.end());
-    std::vector<uint8_t>().swap(p.bytes);
-    std::vector<uint8_t>().swap(p.plen);
+    img.list_bytes[id] = in.bytes;
+    img.docid_tf_bytes += in.bytes;
+    at += (in.bytes + 15) & ~15ull;
+    nb += nbl;
+  }
+  if (nb >= (1ull << 32)) throw std::runtime_error("more than 2^32 blocks in one image");
+  // (every byte of these is written by pass 3, in parallel)
+  img.blob.resize(at + 64);   // tail pad: lanes read whole dwords past a blob end
+  std::memset(&img.blob[at], 0, 64);
+  img.blocks.resize(nb);
+  img.blk_last.resize(nb);
+  img.blk_meta.resize(nb);
+  img.plen.resize(nb * kPackSize);
+  img.tails.resize(ntail);
+  img.dense.resize(ne);
+  img.tf8.resize(ntf8);
+
+  lap("pass 2 (offsets, allocation)");
+  // ---- pass 3: fill in place
+  struct PosPart {   // positions (phrase engines only): the list's box, packs, bag starts
+    std::vector<uint8_t> bytes;
+    std::vector<uint32_t> pk, tail;
+  };
+  std::vector<PosPart> pos_parts(positions ? L : 0);
+  if (positions) img.pos_start.assign(nb * kPackSize, 0);
+  for_each_list(L, threads, [&](int32_t id, int worker) {
+    const Info& in = info[id];
+    if (in.r1 <= in.r0) return;
+    Scratch& s = scratch[worker];
+    uint32_t fcnt;
+    load_rows(id, s, &fcnt);
+    const uint64_t nrows = s.rows.size();
+    const uint64_t r0 = in.r0, r1 = in.r1;
+    const ListDev& ld = img.lists[id];
+    const uint64_t d0 = s.rows[r0].doc_off;
+    const uint64_t d1 = s.rows[r1 - 1].doc_off + blob_bytes(file + s.rows[r1 - 1].doc_off, fend);
+    const uint64_t t0 = s.rows[r0].tf_off;
+    const uint64_t t1 = s.rows[r1 - 1].tf_off + blob_bytes(file + s.rows[r1 - 1].tf_off, fend);
+    std::memcpy(&img.blob[ld.base], file + d0, d1 - d0);
+    std::memcpy(&img.blob[ld.base + (d1 - d0)], file + t0, t1 - t0);
+    const uint64_t gap = ((in.bytes + 15) & ~15ull) - in.bytes;   // alignment padding
+    if (gap) std::memset(&img.blob[ld.base + in.bytes], 0, gap);
+    const uint64_t n_img = (r1 - r0 - 1) * kPackSize + in.tail_cnt;
+    if (in.dense) { s.docs.resize(n_img); s.tfs.resize(n_img); }
+    for (uint64_t r = r0; r < r1; ++r) {
+      const uint64_t j = ld.blk0 + (r - r0);
+      img.blocks[j] = BlockDev{s.rows[r].prev_doc, s.last[r], static_cast<uint32_t>(s.rows[r].doc_off - d0),
+                               static_cast<uint32_t>((d1 - d0) + s.rows[r].tf_off - t0)};
+      img.blk_last[j] = s.last[r];
+      const uint8_t* pd = file + s.rows[r].doc_off;
+      const uint8_t* pf = file + s.rows[r].tf_off;
+      const uint32_t bd = pd[0] == kPackMagic ? pd[1] : 0u;
+      const uint32_t bf = pf[0] == kPackMagic ? pf[1] : 0u;
+      if ((pd[0] != kPackMagic && pd[0] != kVIntsMagic) || (pf[0] != kPackMagic && pf[0] != kVIntsMagic) ||
+          bd > 32 || bf > 32 || (pd[0] == kPackMagic && bd == 0) || (pf[0] == kPackMagic && bf == 0))
+        throw std::runtime_error("bad blob header in '" + idx.term(id) + "'");
+      img.blk_meta[j] = bd | (bf << 8);
+      // doc-length codes in posting order: a block's 128 codes are one
+      // contiguous line for the kernels instead of a gather over the doc ids
+      // (docs past the length records get code 0, as in the kernels)
+      const int cnt = row_cnt(in, r, nrows);
+      uint32_t docs[kPackSize], tfs[kPackSize];
+      if (!host_decode_block(pd, fend, cnt, true, s.rows[r].prev_doc, docs))
+        throw std::runtime_error("cannot decode a block of '" + idx.term(id) + "'");
+      uint8_t* o = &img.plen[j * kPackSize];
+      for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
+      for (int i = cnt; i < kPackSize; ++i) o[i] = 0;
+      const bool last_vints = in.vtail && r + 1 == nrows;
+      if (in.dense || last_vints)
+        if (!host_decode_block(pf, fend, cnt, false, 0, tfs))
+          throw std::runtime_error("cannot decode the tfs of '" + idx.term(id) + "'");
+      if (last_vints) {   // the list's VInts tail, decoded once (the kernels read it as words)
+        std::memcpy(&img.tails[ld.tail], docs, cnt * sizeof(uint32_t));
+        std::memcpy(&img.tails[ld.tail + cnt], tfs, cnt * sizeof(uint32_t));
+      }
+      if (in.dense) {
+        std::memcpy(&s.docs[(r - r0) * kPackSize], docs, cnt * sizeof(uint32_t));
+        std::memcpy(&s.tfs[(r - r0) * kPackSize], tfs, cnt * sizeof(uint32_t));
+      }
+    }
+    if (in.dense) {
+      // rank bitmap: per 32 docs, the postings before them and the doc mask
+      DenseEnt* de = &img.dense[ld.bm];
+      uint64_t i = 0;
+      for (uint64_t e = 0; e < n_ent; ++e) {
+        const uint64_t start = doc_lo + e * kDenseDocs;
+        while (i < n_img && s.docs[i] < start) ++i;
+        de[e].rank = static_cast<uint32_t>(i);
+        uint32_t wbits = 0;
+        for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j)
+          wbits |= 1u << static_cast<uint32_t>(s.docs[j] - start);
+        de[e].w = wbits;
+      }
+      uint8_t* t8 = &img.tf8[ld.tf8];
+      for (uint64_t j = 0; j < n_img; ++j) t8[j] = static_cast<uint8_t>(s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape);
+    }
+    if (positions) {
+      // The list's position cozy box (flash_engine_dumper.h:78-104): the bag of
+      // posting p holds tf(p) entries starting at entry sum(tf before p).  Walked
+      // from row 0's blob; every skip row's (blob, in-blob index) must agree with
+      // the walk (PositionPostingBagIterator::GoToSkipPostingBag, flash_iterators.h:504-513).
+      PosPart& pt = pos_parts[id];
+      const std::string& term = idx.term(id);
+      std::vector<uint64_t> cum(nrows * kPackSize + 1, 0);
+      uint64_t n = 0;
+      for (uint64_t r = 0; r < nrows; ++r) {
+        const int cnt = row_cnt(in, r, nrows);
+        uint32_t tfs[kPackSize];
+        if (!host_decode_block(file + s.rows[r].tf_off, fend, cnt, false, 0, tfs))
+          throw std::runtime_error("cannot decode the tfs of '" + term + "'");
+        for (int i = 0; i < cnt; ++i) { cum[n + 1] = cum[n] + tfs[i]; ++n; }
+      }
+      const uint64_t total = cum[n];
+      if (total >= (1ull << 32)) throw std::runtime_error("position box of '" + term + "' over 2^32 entries");
+      const uint64_t p0 = s.rows[0].pos_off;
+      const uint64_t npk = total / kPackSize, rem = total % kPackSize;
+      std::vector<uint64_t> blob_at(npk + (rem ? 1 : 0));
+      uint64_t pa = p0;
+      for (uint64_t k = 0; k < npk; ++k) {
+        const uint8_t* b = file + pa;
+        if (b + 2 > fend || b[0] != kPackMagic || b[1] < 1 || b[1] > 32)
+          throw std::runtime_error("bad position pack in '" + term + "'");
+        blob_at[k] = pa;
+        pt.pk.push_back(static_cast<uint32_t>(pa - p0));
+        pt.pk.push_back(b[1]);
+        pa += 2 + 16ull * b[1];
+      }
+      if (rem) {
+        blob_at[npk] = pa;
+        pt.tail.resize(rem);
+        if (file[pa] != kVIntsMagic ||
+            !host_decode_block(file + pa, fend, static_cast<int>(rem), false, 0, pt.tail.data()))
+          throw std::runtime_error("bad position VInts blob in '" + term + "'");
+        pa += blob_bytes(file + pa, fend);
+      }
+      if (pa > idx.file_bytes() || pa - p0 >= (1ull << 32))
+        throw std::runtime_error("position box of '" + term + "' out of range");
+      for (uint64_t r = 0; r < nrows; ++r) {
+        const uint64_t e = cum[r * kPackSize];
+        if (s.rows[r].pos_off != blob_at[e / kPackSize] || s.rows[r].pos_idx != e % kPackSize)
+          throw std::runtime_error("skip row position pointer disagrees with the box of '" + term + "'");
+      }
+      pt.bytes.assign(file + p0, file + pa);
+      for (uint64_t r = r0; r < r1; ++r)
+        for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
+          img.pos_start[(ld.blk0 + r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i]);
+    }
+  });
+
+  lap("pass 3 (fill)");
+  if (positions) {
+    uint64_t pb = 0;
+    for (auto& p : pos_parts) pb += (p.bytes.size() + 15) & ~15ull;
+    img.pos_blob.resize(pb + 64, 0);   // tail pad: lanes read whole dwords
+    img.pos_lists.resize(L, PosDev{0, 0, 0, 0});
+    uint64_t pat = 0;
+    for (int32_t id = 0; id < L; ++id) {
+      PosPart& p = pos_parts[id];
+      PosDev& pd = img.pos_lists[id];
+      pd.base = pat;
+      pd.pk0 = static_cast<uint32_t>(img.pos_pk.size() / 2);
+      pd.npk = static_cast<uint32_t>(p.pk.size() / 2);
+      pd.tail = img.pos_tail.size();
+      if (!p.bytes.empty()) std::memcpy(&img.pos_blob[pat], p.bytes.data(), p.bytes.size());
+      pat += (p.bytes.size() + 15) & ~15ull;
+      img.pos_pk.insert(img.pos_pk.end(), p.pk.begin(), p.pk.end());
+      img.pos_tail.insert(img.pos_tail.end(), p.tail.begin(), p.tail.end());
+      PosPart().bytes.swap(p.bytes);
+    }
   }
   return img;
 }

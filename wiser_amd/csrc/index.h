@@ -15,7 +15,9 @@
 
 #include <cstdint>
 #include <string>
+#include <memory>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "engine_types.h"
@@ -56,6 +58,7 @@ class VacuumIndex {
 
   // Skip rows of one list (decoded on demand).
   std::vector<SkipRow> rows(int32_t id) const;
+  void rows_into(int32_t id, std::vector<SkipRow>* out) const;   // reuses out's storage
   const uint8_t* file() const { return map_; }
   bool has_bloom() const { return has_bloom_; }
   uint64_t file_bytes() const { return map_len_; }
@@ -75,21 +78,40 @@ class VacuumIndex {
   bool has_bloom_ = false;
 };
 
+// Allocator whose resize() leaves trivial elements uninitialised: the image's
+// large arrays are written in full by the parallel fill pass, so a serial
+// zeroing first would only fault the pages in twice.
+template <class T>
+struct uninit_alloc : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = uninit_alloc<U>; };
+  uninit_alloc() = default;
+  template <class U>
+  uninit_alloc(const uninit_alloc<U>&) {}
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    if constexpr (sizeof...(A) == 0) ::new (static_cast<void*>(p)) U;
+    else ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using big_vector = std::vector<T, uninit_alloc<T>>;
+
 struct HostImage {
-  std::vector<uint8_t> blob;
+  big_vector<uint8_t> blob;
   std::vector<ListDev> lists;   // indexed by list id
-  std::vector<BlockDev> blocks;
-  std::vector<uint32_t> blk_last;
-  std::vector<uint32_t> blk_meta;    // docid pack bits | tf pack bits << 8 (0 = VInts)
+  big_vector<BlockDev> blocks;
+  big_vector<uint32_t> blk_last;
+  big_vector<uint32_t> blk_meta;    // docid pack bits | tf pack bits << 8 (0 = VInts)
   std::vector<uint64_t> list_bytes;  // docid+tf span bytes per list in the image
   uint32_t doc_lo = 0, doc_hi = 0;
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
-  std::vector<DenseEnt> dense;  // rank bitmaps of the dense lists
-  std::vector<uint8_t> tf8;     // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
+  big_vector<DenseEnt> dense;   // rank bitmaps of the dense lists
+  big_vector<uint8_t> tf8;      // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
   uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
   uint32_t dense_lists = 0;
-  std::vector<uint32_t> tails;  // decoded VInts last blocks (ListDev::tail)
-  std::vector<uint8_t> plen;    // doc-length code (Char4) of every posting: block j of the
+  big_vector<uint32_t> tails;   // decoded VInts last blocks (ListDev::tail)
+  big_vector<uint8_t> plen;     // doc-length code (Char4) of every posting: block j of the
                                 // image at [j * 128, j * 128 + 128), 0 past the length records
   // positions (build_image(..., positions = true)): see PosDev
   bool has_positions = false;

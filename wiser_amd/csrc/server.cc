@@ -110,11 +110,6 @@ struct wsr_server {
     s.busy = false;
   }
 
-  void fail_all(std::vector<Req*>& rs, int rc) {
-    for (Req* r : rs) { r->rc = rc; r->signal(); }
-    rs.clear();
-  }
-
   // Dispatch policy: with the GPU idle, whatever is queued runs at once (the
   // latency of a lone query is one batch); with one batch running, the next
   // fills until max_batch or until its oldest request has waited `window`,
@@ -122,8 +117,8 @@ struct wsr_server {
   void run() {
     uint64_t seq = 0;
     for (;;) {
-      for (auto& s : slots)   // retire finished batches, oldest first
-        if (s.busy && wsr_batch_ready(h, s.b) == 1) complete(s);
+      for (auto& s : slots)   // retire finished batches, oldest first (a HIP error
+        if (s.busy && wsr_batch_ready(h, s.b) != 0) complete(s);   // too: the fetch reports it)
       Slot* oldest = nullptr;
       int n_busy = 0;
       for (auto& s : slots)
@@ -170,7 +165,16 @@ struct wsr_server {
       }
       int rc = wsr_batch_upload(h, s.b, qbuf.data(), static_cast<int32_t>(qbuf.size()));
       if (rc == WSR_OK) rc = wsr_batch_run(h, s.b);
-      if (rc != WSR_OK) { fail_all(take, rc); continue; }
+      if (rc != WSR_OK) {
+        // every request was checked at submit, so this is not one caller's bad
+        // query: the batch is retried one request at a time, and only the
+        // requests that fail on their own get an error
+        for (Req* r : take) {
+          r->rc = wsr_search_batch(h, &r->q, 1, std::max(1, r->q.k), r->out, r->n_out);
+          r->signal();
+        }
+        continue;
+      }
       s.reqs = std::move(take);
       s.busy = true;
       s.seq = ++seq;
@@ -182,8 +186,10 @@ struct wsr_server {
   }
 
   int submit(Req* r) {
-    const wsr_query& q = r->q;
-    if (q.n_terms > WSR_MAX_TERMS || q.k > WSR_MAX_K) return WSR_E_LIMIT;
+    // a bad request fails alone, here, and never joins a batch
+    // (wsr_batch_upload rejects a whole batch for one bad query)
+    const int qrc = wsr_check_query(h, &r->q);
+    if (qrc != WSR_OK) return qrc;
     r->t_enq = Clock::now();
     bool wake;
     {

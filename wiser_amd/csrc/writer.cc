@@ -28,7 +28,11 @@
 #include <memory>
 #include <random>
 #include <stdexcept>
+#include <cstring>
+#include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -674,30 +678,182 @@ BuildStats build_synthetic(const SyntheticSpec& sp, const std::string& out_dir) 
   return st;
 }
 
+// ------------------------------------------------ Wikipedia-shaped stand-in --
+namespace {
+// terms per df decade of the reference's en-Wikipedia index (gen_synthetic_log.py:8-16)
+constexpr int64_t kWikiDecades[7] = {4996891, 520675, 94721, 22139, 5717, 1434, 38};
+constexpr double kWikiAlpha = 1.6;   // df density ~ df^-alpha inside a decade
+
+std::string wiki_term(int64_t id) {
+  char b[32];
+  std::snprintf(b, sizeof b, "w%08lld", static_cast<long long>(id));
+  return b;
+}
+
+// df drawn from density ~ x^-alpha on [lo, hi) (inverse CDF), as an integer
+uint32_t powerlaw_df(std::mt19937_64& g, double lo, double hi) {
+  const double a = 1.0 - kWikiAlpha;
+  const double u = unit(g);
+  const double x = std::pow(std::pow(lo, a) + u * (std::pow(hi, a) - std::pow(lo, a)), 1.0 / a);
+  const double f = std::floor(x);
+  return static_cast<uint32_t>(f < lo ? lo : (f >= hi ? hi - 1 : f));
+}
+}  // namespace
+
+BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
+  const int64_t N = sp.n_docs;
+  if (N < 16 || N > (1ll << 31) - 1) throw std::runtime_error("wiki stand-in: n_docs out of range");
+  int threads = sp.threads > 0 ? sp.threads : static_cast<int>(std::thread::hardware_concurrency());
+  if (threads < 1) threads = 1;
+  // 1) df of every term: decade by decade, then shuffled over the term ids (so
+  //    that sorted term strings are not sorted by df, as in a real dictionary)
+  std::vector<uint32_t> dfs;
+  {
+    std::mt19937_64 g(sp.seed);
+    for (int e = 0; e < 7; ++e) {
+      const double lo = std::pow(10.0, e);
+      const double hi = std::min(std::pow(10.0, e + 1), static_cast<double>(N) + 1);
+      if (lo >= hi) break;
+      const int64_t n = std::llround(kWikiDecades[e] * sp.term_scale);
+      for (int64_t i = 0; i < n; ++i) dfs.push_back(powerlaw_df(g, lo, hi));
+    }
+    for (size_t i = dfs.size(); i > 1; --i) std::swap(dfs[i - 1], dfs[g() % i]);
+  }
+  const int64_t V = static_cast<int64_t>(dfs.size());
+  if (V == 0) throw std::runtime_error("wiki stand-in: empty vocabulary");
+  // 2) per-doc verbosity (lognormal): longer docs repeat their terms more
+  std::vector<float> verb(N);
+  {
+    std::mt19937_64 g(sp.seed ^ 0x5151515151515151ull);
+    for (int64_t d = 0; d < N; ++d) {
+      const double z = std::sqrt(-2.0 * std::log(unit(g))) * std::cos(2.0 * M_PI * unit(g));
+      verb[d] = static_cast<float>(std::exp(0.6 * z));
+    }
+  }
+  std::unique_ptr<std::atomic<uint32_t>[]> len(new std::atomic<uint32_t>[N]);
+  for (int64_t d = 0; d < N; ++d) len[d].store(0, std::memory_order_relaxed);
+
+  // one term's postings, from its own seed (independent of the thread count)
+  auto make_list = [&](int64_t id, TermPostings* tp) {
+    std::mt19937_64 g(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(id + 1)));
+    const uint32_t df = dfs[id];
+    std::vector<uint32_t>& docs = tp->docs;
+    if (static_cast<int64_t>(df) * 16 < N) {
+      // rare term: distinct uniform ids by rejection
+      while (docs.size() < df) {
+        const size_t need = df - docs.size();
+        for (size_t i = 0; i < need; ++i) docs.push_back(static_cast<uint32_t>(g() % static_cast<uint64_t>(N)));
+        std::sort(docs.begin(), docs.end());
+        docs.erase(std::unique(docs.begin(), docs.end()), docs.end());
+      }
+    } else {
+      // common term: selection sampling (Knuth's algorithm S), exactly df ids
+      docs.reserve(df);
+      uint64_t need = df;
+      for (int64_t d = 0; d < N && need; ++d)
+        if (static_cast<double>(N - d) * unit(g) < static_cast<double>(need)) { docs.push_back(static_cast<uint32_t>(d)); --need; }
+    }
+    const double base = 0.3 + 5.0 * static_cast<double>(df) / static_cast<double>(N);
+    const uint32_t p0 = static_cast<uint32_t>(id % 61);
+    tp->tfs.resize(docs.size());
+    for (size_t i = 0; i < docs.size(); ++i) {
+      const double lam = base * verb[docs[i]];
+      const double t = 1.0 + std::floor(-std::log(unit(g)) * lam);
+      const uint32_t tf = static_cast<uint32_t>(t > 60000.0 ? 60000.0 : t);
+      tp->tfs[i] = tf;
+      len[docs[i]].fetch_add(tf, std::memory_order_relaxed);
+      // bag: tf consecutive positions from p0 (delta coded: p0, 1, 1, ...) and
+      // their offset pairs [9p, 9p + 7] (delta coded inside the bag)
+      tp->pos_vals.push_back(p0);
+      tp->off_vals.push_back(9 * p0);
+      tp->off_vals.push_back(7);
+      for (uint32_t r = 1; r < tf; ++r) {
+        tp->pos_vals.push_back(1);
+        tp->off_vals.push_back(2);
+        tp->off_vals.push_back(7);
+      }
+      tp->pos_sizes.push_back(tf);
+      tp->off_sizes.push_back(2 * tf);
+    }
+  };
+
+  VacuumFileWriter w(out_dir);
+  BuildStats st;
+  const int64_t BATCH = 16384;
+  for (int64_t b0 = 0; b0 < V; b0 += BATCH) {
+    const int64_t b1 = std::min(V, b0 + BATCH);
+    std::vector<std::unique_ptr<EncodedList>> enc(b1 - b0);
+    std::atomic<int64_t> next{b0};
+    std::atomic<bool> failed{false};
+    std::string err;
+    auto work = [&] {
+      try {
+        for (int64_t v; (v = next++) < b1 && !failed;) {
+          TermPostings tp;
+          make_list(v, &tp);
+          auto el = std::make_unique<EncodedList>();
+          encode_list(tp, el.get());
+          enc[v - b0] = std::move(el);
+        }
+      } catch (const std::exception& ex) {
+        if (!failed.exchange(true)) err = ex.what();
+      }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+    if (failed) throw std::runtime_error(err);
+    for (int64_t v = b0; v < b1; ++v) { w.add(wiki_term(v), *enc[v - b0]); st.n_postings += enc[v - b0]->df; }
+  }
+  w.close();
+  DocLengths lens;
+  lens.c4.reserve(N);
+  for (int64_t d = 0; d < N; ++d) lens.add(len[d].load(std::memory_order_relaxed));
+  lens.write(out_dir);
+  st.n_docs = N;
+  st.n_terms = w.terms();
+  st.vacuum_bytes = static_cast<int64_t>(w.bytes());
+  st.docs_char4_ge_0x80 = lens.big;
+  st.avg_length = lens.avg;
+  return st;
+}
+
 // --------------------------------------------------------- query log gen --
 namespace {
 // The df groups of tools/gen_synthetic_log.py:21-28 over an index's df table:
-// "low" = floor(log10 df) in 0..3, "high" = 4..6.
+// "low" = floor(log10 df) in 0..3, "high" = 4..6.  (my.vacuum is mapped: an
+// index of millions of terms would cost a seek per term through a stream.)
 void df_groups(const std::string& dir, std::vector<std::string>* low, std::vector<std::string>* high) {
   std::ifstream tip(dir + "/my.tip", std::ios::binary);
-  std::ifstream vac(dir + "/my.vacuum", std::ios::binary);
-  if (!tip || !vac) throw std::runtime_error("cannot open index in " + dir);
-  for (;;) {
+  if (!tip) throw std::runtime_error("cannot open index in " + dir);
+  const int fd = ::open((dir + "/my.vacuum").c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + dir + "/my.vacuum");
+  struct stat sb;
+  if (::fstat(fd, &sb) != 0) { ::close(fd); throw std::runtime_error("stat my.vacuum"); }
+  const uint64_t flen = static_cast<uint64_t>(sb.st_size);
+  void* mp = flen ? ::mmap(nullptr, flen, PROT_READ, MAP_PRIVATE, fd, 0) : MAP_FAILED;
+  ::close(fd);
+  if (mp == MAP_FAILED) throw std::runtime_error("mmap my.vacuum failed");
+  const uint8_t* file = static_cast<const uint8_t*>(mp);
+  std::string all((std::istreambuf_iterator<char>(tip)), std::istreambuf_iterator<char>());
+  for (size_t at = 0; at + 4 <= all.size();) {
     uint32_t len;
-    if (!tip.read(reinterpret_cast<char*>(&len), 4)) break;
-    std::string term(len, '\0');
+    std::memcpy(&len, &all[at], 4);
+    if (at + 4 + len + 8 > all.size()) break;
+    std::string term = all.substr(at + 4, len);
     int64_t v;
-    tip.read(&term[0], len);
-    tip.read(reinterpret_cast<char*>(&v), 8);
-    uint8_t buf[16] = {0};
-    vac.seekg(static_cast<std::streamoff>(tip_offset(v)));
-    vac.read(reinterpret_cast<char*>(buf), sizeof buf);
+    std::memcpy(&v, &all[at + 4 + len], 8);
+    at += 4 + len + 8;
+    const uint64_t off = tip_offset(v);
     uint64_t df = 0;
-    if (buf[0] != kPostingListMagic || !get_varint(buf + 1, buf + sizeof buf, &df))
+    if (off + 2 > flen || file[off] != kPostingListMagic || !get_varint(file + off + 1, file + flen, &df)) {
+      ::munmap(mp, flen);
       throw std::runtime_error("bad posting list header for " + term);
-    if (df >= 1 && df < 10000) low->push_back(term);
-    else if (df >= 10000 && df < 10000000) high->push_back(term);
+    }
+    if (df >= 1 && df < 10000) low->push_back(std::move(term));
+    else if (df >= 10000 && df < 10000000) high->push_back(std::move(term));
   }
+  ::munmap(mp, flen);
   if (low->empty() || high->empty() || low->size() + high->size() < 2)
     throw std::runtime_error("df table has an empty low or high group");
 }

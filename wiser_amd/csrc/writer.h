@@ -50,6 +50,27 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
 
 BuildStats build_synthetic(const SyntheticSpec& spec, const std::string& out_dir);
 
+// English-Wikipedia-shaped stand-in (BASELINE configs[2], "C3"): no Wikipedia
+// dump exists offline, so the posting lists are drawn straight from the df
+// histogram the reference records for its en-Wikipedia index
+// (tools/gen_synthetic_log.py:8-16: terms per df decade 4,996,891 / 520,675 /
+// 94,721 / 22,139 / 5,717 / 1,434 / 38), times term_scale.  Per term: df from
+// a power law inside its decade (density ~ df^-1.6, the decade-to-decade
+// ratio of that histogram), df distinct uniform doc ids, tf = 1 + Exp(lambda)
+// with lambda growing with the doc's verbosity (lognormal) and the term's
+// df / N.  Doc length = sum of its tfs (every token is indexed), stored as
+// Char4 with the reference's incremental mean.  Lists are generated per term
+// from per-term seeds and written in term order, a few thousand at a time, so
+// host memory stays bounded whatever the corpus size; position bags hold tf
+// consecutive positions and the matching offset pairs (reference layout).
+struct WikiSpec {
+  int64_t n_docs = 5500000;
+  double term_scale = 1.0;
+  uint64_t seed = 0x3C3C2026ull;
+  int threads = 0;
+};
+BuildStats build_wiki_standin(const WikiSpec& spec, const std::string& out_dir);
+
 // Two-term query log restating tools/gen_synthetic_log.py:191-214 over the
 // df table of an index: group "low" = floor(log10 df) in 0..3, "high" = 4..6;
 // each term picks a group uniformly then a term uniformly; t1 != t2; the pair

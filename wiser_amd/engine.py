@@ -384,6 +384,16 @@ def build_synthetic(out_dir: str, n_docs: int = 1_000_000, vocab: int = 500_000,
     return st
 
 
+def build_wiki_standin(out_dir: str, n_docs: int = 5_500_000, term_scale: float = 1.0,
+                       seed: int = 0x3C3C2026, threads: int = 0) -> _capi.BuildStats:
+    """BASELINE configs[2] stand-in: df histogram of the reference's en-Wikipedia
+    index (tools/gen_synthetic_log.py:8-16) x term_scale over n_docs docs."""
+    st = _capi.BuildStats()
+    check(lib.wsr_build_wiki_standin(out_dir.encode(), n_docs, term_scale, seed, threads,
+                                     C.byref(st)))
+    return st
+
+
 def gen_two_term_log(index_dir: str, out_path: str, n_queries: int = 100_000, seed: int = 7) -> int:
     n = C.c_int64()
     check(lib.wsr_gen_two_term_log(index_dir.encode(), n_queries, seed, out_path.encode(),
