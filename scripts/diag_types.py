@@ -14,20 +14,31 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--index", default="/tmp/wiser_bench/c2_1000000_500000")
 ap.add_argument("--only", default="")
 ap.add_argument("--repeat", type=int, default=1)
+ap.add_argument("--wiki", action="store_true", help="the C3 stand-in (bench.py c3_leg's index)")
 args = ap.parse_args()
+if args.wiki and args.index == ap.get_default("index"):
+    args.index = "/tmp/wiser_bench/c3_wiki_5500000_1"
 idx = args.index
 if not os.path.exists(os.path.join(idx, "READY")):
     os.makedirs(idx, exist_ok=True)
-    w.build_synthetic(idx, threads=16)
+    if args.wiki:
+        w.build_wiki_standin(idx, threads=16)
+    else:
+        w.build_synthetic(idx, threads=16)
     w.gen_two_term_log(idx, os.path.join(idx, "two_term_100000.log"), 100000, 7)
     open(os.path.join(idx, "READY"), "w").write("ok")
-eng = w.VacuumEngine(idx)
+eng = w.VacuumEngine(idx, positions=False)
 eng.Load()
 lines = [l.split() for l in open(os.path.join(idx, "two_term_100000.log")).read().splitlines()]
-cls = {"mixed": lines[:4096], "low-low": [], "low-high": [], "high-high": []}
+cls = {"mixed": lines[:4096], "low-low": [], "low-high": [], "high-high": [],
+       "hh-lean": [], "hh-general": []}
+n_docs = eng.NumDocs()
 for t in lines:
-    h = sum(1 for x in t if eng.lookup(x)[1] >= 10000)
+    dfs = [eng.lookup(x)[1] for x in t]
+    h = sum(1 for d in dfs if d >= 10000)
     cls[["low-low", "low-high", "high-high"][h]].append(t)
+    if h == 2:   # the other (longer) list has a rank bitmap: df >= N / 128 (WSR_DENSE_DIV)
+        cls["hh-lean" if max(dfs) * 128 >= n_docs else "hh-general"].append(t)
 import ctypes as C
 for name, qs in cls.items():
     if args.only and name != args.only:

@@ -103,6 +103,7 @@ struct wsr_batch {
   QueryIn* d_q = nullptr;
   QueryPlan* d_plan = nullptr;
   QueryDesc* d_desc = nullptr;     // lean queries' work records
+  PlanPart* d_part = nullptr;      // plan pass 1 -> 2 partial sums, per kPlanThreads queries
   uint32_t* d_ctr = nullptr;
   Event* d_events = nullptr;
   uint64_t ev_cap = 0;
@@ -461,6 +462,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_q, sizeof(QueryIn) * max_q));
     HIP_OK(hipMalloc(&b->d_plan, sizeof(QueryPlan) * max_q));
     HIP_OK(hipMalloc(&b->d_desc, sizeof(QueryDesc) * max_q));
+    HIP_OK(hipMalloc(&b->d_part, sizeof(PlanPart) * ((max_q + kPlanThreads - 1) / kPlanThreads + 1)));
     HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
@@ -485,7 +487,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (b->st) (void)hipStreamSynchronize(b->st);
   if (b->st2) (void)hipStreamSynchronize(b->st2);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
-                  static_cast<void*>(b->d_desc),
+                  static_cast<void*>(b->d_desc), static_cast<void*>(b->d_part),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
                   static_cast<void*>(b->d_evcnt), static_cast<void*>(b->d_hits),
                   static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
@@ -620,7 +622,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
                        kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq,
-                       h->seg_floor ? b->d_pub : nullptr, b->d_desc, st));
+                       h->seg_floor ? b->d_pub : nullptr, b->d_desc, b->d_part, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
     // own queue, then the streams join

@@ -93,14 +93,23 @@ struct FusedReplay {
   int32_t* n_hits;
 };
 
+// Plan pass 1 -> pass 2: per plan workgroup (kPlanThreads queries), its items
+// per item key (class, cost bucket) and its event capacity.
+constexpr int kPlanThreads = 256;
+struct PlanPart {
+  uint32_t items[2 * kCostBuckets];
+  uint64_t cap;
+};
+
 // phrase scratch words per general workgroup / lean wave (null when the batch
 // has no phrase query)
 constexpr int kPhraseScratch = kMaxTerms * 256;
 
+// plan queries (2 launches); part: per plan workgroup of kPlanThreads queries
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
-                       uint64_t* pub, QueryDesc* desc, hipStream_t st);
+                       uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                            int grid, const FusedReplay& fr, const uint32_t* item_q,

@@ -40,6 +40,7 @@
 // left-to-right sum are each rounded once, exactly as on the host.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "kernels.h"
@@ -343,187 +344,235 @@ __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev
 }
 
 // ----------------------------------------------------------------- plan --
-// Pass 1, one thread per query: driver (shortest list here), segment length
-// (driver blocks per work item, so that items cost about kSegCost block
-// decodes) and the item count.  item_base / ev_base are filled by pass 2.
-__global__ __launch_bounds__(256) void plan_query_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
-                                                         int nq, QueryPlan* __restrict__ plan,
-                                                         uint32_t* __restrict__ counters, FusedReplay fr,
-                                                         QueryDesc* __restrict__ desc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq) return;
-  const QueryIn q = qs[i];
-  QueryPlan p{0, 0, 1, 0, 0};
-  bool ok = q.n_terms > 0 && q.k > 0;
-  if (q.n_terms > kMaxTerms || q.k > kMaxK) {
-    ok = false;
-    atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
-  }
-  uint32_t nb[kMaxTerms];
-  bool dn[kMaxTerms];
-#pragma unroll
-  for (int s = 0; s < kMaxTerms; ++s) {
-    nb[s] = 0xFFFFFFFFu;
-    dn[s] = false;
-    if (ok && s < q.n_terms) {
-      const int32_t id = q.list[s];
-      if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) ok = false;
-      else { nb[s] = ix.lists[id].nblk; dn[s] = ix.lists[id].bm != kNoDense; }
-      if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
-    }
-  }
-  if (ok) {
-    uint32_t d = 0, nd = nb[0];
-#pragma unroll
-    for (int s = 1; s < kMaxTerms; ++s) if (nb[s] < nd) { d = s; nd = nb[s]; }
-    float cost = 1.0f;
-#pragma unroll
-    for (int s = 0; s < kMaxTerms; ++s)
-      if (s < q.n_terms && s != static_cast<int>(d))
-        cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
-                                                : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
-    const bool ph = q.n_terms > 1 && (q.flags & kQueryPhrase);
-    // lean class: every other list is probed through its bitmap (or none)
-    bool lean = true;
-#pragma unroll
-    for (int s = 0; s < kMaxTerms; ++s)
-      if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
-    uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : lean ? kSegCost : kSegCostGeneral) / cost);
-    seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
-    // cost class of one item (log2 of its block decodes, plus a fixed part
-    // for the per-item setup): the queue hands out heavy items first
-    const float item_cost = static_cast<float>(seg) * cost + kItemFixedCost;
-    const uint32_t ic = static_cast<uint32_t>(item_cost);
-    const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
-    const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-    p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
-    p.seg_blocks = seg;
-    p.n_items = (nd + seg - 1) / seg;
-    if (lean) {
-      // the lean kernel's record: driver, the most selective other list (O1),
-      // the smallest last doc of the others (bases are added by plan_scan_kernel)
-      const ListDev A = ix.lists[q.list[d]];
-      QueryDesc D;
-      D.a_base = A.base;
-      D.a_tail = A.tail;
-      D.a_idf = A.idf;
-      D.a_blk0 = A.blk0;
-      D.a_nblk = A.nblk;
-      D.a_tail_cnt = A.tail_cnt;
-      uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
-      for (int s = 0; s < q.n_terms; ++s) {
-        if (s == static_cast<int>(d)) continue;
-        const ListDev B = ix.lists[q.list[s]];
-        const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
-        min_last = bl < min_last ? bl : min_last;
-        if (B.nblk < o_nb) { o1 = s; o_nb = B.nblk; }
-      }
-      D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
-      if (o1 < kMaxTerms) {
-        const ListDev O = ix.lists[q.list[o1]];
-        D.o_bm = O.bm; D.o_tf8 = O.tf8; D.o_idf = O.idf;
-        D.o_list = static_cast<uint32_t>(q.list[o1]);
-      }
-      D.min_last = min_last;
-      D.a_bm = A.bm;
-      D.a_tf8 = A.tf8;
-      D.ev_base = 0;
-      D.item_base = 0;
-      D.n_items = p.n_items;
-      D.seg = seg;
-      D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16) |
-                (static_cast<uint32_t>(q.k) << 24);
-      for (int t = 0; t < 5; ++t) D.pad[t] = 0;
-      desc[i] = D;
-    }
-  }
-  plan[i] = p;
-  if (fr.q_done) {
-    fr.q_done[i] = 0;
-    if (p.n_items == 0) fr.n_hits[i] = 0;   // no item will replay an empty query
-  }
-}
-
-// Pass 2, one workgroup of 1024: event capacities are scanned in query order;
-// items are numbered class-major (lean items first, then general ones), then
-// bucket-major, heaviest cost bucket first (query order inside a bucket, a
-// query's items consecutive), so the persistent workers take the long items
-// first and the short ones fill the tail (longest-first list scheduling).
+// Item order: class-major (lean items first, then general ones), then cost
+// bucket-major, heaviest bucket first (query order inside a bucket, a query's
+// items consecutive), so the persistent workers take the long items first and
+// the short ones fill the tail (longest-first list scheduling).
 constexpr int kPlanKeys = 2 * kCostBuckets;
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
   const uint32_t bucket = (drv >> 8) & 0xFFu;
   return ((drv & kPlanLean) ? 0u : static_cast<uint32_t>(kCostBuckets)) + (kCostBuckets - 1 - bucket);
 }
-__global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __restrict__ plan,
-                                                         uint32_t* __restrict__ counters,
-                                                         uint64_t ev_capacity, uint32_t item_capacity,
-                                                         uint32_t lean_grid, uint32_t seg_grid,
-                                                         uint32_t* __restrict__ item_q,
-                                                         uint64_t* __restrict__ pub,
-                                                         QueryDesc* __restrict__ desc) {
-  constexpr int kWaves = 1024 / 64;
-  __shared__ uint64_t s_cap[1024];
-  __shared__ uint32_t s_bt[kPlanKeys][kWaves];   // per key, per wave item totals
-  const int t = threadIdx.x, T = blockDim.x;
-  const uint32_t wv = t / 64, l = t & 63;
-  const int per = (nq + T - 1) / T;
-  const int q0 = t * per, q1 = min(nq, q0 + per);
-  uint32_t cnt[kPlanKeys];
+
+// block-wide sums over the 256 threads of a plan workgroup (4 waves)
+template <class T>
+__device__ __forceinline__ T wave_incl_scan_any(T x) {
+  const uint32_t l = threadIdx.x & 63;
 #pragma unroll
-  for (int bk = 0; bk < kPlanKeys; ++bk) cnt[bk] = 0;
-  uint64_t cap = 0;
-  for (int i = q0; i < q1; ++i) {
-    const QueryPlan p = plan[i];
-    const uint32_t bk = plan_key(p.driver);
-#pragma unroll
-    for (int b = 0; b < kPlanKeys; ++b) cnt[b] += bk == static_cast<uint32_t>(b) ? p.n_items : 0u;
-    cap += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
+  for (int d = 1; d < 64; d <<= 1) {
+    const T y = __shfl_up(x, d, 64);
+    if (l >= static_cast<uint32_t>(d)) x += y;
   }
-  s_cap[t] = cap;
-  uint32_t ex[kPlanKeys];   // items of this key in lower lanes of the wave
-#pragma unroll
-  for (int b = 0; b < kPlanKeys; ++b) {
-    const uint32_t inc = wave_incl_scan(cnt[b]);
-    ex[b] = inc - cnt[b];
-    if (l == 63) s_bt[b][wv] = inc;
-  }
+  return x;
+}
+// exclusive prefix of x over the workgroup's threads, and the workgroup total
+template <class T>
+__device__ __forceinline__ T block_excl_scan(T x, T* s_w /*[4]*/, T* total) {
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const T inc = wave_incl_scan_any(x);
   __syncthreads();
-  for (int d = 1; d < T; d <<= 1) {  // Hillis-Steele over the thread capacities
-    uint64_t c = 0;
-    if (t >= d) c = s_cap[t - d];
-    __syncthreads();
-    s_cap[t] += c;
-    __syncthreads();
+  if (l == 63) s_w[w] = inc;
+  __syncthreads();
+  T below = 0, tot = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPlanThreads / 64; ++i) {
+    below += i < w ? s_w[i] : T(0);
+    tot += s_w[i];
   }
-  // base of every key (ascending) and of this wave inside it
-  uint32_t ib[kPlanKeys];
+  *total = tot;
+  return below + inc - x;
+}
+
+// Pass 1, one thread per query: driver (shortest list here), segment length
+// (driver blocks per work item, so that items cost about kSegCost block
+// decodes), item count and cost bucket; then the workgroup's item totals per
+// key and its event capacity go to part[blockIdx.x] for pass 2.
+__global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+                                                         int nq, QueryPlan* __restrict__ plan,
+                                                         uint32_t* __restrict__ counters, FusedReplay fr,
+                                                         QueryDesc* __restrict__ desc,
+                                                         PlanPart* __restrict__ part) {
+  __shared__ uint32_t s_w[kPlanThreads / 64];
+  __shared__ uint64_t s_w64[kPlanThreads / 64];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  QueryPlan p{0, 0, 1, 0, 0};
+  if (i < nq) {
+    const QueryIn q = qs[i];
+    bool ok = q.n_terms > 0 && q.k > 0;
+    if (q.n_terms > kMaxTerms || q.k > kMaxK) {
+      ok = false;
+      atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
+    }
+    uint32_t nb[kMaxTerms];
+    bool dn[kMaxTerms];
+#pragma unroll
+    for (int s = 0; s < kMaxTerms; ++s) {
+      nb[s] = 0xFFFFFFFFu;
+      dn[s] = false;
+      if (ok && s < q.n_terms) {
+        const int32_t id = q.list[s];
+        if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) ok = false;
+        else { nb[s] = ix.lists[id].nblk; dn[s] = ix.lists[id].bm != kNoDense; }
+        if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
+      }
+    }
+    if (ok) {
+      uint32_t d = 0, nd = nb[0];
+#pragma unroll
+      for (int s = 1; s < kMaxTerms; ++s) if (nb[s] < nd) { d = s; nd = nb[s]; }
+      float cost = 1.0f;
+#pragma unroll
+      for (int s = 0; s < kMaxTerms; ++s)
+        if (s < q.n_terms && s != static_cast<int>(d))
+          cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
+                                                  : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+      const bool ph = q.n_terms > 1 && (q.flags & kQueryPhrase);
+      // lean class: every other list is probed through its bitmap (or none)
+      bool lean = true;
+#pragma unroll
+      for (int s = 0; s < kMaxTerms; ++s)
+        if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
+      uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : lean ? kSegCost : kSegCostGeneral) / cost);
+      seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
+      // cost class of one item (log2 of its block decodes, plus a fixed part
+      // for the per-item setup): the queue hands out heavy items first
+      const float item_cost = static_cast<float>(seg) * cost + kItemFixedCost;
+      const uint32_t ic = static_cast<uint32_t>(item_cost);
+      const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
+      const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
+      p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
+      p.seg_blocks = seg;
+      p.n_items = (nd + seg - 1) / seg;
+      if (lean) {
+        // the lean kernel's record: driver, the most selective other list (O1),
+        // the smallest last doc of the others (bases are added by plan_fill_kernel)
+        const ListDev A = ix.lists[q.list[d]];
+        QueryDesc D;
+        D.a_base = A.base;
+        D.a_tail = A.tail;
+        D.a_idf = A.idf;
+        D.a_blk0 = A.blk0;
+        D.a_nblk = A.nblk;
+        D.a_tail_cnt = A.tail_cnt;
+        uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
+        for (int s = 0; s < q.n_terms; ++s) {
+          if (s == static_cast<int>(d)) continue;
+          const ListDev B = ix.lists[q.list[s]];
+          const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
+          min_last = bl < min_last ? bl : min_last;
+          if (B.nblk < o_nb) { o1 = s; o_nb = B.nblk; }
+        }
+        D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
+        if (o1 < kMaxTerms) {
+          const ListDev O = ix.lists[q.list[o1]];
+          D.o_bm = O.bm; D.o_tf8 = O.tf8; D.o_idf = O.idf;
+          D.o_list = static_cast<uint32_t>(q.list[o1]);
+        }
+        D.min_last = min_last;
+        D.a_bm = A.bm;
+        D.a_tf8 = A.tf8;
+        D.ev_base = 0;
+        D.item_base = 0;
+        D.n_items = p.n_items;
+        D.seg = seg;
+        D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16) |
+                  (static_cast<uint32_t>(q.k) << 24);
+        for (int t = 0; t < 5; ++t) D.pad[t] = 0;
+        desc[i] = D;
+      }
+    }
+    plan[i] = p;
+    if (fr.q_done) {
+      fr.q_done[i] = 0;
+      if (p.n_items == 0) fr.n_hits[i] = 0;   // no item will replay an empty query
+    }
+  }
+  // the workgroup's items per key and event capacity (pass 2 scans them)
+  const uint32_t key = plan_key(p.driver);
+  uint32_t tot;
+#pragma unroll
+  for (int k = 0; k < kPlanKeys; ++k) {
+    (void)block_excl_scan<uint32_t>(key == static_cast<uint32_t>(k) ? p.n_items : 0u, s_w, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x].items[k] = tot;
+  }
+  uint64_t ctot;
+  (void)block_excl_scan<uint64_t>(static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128, s_w64, &ctot);
+  if (threadIdx.x == 0) part[blockIdx.x].cap = ctot;
+}
+
+// Pass 2, the same workgroups: every workgroup sums the partials of all
+// workgroups (their totals give the key bases, those of the lower workgroups
+// its own offsets), scans its queries per key, and writes each query's item and
+// event bases, its lean record's bases, and its items' item -> query map and
+// zeroed score floors (one thread per query, a few stores each; at most the
+// query's driver blocks / segment length).
+__global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPlan* __restrict__ plan,
+                                                        const PlanPart* __restrict__ part, int n_part,
+                                                        uint32_t* __restrict__ counters,
+                                                        uint64_t ev_capacity, uint32_t item_capacity,
+                                                        uint32_t lean_grid, uint32_t seg_grid,
+                                                        uint32_t* __restrict__ item_q,
+                                                        uint64_t* __restrict__ pub,
+                                                        QueryDesc* __restrict__ desc) {
+  __shared__ uint32_t s_w[kPlanThreads / 64];
+  __shared__ uint64_t s_w64[kPlanThreads / 64];
+  __shared__ uint32_t s_key_all[kPlanKeys], s_key_below[kPlanKeys];
+  __shared__ uint64_t s_cap_all, s_cap_below;
+  const uint32_t t = threadIdx.x;
+  // partial sums of all workgroups / of the lower ones (strided over threads)
+  uint32_t all[kPlanKeys], below[kPlanKeys];
+#pragma unroll
+  for (int k = 0; k < kPlanKeys; ++k) all[k] = below[k] = 0;
+  uint64_t call = 0, cbelow = 0;
+  for (int g = static_cast<int>(t); g < n_part; g += kPlanThreads) {
+    const PlanPart P = part[g];
+    const bool lo = g < static_cast<int>(blockIdx.x);
+#pragma unroll
+    for (int k = 0; k < kPlanKeys; ++k) { all[k] += P.items[k]; below[k] += lo ? P.items[k] : 0u; }
+    call += P.cap;
+    cbelow += lo ? P.cap : 0ull;
+  }
+  uint32_t tot;
+#pragma unroll
+  for (int k = 0; k < kPlanKeys; ++k) {
+    (void)block_excl_scan<uint32_t>(all[k], s_w, &tot);
+    if (t == 0) s_key_all[k] = tot;
+    (void)block_excl_scan<uint32_t>(below[k], s_w, &tot);
+    if (t == 0) s_key_below[k] = tot;
+  }
+  uint64_t ctot;
+  (void)block_excl_scan<uint64_t>(call, s_w64, &ctot);
+  if (t == 0) s_cap_all = ctot;
+  (void)block_excl_scan<uint64_t>(cbelow, s_w64, &ctot);
+  if (t == 0) s_cap_below = ctot;
+  __syncthreads();
+  uint32_t key_base[kPlanKeys];
   uint32_t run = 0, n_lean = 0;
 #pragma unroll
-  for (int b = 0; b < kPlanKeys; ++b) {
-    uint32_t below = 0, tot = 0;
-    for (uint32_t w = 0; w < static_cast<uint32_t>(kWaves); ++w) {
-      const uint32_t v = s_bt[b][w];
-      below += w < wv ? v : 0u;
-      tot += v;
-    }
-    ib[b] = run + below + ex[b];
-    run += tot;
-    if (b == kCostBuckets - 1) n_lean = run;
+  for (int k = 0; k < kPlanKeys; ++k) {
+    key_base[k] = run + s_key_below[k];
+    run += s_key_all[k];
+    if (k == kCostBuckets - 1) n_lean = run;
   }
   const uint32_t total_items = run;
-  const bool fits = s_cap[T - 1] <= ev_capacity && total_items <= item_capacity;
-  uint64_t cb = s_cap[t] - cap;
-  for (int i = q0; i < q1; ++i) {
-    QueryPlan& p = plan[i];
-    const uint32_t bk = plan_key(p.driver);
-    uint32_t base = 0;
+  const bool fits = s_cap_all <= ev_capacity && total_items <= item_capacity;
+  // this workgroup's queries: offsets inside their key and event bases
+  const int i = blockIdx.x * blockDim.x + t;
+  QueryPlan p{0, 0, 1, 0, 0};
+  if (i < nq) p = plan[i];
+  const uint32_t key = plan_key(p.driver);
+  uint32_t base = 0;
 #pragma unroll
-    for (int b = 0; b < kPlanKeys; ++b)
-      if (bk == static_cast<uint32_t>(b)) { base = ib[b]; ib[b] += p.n_items; }
-    p.item_base = base;
-    p.ev_base = cb;
-    // the item -> query map, the zeroed per-item floors and the lean
-    // record's bases (skipped when the plan does not fit the workspace)
+  for (int k = 0; k < kPlanKeys; ++k) {
+    const uint32_t ex = block_excl_scan<uint32_t>(key == static_cast<uint32_t>(k) ? p.n_items : 0u, s_w, &tot);
+    if (key == static_cast<uint32_t>(k)) base = key_base[k] + ex;
+  }
+  const uint64_t cap = static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
+  const uint64_t cb = s_cap_below + block_excl_scan<uint64_t>(cap, s_w64, &ctot);
+  if (i < nq) {
+    plan[i].item_base = base;
+    plan[i].ev_base = cb;
+    // (skipped when the plan does not fit the workspace: never written past it)
     if (fits) {
       if (p.driver & kPlanLean) {
         desc[i].item_base = base;
@@ -534,20 +583,21 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(int nq, QueryPlan* __re
         if (pub) pub[base + j] = 0;
       }
     }
-    cb += static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
   }
-  if (t == T - 1) {
-    if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
-    counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
-    counters[kCtrLean] = fits ? n_lean : 0u;
-    counters[kCtrEvCap] = static_cast<uint32_t>(s_cap[t] > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap[t]);
-  }
-  // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
-  // starts on relative item w without a dequeue, so shard s's head starts past
-  // those first items (lean: one worker per wave; general: per workgroup).
-  if (t < kQueueShards) {
-    counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
-    counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
+  if (blockIdx.x == 0) {
+    if (t == 0) {
+      if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
+      counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
+      counters[kCtrLean] = fits ? n_lean : 0u;
+      counters[kCtrEvCap] = static_cast<uint32_t>(s_cap_all > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap_all);
+    }
+    // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
+    // starts on relative item w without a dequeue, so shard s's head starts past
+    // those first items (lean: one worker per wave; general: per workgroup).
+    if (t < kQueueShards) {
+      counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
+      counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
+    }
   }
 }
 
@@ -1612,7 +1662,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
   for (;;) {
     if (item >= total) item = next_item(&counters[kCtrGHead0], n_lean, total, shard, tried);
     if (item >= total) break;
-    const uint32_t qi = uni(item_q[item]);   // written by plan_scan_kernel
+    const uint32_t qi = uni(item_q[item]);   // written by plan_fill_kernel
     const QueryPlan P = plan[qi];
     const int32_t* qlist = qs[qi].list;
     const uint32_t r = item - P.item_base;
@@ -2236,13 +2286,13 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
                        int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
-                       uint64_t* pub, QueryDesc* desc, hipStream_t st) {
-  if (nq > 0)
-    hipLaunchKernelGGL(plan_query_kernel, dim3((nq + 255) / 256), dim3(256), 0, st, ix, q, nq, plan,
-                       counters, fr, desc);
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, nq, plan, counters, ev_capacity,
-                     item_capacity, static_cast<uint32_t>(lean_grid), static_cast<uint32_t>(seg_grid),
-                     item_q, pub, desc);
+                       uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st) {
+  const int n_part = std::max(1, (nq + kPlanThreads - 1) / kPlanThreads);
+  hipLaunchKernelGGL(plan_query_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, ix, q, nq, plan,
+                     counters, fr, desc, part);
+  hipLaunchKernelGGL(plan_fill_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, nq, plan, part, n_part,
+                     counters, ev_capacity, item_capacity, static_cast<uint32_t>(lean_grid),
+                     static_cast<uint32_t>(seg_grid), item_q, pub, desc);
   return hipGetLastError();
 }
 
