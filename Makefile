@@ -30,7 +30,7 @@ $(OBJDIR)/%.o: wiser_amd/csrc/% $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread -l:liblz4.so.1
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lpthread -l:liblz4.so.1 -lrccl
 
 $(ORACLE): oracle/oracle.cc oracle/oracle.h
 	@mkdir -p oracle/_build
@@ -41,12 +41,12 @@ PROFLIB := wiser_amd/_lib/prof/libwiser_hip.so
 prof: $(PROFLIB)
 $(PROFLIB): $(SRCS) $(HDRS)
 	@mkdir -p wiser_amd/_lib/prof
-	$(HIPCC) $(HIPFLAGS) -DWSR_PROFILE -shared -o $@ $(SRCS) -lpthread -l:liblz4.so.1
+	$(HIPCC) $(HIPFLAGS) -DWSR_PROFILE -shared -o $@ $(SRCS) -lpthread -l:liblz4.so.1 -lrccl
 
 # tuning variants (diagnostics only): make variant V=name F="-DFLAG=..."
 variant: $(SRCS) $(HDRS)
 	@mkdir -p wiser_amd/_lib/var_$(V)
-	$(HIPCC) $(HIPFLAGS) $(F) -shared -o wiser_amd/_lib/var_$(V)/libwiser_hip.so $(SRCS) -lpthread -l:liblz4.so.1
+	$(HIPCC) $(HIPFLAGS) $(F) -shared -o wiser_amd/_lib/var_$(V)/libwiser_hip.so $(SRCS) -lpthread -l:liblz4.so.1 -lrccl
 
 clean:
 	rm -rf wiser_amd/_lib oracle/_build

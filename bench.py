@@ -55,8 +55,9 @@ def parse():
                    help="N>1: replica = full index per GPU, queries split across ranks (the "
                         "value when the index fits one GPU: auto); shard = doc-range shards "
                         "with the RCCL event exchange (auto also measures it, as 'docshard')")
-    p.add_argument("--dist-backend", default="nccl",
-                   help="shard exchange backend (nccl = RCCL over xGMI; gloo for 1-GPU rehearsals)")
+    p.add_argument("--dist-backend", default="gloo",
+                   help="the launcher's host-side group (rendezvous, RCCL id, barriers, timing "
+                        "reduction); the data path is the engine's own RCCL exchange")
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
     p.add_argument("--vacuum-dir", default=None,
                    help="configs[2]: an existing Vacuum dump (my.vacuum, my.tip, my.doc_length), "
@@ -536,9 +537,15 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     engine, checked, searcher)."""
     import torch
     import wiser_amd as w
-    from wiser_amd.shard import ShardedSearcher
+    from wiser_amd.shard import NativeShardedSearcher, slot_for_fill
     t = time.time()
-    S = ShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
+
+    def share_id(x):   # rank 0's RCCL id to every rank, over the launcher's gloo group
+        box = [x]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
     log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
     eng = S.engine
     Q = a.batch * world
@@ -549,9 +556,21 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         b.upload(resolve(eng, chunk, a.k))
         gb.append((b, chunk))
     nb = len(gb)
+    # exchange slot: every batch once with a generous slot, then twice the
+    # largest fill any rank saw (wsr_shard_fill), agreed over the group
+    big = 64 * a.batch
+    fill = 0
+    for b, _ in gb:
+        S.step(b, a.batch, big)
+        fill = max(fill, S.max_fill(b))
+    mx = torch.tensor([float(fill)])
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    slot = slot_for_fill(int(mx.item()), a.batch)
 
     def step(i, fetch=False):
-        return S.run(gb[i % nb][0], a.batch, fetch=fetch)
+        b = gb[i % nb][0]
+        S.step(b, a.batch, slot)
+        return S.fetch_owned(b, a.batch) if fetch else None
 
     checked = 0
     if a.check:   # every rank takes part in the collectives; rank 0 checks
@@ -560,6 +579,7 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
             checked = check_against_oracle(idx, gb[0][1][:a.batch], hits, nh, a.k, a.check)
     for s in range(a.warmup):
         step(s)
+    w.sync(eng)
     lat = []
     for i in range(nb):
         dist.barrier()
@@ -567,13 +587,16 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         step(i, fetch=True)
         lat.append((time.perf_counter() - t0) * 1e3)
     dist.barrier()
-    torch.cuda.synchronize()
+    w.sync(eng)
     t0 = time.perf_counter()
     for s in range(a.steps):
         step(s)
-    torch.cuda.synchronize()
+    w.sync(eng)
     el = time.perf_counter() - t0
+    for b, _ in gb:   # error flags (a slot overflow among them) of every batch's last step
+        S.fetch_owned(b, a.batch)
     queries = a.steps * Q  # every rank completes its owned 1/W of each global batch
+    S.slot = slot
     return queries, el, statistics.median(lat), [b for b, _ in gb], eng, checked, S
 
 
@@ -646,30 +669,39 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     mode = a.mode if world > 1 else "replica"
+    # the engine (and with it /opt/rocm's HIP runtime and RCCL) loads first: torch,
+    # imported after it for the launcher's rendezvous only, binds to the same
+    # libamdhip64 instead of bringing its own
+    import wiser_amd
+    from wiser_amd import _capi
+    runtime = _capi.runtime_info()
     if world > 1:
         import torch
         import torch.distributed as dist
         # one GPU per rank; rehearsals with more ranks than GPUs share devices
+        # (device_count does not initialise the GPU, torch never touches it)
         local = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
+        # host-side group (gloo): rendezvous, the RCCL id, barriers and the
+        # max-over-ranks timing; the data path is the engine's own RCCL exchange
         dist.init_process_group(a.dist_backend)
-    on_gpu = dist is not None and a.dist_backend == "nccl"
+    on_gpu = False
 
     idx, qlog = ensure_index(a, rank, dist)
     a.qlog = qlog
     lines = [l.split() for l in open(qlog).read().splitlines()]
     threads = min(16, os.cpu_count())
 
-    runner = run_shard if mode == "shard" else run_replica
+    sharded = mode in ("auto", "shard")
+    runner = run_shard if sharded else run_replica
     queries, el, p50, batches, eng, checked, S = runner(a, idx, lines, rank, world, local, dist, threads)
-    parallelism = f"docshard{world}" if mode == "shard" else f"replicas{world}"
+    parallelism = f"docshard{world}" if sharded else f"replicas{world}"
     global_batch = a.batch * world
     acc = kernel_accounting(eng, batches)
     nbk = len(batches)
     seg_avg_ms = acc["seg"] / nbk
     achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
     if dist:
-        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=(mode != "shard"))
+        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=not sharded)
     qps = queries / el
     for b in batches:
         b.close()
@@ -678,21 +710,21 @@ def main():
     else:
         eng.close()
 
-    # auto at N > 1: the doc-range sharded path, measured the same way, beside
-    # the replica value (the index fits one GPU, so replicas carry the value)
-    docshard = None
+    # auto at N > 1: the doc-range sharded path carries the value (SURVEY 8e,
+    # north_star); full-index replicas, queries split across ranks with no
+    # collective, are measured the same way beside it as the control
+    control = None
     if dist and a.mode == "auto":
-        sq, sel, sp50, sb, seng, _, SS = run_shard(
-            a, idx, lines, rank, world, local, dist, threads)
-        sel, sq, sp50 = reduce_timing(dist, sel, sq, sp50, on_gpu, summed=False)
-        docshard = {"value": round(sq / sel, 1), "ms_per_step": round(sel / a.steps * 1e3, 4),
-                    "global_batch": a.batch * world, "p50_ms": round(sp50, 3),
-                    "exchange": "all_to_all over " + ("RCCL" if a.dist_backend == "nccl" else a.dist_backend),
-                    "note": "each rank runs every query over its doc range; events exchanged; "
-                            "each query replayed by its owner"}
-        for b in sb:
+        rq, rel, rp50, rb, reng, _, _ = run_replica(a, idx, lines, rank, world, local, dist, threads)
+        rel, rq, rp50 = reduce_timing(dist, rel, rq, rp50, on_gpu, summed=True)
+        control = {"value": round(rq / rel, 1), "ms_per_step": round(rel / a.steps * 1e3, 4),
+                   "global_batch": a.batch * world, "p50_alone_ms": round(rp50, 3),
+                   "parallelism": f"replicas{world}",
+                   "note": "control: the full index on every GPU, each rank its own 4096 queries, "
+                           "no collective"}
+        for b in rb:
             b.close()
-        SS.close()
+        reng.close()
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -749,8 +781,13 @@ def main():
                           "other_blocks": int(acc["oblk"] / nbk), "work_items": int(acc["items"] / nbk)},
             "parity_checked_queries": checked,
         }
-        if docshard:
-            out["docshard"] = docshard
+        out["runtime"] = runtime
+        if sharded:
+            out["exchange"] = {"kind": "RCCL grouped send/recv per peer over xGMI (wsr_shard_step), "
+                                       "fixed slots, no host round trip inside a step",
+                               "slot_events": getattr(S, "slot", None)}
+        if control:
+            out["control"] = control
         if extra:
             out["legs"] = extra
         print(json.dumps(out), flush=True)

@@ -137,6 +137,9 @@ typedef struct wsr_batch_stats {
 
 const char* wsr_last_error(void);
 const char* wsr_version(void);
+/* the HIP runtime this process runs the engine on: hipRuntimeGetVersion and
+ * the paths of the loaded libamdhip64 / librccl (one runtime per process) */
+int wsr_runtime_info(char* buf, int32_t cap);
 
 /* ---- engine ---------------------------------------------------------- */
 int wsr_open(const char* vacuum_dir, const wsr_open_opts* opts, wsr_handle** out);
@@ -242,6 +245,39 @@ int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, w
                           int32_t* n_hits);
 /* the engine's HIP stream (a hipStream_t) for ordering the caller's work */
 int wsr_stream(wsr_handle* h, void** stream);
+/* the batch's own stream (a hipStream_t): its runs, packs and replays are
+ * ordered on it, so a caller's collectives enqueued there need no host wait */
+int wsr_batch_stream(wsr_handle* h, wsr_batch* b, void** stream);
+
+/* ---- fixed-slot exchange: no host round trip inside a step -----------
+ * Every (shard, owner) pair gets a slot of `slot` events, so the exchange
+ * sizes are known without reading counts back: a step is run_events ->
+ * pack_fixed -> all-to-all of counts (q_per_owner int32 per pair) and slots
+ * (slot * 16 B per pair) -> owner_replay_fixed, all on the batch's stream.  A
+ * query whose events would overflow its slot is flagged (count -1 and an error
+ * flag that wsr_batch_fetch* reports); the caller re-runs with a larger slot.
+ * wsr_shard_fill reads back the events per owner of the last pack (it waits
+ * for the batch), to size the slot. */
+int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
+                         int64_t slot, int32_t* d_counts, void* d_send);
+int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals);
+/* d_rcounts: n_shards x nq_owned (shard-major); d_recv: n_shards slots */
+int wsr_owner_replay_fixed(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                           int64_t slot, const int32_t* d_rcounts, const void* d_recv);
+
+/* ---- native RCCL exchange (one process per GPU; a C++ host needs no Python):
+ * rank 0 makes the id, every rank opens the communicator with it (the id
+ * travels by the caller's own rendezvous), then each step is one call:
+ * wsr_batch_run_events + wsr_shard_pack_fixed + grouped ncclSend / ncclRecv of
+ * counts and slots with every peer over xGMI + wsr_owner_replay_fixed, all
+ * enqueued on the batch's stream; rank r's owned queries are
+ * [r * q_per_owner, (r + 1) * q_per_owner) of a batch of world * q_per_owner. */
+#define WSR_COMM_ID_BYTES 128
+typedef struct wsr_comm wsr_comm;
+int wsr_comm_unique_id(uint8_t* id /* WSR_COMM_ID_BYTES */);
+int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device, wsr_comm** out);
+void wsr_comm_close(wsr_comm* c);
+int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot);
 
 /* Decode one block of a list on the device (test hook for the decoder):
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */

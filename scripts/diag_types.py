@@ -44,6 +44,9 @@ for name, qs in cls.items():
     if args.only and name != args.only:
         continue
     qs = qs[:4096]
+    if not qs:
+        print(f"{name:10s} n=0")
+        continue
     arr = (_capi.Query * len(qs))()
     for i, t in enumerate(qs):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=10))[0]

@@ -14,11 +14,16 @@ def pytest_configure(config):
 
 
 @pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first():
-    """torch ships its own HIP runtime; libwiser_hip.so links the system ROCm
-    one.  Both work in one process when torch initialises first (as bench.py's
-    distributed path does); a torch first touched after the engine has opened
-    a device finds no GPU.  So touch it first, whatever subset of tests runs."""
+def _engine_runtime_first():
+    """One HIP runtime per process, the one bench.py runs on: libwiser_hip.so
+    (linked against /opt/rocm's libamdhip64 and librccl) loads before torch, so
+    torch -- used by a few tests for device buffers and gloo -- binds to the
+    same already-loaded libamdhip64.so.7 instead of its bundled copy.  Then
+    torch's device state is initialised once, whatever subset of tests runs."""
+    try:
+        import wiser_amd  # noqa: F401
+    except Exception:
+        pass
     try:
         import torch
         torch.cuda.is_available()

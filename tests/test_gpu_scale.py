@@ -101,3 +101,14 @@ def test_search_text_chain(c3_small):
     assert rc == _capi.E_INVALID
     eng.close()
     orc.close()
+
+
+def test_runtime_is_system_rocm():
+    """The GPU suite runs the engine on the same runtime as bench.py: /opt/rocm's
+    libamdhip64 and librccl, loaded by libwiser_hip.so (conftest loads it before
+    torch).  Printed so that the GPU log records it."""
+    from wiser_amd import _capi
+    info = _capi.runtime_info()
+    print(info)
+    assert "/opt/rocm" in info.split("libamdhip64=")[1].split()[0], info
+    assert "/opt/rocm" in info.split("librccl=")[1], info

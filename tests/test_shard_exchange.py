@@ -37,14 +37,14 @@ def _scored_survivors(post, lens, avg, n, terms):
     return out
 
 
-def _worker(rank, world, port, index_dir, queries, k, result_q):
+def _worker(rank, world, port, index_dir, queries, k, result_q, fixed=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import heapmodel as hm
     import struct
     from oracle.oracle import OracleVacuum
-    from wiser_amd.shard import exchange, shard_range, index_doc_count
+    from wiser_amd.shard import exchange, exchange_fixed, shard_range, index_doc_count
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -74,7 +74,18 @@ def _worker(rank, world, port, index_dir, queries, k, result_q):
     for i, (s, d) in enumerate(events):
         send[i, 0] = struct.unpack("<q", struct.pack("<d", s))[0]
         send[i, 1] = d
-    rcounts, recv, rbase = exchange(torch.tensor(counts, dtype=torch.int32), send, totals, world, qpr)
+    if fixed:
+        # the product's fixed slots: owner o's events at [o * slot, ...), query order
+        slot = max(totals) + 3
+        fsend = torch.zeros((world * slot, 2), dtype=torch.int64)
+        at = 0
+        for o_ in range(world):
+            fsend[o_ * slot:o_ * slot + totals[o_]] = send[at:at + totals[o_]]
+            at += totals[o_]
+        rcounts, recv = exchange_fixed(torch.tensor(counts, dtype=torch.int32), fsend, world, qpr, slot)
+        rbase = [g * slot for g in range(world)]
+    else:
+        rcounts, recv, rbase = exchange(torch.tensor(counts, dtype=torch.int32), send, totals, world, qpr)
     res = []
     for qi in range(qpr):
         stream = []
@@ -89,8 +100,8 @@ def _worker(rank, world, port, index_dir, queries, k, result_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [3, 10])
-def test_gloo_two_rank_exchange_is_exact(indexes, k):
+@pytest.mark.parametrize("k,fixed", [(3, False), (10, False), (10, True)])
+def test_gloo_two_rank_exchange_is_exact(indexes, k, fixed):
     import random
     from oracle.oracle import OracleVacuum
     d = indexes["wiki5"][0]
@@ -103,7 +114,7 @@ def test_gloo_two_rank_exchange_is_exact(indexes, k):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, d, queries, k, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, d, queries, k, q, fixed)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}

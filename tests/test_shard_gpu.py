@@ -92,3 +92,111 @@ def test_sharded_equals_oracle_synthetic(synth_small, world):
     qs2, got = _run_sharded(d, qs, 10, world)
     for q, g in zip(qs2, got):
         assert g == o.search(q, 10)[0], q
+
+
+def _run_sharded_fixed(index_dir, queries, k, world, slot):
+    """The fixed-slot exchange (wsr_shard_pack_fixed / wsr_owner_replay_fixed):
+    slot o of shard g's send buffer goes to owner o as its slot g."""
+    import torch
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd._capi import check, lib
+    from wiser_amd.shard import index_doc_count, shard_range
+    qpr = len(queries) // world
+    queries = queries[:qpr * world]
+    n = index_doc_count(index_dir)
+    engs, batches, counts, sends = [], [], [], []
+    for r in range(world):
+        e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
+        e.Load()
+        arr = (_capi.Query * len(queries))()
+        for i, q in enumerate(queries):
+            arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
+        b = w.ResidentBatch(e, len(queries), k)
+        b.upload(arr)
+        check(lib.wsr_batch_run_events(e._h, b._b))
+        cnt = torch.empty(len(queries), dtype=torch.int32, device="cuda")
+        send = torch.empty((world * slot, 2), dtype=torch.int64, device="cuda")
+        check(lib.wsr_shard_pack_fixed(e._h, b._b, qpr, world, slot, C.c_void_p(cnt.data_ptr()),
+                                       C.c_void_p(send.data_ptr())))
+        check(lib.wsr_sync(e._h))
+        engs.append(e); batches.append(b); counts.append(cnt); sends.append(send)
+    out = []
+    for o in range(world):
+        rcounts = torch.stack([counts[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
+        recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
+        e, b = engs[o], batches[o]
+        check(lib.wsr_owner_replay_fixed(e._h, b._b, o * qpr, qpr, world, slot,
+                                         C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr())))
+        hits = (_capi.Hit * (qpr * k))()
+        nh = (C.c_int32 * qpr)()
+        rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
+        if rc:
+            for x in batches:
+                x.close()
+            for x in engs:
+                x.close()
+            raise _capi.WiserError(rc, lib.wsr_last_error().decode())
+        for i in range(qpr):
+            out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
+    for b in batches:
+        b.close()
+    for e in engs:
+        e.close()
+    return queries, out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_fixed_slot_exchange_equals_oracle(synth_small, world):
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_fixed.log")
+    w.gen_two_term_log(d, log, n_queries=960, seed=12)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    o = OracleVacuum(d)
+    qpr = len(qs) // world
+    qs2, got = _run_sharded_fixed(d, qs, 10, world, slot=64 * qpr)
+    for q, g in zip(qs2, got):
+        assert g == o.search(q, 10)[0], (world, q)
+
+
+def test_fixed_slot_overflow_is_loud(synth_small):
+    """A slot too small for a shard's events fails the owner's fetch (exchange
+    flag) instead of returning a result built from dropped events."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    d, _ = synth_small
+    head = [f"t{i:07d}" for i in range(8)]
+    qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
+    with pytest.raises(_capi.WiserError, match="exchange slot"):
+        _run_sharded_fixed(d, qs, 10, 2, slot=4)
+
+
+def test_native_rccl_step_one_rank(synth_small):
+    """wsr_shard_step (RCCL communicator, grouped send/recv, replay on the batch
+    stream) with a communicator of one rank: equal to the oracle."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import NativeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_native.log")
+    w.gen_two_term_log(d, log, n_queries=512, seed=13)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    S = NativeShardedSearcher(d, 0, 1, share_id=lambda x: x)
+    eng = S.engine
+    arr = (_capi.Query * len(qs))()
+    for i, q in enumerate(qs):
+        arr[i] = eng.resolve(w.SearchQuery(q, n_results=10))[0]
+    b = w.ResidentBatch(eng, len(qs), 10)
+    b.upload(arr)
+    for _ in range(3):
+        S.step(b, len(qs), 16 * len(qs))
+    hits, nh = S.fetch_owned(b, len(qs))
+    assert S.max_fill(b) > 0
+    o = OracleVacuum(d)
+    for i, q in enumerate(qs):
+        assert [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] == o.search(q, 10)[0], q
+    b.close()
+    S.close()

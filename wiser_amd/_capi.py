@@ -78,6 +78,7 @@ _P = C.c_void_p
 _sigs = {
     "wsr_last_error": (C.c_char_p, []),
     "wsr_version": (C.c_char_p, []),
+    "wsr_runtime_info": (C.c_int, [C.c_char_p, C.c_int32]),
     "wsr_open": (C.c_int, [C.c_char_p, C.POINTER(OpenOpts), C.POINTER(_P)]),
     "wsr_close": (None, [_P]),
     "wsr_term_count": (C.c_int, [_P, C.POINTER(C.c_int32)]),
@@ -107,6 +108,14 @@ _sigs = {
     "wsr_batch_fetch_range": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.POINTER(Hit),
                                         C.POINTER(C.c_int32)]),
     "wsr_stream": (C.c_int, [_P, C.POINTER(_P)]),
+    "wsr_batch_stream": (C.c_int, [_P, _P, C.POINTER(_P)]),
+    "wsr_shard_pack_fixed": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
+    "wsr_shard_fill": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int64)]),
+    "wsr_owner_replay_fixed": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
+    "wsr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    "wsr_comm_close": (None, [_P]),
+    "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
@@ -216,3 +225,10 @@ def header_symbols(path: str = HEADER):
     """Function names declared in include/wiser_hip.h."""
     text = open(path).read()
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(wsr_\w+)\s*\(", text, re.M)))
+
+
+def runtime_info() -> str:
+    """hipRuntimeGetVersion and the loaded libamdhip64 / librccl paths."""
+    buf = C.create_string_buffer(1024)
+    check(lib.wsr_runtime_info(buf, 1024))
+    return buf.value.decode()

@@ -1,6 +1,10 @@
 // C ABI (include/wiser_hip.h) over the HIP engine: index load + HBM upload,
 // resident query batches, kernel launches, result download.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+
+#include <cstdio>
 
 #include <algorithm>
 #include <atomic>
@@ -126,6 +130,15 @@ struct wsr_batch {
   uint64_t* d_roff = nullptr;     // owner side per (shard, query) offsets
   uint64_t* d_rbase = nullptr;
   size_t roff_cap = 0;
+  // native fixed-slot exchange (wsr_shard_step): counts, owner-major send slots,
+  // shard-major receive slots, allocated on first use
+  int32_t* d_xcount = nullptr;
+  int32_t* d_xrcount = nullptr;
+  Event* d_xsend = nullptr;
+  Event* d_xrecv = nullptr;
+  uint64_t x_slots = 0;     // slot capacity * pairs the two event buffers were sized for
+  int x_pairs = 0;
+  hipEvent_t xev[2] = {nullptr, nullptr};   // pack done -> comm stream; exchange done -> replay
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
@@ -139,7 +152,18 @@ struct wsr_batch {
 extern "C" {
 
 const char* wsr_last_error(void) { return g_err.c_str(); }
-const char* wsr_version(void) { return "wiser-hip 0.1 (gfx950)"; }
+const char* wsr_version(void) { return "wiser-hip 0.2 (gfx950)"; }
+
+int wsr_runtime_info(char* buf, int32_t cap) {
+  if (!buf || cap <= 0) return fail(WSR_E_INVALID, "null argument");
+  int ver = 0;
+  (void)hipRuntimeGetVersion(&ver);
+  Dl_info hip{}, rccl{};
+  const char* hp = dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &hip) && hip.dli_fname ? hip.dli_fname : "?";
+  const char* rp = dladdr(reinterpret_cast<void*>(&ncclGetUniqueId), &rccl) && rccl.dli_fname ? rccl.dli_fname : "?";
+  std::snprintf(buf, static_cast<size_t>(cap), "hipRuntimeGetVersion=%d libamdhip64=%s librccl=%s", ver, hp, rp);
+  return WSR_OK;
+}
 
 int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
   if (!dir || !out) return fail(WSR_E_INVALID, "null argument");
@@ -164,7 +188,12 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     int threads = opts && opts->threads > 0 ? opts->threads : static_cast<int>(std::thread::hardware_concurrency());
     // dense-list bitmaps: lists with >= span/div postings (WSR_DENSE_DIV, 0 = off);
     // probed by bitmap when >= ratio x the driver's blocks (WSR_DENSE_RATIO)
-    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 128));
+    // (1024: every list that is at least 1/1024 of the doc range -- on the
+    // en-Wikipedia-shaped C3 corpus this halves the mixed batch against 128,
+    // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
+    // caps the bitmaps' HBM, longest lists first)
+    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 1024));
+    const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 32) * 1e9);
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
     // replay inside the segment kernel (WSR_FUSE_REPLAY=0: separate launch)
     h->fuse_replay = env_number("WSR_FUSE_REPLAY", 1) != 0;
@@ -172,7 +201,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // (WSR_SEG_FLOOR=0: every segment from an empty top-k)
     h->seg_floor = env_number("WSR_SEG_FLOOR", 1) != 0;
     h->positions = opts && opts->positions;
-    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions);
+    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions, dense_budget);
     if (h->positions) {
       dev_upload(&h->d_pos_blob, img.pos_blob);
       dev_upload(&h->d_pos_lists, img.pos_lists);
@@ -232,7 +261,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->grid = prop.multiProcessorCount * std::min(occ, 32);
     // general workers hold 12 KB of LDS each: at most 4 per CU, so that the
     // concurrent lean kernel keeps its occupancy
-    h->gen_cap = prop.multiProcessorCount * std::min(std::min(occ, 32), 4);
+    const int gen_per_cu = static_cast<int>(env_number("WSR_GEN_PER_CU", 4));
+    h->gen_cap = prop.multiProcessorCount * std::max(1, std::min(std::min(occ, 32), gen_per_cu));
     int locc = lean_kernel_occupancy();
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
@@ -494,9 +524,12 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_qdone), static_cast<void*>(b->d_itemq),
                   static_cast<void*>(b->d_pub), static_cast<void*>(b->d_ph),
                   static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
-                  static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase)})
+                  static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase),
+                  static_cast<void*>(b->d_xcount), static_cast<void*>(b->d_xrcount),
+                  static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
   if (b->fork) (void)hipEventDestroy(b->fork);
   if (b->join) (void)hipEventDestroy(b->join);
   if (b->st) (void)hipStreamDestroy(b->st);
@@ -927,13 +960,190 @@ int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, 
   return WSR_OK;
 }
 
-int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
-                          int32_t* n_hits) {
-  if (!h || !b || q0 < 0 || nq < 0 || q0 + nq > b->nq) return fail(WSR_E_INVALID, "bad range");
-  std::lock_guard<std::mutex> g(h->mu);
+int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
+                         int64_t slot, int32_t* d_counts, void* d_send) {
+  if (!h || !b || !b->ran || !d_counts || !d_send || q_per_owner <= 0 || n_owners <= 0 || slot <= 0 ||
+      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
+    return fail(WSR_E_INVALID, "bad shard_pack_fixed arguments");
+  if (n_owners > 1024) return fail(WSR_E_LIMIT, "more than 1024 owners");
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = b->st;
+    if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
+    if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
+    HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
+    HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
+    HIP_OK(launch_pack_fixed(b->d_plan, b->nq, b->d_events, d_counts, b->d_soff, q_per_owner,
+                             static_cast<uint64_t>(slot), static_cast<Event*>(d_send), b->d_ctr, st));
+    b->d_scount = d_counts;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals) {
+  if (!h || !b || !b->d_otot || !owner_totals || n_owners <= 0 || n_owners > 1024)
+    return fail(WSR_E_INVALID, "call wsr_shard_pack_fixed first");
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
+    HIP_OK(hipMemcpy(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_owner_replay_fixed(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                           int64_t slot, const int32_t* d_rcounts, const void* d_recv) {
+  if (!h || !b || n_shards <= 0 || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq || slot <= 0 ||
+      (nq_owned && (!d_rcounts || !d_recv)))
+    return fail(WSR_E_INVALID, "bad owner_replay_fixed arguments");
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    const size_t n = static_cast<size_t>(n_shards) * nq_owned;
+    if (n > b->roff_cap) {
+      if (b->d_roff) HIP_OK(hipFree(b->d_roff));
+      b->d_roff = nullptr;
+      b->roff_cap = n + 1024;
+      HIP_OK(hipMalloc(&b->d_roff, sizeof(uint64_t) * b->roff_cap));
+    }
+    HIP_OK(launch_owner_replay_fixed(b->d_q, q0, nq_owned, n_shards, d_rcounts, b->d_roff,
+                                     static_cast<uint64_t>(slot), static_cast<const Event*>(d_recv),
+                                     b->d_hits, b->stride, b->d_nhits, b->d_ctr, b->st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_batch_stream(wsr_handle* h, wsr_batch* b, void** stream) {
+  if (!h || !b || !stream) return fail(WSR_E_INVALID, "null argument");
+  *stream = b->st;
+  return WSR_OK;
+}
+
+// ---- native RCCL exchange (one process per GPU, no Python in the loop) ----
+// Every collective of a communicator runs on its one stream, in issue order
+// (the same order on every rank), whatever batch stream it serves: a step's
+// pack is joined into it by an event and its replay waits for it by another,
+// so consecutive batches still overlap their kernels.
+struct wsr_comm {
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  int world = 0, rank = 0, device = 0;
+};
+
+int wsr_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(WSR_E_INVALID, "null argument");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(WSR_E_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  static_assert(sizeof(ncclUniqueId) == WSR_COMM_ID_BYTES, "RCCL unique id size");
+  std::memcpy(id, &u, sizeof u);
+  return WSR_OK;
+}
+
+int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device, wsr_comm** out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) return fail(WSR_E_INVALID, "bad comm arguments");
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return fail(WSR_E_HIP, "hipSetDevice failed");
+  std::unique_ptr<wsr_comm> c(new wsr_comm());
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+  if (r != ncclSuccess) return fail(WSR_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)ncclCommDestroy(c->comm);
+    return fail(WSR_E_HIP, "hipStreamCreate failed");
+  }
+  c->world = world;
+  c->rank = rank;
+  c->device = device;
+  *out = c.release();
+  return WSR_OK;
+}
+
+void wsr_comm_close(wsr_comm* c) {
+  if (!c) return;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
+  if (!h || !b || !c || q_per_owner <= 0 || slot <= 0 ||
+      static_cast<int64_t>(q_per_owner) * c->world != b->nq)
+    return fail(WSR_E_INVALID, "bad shard_step arguments (the batch must hold world * q_per_owner queries)");
+  int rc = batch_run(h, b, false);
+  if (rc) return rc;
+  const int W = c->world;
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    const uint64_t need = static_cast<uint64_t>(slot) * W;
+    if (!b->d_xcount) {
+      HIP_OK(hipMalloc(&b->d_xcount, sizeof(int32_t) * b->max_q));
+      HIP_OK(hipMalloc(&b->d_xrcount, sizeof(int32_t) * b->max_q));
+    }
+    if (need > b->x_slots || W != b->x_pairs) {
+      if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
+      if (b->d_xrecv) HIP_OK(hipFree(b->d_xrecv));
+      b->d_xsend = b->d_xrecv = nullptr;
+      HIP_OK(hipMalloc(&b->d_xsend, sizeof(Event) * need));
+      HIP_OK(hipMalloc(&b->d_xrecv, sizeof(Event) * need));
+      b->x_slots = need;
+      b->x_pairs = W;
+    }
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  rc = wsr_shard_pack_fixed(h, b, q_per_owner, W, slot, b->d_xcount, b->d_xsend);
+  if (rc) return rc;
+  // counts and event slots, every pair at once (xGMI is point to point: one
+  // send / receive per peer, no ring)
+  auto nc = [](ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+  };
+  try {
+    if (!b->xev[0]) {
+      HIP_OK(hipEventCreateWithFlags(&b->xev[0], hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&b->xev[1], hipEventDisableTiming));
+    }
+    HIP_OK(hipEventRecord(b->xev[0], b->st));
+    HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
+    nc(ncclGroupStart(), "ncclGroupStart");
+    for (int p = 0; p < W; ++p) {
+      nc(ncclSend(b->d_xcount + static_cast<size_t>(p) * q_per_owner, q_per_owner, ncclInt32, p, c->comm,
+                  c->stream), "ncclSend counts");
+      nc(ncclRecv(b->d_xrcount + static_cast<size_t>(p) * q_per_owner, q_per_owner, ncclInt32, p, c->comm,
+                  c->stream), "ncclRecv counts");
+      nc(ncclSend(b->d_xsend + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
+                  c->comm, c->stream), "ncclSend events");
+      nc(ncclRecv(b->d_xrecv + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
+                  c->comm, c->stream), "ncclRecv events");
+    }
+    nc(ncclGroupEnd(), "ncclGroupEnd");
+    HIP_OK(hipEventRecord(b->xev[1], c->stream));
+    HIP_OK(hipStreamWaitEvent(b->st, b->xev[1], 0));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return wsr_owner_replay_fixed(h, b, c->rank * q_per_owner, q_per_owner, W, slot, b->d_xrcount, b->d_xrecv);
+}
+
+int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
+                          int32_t* n_hits) {
+  if (!h || !b || q0 < 0 || nq < 0 || q0 + nq > b->nq) return fail(WSR_E_INVALID, "bad range");
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(b->st));
+    uint32_t ctr[kNumCounters];
+    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    if (ctr[kCtrError])
+      return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]) +
+                                      (ctr[kCtrError] & kErrExchange ? " (an exchange slot overflowed)" : ""));
     if (nq && hits)
       HIP_OK(hipMemcpy(hits, b->d_hits + static_cast<size_t>(q0) * b->stride,
                        sizeof(HitDev) * static_cast<size_t>(nq) * b->stride, hipMemcpyDeviceToHost));

@@ -271,7 +271,7 @@ void for_each_list(int32_t L, int threads, F&& fn) {
 // the arrays in place.  (Millions of one-block lists -- the en-Wikipedia shape
 // -- made per-list vectors and their serial concatenation the load's cost.)
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div, bool positions) {
+                      uint32_t dense_div, bool positions, uint64_t dense_budget) {
   const int32_t L = idx.n_lists();
   const uint8_t* file = idx.file();
   const uint8_t* fend = file + idx.file_bytes();
@@ -369,6 +369,23 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   });
 
   lap("pass 1 (sizes)");
+  // bitmap budget: when the dense lists' bitmaps + 1-byte tfs would exceed it,
+  // the longest lists keep theirs (they are the ones probed most)
+  if (dense_budget) {
+    std::vector<std::pair<uint64_t, int32_t>> cand;   // (postings in the image, list)
+    for (int32_t id = 0; id < L; ++id)
+      if (info[id].dense)
+        cand.emplace_back((info[id].r1 - info[id].r0 - 1) * uint64_t{kPackSize} + info[id].tail_cnt, id);
+    std::sort(cand.begin(), cand.end(), [](const auto& a, const auto& b) {
+      return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    uint64_t used = 0;
+    for (const auto& c : cand) {
+      const uint64_t bytes = n_ent * sizeof(DenseEnt) + c.first;
+      if (used + bytes > dense_budget) info[c.second].dense = 0;
+      else used += bytes;
+    }
+  }
   // ---- pass 2: offsets in list-id order
   HostImage img;
   img.doc_lo = doc_lo;

@@ -128,9 +128,10 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
                        uint32_t prev, uint32_t* out);
 
 // dense_div > 0: lists with at least span / dense_div postings in the image get
-// a rank bitmap + 1-byte tf array (0 disables them).
+// a rank bitmap + 1-byte tf array (0 disables them); dense_budget > 0 caps the
+// bytes of all bitmaps + tf arrays (the longest lists keep theirs).
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div = 0, bool positions = false);
+                      uint32_t dense_div = 0, bool positions = false, uint64_t dense_budget = 0);
 
 // Host restatement of the device's dense probe (segment kernel): tf of doc in
 // list L of the image, -1 when absent or when L has no bitmap.

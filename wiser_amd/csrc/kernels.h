@@ -57,7 +57,7 @@ constexpr int kStatStride = 16;  // + section cycles: 4 dequeue/setup, 5 driver,
 #else
 constexpr int kStatStride = 4;
 #endif
-enum { kErrLimit = 1, kErrCapacity = 2 };
+enum { kErrLimit = 1, kErrCapacity = 2, kErrExchange = 4 };
 
 #ifndef WSR_SEG_COST
 #define WSR_SEG_COST 63
@@ -138,6 +138,14 @@ hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events
 hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
                                const uint64_t* roff, const uint64_t* rbase, const Event* recv,
                                HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st);
+// fixed-slot exchange: pack (shard side, after launch_shard_reduce + scan) and
+// scan + replay (owner side); slot = events per (shard, owner) pair
+hipError_t launch_pack_fixed(const QueryPlan* plan, int nq, const Event* events, int32_t* scount,
+                             const uint64_t* off, int q_per_owner, uint64_t slot, Event* send,
+                             uint32_t* counters, hipStream_t st);
+hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
+                                     uint64_t* roff, uint64_t slot, const Event* recv, HitDev* hits,
+                                     int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st);
 // resident 64-thread segment workgroups per CU
 int segment_kernel_occupancy();
 

@@ -2262,6 +2262,7 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
                                                           const int32_t* __restrict__ rcount,
                                                           const uint64_t* __restrict__ roff,
                                                           const uint64_t* __restrict__ rbase,
+                                                          uint64_t slot,
                                                           const Event* __restrict__ recv,
                                                           HitDev* __restrict__ hits, int hit_stride,
                                                           int32_t* __restrict__ n_hits) {
@@ -2276,10 +2277,77 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
   sink.k = k;
   consume_stream(
       F, static_cast<uint32_t>(n_shards),
-      [&](uint32_t g) { return static_cast<uint32_t>(rcount[static_cast<int64_t>(g) * nq + qi]); },
-      [&](uint32_t g) { return recv + rbase[g] + roff[static_cast<int64_t>(g) * nq + qi]; }, s_off,
+      [&](uint32_t g) {   // (a negative count marks a sender's slot overflow: flagged, read as 0)
+        const int32_t c = rcount[static_cast<int64_t>(g) * nq + qi];
+        return static_cast<uint32_t>(c > 0 ? c : 0);
+      },
+      [&](uint32_t g) {
+        return recv + (rbase ? rbase[g] : g * slot) + roff[static_cast<int64_t>(g) * nq + qi];
+      }, s_off,
       [&](double sv, int32_t dv) { sink.insert(sv, dv); });
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+}
+
+// Fixed-slot exchange (no host round trip): owner o's events from this shard
+// go to send[o * slot ...] in query order; a query whose events would pass the
+// slot's end is not copied, its count becomes -1 and the error flag is set (the
+// owner's replay flags it again).  off = exclusive scan of scount over all the
+// batch's queries (scan_counts_kernel).
+__global__ __launch_bounds__(64) void pack_fixed_kernel(const QueryPlan* __restrict__ plan, int nq,
+                                                        const Event* __restrict__ events,
+                                                        int32_t* __restrict__ scount,
+                                                        const uint64_t* __restrict__ off, int q_per_owner,
+                                                        uint64_t slot, Event* __restrict__ send,
+                                                        uint32_t* __restrict__ counters) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int o = qi / q_per_owner;
+  const uint64_t rel = off[qi] - off[o * q_per_owner];
+  const int n = scount[qi];
+  if (rel + static_cast<uint64_t>(n) > slot) {
+    if (threadIdx.x == 0) {
+      scount[qi] = -1;
+      atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
+    }
+    return;
+  }
+  const Event* src = events + plan[qi].ev_base;
+  Event* dst = send + o * slot + rel;
+  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+
+// Owner side: per shard row g of rcount (n counts each), the exclusive scan of
+// its counts (negative = a sender's overflow: flagged, counted as 0).
+__global__ __launch_bounds__(1024) void scan_rows_kernel(const int32_t* __restrict__ cnt, int n,
+                                                         uint64_t* __restrict__ off,
+                                                         uint32_t* __restrict__ counters) {
+  __shared__ uint64_t s[1024];
+  const int t = threadIdx.x, T = blockDim.x;
+  const int32_t* c = cnt + static_cast<int64_t>(blockIdx.x) * n;
+  uint64_t* o = off + static_cast<int64_t>(blockIdx.x) * n;
+  const int per = (n + T - 1) / T;
+  const int i0 = t * per, i1 = min(n, i0 + per);
+  uint64_t sum = 0;
+  bool bad = false;
+  for (int i = i0; i < i1; ++i) {
+    const int32_t v = c[i];
+    bad |= v < 0;
+    sum += v > 0 ? static_cast<uint64_t>(v) : 0ull;
+  }
+  if (bad) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
+  s[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < T; d <<= 1) {
+    const uint64_t a = t >= d ? s[t - d] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  uint64_t run = s[t] - sum;
+  for (int i = i0; i < i1; ++i) {
+    o[i] = run;
+    run += c[i] > 0 ? static_cast<uint64_t>(c[i]) : 0ull;
+  }
 }
 
 // ------------------------------------------------------------ launchers --
@@ -2373,12 +2441,31 @@ hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events
   return hipGetLastError();
 }
 
+hipError_t launch_pack_fixed(const QueryPlan* plan, int nq, const Event* events, int32_t* scount,
+                             const uint64_t* off, int q_per_owner, uint64_t slot, Event* send,
+                             uint32_t* counters, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_fixed_kernel, dim3(nq), dim3(64), 0, st, plan, nq, events, scount, off,
+                     q_per_owner, slot, send, counters);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
+                                     uint64_t* roff, uint64_t slot, const Event* recv, HitDev* hits,
+                                     int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(n_shards), dim3(1024), 0, st, rcount, nq, roff, counters);
+  hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount, roff,
+                     static_cast<const uint64_t*>(nullptr), slot, recv, hits, hit_stride, n_hits);
+  return hipGetLastError();
+}
+
 hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
                                const uint64_t* roff, const uint64_t* rbase, const Event* recv,
                                HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st) {
   if (nq <= 0) return hipSuccess;
   hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount,
-                     roff, rbase, recv, hits, hit_stride, n_hits);
+                     roff, rbase, static_cast<uint64_t>(0), recv, hits, hit_stride, n_hits);
   return hipGetLastError();
 }
 

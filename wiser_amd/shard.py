@@ -8,6 +8,17 @@ GPUs, gloo on CPU in tests) and replayed by the query's owner rank in shard
 order, which reproduces the single-engine result bit for bit.
 
 Queries of a global batch are owned by contiguous slices: owner(q) = q // qpr.
+
+Two exchanges, both with every size known before the step runs (no host
+round trip inside a step):
+  * NativeShardedSearcher: wsr_shard_step, one C call per step -- the engine
+    packs each owner's events into a fixed slot, RCCL moves counts and slots
+    with grouped send / recv over xGMI, the owner replays; all on the batch's
+    HIP stream.  torch is only the launcher's rendezvous (gloo, host side).
+  * ShardedSearcher: the same fixed slots exchanged by torch.distributed
+    all_to_all (gloo on the CPU in tests, or RCCL through torch).
+A slot that overflows fails the batch loudly (error flag at fetch); the slot
+size comes from the measured fill (slot_for_fill).
 """
 from __future__ import annotations
 
@@ -66,6 +77,81 @@ def exchange(counts, send, owner_totals: Sequence[int], world: int, qpr: int, gr
     return rcounts, recv, rbase
 
 
+def exchange_fixed(counts, send, world: int, qpr: int, slot: int, group=None, out=None):
+    """Fixed-slot exchange: counts int32 [world * qpr] (query order), send
+    int64 [world * slot, 2] (owner-major slots) -> (rcounts int32 [world, qpr]
+    shard-major, recv int64 [world * slot, 2] shard-major), into `out` when
+    given.  Equal splits, so no size is read back."""
+    import torch
+    import torch.distributed as dist
+    dev = counts.device
+    if out is None:
+        out = (torch.empty((world, qpr), dtype=torch.int32, device=dev),
+               torch.empty((world * slot, EVENT_WORDS), dtype=torch.int64, device=dev))
+    rcounts, recv = out
+    if dist.get_backend(group) == "gloo" and dev.type != "cpu":
+        rc, rv = exchange_fixed(counts.cpu(), send.cpu(), world, qpr, slot, group)
+        rcounts.copy_(rc)
+        recv.copy_(rv)
+        return rcounts, recv
+    dist.all_to_all_single(rcounts.view(-1), counts.view(-1), group=group)
+    dist.all_to_all_single(recv, send, group=group)
+    return rcounts, recv
+
+
+def slot_for_fill(max_fill: int, qpr: int) -> int:
+    """Slot size (events per shard -> owner pair) for an observed largest fill:
+    twice it, and never under 8 events per owned query."""
+    return int(max(2 * max_fill, 8 * qpr, 1024))
+
+
+class NativeShardedSearcher:
+    """One rank of a doc-range sharded engine whose whole step runs in C++
+    (wsr_shard_step: run + pack + RCCL grouped send/recv + owner replay)."""
+
+    def __init__(self, index_dir: str, rank: int, world: int, share_id, device: int = 0,
+                 threads: int = 0, positions: bool = False):
+        """share_id(bytes_or_None) -> bytes: the launcher's rendezvous; rank 0
+        passes the RCCL id it made, every rank gets rank 0's id back."""
+        from .engine import VacuumEngine
+        self.rank, self.world = rank, world
+        self.n_docs = index_doc_count(index_dir)
+        self.doc_range = shard_range(self.n_docs, rank, world)
+        self.engine = VacuumEngine(index_dir, device=device, threads=threads,
+                                   doc_range=self.doc_range if world > 1 else None, positions=positions)
+        self.engine.Load()
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            check(lib.wsr_comm_unique_id(uid))
+        got = share_id(bytes(uid) if rank == 0 else None)
+        uid = (C.c_uint8 * 128).from_buffer_copy(got)
+        c = C.c_void_p()
+        check(lib.wsr_comm_open(uid, world, rank, device, C.byref(c)))
+        self._c = c
+
+    def step(self, b, qpr: int, slot: int):
+        """Enqueue one step of an uploaded global batch (world * qpr queries);
+        results of the owned slice stay in HBM (fetch_owned reads them)."""
+        check(lib.wsr_shard_step(self.engine._h, b._b, self._c, qpr, slot))
+
+    def max_fill(self, b) -> int:
+        tot = (C.c_int64 * self.world)()
+        check(lib.wsr_shard_fill(self.engine._h, b._b, self.world, tot))
+        return max(tot)
+
+    def fetch_owned(self, b, qpr: int):
+        hits = (_capi.Hit * (qpr * b.stride))()
+        nh = (C.c_int32 * qpr)()
+        check(lib.wsr_batch_fetch_range(self.engine._h, b._b, self.rank * qpr, qpr, hits, nh))
+        return hits, nh
+
+    def close(self):
+        if self._c:
+            lib.wsr_comm_close(self._c)
+            self._c = None
+        self.engine.close()
+
+
 class ShardedSearcher:
     """One rank of a doc-range sharded engine (device = local GPU)."""
 
@@ -80,6 +166,7 @@ class ShardedSearcher:
                                    positions=positions)
         self.engine.Load()
         self._batches = {}
+        self._xbufs = {}
 
     def batch(self, max_queries: int, k: int):
         from .engine import ResidentBatch
@@ -88,30 +175,43 @@ class ShardedSearcher:
             self._batches[key] = ResidentBatch(self.engine, max_queries, k)
         return self._batches[key]
 
-    def run(self, b, qpr: int, fetch: bool = True):
+    def run(self, b, qpr: int, fetch: bool = True, slot: int = 0):
         """Run an uploaded global batch (world * qpr queries); returns this
         rank's owned slice [rank*qpr, (rank+1)*qpr) as (hits, n_hits) ctypes
-        arrays (None when fetch is False: results stay in HBM)."""
+        arrays (None when fetch is False: results stay in HBM).  The fixed-slot
+        exchange (slot events per pair; 0 = 32 per owned query) is ordered on
+        the batch's stream, so nothing waits on the host inside the step."""
         import torch
         eng = self.engine
         Q = b.nq
         assert Q == qpr * self.world
+        slot = slot or 32 * qpr
         check(lib.wsr_batch_run_events(eng._h, b._b))
-        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
-            else torch.device("cpu")
-        counts = torch.empty(Q, dtype=torch.int32, device=dev)
-        totals = (C.c_int64 * self.world)()
-        check(lib.wsr_shard_reduce(eng._h, b._b, qpr, self.world, C.c_void_p(counts.data_ptr()),
-                                   totals))
-        tot = list(totals)
-        send = torch.empty((max(sum(tot), 1), EVENT_WORDS), dtype=torch.int64, device=dev)
-        check(lib.wsr_shard_pack(eng._h, b._b, C.c_void_p(send.data_ptr())))
-        rcounts, recv, rbase = exchange(counts, send, tot, self.world, qpr, self.group)
-        torch.cuda.synchronize()
-        rb = (C.c_uint64 * self.world)(*rbase)
+        on_gpu = torch.cuda.is_available()
+        dev = torch.device("cuda", eng.device) if on_gpu else torch.device("cpu")
+        # per batch and slot size: buffers used only in the batch's stream order
+        key = (id(b), slot)
+        if key not in self._xbufs:
+            self._xbufs[key] = (
+                torch.empty(Q, dtype=torch.int32, device=dev),
+                torch.empty((self.world * slot, EVENT_WORDS), dtype=torch.int64, device=dev),
+                torch.empty((self.world, qpr), dtype=torch.int32, device=dev),
+                torch.empty((self.world * slot, EVENT_WORDS), dtype=torch.int64, device=dev))
+        counts, send, rc_buf, rv_buf = self._xbufs[key]
+        check(lib.wsr_shard_pack_fixed(eng._h, b._b, qpr, self.world, slot, C.c_void_p(counts.data_ptr()),
+                                       C.c_void_p(send.data_ptr())))
+        st = C.c_void_p()
+        check(lib.wsr_batch_stream(eng._h, b._b, C.byref(st)))
+        if on_gpu:   # the collectives go on the batch's stream, after the pack
+            with torch.cuda.stream(torch.cuda.ExternalStream(st.value, device=dev)):
+                rcounts, recv = exchange_fixed(counts, send, self.world, qpr, slot, self.group,
+                                               out=(rc_buf, rv_buf))
+        else:
+            rcounts, recv = exchange_fixed(counts, send, self.world, qpr, slot, self.group,
+                                           out=(rc_buf, rv_buf))
         q0 = self.rank * qpr
-        check(lib.wsr_owner_replay(eng._h, b._b, q0, qpr, self.world,
-                                   C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr()), rb))
+        check(lib.wsr_owner_replay_fixed(eng._h, b._b, q0, qpr, self.world, slot,
+                                         C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr())))
         if not fetch:
             return None
         hits = (_capi.Hit * (qpr * b.stride))()
@@ -123,4 +223,5 @@ class ShardedSearcher:
         for b in self._batches.values():
             b.close()
         self._batches.clear()
+        self._xbufs.clear()
         self.engine.close()
