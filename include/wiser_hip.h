@@ -42,15 +42,17 @@
 extern "C" {
 #endif
 
-#define WSR_MAX_TERMS 8
-#define WSR_MAX_K 64
+#define WSR_MAX_TERMS 16        /* terms of a conjunctive query */
+#define WSR_MAX_PHRASE_TERMS 8  /* terms of a phrase query (the reference's cap, query_processing.h:695) */
+#define WSR_MAX_K 1024          /* n_results (k > 64 keeps the replay's heap in LDS) */
+#define WSR_SERVER_MAX_K 64     /* n_results through the micro-batcher (wsr_server_*) */
 
 enum {
   WSR_OK = 0,
   WSR_E_INVALID = -1,   /* bad argument */
   WSR_E_IO = -2,        /* missing / malformed index files */
   WSR_E_HIP = -3,       /* HIP runtime error (no device, out of memory, ...) */
-  WSR_E_LIMIT = -4,     /* n_terms > WSR_MAX_TERMS or k > WSR_MAX_K */
+  WSR_E_LIMIT = -4,     /* n_terms > WSR_MAX_TERMS (phrase: WSR_MAX_PHRASE_TERMS) or k > WSR_MAX_K */
   WSR_E_INTERNAL = -5
 };
 
@@ -213,7 +215,7 @@ typedef struct wsr_serve_stats {
 } wsr_serve_stats;
 int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_server** out);
 void wsr_server_close(wsr_server* s);
-/* one query (k <= WSR_MAX_K): hits receives n_hits <= k entries */
+/* one query (k <= WSR_SERVER_MAX_K): hits receives n_hits <= k entries */
 int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t* n_hits);
 /* closed-loop load (the reference client's threads, grpc_client_impl.h:557-620):
  * n_clients threads keep `depth` queries each in flight, drawn round-robin from

@@ -63,4 +63,4 @@ def test_struct_layouts(built, tmp_path):
     assert got == [C.sizeof(_capi.Query), _capi.Query.flags.offset, C.sizeof(_capi.Hit),
                    C.sizeof(_capi.OpenOpts), _capi.OpenOpts.positions.offset,
                    C.sizeof(_capi.BatchStats), C.sizeof(_capi.BuildStats)]
-    assert C.sizeof(_capi.Query) == 44 and C.sizeof(_capi.Hit) == 16
+    assert C.sizeof(_capi.Query) == 76 and C.sizeof(_capi.Hit) == 16

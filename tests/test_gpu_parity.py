@@ -220,7 +220,9 @@ def test_limits_fail_loudly(gpu_indexes):
     import wiser_amd as w
     eng, _, _ = gpu_indexes["three"]
     with pytest.raises(NotImplementedError):
-        eng.Search(w.SearchQuery(["hello"], n_results=65))
+        eng.Search(w.SearchQuery(["hello"], n_results=1025))
+    with pytest.raises(NotImplementedError):
+        eng.Search(w.SearchQuery(["hello"] * 17))
 
 
 @pytest.mark.parametrize("mode", sorted(DENSE_MODES))
@@ -250,3 +252,54 @@ def test_large_tf_dense_escape(tmp_path, mode):
                       ["x", "w299"]], 64)
     eng.close()
     orc.close()
+
+
+@pytest.mark.parametrize("mode", list(DENSE_MODES))
+def test_wide_k(synth_small, mode):
+    """k > 64 (refused before): every survivor of a wide query is
+    an event and the replay keeps the libstdc++ heap in LDS; k = 65, 100, 500
+    and the limit 1024, mixed with k = 10 queries in one batch."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    eng = _engine(d, mode)
+    orc = OracleVacuum(d)
+    log = os.path.join(d, "qwide.log")
+    w.gen_two_term_log(d, log, n_queries=300, seed=21)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    head = [f"t{i:07d}" for i in range(12)]
+    rng = random.Random(5)
+    qs += [[h] for h in head] + [rng.sample(head, 2) for _ in range(40)]
+    ks = [65, 100, 500, 1024, 10]
+    items = [(q, ks[i % len(ks)]) for i, q in enumerate(qs)]
+    res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q, k in items])
+    for (q, k), r in zip(items, res):
+        assert [(e.doc_id, e.doc_score) for e in r.entries] == orc.search(q, k)[0], (q, k)
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", ["blocks", "dense", "dense_all"])
+def test_many_terms(synth_small, mode):
+    """Conjunctive queries of 9 to 16 terms (at most 8 before); the
+    phrase cap stays 8 (query_processing.h:695) and a longer phrase is refused."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    from wiser_amd import _capi
+    d, _ = synth_small
+    eng = _engine(d, mode)
+    orc = OracleVacuum(d)
+    head = [f"t{i:07d}" for i in range(24)]
+    rng = random.Random(6)
+    qs = [rng.sample(head, n) for n in (9, 10, 12, 12, 14, 16, 16) for _ in range(6)]
+    qs += [head[:12] + head[:4]]   # duplicates: each occurrence scores
+    for k in (10, 100):
+        res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
+        for q, r in zip(qs, res):
+            assert [(e.doc_id, e.doc_score) for e in r.entries] == orc.search(q, k)[0], (q, k)
+    nonempty = sum(1 for r in eng.SearchBatch([w.SearchQuery(q) for q in qs]) if r.Size())
+    assert nonempty > 10
+    with pytest.raises(_capi.WiserError, match="LIMIT"):
+        eng.SearchBatch([w.SearchQuery(head[:9], is_phrase=True)])
+    with pytest.raises(_capi.WiserError, match="LIMIT"):
+        eng.SearchBatch([w.SearchQuery(head[:17])])
+    eng.close()

@@ -200,3 +200,20 @@ def test_native_rccl_step_one_rank(synth_small):
         assert [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] == o.search(q, 10)[0], q
     b.close()
     S.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fixed_slot_wide_k(synth_small, world):
+    """k > 64 through doc-range shards: the shard reduce keeps every survivor of
+    a wide query and the owner replays them with the heap in LDS."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_wide.log")
+    w.gen_two_term_log(d, log, n_queries=240, seed=14)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    o = OracleVacuum(d)
+    qpr = len(qs) // world
+    qs2, got = _run_sharded_fixed(d, qs, 200, world, slot=4096 * qpr)
+    for q, g in zip(qs2, got):
+        assert g == o.search(q, 200)[0], (world, q)

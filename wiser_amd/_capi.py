@@ -15,8 +15,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WISER_HIP_LIB") or os.path.join(HERE, "_lib", "libwiser_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "wiser_hip.h")
 
-MAX_TERMS = 8
-MAX_K = 64
+MAX_TERMS = 16
+MAX_PHRASE_TERMS = 8
+MAX_K = 1024
+SERVER_MAX_K = 64
 
 WSR_OK = 0
 E_INVALID, E_IO, E_HIP, E_LIMIT, E_INTERNAL = -1, -2, -3, -4, -5

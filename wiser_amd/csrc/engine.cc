@@ -121,6 +121,7 @@ struct wsr_batch {
   uint32_t* d_stats = nullptr;   // per general workgroup, then per lean wave: survivors, blocks
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
+  bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   int seg_grid = 0;
   int lean_wgs = 0;
   // doc-range shard exchange
@@ -541,6 +542,8 @@ int wsr_check_query(wsr_handle* h, const wsr_query* q) {
   if (!h || !q) return fail(WSR_E_INVALID, "null argument");
   if (q->n_terms > WSR_MAX_TERMS || q->k > WSR_MAX_K)
     return fail(WSR_E_LIMIT, "n_terms or k over the limit");
+  if ((q->flags & WSR_QUERY_PHRASE) && q->n_terms > WSR_MAX_PHRASE_TERMS)
+    return fail(WSR_E_LIMIT, "a phrase query has at most WSR_MAX_PHRASE_TERMS terms");
   if (q->flags & ~WSR_QUERY_PHRASE) return fail(WSR_E_INVALID, "unknown flags");
   if ((q->flags & WSR_QUERY_PHRASE) && q->n_terms > 1 && !h->positions)
     return fail(WSR_E_INVALID, "phrase query on an engine opened without positions");
@@ -558,7 +561,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
-  bool has_phrase = false;
+  bool has_phrase = false, has_wide = false;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
     if (s.k > b->stride)
@@ -567,6 +570,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     if (qrc) return fail(qrc, "query " + std::to_string(i) + ": " + g_err);
     const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
     has_phrase = has_phrase || phrase;
+    has_wide = has_wide || s.k > kMaxK;
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
@@ -628,6 +632,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   }
   b->nq = nq;
   b->has_phrase = has_phrase;
+  b->has_wide = has_wide;
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
@@ -677,6 +682,9 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
     if (replay && !fused)
       HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
                            b->d_nhits, st));
+    if (replay && b->has_wide)
+      HIP_OK(launch_wide_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
+                                b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());

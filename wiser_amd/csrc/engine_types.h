@@ -6,8 +6,11 @@
 
 namespace wiser {
 
-constexpr int kMaxTerms = 8;    // terms per conjunctive query (reference phrase cap, query_processing.h:695)
-constexpr int kMaxK = 64;       // n_results per query: the running top-k lives in one wave's lanes
+constexpr int kMaxTerms = 16;        // terms per conjunctive query
+constexpr int kMaxPhraseTerms = 8;   // terms per phrase query (the reference's cap, query_processing.h:695)
+constexpr int kMaxK = 64;            // n_results of the wave top-k: running top-k and heap in one wave's lanes
+constexpr int kMaxKWide = 1024;      // n_results per query; k > kMaxK: every survivor is an event and the
+                                     // replay keeps the heap in LDS (wide_replay_kernel)
 
 // One posting list in the HBM image.
 struct ListDev {
@@ -56,7 +59,7 @@ struct QueryIn {
   int32_t list[kMaxTerms];  // list ids in query order; -1 => term missing => empty
   int32_t flags;            // kQueryPhrase: SearchQuery::is_phrase (types.h:205-256)
 };
-static_assert(sizeof(QueryIn) == 44, "QueryIn layout");
+static_assert(sizeof(QueryIn) == 76, "QueryIn layout");
 constexpr int32_t kQueryPhrase = 1;
 
 // Positions of one posting list in the image (phrase queries).  The list's
@@ -100,9 +103,10 @@ struct QueryDesc {
   uint32_t a_blk0, a_nblk, a_tail_cnt;
   uint32_t min_last;    // smallest last doc id over the other lists
   uint32_t item_base, n_items, seg;
-  uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16 | k << 24
+  uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16
   uint32_t o_list;      // O1's list id
-  uint32_t pad[5];
+  uint32_t k;           // n_results (> kMaxK: wide, every survivor is an event)
+  uint32_t pad[4];
 };
 static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
 

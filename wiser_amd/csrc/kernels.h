@@ -103,7 +103,7 @@ struct PlanPart {
 
 // phrase scratch words per general workgroup / lean wave (null when the batch
 // has no phrase query)
-constexpr int kPhraseScratch = kMaxTerms * 256;
+constexpr int kPhraseScratch = kMaxPhraseTerms * 256;
 
 // plan queries (2 launches); part: per plan workgroup of kPlanThreads queries
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
@@ -125,6 +125,10 @@ int lean_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);
+// queries with k > kMaxK (their segments emitted every survivor): heap in LDS
+hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
+                              const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
+                              hipStream_t st);
 hipError_t launch_decode_probe(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
                                uint32_t seed, uint32_t* out, hipStream_t st);
 // doc-range shards (multi-GPU)

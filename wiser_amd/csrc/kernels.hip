@@ -399,7 +399,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
   if (i < nq) {
     const QueryIn q = qs[i];
     bool ok = q.n_terms > 0 && q.k > 0;
-    if (q.n_terms > kMaxTerms || q.k > kMaxK) {
+    if (q.n_terms > kMaxTerms || q.k > kMaxKWide ||
+        (q.n_terms > kMaxPhraseTerms && (q.flags & kQueryPhrase))) {
       ok = false;
       atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
     }
@@ -475,9 +476,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.item_base = 0;
         D.n_items = p.n_items;
         D.seg = seg;
-        D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16) |
-                  (static_cast<uint32_t>(q.k) << 24);
-        for (int t = 0; t < 5; ++t) D.pad[t] = 0;
+        D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16);
+        D.k = static_cast<uint32_t>(q.k);
+        for (int t = 0; t < 4; ++t) D.pad[t] = 0;
         desc[i] = D;
       }
     }
@@ -848,8 +849,8 @@ struct EventFilter {
 // s_off (LDS); each lane finds its event's segment by binary search there, and
 // the next chunk's loads are issued before the current chunk is filtered.
 // count_of(r) and base_of(r) give segment r's event count and first event.
-template <bool kCoherent = false, class CountOf, class BaseOf, class Emit>
-__device__ __forceinline__ void consume_stream(EventFilter& F, uint32_t nseg, CountOf count_of,
+template <bool kCoherent = false, class Filter, class CountOf, class BaseOf, class Emit>
+__device__ __forceinline__ void consume_stream(Filter& F, uint32_t nseg, CountOf count_of,
                                                BaseOf base_of, uint32_t* s_off, Emit&& emit) {
   const uint32_t l = threadIdx.x & 63;
   for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
@@ -885,6 +886,105 @@ __device__ __forceinline__ void consume_stream(EventFilter& F, uint32_t nseg, Co
     __builtin_amdgcn_wave_barrier();
   }
 }
+
+// Every event, in order (wide queries: the shard reduce keeps all of them).
+struct PassFilter {
+  template <class Emit>
+  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&& emit) {
+    uint64_t cm = __ballot(valid);
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      emit(readlane_f64(sc, fl),
+           static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl)));
+    }
+  }
+};
+
+// The libstdc++ heap of a wide query (k up to kMaxKWide) in LDS: the same
+// __push_heap / __adjust_heap walks as WaveHeap, as wave-uniform code (every
+// lane reads the same LDS word, lane 0 writes), then RankDoc / SortHeap.
+struct LdsHeapSink {
+  double* hs;
+  int32_t* hd;
+  uint32_t n = 0, k = 0;
+  __device__ __forceinline__ double at(uint32_t i) const { return hs[i]; }
+  __device__ __forceinline__ void set(uint32_t i, double vs, int32_t vd) {
+    __builtin_amdgcn_wave_barrier();
+    if ((threadIdx.x & 63) == 0) { hs[i] = vs; hd[i] = vd; }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ void push_hole(uint32_t hole, double vs, int32_t vd) {
+    while (hole > 0) {
+      const uint32_t parent = (hole - 1) >> 1;
+      const double ps = at(parent);
+      if (!(ps > vs)) break;
+      set(hole, ps, hd[parent]);
+      hole = parent;
+    }
+    set(hole, vs, vd);
+  }
+  __device__ __forceinline__ void pop() {
+    if (n > 1) {
+      const uint32_t len = n - 1;
+      const double vs = at(len);
+      const int32_t vd = hd[len];
+      uint32_t hole = 0, child = 0;
+      while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (at(child) > at(child - 1)) --child;
+        set(hole, at(child), hd[child]);
+        hole = child;
+      }
+      if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        set(hole, at(child - 1), hd[child - 1]);
+        hole = child - 1;
+      }
+      push_hole(hole, vs, vd);
+    }
+    --n;
+  }
+  // RankDoc (query_processing.h:595-602)
+  __device__ __forceinline__ void insert(double sv, int32_t dv) {
+    if (n < k) { push_hole(n, sv, dv); ++n; }
+    else if (sv > at(0)) { pop(); push_hole(n, sv, dv); ++n; }
+  }
+  // candidates of a chunk: those that beat the heap's minimum as it stands
+  // (it only grows), each applied in doc order through insert
+  template <class Emit>
+  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&&) {
+    const double mn = n < k ? -1.0 : at(0);
+    uint64_t cm = __ballot(valid && sc > mn);
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      insert(readlane_f64(sc, fl),
+             static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl)));
+    }
+  }
+  // SortHeap (query_processing.h:551-562): pop into LDS in descending order, one store
+  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t m = n;
+    for (uint32_t i = 0; i < m; ++i) {
+      const double ts = at(0);
+      const int32_t td = hd[0];
+      pop();
+      // slot m-1-i is past the live heap (size m-1-i after the pop): free
+      set(m - 1 - i, ts, td);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = l; i < m; i += 64) {
+      HitDev h;
+      h.doc = hd[i];
+      h.pad = 0;
+      h.score = hs[i];
+      out[i] = h;
+    }
+    if (l == 0) *n_out = static_cast<int32_t>(m);
+  }
+};
 
 // RankDoc (query_processing.h:595-602) on the restated heap, then SortHeap
 // (query_processing.h:551-562): results leave with one coalesced store.
@@ -955,8 +1055,35 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
                                                     int32_t* __restrict__ n_hits) {
   __shared__ uint32_t s_off[64];
   const int qi = blockIdx.x;
-  if (qi >= nq) return;
+  if (qi >= nq || qs[qi].k > kMaxK) return;   // (wide queries: wide_replay_kernel)
   replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
+}
+
+// Wide queries (k > kMaxK): their segments emitted every survivor; one wave
+// per query applies the whole stream, in doc order, to the heap in LDS.
+__global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restrict__ qs,
+                                                         const QueryPlan* __restrict__ plan, int nq,
+                                                         const Event* __restrict__ events,
+                                                         const uint32_t* __restrict__ ev_cnt,
+                                                         HitDev* __restrict__ hits, int hit_stride,
+                                                         int32_t* __restrict__ n_hits) {
+  __shared__ uint32_t s_off[64];
+  __shared__ double s_hs[kMaxKWide];
+  __shared__ int32_t s_hd[kMaxKWide];
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int32_t kq = qs[qi].k;
+  if (kq <= kMaxK) return;
+  const QueryPlan P = plan[qi];
+  LdsHeapSink sink;
+  sink.hs = s_hs;
+  sink.hd = s_hd;
+  sink.k = static_cast<uint32_t>(kq);
+  consume_stream<false>(
+      sink, P.n_items, [&](uint32_t r) { return ev_cnt[P.item_base + r]; },
+      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
+      s_off, [](double, int32_t) {});
+  sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
 }
 
 // ------------------------------------------------------ item plumbing --
@@ -1034,8 +1161,14 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     }
     ev_n = kept;
   }
+  // (The hand-off is relaxed agent-scope atomics plus a full s_waitcnt: on
+  // gfx950 the events went out as sc1 stores, which write through to memory,
+  // and the waitcnt retires them before the counter moves; the replay reads
+  // them with sc1 loads.  A release / acquire pair at agent scope would add a
+  // buffer_wbl2 / buffer_inv of the whole L2 to every item.)
   if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (fr.q_done) {
+  // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the segments
+  if (fr.q_done && uni(static_cast<uint32_t>(qs[qi].k)) <= static_cast<uint32_t>(kMaxK)) {
     __builtin_amdgcn_s_waitcnt(0);
     block_sync<kWave>();
     uint32_t old = 0;
@@ -1144,9 +1277,9 @@ __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* ql
       else if (!s1.next(ix, P1)) return false;
     }
   }
-  PosStream st[kMaxTerms];
+  PosStream st[kMaxPhraseTerms];
 #pragma unroll
-  for (uint32_t i = 0; i < kMaxTerms; ++i) {
+  for (uint32_t i = 0; i < kMaxPhraseTerms; ++i) {
     st[i].init(ix, ph[i * 256 + v], i < nt ? ph[i * 256 + 128 + v] : 0u);
     if (i < nt && !st[i].next(ix, ix.pos_lists[qlist[i]])) return false;
   }
@@ -1154,7 +1287,7 @@ __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* ql
   for (;;) {
     bool moved = false;
 #pragma unroll
-    for (uint32_t i = 0; i < kMaxTerms; ++i) {
+    for (uint32_t i = 0; i < kMaxPhraseTerms; ++i) {
       if (i < nt) {
         const int32_t ii = static_cast<int32_t>(i);
         if (st[i].cur - ii < a) {
@@ -1278,7 +1411,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
   const uint32_t d = Q.slots & 0xFFu, o1 = (Q.slots >> 8) & 0xFFu;
-  const uint32_t nt = (Q.slots >> 16) & 0xFFu, k = Q.slots >> 24;
+  const uint32_t nt = (Q.slots >> 16) & 0xFFu, k = Q.k;
+  // k > kMaxK: every survivor is an event; the replay's heap in LDS decides
+  const bool wide = k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
   const bool single = o1 >= kMaxTerms;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
@@ -1368,6 +1503,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     const uint64_t am = __ballot(alive);
     if (am == 0) return;
     n_surv += __popcll(am);
+    if (wide) {   // all of them, in doc order (lane order), no floor
+      if (alive) {
+        Event ev;
+        ev.score = sc;
+        ev.doc = static_cast<int32_t>(doc);
+        ev.pad = 0;
+        S.evs[evb + __popcll(am & lt)] = ev;
+      }
+      ev_n += __popcll(am);
+      evb += __popcll(am);
+      if (evb >= WSR_LEAN_EVS - 64) flush();
+      return;
+    }
     // running top-k: candidates beat the k-th best so far and the floor of the
     // query's earlier segments (scores are > 0, so bits order as values)
     const uint64_t fb = floor_bits;
@@ -1669,6 +1817,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     const uint32_t d = uni(P.driver & 0xFFu);
     const uint32_t nt = uni(static_cast<uint32_t>(qs[qi].n_terms));
     const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
+    const bool wide = k > static_cast<uint32_t>(kMaxK);   // every survivor is an event
     const ListDev A = ix.lists[qlist[d]];
     const uint32_t seg = uni(P.seg_blocks);
     // phrase query: every term's posting of each candidate is recorded in this
@@ -2007,16 +2156,16 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
           uni(static_cast<uint32_t>(floor_bits))));
       const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-      uint64_t cm0 = __ballot(al0 && s0 > flo && (pt_n < k || s0 > kth));
-      uint64_t cm1 = __ballot(al1 && s1 > flo && (pt_n < k || s1 > kth));
+      uint64_t cm0 = __ballot(al0 && (wide || (s0 > flo && (pt_n < k || s0 > kth))));
+      uint64_t cm1 = __ballot(al1 && (wide || (s1 > flo && (pt_n < k || s1 > kth))));
       while (cm0 | cm1) {
         const int fl = __builtin_ctzll(cm0 | cm1);
         const bool second = !((cm0 >> fl) & 1);
         if (second) cm1 &= cm1 - 1; else cm0 &= ~(1ull << fl);
         const double sv = readlane_f64(second ? s1 : s0, fl);
         const uint32_t dv = __builtin_amdgcn_readlane(second ? a1 : a0, fl);
-        const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
-        if (pos < k) {
+        const uint32_t pos = wide ? 0u : __popcll(__ballot(l < pt_n && pt >= sv));
+        if (wide || pos < k) {
           if (l == 0) {
             Event e;
             e.score = sv;
@@ -2026,13 +2175,15 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           }
           ++ev_n;
           if (++evb == 64) { flush_events(64); evb = 0; }
-          const double up = wave_shr1_f64(pt);
-          if (l > pos) pt = up;
-          else if (l == pos) pt = sv;
-          pt_n = pt_n + 1 > k ? k : pt_n + 1;
+          if (!wide) {
+            const double up = wave_shr1_f64(pt);
+            if (l > pos) pt = up;
+            else if (l == pos) pt = sv;
+            pt_n = pt_n + 1 > k ? k : pt_n + 1;
+          }
         }
       }
-      if (my_pub) {
+      if (my_pub && !wide) {
         const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
         const double pv = kn > flo ? kn : flo;
         if (pv > last_pub) {
@@ -2195,19 +2346,25 @@ __global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restr
   if (qi >= nq) return;
   const QueryPlan P = plan[qi];
   __shared__ uint32_t s_off[64];
-  EventFilter F;
-  F.k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
   Event* out = events + P.ev_base;
   uint32_t n = 0;
   // writes land at out[n], below the address of every event not yet read
   // (event g of the stream sits at or above out + g, and n <= g)
-  consume_stream(
-      F, P.n_items, [&](uint32_t r) { return ev_cnt[P.item_base + r]; },
-      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
-      s_off, [&](double sv, int32_t dv) {
-        if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
-        ++n;
-      });
+  auto emit = [&](double sv, int32_t dv) {
+    if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
+    ++n;
+  };
+  auto count_of = [&](uint32_t r) { return ev_cnt[P.item_base + r]; };
+  auto base_of = [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; };
+  if (k > static_cast<uint32_t>(kMaxK)) {   // wide: every survivor goes to the owner
+    PassFilter F;
+    consume_stream(F, P.n_items, count_of, base_of, s_off, emit);
+  } else {
+    EventFilter F;
+    F.k = k;
+    consume_stream(F, P.n_items, count_of, base_of, s_off, emit);
+  }
   if ((threadIdx.x & 63) == 0) scount[qi] = static_cast<int32_t>(n);
 }
 
@@ -2271,20 +2428,30 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
   if (qi >= nq) return;
   const int gq = q0 + qi;
   const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
+  auto count_of = [&](uint32_t g) {   // (a negative count marks a sender's slot overflow: flagged, read as 0)
+    const int32_t c = rcount[static_cast<int64_t>(g) * nq + qi];
+    return static_cast<uint32_t>(c > 0 ? c : 0);
+  };
+  auto base_of = [&](uint32_t g) {
+    return recv + (rbase ? rbase[g] : g * slot) + roff[static_cast<int64_t>(g) * nq + qi];
+  };
+  if (k > static_cast<uint32_t>(kMaxK)) {   // wide: the heap in LDS
+    __shared__ double s_hs[kMaxKWide];
+    __shared__ int32_t s_hd[kMaxKWide];
+    LdsHeapSink sink;
+    sink.hs = s_hs;
+    sink.hd = s_hd;
+    sink.k = k;
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, s_off, [](double, int32_t) {});
+    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+    return;
+  }
   EventFilter F;
   F.k = k;
   HeapSink sink;
   sink.k = k;
-  consume_stream(
-      F, static_cast<uint32_t>(n_shards),
-      [&](uint32_t g) {   // (a negative count marks a sender's slot overflow: flagged, read as 0)
-        const int32_t c = rcount[static_cast<int64_t>(g) * nq + qi];
-        return static_cast<uint32_t>(c > 0 ? c : 0);
-      },
-      [&](uint32_t g) {
-        return recv + (rbase ? rbase[g] : g * slot) + roff[static_cast<int64_t>(g) * nq + qi];
-      }, s_off,
-      [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+  consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of, s_off,
+                 [&](double sv, int32_t dv) { sink.insert(sv, dv); });
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
@@ -2400,6 +2567,15 @@ int lean_kernel_occupancy() {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false, false>, 64 * kLeanWaves, 0) != hipSuccess)
     return 1;
   return n;
+}
+
+hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
+                              const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
+                              hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wide_replay_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events, ev_cnt, hits,
+                     hit_stride, n_hits);
+  return hipGetLastError();
 }
 
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,

@@ -190,6 +190,7 @@ struct wsr_server {
     // (wsr_batch_upload rejects a whole batch for one bad query)
     const int qrc = wsr_check_query(h, &r->q);
     if (qrc != WSR_OK) return qrc;
+    if (r->q.k > WSR_SERVER_MAX_K) return WSR_E_LIMIT;   // the slots' result columns
     r->t_enq = Clock::now();
     bool wake;
     {
@@ -219,7 +220,7 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
   s->max_batch = max_batch;
   s->window = std::chrono::microseconds(window_us);
   for (auto& sl : s->slots) {
-    int rc = wsr_batch_create(h, max_batch, WSR_MAX_K, &sl.b);
+    int rc = wsr_batch_create(h, max_batch, WSR_SERVER_MAX_K, &sl.b);
     if (rc != WSR_OK) {
       for (auto& x : s->slots)
         if (x.b) wsr_batch_destroy(h, x.b);
@@ -227,7 +228,7 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
     }
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&s->hits),
-                    sizeof(wsr_hit) * static_cast<size_t>(max_batch) * WSR_MAX_K) != hipSuccess ||
+                    sizeof(wsr_hit) * static_cast<size_t>(max_batch) * WSR_SERVER_MAX_K) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&s->nh), sizeof(int32_t) * static_cast<size_t>(max_batch)) !=
           hipSuccess) {
     for (auto& x : s->slots) wsr_batch_destroy(h, x.b);
@@ -277,7 +278,7 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
                                    std::chrono::duration<double>(seconds));
   auto client = [&](int c) {
     std::vector<Req> rq(static_cast<size_t>(depth));
-    std::vector<std::vector<wsr_hit>> out(static_cast<size_t>(depth), std::vector<wsr_hit>(WSR_MAX_K));
+    std::vector<std::vector<wsr_hit>> out(static_cast<size_t>(depth), std::vector<wsr_hit>(WSR_SERVER_MAX_K));
     std::vector<int32_t> nout(static_cast<size_t>(depth));
     std::vector<Clock::time_point> t0(static_cast<size_t>(depth));
     uint64_t next_q = static_cast<uint64_t>(c) * 7919u;

@@ -326,7 +326,7 @@ class Server:
 
     def Search(self, query: SearchQuery) -> SearchResult:
         q, freqs = self.engine.resolve(query)
-        hits = (_capi.Hit * _capi.MAX_K)()
+        hits = (_capi.Hit * _capi.SERVER_MAX_K)()
         n = C.c_int32()
         check(lib.wsr_server_search(self._s, C.byref(q), hits, C.byref(n)))
         r = SearchResult()
