@@ -652,27 +652,152 @@ class VacuumIter {
   std::shared_ptr<PosBagIter> pos_;
 };
 
-// In-memory posting list iterator for the QqMem restatement (posting_list_delta.h:161-394:
-// SkipForward = first posting >= doc id; the result set is codec-independent).
-class MemIter {
+// ----------------------------------------------- qq_mem varint postings ----
+// StandardPosting::Encode (posting.h:130-151): content_size | doc_id_delta | TF |
+// off_size | offsets (start, end), each a delta to the previous value, from an
+// imaginary 0 (:85-99) | positions, deltas from an imaginary 0 (:101-113);
+// content_size counts everything after itself, off_size the offset bytes.
+void vb_append(std::string* s, uint64_t v) {
+  uint8_t b[10];
+  const int n = varint_encode(v, b);
+  s->append(reinterpret_cast<const char*>(b), n);
+}
+
+std::string standard_posting_encode(uint32_t doc_delta, uint32_t tf,
+                                    const std::vector<std::pair<uint32_t, uint32_t>>& offs,
+                                    const std::vector<uint32_t>& pos) {
+  std::string info, off, pbuf, out;
+  vb_append(&info, doc_delta);
+  vb_append(&info, tf);
+  uint32_t last = 0;
+  for (auto& pr : offs) {
+    vb_append(&off, pr.first - last);
+    last = pr.first;
+    vb_append(&off, pr.second - last);
+    last = pr.second;
+  }
+  std::string off_sized;
+  vb_append(&off_sized, off.size());   // VarintBuffer::Prepend(Size())
+  off_sized += off;
+  last = 0;
+  for (uint32_t p : pos) { vb_append(&pbuf, p - last); last = p; }
+  vb_append(&out, info.size() + off_sized.size() + pbuf.size());
+  out += info;
+  out += off_sized;
+  out += pbuf;
+  return out;
+}
+
+// PostingListDelta (posting_list_delta.h:397-470): postings appended as
+// StandardPosting bytes with doc-id deltas (posting[-1] = posting[0], so the
+// first delta is 0); every skip_span postings a skip entry (doc id of the
+// posting before, byte offset of the span's first posting).
+struct PostingListDelta {
+  int span = 100;   // :399
+  std::string data;
+  std::vector<std::pair<uint32_t, uint64_t>> skip;   // (prev_doc_id, start_offset)
+  int n = 0;
+  uint32_t last = 0;
+  void add(uint32_t doc, uint32_t tf, const std::vector<std::pair<uint32_t, uint32_t>>& offs,
+           const std::vector<uint32_t>& pos) {
+    if (n == 0) last = doc;
+    else if (doc <= last) throw std::runtime_error("doc ids must increase in a posting list");
+    if (n % span == 0) skip.emplace_back(last, data.size());
+    data += standard_posting_encode(doc - last, tf, offs, pos);
+    last = doc;
+    ++n;
+  }
+};
+
+// PostingListDeltaIterator (posting_list_delta.h:161-394): DecodeToCache reads
+// content size, doc delta, tf, offset size; Advance moves to the next posting;
+// SkipForward walks postings, jumping a whole span when the next span's first
+// doc (its skip entry's prev_doc_id) is still below the target.
+class DeltaIter {
  public:
-  MemIter(const std::vector<uint32_t>* d, const std::vector<uint32_t>* t) : d_(d), t_(t) {}
-  int size() const { return static_cast<int>(d_->size()); }
-  bool is_end() const { return i_ >= d_->size(); }
-  int doc_id() const { return static_cast<int>((*d_)[i_]); }
-  int term_freq() const { return static_cast<int>((*t_)[i_]); }
-  void advance() { ++i_; }
-  void skip_forward(uint32_t v) { while (i_ < d_->size() && (*d_)[i_] < v) ++i_; }
-  int posting_index() const { return static_cast<int>(i_); }
+  explicit DeltaIter(const PostingListDelta* pl) : pl_(pl), addr_(0), idx_(0), prev_(pl->skip[0].first) {
+    decode();
+  }
+  int size() const { return pl_->n; }
+  bool is_end() const { return idx_ == pl_->n; }
+  int doc_id() const { return static_cast<int>(doc_); }
+  int term_freq() const { return static_cast<int>(tf_); }
+  int posting_index() const { return idx_; }
+  void advance() {
+    addr_ = next_;
+    ++idx_;
+    prev_ = doc_;
+    decode();
+  }
+  bool has_skip() const { return idx_ % pl_->span == 0 && idx_ + pl_->span < pl_->n; }
+  uint32_t next_span_doc_id() const { return pl_->skip[idx_ / pl_->span + 1].first; }
+  void skip_to_next_span() {
+    const int s = idx_ / pl_->span + 1;
+    addr_ = pl_->skip[s].second;
+    idx_ = s * pl_->span;
+    prev_ = pl_->skip[s].first;
+    decode();
+  }
+  void skip_forward(uint32_t v) {
+    while (idx_ < pl_->n && doc_ < v) {
+      if (has_skip() && next_span_doc_id() < v) skip_to_next_span();
+      else advance();
+    }
+  }
+  // the current posting's offset pairs and positions (CompressedPairIterator /
+  // CompressedPositionIterator, posting_list_delta.h:281-296)
+  std::vector<std::pair<uint32_t, uint32_t>> offsets() const {
+    std::vector<std::pair<uint32_t, uint32_t>> out;
+    uint64_t at = off_start_, last = 0;
+    while (at < pos_start_) {
+      uint64_t a, b;
+      at += varint_decode(raw() + at, &a);
+      at += varint_decode(raw() + at, &b);
+      const uint32_t s = static_cast<uint32_t>(last + a);
+      const uint32_t e = static_cast<uint32_t>(s + b);
+      out.emplace_back(s, e);
+      last = e;
+    }
+    return out;
+  }
+  std::vector<uint32_t> positions() const {
+    std::vector<uint32_t> out;
+    uint64_t at = pos_start_, last = 0;
+    while (at < next_) {
+      uint64_t d;
+      at += varint_decode(raw() + at, &d);
+      last += d;
+      out.push_back(static_cast<uint32_t>(last));
+    }
+    return out;
+  }
   PosBagIter* position_begin() { throw std::runtime_error("phrase queries need a Vacuum index"); }
   const std::string& term() const { throw std::runtime_error("phrase queries need a Vacuum index"); }
   int has_prior_term(const std::string&) { return 1; }
   int has_next_term(const std::string&) { return 1; }
 
  private:
-  const std::vector<uint32_t>* d_;
-  const std::vector<uint32_t>* t_;
-  size_t i_ = 0;
+  const uint8_t* raw() const { return reinterpret_cast<const uint8_t*>(pl_->data.data()); }
+  void decode() {   // DecodeToCache (:299-318); nothing to read past the last posting
+    if (idx_ >= pl_->n) return;
+    uint64_t content, delta, tf, osz;
+    uint64_t at = addr_;
+    at += varint_decode(raw() + at, &content);
+    next_ = at + content;
+    at += varint_decode(raw() + at, &delta);
+    doc_ = static_cast<uint32_t>(prev_ + delta);
+    at += varint_decode(raw() + at, &tf);
+    tf_ = static_cast<uint32_t>(tf);
+    at += varint_decode(raw() + at, &osz);
+    off_start_ = at;
+    pos_start_ = at + osz;
+  }
+  const PostingListDelta* pl_;
+  uint64_t addr_;
+  int idx_;
+  uint32_t prev_;
+  uint32_t doc_ = 0, tf_ = 0;
+  uint64_t next_ = 0, off_start_ = 0, pos_start_ = 0;
 };
 
 // ----------------------------------------------------------- the heap ----
@@ -1152,7 +1277,7 @@ struct orc_vacuum {
 };
 
 struct orc_qqmem {
-  std::map<std::string, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> index;
+  std::map<std::string, PostingListDelta> index;   // varint postings (posting_list_delta.h)
   std::vector<uint8_t> lens;
   double avg = 0;
   int n_docs = 0;
@@ -1516,34 +1641,58 @@ orc_qqmem* orc_qqmem_load(const char* linedoc, int64_t n_rows, const char* forma
       auto items = explode_strict(line, '\t');
       int length;
       if (tok_only) {
-        std::map<std::string, int> counts;
-        auto toks = explode(items[2], ' ');
-        for (auto& t : toks) ++counts[t];
-        for (auto& kv : counts) {
-          auto& pl = h->index[kv.first];
-          pl.first.push_back(doc);
-          pl.second.push_back(kv.second);
+        // AddDocumentNaive (qq_mem_engine.h:217-239): tf = count_tokens, the
+        // offsets of extract_offset_pairs (utils.cc:184-217: [start, end]
+        // inclusive of each occurrence in the token text), no positions
+        const std::string& text = items[2];
+        std::map<std::string, std::vector<std::pair<uint32_t, uint32_t>>> occ;
+        size_t i = 0;
+        while (i < text.size()) {
+          if (text[i] == ' ') { ++i; continue; }
+          size_t j = i;
+          while (j < text.size() && text[j] != ' ') ++j;
+          occ[text.substr(i, j - i)].emplace_back(static_cast<uint32_t>(i), static_cast<uint32_t>(j - 1));
+          i = j;
         }
-        length = static_cast<int>(toks.size());
+        int ntok = 0;
+        for (auto& kv : occ) {
+          h->index[kv.first].add(doc, static_cast<uint32_t>(kv.second.size()), kv.second, {});
+          ntok += static_cast<int>(kv.second.size());
+        }
+        length = ntok;
       } else {
+        // AddDocumentWithPositions (qq_mem_engine.h:194-215): tf = the term's
+        // offset pairs (utils::parse_offsets, utils.cc:105-141), positions column 4
         auto toks = explode(items[2], ' ');
-        // utils::parse_offsets (utils.cc:105-141): groups by '.', pairs end with ';'
-        std::vector<int> tf;
-        std::string grp;
-        for (char ch : items[3]) {
-          if (ch != '.') grp += ch;
-          else if (!grp.empty()) {
-            int n = 0;
-            for (char c2 : grp) if (c2 == ';') ++n;
-            tf.push_back(n);
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> offs;
+        std::vector<std::vector<uint32_t>> poss;
+        {
+          std::string grp;
+          for (char ch : items[3]) {
+            if (ch != '.') { grp += ch; continue; }
+            if (grp.empty()) continue;
+            std::vector<std::pair<uint32_t, uint32_t>> term;
+            std::string buf;
+            for (char c2 : grp) {
+              if (c2 != ';') buf += c2;
+              else if (!buf.empty()) {
+                const size_t c = buf.find(',');
+                term.emplace_back(std::stoul(buf.substr(0, c)), std::stoul(buf.substr(c + 1)));
+                buf.clear();
+              }
+            }
+            offs.push_back(term);
             grp.clear();
           }
         }
-        for (size_t i = 0; i < toks.size(); ++i) {
-          auto& pl = h->index[toks[i]];
-          pl.first.push_back(doc);
-          pl.second.push_back(tf.at(i));
+        for (auto& g : explode(items[4], '.')) {
+          std::vector<uint32_t> pv;
+          for (auto& x : explode(g, ';')) pv.push_back(static_cast<uint32_t>(std::stoul(x)));
+          poss.push_back(pv);
         }
+        for (size_t i = 0; i < toks.size(); ++i)
+          h->index[toks[i]].add(doc, static_cast<uint32_t>(offs.at(i).size()), offs.at(i),
+                                i < poss.size() ? poss[i] : std::vector<uint32_t>{});
         length = static_cast<int>(explode(items[1], ' ').size());
       }
       // DocLengthCharStore::AddLength (doc_length_store.h:104-112)
@@ -1569,15 +1718,82 @@ int orc_qqmem_term_count(orc_qqmem* h) { return static_cast<int>(h->index.size()
 int orc_qqmem_search(orc_qqmem* h, const char* const* terms, int n_terms, int k, int32_t* docs,
                      double* scores, int32_t* doc_freqs) {
   if (k == 0) return 0;
-  std::vector<MemIter> its;
+  std::vector<DeltaIter> its;
   for (int i = 0; i < n_terms; ++i) {
     auto f = h->index.find(terms[i]);
-    if (f != h->index.end()) its.emplace_back(&f->second.first, &f->second.second);
+    if (f != h->index.end()) its.emplace_back(&f->second);
   }
   if (its.empty() || static_cast<int>(its.size()) < n_terms) return 0;
   if (doc_freqs) for (size_t i = 0; i < its.size(); ++i) doc_freqs[i] = its[i].size();
-  Processor<MemIter> p(h->sim, &its, h->lens, h->n_docs, k);
+  Processor<DeltaIter> p(h->sim, &its, h->lens, h->n_docs, k);
   return emit(p.run(), docs, scores);
+}
+
+// A whole varint posting list through PostingListDeltaIterator: docs, tfs and
+// (optionally) the i-th posting's offset pairs / positions; returns the size.
+int orc_qqmem_list(orc_qqmem* h, const char* term, uint32_t* docs, uint32_t* tfs, int cap) {
+  auto f = h->index.find(term);
+  if (f == h->index.end()) return 0;
+  DeltaIter it(&f->second);
+  int n = 0;
+  for (; !it.is_end(); it.advance(), ++n)
+    if (n < cap) { docs[n] = static_cast<uint32_t>(it.doc_id()); tfs[n] = static_cast<uint32_t>(it.term_freq()); }
+  return n;
+}
+
+int orc_qqmem_posting(orc_qqmem* h, const char* term, int posting, uint32_t* offs, int* n_offs,
+                      uint32_t* pos, int* n_pos, int cap) {
+  auto f = h->index.find(term);
+  if (f == h->index.end() || posting < 0 || posting >= f->second.n) { g_err = "no such posting"; return -1; }
+  DeltaIter it(&f->second);
+  for (int i = 0; i < posting; ++i) it.advance();
+  auto o = it.offsets();
+  auto p = it.positions();
+  *n_offs = static_cast<int>(o.size());
+  *n_pos = static_cast<int>(p.size());
+  for (int i = 0; i < static_cast<int>(o.size()) && 2 * i + 1 < cap; ++i) { offs[2 * i] = o[i].first; offs[2 * i + 1] = o[i].second; }
+  for (int i = 0; i < static_cast<int>(p.size()) && i < cap; ++i) pos[i] = p[i];
+  return it.doc_id();
+}
+
+// StandardPosting::Encode of one posting (tests_4.cc:114-146)
+int orc_posting_encode(uint32_t doc_delta, uint32_t tf, const uint32_t* offs, int n_pairs,
+                       const uint32_t* pos, int n_pos, uint8_t* out, int cap) {
+  std::vector<std::pair<uint32_t, uint32_t>> o;
+  for (int i = 0; i < n_pairs; ++i) o.emplace_back(offs[2 * i], offs[2 * i + 1]);
+  const std::string b = standard_posting_encode(doc_delta, tf, o, std::vector<uint32_t>(pos, pos + n_pos));
+  if (static_cast<int>(b.size()) > cap) return -1;
+  std::memcpy(out, b.data(), b.size());
+  return static_cast<int>(b.size());
+}
+
+// PostingListDelta with skip span `span` over (doc, tf) postings without
+// offsets (tests_4.cc:240-330): the skip entries and, per posting, HasSkip /
+// NextSpanDocId, and SkipForward / SkipToNextSpan walks.
+int orc_pld_probe(const uint32_t* docs, const uint32_t* tfs, int n, int span, uint32_t* skip_prev,
+                  uint64_t* skip_off, int* n_skip, int32_t* has_skip, uint32_t* span_doc,
+                  const uint32_t* targets, int n_targets, int32_t* found) {
+  try {
+    PostingListDelta pl;
+    pl.span = span;
+    for (int i = 0; i < n; ++i) pl.add(docs[i], tfs[i], {}, {});
+    *n_skip = static_cast<int>(pl.skip.size());
+    for (size_t i = 0; i < pl.skip.size(); ++i) { skip_prev[i] = pl.skip[i].first; skip_off[i] = pl.skip[i].second; }
+    DeltaIter it(&pl);
+    for (int i = 0; i < n; ++i, it.advance()) {
+      has_skip[i] = it.has_skip() ? 1 : 0;
+      span_doc[i] = it.has_skip() ? it.next_span_doc_id() : 0;
+    }
+    DeltaIter st(&pl);   // SkipForward over increasing targets
+    for (int i = 0; i < n_targets; ++i) {
+      st.skip_forward(targets[i]);
+      found[i] = st.is_end() ? -1 : st.doc_id();
+    }
+    return pl.n;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
 }
 
 }  // extern "C"

@@ -93,6 +93,18 @@ void orc_qqmem_close(orc_qqmem* h);
 int orc_qqmem_term_count(orc_qqmem* h);
 int orc_qqmem_search(orc_qqmem* h, const char* const* terms, int n_terms, int k,
                      int32_t* docs, double* scores, int32_t* doc_freqs);
+/* the term's varint posting list through PostingListDeltaIterator; returns its size */
+int orc_qqmem_list(orc_qqmem* h, const char* term, uint32_t* docs, uint32_t* tfs, int cap);
+/* one posting's offset pairs (2 per pair) and positions; returns its doc id */
+int orc_qqmem_posting(orc_qqmem* h, const char* term, int posting, uint32_t* offs, int* n_offs,
+                      uint32_t* pos, int* n_pos, int cap);
+/* StandardPosting::Encode (posting.h:130-151); returns the byte count */
+int orc_posting_encode(uint32_t doc_delta, uint32_t tf, const uint32_t* offs, int n_pairs,
+                       const uint32_t* pos, int n_pos, uint8_t* out, int cap);
+/* PostingListDelta skip index and iterator walks (posting_list_delta.h:161-470) */
+int orc_pld_probe(const uint32_t* docs, const uint32_t* tfs, int n, int span, uint32_t* skip_prev,
+                  uint64_t* skip_off, int* n_skip, int32_t* has_skip, uint32_t* span_doc,
+                  const uint32_t* targets, int n_targets, int32_t* found);
 
 /* counters of reference-UB situations hit so far (negative cache index) */
 int64_t orc_ub_negative_char_index(void);

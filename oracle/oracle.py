@@ -56,6 +56,14 @@ for name, res, args in [
     ("orc_qqmem_search", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_int, C.c_int, _I32P, _F64P,
                                    _I32P]),
     ("orc_ub_negative_char_index", C.c_int64, []),
+    ("orc_qqmem_list", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int]),
+    ("orc_qqmem_posting", C.c_int, [_P, C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_uint32), C.POINTER(C.c_int), C.c_int]),
+    ("orc_posting_encode", C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int,
+                                     C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_uint8), C.c_int]),
+    ("orc_pld_probe", C.c_int, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int, C.c_int,
+                                C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_int),
+                                _I32P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int, _I32P]),
     ("orc_vacuum_set_bloom_factor", None, [_P, C.c_int]),
     ("orc_vacuum_has_bloom", C.c_int, [_P]),
     ("orc_bloom_stats", None, [C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -224,6 +232,52 @@ class OracleQqMem:
 
     def search(self, terms, k):
         return _search(lib.orc_qqmem_search, self.h, terms, k)
+
+    def postings(self, term):
+        """(docs, tfs) through PostingListDeltaIterator (varint postings)"""
+        n = lib.orc_qqmem_list(self.h, term.encode(), None, None, 0)
+        d = (C.c_uint32 * max(n, 1))()
+        t = (C.c_uint32 * max(n, 1))()
+        n = lib.orc_qqmem_list(self.h, term.encode(), d, t, n)
+        return list(d[:n]), list(t[:n])
+
+    def posting(self, term, i, cap=1 << 14):
+        """(doc, [(start, end)], [positions]) of posting i"""
+        o = (C.c_uint32 * cap)()
+        p = (C.c_uint32 * cap)()
+        no, np_ = C.c_int(), C.c_int()
+        doc = lib.orc_qqmem_posting(self.h, term.encode(), i, o, C.byref(no), p, C.byref(np_), cap)
+        if doc < 0:
+            raise RuntimeError(_err())
+        return doc, [(o[2 * j], o[2 * j + 1]) for j in range(no.value)], list(p[:np_.value])
+
+
+def posting_encode(doc_delta, tf, offsets=(), positions=()):
+    """StandardPosting::Encode (posting.h:130-151)"""
+    flat = [v for pr in offsets for v in pr]
+    o = (C.c_uint32 * max(1, len(flat)))(*flat)
+    p = (C.c_uint32 * max(1, len(positions)))(*positions)
+    out = (C.c_uint8 * 4096)()
+    n = lib.orc_posting_encode(doc_delta, tf, o, len(offsets), p, len(positions), out, 4096)
+    return bytes(out[:n])
+
+
+def pld_probe(docs, tfs, span, targets):
+    """PostingListDelta(span) over (doc, tf) postings -> (skip prev docs, skip
+    offsets, HasSkip per posting, NextSpanDocId per posting, SkipForward hits)"""
+    n = len(docs)
+    d = (C.c_uint32 * n)(*docs)
+    t = (C.c_uint32 * n)(*tfs)
+    sp = (C.c_uint32 * (n + 1))()
+    so = (C.c_uint64 * (n + 1))()
+    ns = C.c_int()
+    hs = (C.c_int32 * n)()
+    sd = (C.c_uint32 * n)()
+    tg = (C.c_uint32 * max(1, len(targets)))(*targets)
+    fd = (C.c_int32 * max(1, len(targets)))()
+    if lib.orc_pld_probe(d, t, n, span, sp, so, C.byref(ns), hs, sd, tg, len(targets), fd) < 0:
+        raise RuntimeError(_err())
+    return (list(sp[:ns.value]), list(so[:ns.value]), list(hs), list(sd), list(fd[:len(targets)]))
 
 
 def pack128(values):
