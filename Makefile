@@ -19,8 +19,14 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 ORAFLAGS := -O3 -DNDEBUG -std=c++17 -fPIC -ffp-contract=off -Wall -shared
 
 CLI     := wiser_amd/_lib/engine_cli
+CALIB   := wiser_amd/_lib/calib_ea
 
-all: $(LIB) $(ORACLE) $(CLI)
+all: $(LIB) $(ORACLE) $(CLI) $(CALIB)
+
+# counter calibration (profiles only): known-byte reads for rocprofv3 --pmc
+$(CALIB): scripts/calib_ea.hip
+	@mkdir -p wiser_amd/_lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -o $@ $<
 
 $(CLI): tests/cpp/engine_cli.cc include/wiser_hip_engine.hpp include/wiser_hip.h $(LIB)
 	$(CXX) -O2 -std=c++17 -Iinclude -o $@ tests/cpp/engine_cli.cc -Lwiser_amd/_lib -lwiser_hip -Wl,-rpath,'$$ORIGIN'

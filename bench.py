@@ -470,6 +470,11 @@ def snippet_leg(a, local, threads):
                         f"distinct token ({len(distinct)}) + 10000 sampled (seed 1), return_snippets, "
                         "3 passages; per batch of 4096: GPU top-k (wsr_search_batch, host arrays in and "
                         "out) then the snippet stage (wsr_snippets_batch)")}
+    # the top-k alone (no snippets): the GPU path against config 1's own CPU
+    # engine, QqMemEngineDelta over varint postings (oracle restatement)
+    t_topk_only, _, _ = run(False)
+    out["topk_only"] = {"value": round(len(terms) / t_topk_only, 1), "unit": "queries/s",
+                        "note": "wsr_search_batch per 4096 (host arrays in and out), no snippets"}
     if not a.no_cpu:
         t0, n, i = time.time(), 0, 0
         while time.time() - t0 < 2.0:
@@ -478,6 +483,18 @@ def snippet_leg(a, local, threads):
             i += 1
         out["cpu_baseline"] = {"value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
                                "sample": f"{n} queries of the leg's list, oracle Search + GenerateSnippet, 2s"}
+        from oracle.oracle import OracleQqMem
+        qq = OracleQqMem(src, "TOKEN_ONLY")
+        t0, n, i = time.time(), 0, 0
+        while time.time() - t0 < 2.0:
+            qq.search([terms[i % len(terms)]], a.k)
+            n += 1
+            i += 1
+        out["topk_only"]["cpu_baseline"] = {
+            "value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
+            "sample": f"{n} single-term top-{a.k} queries of the leg's list through the oracle's "
+                      "QqMemEngineDelta (varint PostingListDelta, skip span 100), 2s"}
+        qq.close()
     orc.close()
     eng.close()
     return out
