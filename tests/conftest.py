@@ -8,6 +8,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DATA = os.path.join(ROOT, "tests", "golden", "data")
 
+# The engine's library first, at collection time (test modules that import
+# torch are collected after this file): libwiser_hip.so brings /opt/rocm's
+# libamdhip64 and librccl, and torch then binds to those instead of loading its
+# bundled copies -- the GPU suite runs on the runtime bench.py runs on.
+try:
+    import wiser_amd  # noqa: F401,E402
+except ImportError:   # not built yet (the `built` fixture makes it)
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
