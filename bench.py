@@ -10,11 +10,14 @@ k = 10.  The English-Wikipedia index of configs[2..4] is not available offline.
 A step = one batch through the engine with the batch's resolved queries
 already resident in HBM:
   N = 1          plan + segment + replay kernels over the whole index;
-  N > 1 (shard)  every rank holds the doc-id range [N*r/W, N*(r+1)/W); a global
-                 batch of 4096*W queries runs on every shard, shard events are
-                 exchanged with RCCL all_to_all over xGMI and each rank replays
-                 the 4096 queries it owns (per-GPU work ~constant: weak scaling);
-  N > 1 (replica, --mode replica) full index per GPU, 4096 queries per rank.
+  N > 1 (shard, the value)  every rank holds the doc-id range [N*r/W, N*(r+1)/W)
+                 and takes 4096 queries per step; the heavy ones (driver list >=
+                 --heavy-blocks blocks) run on every shard, their events move
+                 through fixed slots by the engine's own RCCL send/recv over
+                 xGMI (wsr_shard_step) and each owner replays its queries; the
+                 light ones run whole on the rank's full-index image (per-GPU
+                 work ~constant: weak scaling);
+  N > 1 (replica, the control) full index per GPU, 4096 queries per rank.
 value = queries completed by all ranks / max-over-ranks wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -52,9 +55,9 @@ def parse():
     p.add_argument("--batch", type=int, default=4096, help="queries per GPU per step")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--mode", choices=["auto", "shard", "replica"], default="auto",
-                   help="N>1: replica = full index per GPU, queries split across ranks (the "
-                        "value when the index fits one GPU: auto); shard = doc-range shards "
-                        "with the RCCL event exchange (auto also measures it, as 'docshard')")
+                   help="N>1: shard = doc-range shards with the RCCL event exchange (the value; "
+                        "auto also measures replica as the control); replica = full index per "
+                        "GPU, queries split across ranks, no collective")
     p.add_argument("--dist-backend", default="gloo",
                    help="the launcher's host-side group (rendezvous, RCCL id, barriers, timing "
                         "reduction); the data path is the engine's own RCCL exchange")
@@ -74,6 +77,10 @@ def parse():
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
+    p.add_argument("--heavy-blocks", type=int, default=64,
+                   help="N>1 shards: queries whose driver list has at least this many 128-posting "
+                        "blocks run on every shard (RCCL exchange); the others run whole on the "
+                        "rank's full-index image (0: every query is sharded)")
     return p.parse_args()
 
 
@@ -548,10 +555,15 @@ def kernel_accounting(eng, batches):
 
 
 def run_shard(a, idx, lines, rank, world, local, dist, threads):
-    """Doc-range shards: every rank runs each global batch (4096*W queries) over
-    its doc range, events are exchanged with RCCL all_to_all, each rank replays
-    the 4096 queries it owns.  Returns (queries, seconds, p50 ms, batches,
-    engine, checked, searcher)."""
+    """Doc-range shards, the N > 1 value.  Every rank holds the
+    doc-id range [N*r/W, N*(r+1)/W) and takes its own 4096 queries per step.
+    Heavy queries (driver list of >= --heavy-blocks blocks, where the work is)
+    run on every rank over its range: wsr_shard_step packs each owner's events
+    into a fixed slot, RCCL moves counts and slots between all pairs, and the
+    owner replays its queries; the rest run whole on the rank's full-index
+    image with no collective (--heavy-blocks 0: every query is sharded).
+    Returns (queries, seconds, p50 ms, batches, engine, checked, closer)."""
+    import math
     import torch
     import wiser_amd as w
     from wiser_amd.shard import NativeShardedSearcher, slot_for_fill
@@ -563,40 +575,84 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         return box[0]
 
     S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
-    log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
-    eng = S.engine
-    Q = a.batch * world
-    gb = []
-    for s in range(0, len(lines) - Q + 1, Q):
-        chunk = lines[s:s + Q]
-        b = w.ResidentBatch(eng, Q, a.k)
-        b.upload(resolve(eng, chunk, a.k))
-        gb.append((b, chunk))
-    nb = len(gb)
-    # exchange slot: every batch once with a generous slot, then twice the
+    full = None
+    if a.heavy_blocks > 0:
+        full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+        full.Load()
+    log(f"rank {rank}: shard {S.doc_range}{' + full image' if full else ''} loaded in {time.time()-t:.1f}s")
+    B = a.batch
+    per_rank = len(lines) // world
+    nb = max(1, per_rank // B)
+    df = {}
+
+    def is_heavy(q):
+        if a.heavy_blocks <= 0:
+            return True
+        ds = []
+        for x in q:
+            if x not in df:
+                df[x] = S.engine.lookup(x)[1]   # global df, as every image keeps
+            ds.append(df[x])
+        return bool(ds) and min(ds) > 0 and min(math.ceil(d / 128) for d in ds) >= a.heavy_blocks
+
+    # every rank builds the same global heavy batches from the same log split
+    steps = []   # per batch index: (heavy ResidentBatch or None, q_per_owner, heavy chunk,
+                 #                   cheap ResidentBatch or None, cheap chunk)
+    for j in range(nb):
+        parts = []
+        for g in range(world):
+            chunk = lines[g * per_rank + j * B: g * per_rank + (j + 1) * B]
+            parts.append([q for q in chunk if is_heavy(q)])
+        hq = max(len(p) for p in parts)
+        hb, hchunk = None, []
+        if hq:
+            for p in parts:
+                hchunk += p + [[]] * (hq - len(p))   # (an empty query: an empty result)
+            hb = w.ResidentBatch(S.engine, hq * world, a.k)
+            hb.upload(resolve(S.engine, hchunk, a.k))
+        mine = lines[rank * per_rank + j * B: rank * per_rank + (j + 1) * B]
+        cheap = [q for q in mine if not is_heavy(q)]
+        cb = None
+        if cheap:
+            cb = w.ResidentBatch(full, len(cheap), a.k)
+            cb.upload(resolve(full, cheap, a.k))
+        steps.append((hb, hq, hchunk, cb, cheap))
+    # exchange slot: every heavy batch once with a generous slot, then twice the
     # largest fill any rank saw (wsr_shard_fill), agreed over the group
-    big = 64 * a.batch
     fill = 0
-    for b, _ in gb:
-        S.step(b, a.batch, big)
-        fill = max(fill, S.max_fill(b))
+    for hb, hq, _, _, _ in steps:
+        if hb:
+            S.step(hb, hq, 64 * hq)
+            fill = max(fill, S.max_fill(hb))
     mx = torch.tensor([float(fill)])
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    slot = slot_for_fill(int(mx.item()), a.batch)
+    max_hq = max(1, max(st[1] for st in steps))
+    slot = slot_for_fill(int(mx.item()), max_hq)
 
     def step(i, fetch=False):
-        b = gb[i % nb][0]
-        S.step(b, a.batch, slot)
-        return S.fetch_owned(b, a.batch) if fetch else None
+        hb, hq, _, cb, _ = steps[i % nb]
+        if cb:
+            cb.run()
+        if hb:
+            S.step(hb, hq, slot)
+        if fetch:
+            return (S.fetch_owned(hb, hq) if hb else None), (cb.fetch() if cb else None)
+        return None
 
     checked = 0
     if a.check:   # every rank takes part in the collectives; rank 0 checks
-        hits, nh = step(0, fetch=True)
+        (hres, cres) = step(0, fetch=True)
         if rank == 0:
-            checked = check_against_oracle(idx, gb[0][1][:a.batch], hits, nh, a.k, a.check)
+            hb, hq, hchunk, cb, cheap = steps[0]
+            if hres:
+                checked += check_against_oracle(idx, hchunk[:hq], hres[0], hres[1], a.k, a.check)
+            if cres:
+                checked += check_against_oracle(idx, cheap, cres[0], cres[1], a.k, a.check)
     for s in range(a.warmup):
         step(s)
-    w.sync(eng)
+    w.sync(S.engine)
+    if full:
+        w.sync(full)
     lat = []
     for i in range(nb):
         dist.barrier()
@@ -604,17 +660,43 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         step(i, fetch=True)
         lat.append((time.perf_counter() - t0) * 1e3)
     dist.barrier()
-    w.sync(eng)
+    w.sync(S.engine)
+    if full:
+        w.sync(full)
     t0 = time.perf_counter()
     for s in range(a.steps):
         step(s)
-    w.sync(eng)
+    w.sync(S.engine)
+    if full:
+        w.sync(full)
     el = time.perf_counter() - t0
-    for b, _ in gb:   # error flags (a slot overflow among them) of every batch's last step
-        S.fetch_owned(b, a.batch)
-    queries = a.steps * Q  # every rank completes its owned 1/W of each global batch
+    for hb, hq, _, cb, _ in steps:   # error flags (a slot overflow among them) of every last step
+        if hb:
+            S.fetch_owned(hb, hq)
+        if cb:
+            cb.fetch()
+    # every rank completes its own 4096 queries per step (heavy owned + cheap)
+    queries = sum(len(steps[s % nb][4]) + sum(1 for q in steps[s % nb][2][rank * steps[s % nb][1]:
+                                                                       (rank + 1) * steps[s % nb][1]] if q)
+                  for s in range(a.steps))
     S.slot = slot
-    return queries, el, statistics.median(lat), [b for b, _ in gb], eng, checked, S
+    S.heavy_share = sum(st[1] for st in steps) / max(1, nb * B)
+    batches = [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]]
+    eng = full if (full and any(st[3] for st in steps)) else S.engine
+
+    class Closer:
+        slot = S.slot
+        heavy_share = S.heavy_share
+
+        def close(self):
+            for hb, _, _, cb, _ in steps:
+                for x in (hb, cb):
+                    if x and x not in batches:
+                        x.close()
+            S.close()
+            if full:
+                full.close()
+    return queries, el, statistics.median(lat), batches, eng, checked, Closer()
 
 
 def run_replica(a, idx, lines, rank, world, local, dist, threads):
@@ -686,14 +768,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     mode = a.mode if world > 1 else "replica"
-    # the engine (and with it /opt/rocm's HIP runtime and RCCL) loads first: torch,
-    # imported after it for the launcher's rendezvous only, binds to the same
-    # libamdhip64 instead of bringing its own
-    import wiser_amd
+    # One HIP runtime per process, the same as the GPU test suite's: torch loads
+    # first (it maps its libamdhip64 / librccl), then libwiser_hip.so binds to
+    # those sonames; torch itself is only the launcher's rendezvous (N > 1)
+    try:
+        import torch
+    except ImportError:
+        torch = None
+    import wiser_amd  # noqa: F401
     from wiser_amd import _capi
     runtime = _capi.runtime_info()
     if world > 1:
-        import torch
         import torch.distributed as dist
         # one GPU per rank; rehearsals with more ranks than GPUs share devices
         # (device_count does not initialise the GPU, torch never touches it)
@@ -723,7 +808,7 @@ def main():
     for b in batches:
         b.close()
     if S is not None:
-        S.close()
+        S.close()   # (the shard searcher and, hybrid, the full image and its batches)
     else:
         eng.close()
 

@@ -8,13 +8,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 DATA = os.path.join(ROOT, "tests", "golden", "data")
 
-# The engine's library first, at collection time (test modules that import
-# torch are collected after this file): libwiser_hip.so brings /opt/rocm's
-# libamdhip64 and librccl, and torch then binds to those instead of loading its
-# bundled copies -- the GPU suite runs on the runtime bench.py runs on.
+# One HIP runtime per process, the same one bench.py uses: torch loads first,
+# at collection time, and libwiser_hip.so (NEEDED libamdhip64.so.7 /
+# librccl.so.1) then binds to the copies torch already mapped under those
+# sonames.  (The other order maps a second libamdhip64 for torch, whose
+# NEEDED name differs, and the two runtimes fight over the device.)
 try:
-    import wiser_amd  # noqa: F401,E402
-except ImportError:   # not built yet (the `built` fixture makes it)
+    import torch  # noqa: F401,E402
+except ImportError:
     pass
 
 
@@ -23,16 +24,9 @@ def pytest_configure(config):
 
 
 @pytest.fixture(scope="session", autouse=True)
-def _engine_runtime_first():
-    """One HIP runtime per process, the one bench.py runs on: libwiser_hip.so
-    (linked against /opt/rocm's libamdhip64 and librccl) loads before torch, so
-    torch -- used by a few tests for device buffers and gloo -- binds to the
-    same already-loaded libamdhip64.so.7 instead of its bundled copy.  Then
-    torch's device state is initialised once, whatever subset of tests runs."""
-    try:
-        import wiser_amd  # noqa: F401
-    except Exception:
-        pass
+def _torch_device_first():
+    """torch's device state is initialised once, before any engine opens the
+    device, whatever subset of tests runs (torch is imported above)."""
     try:
         import torch
         torch.cuda.is_available()

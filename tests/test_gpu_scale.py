@@ -103,12 +103,15 @@ def test_search_text_chain(c3_small):
     orc.close()
 
 
-def test_runtime_is_system_rocm():
-    """The GPU suite runs the engine on the same runtime as bench.py: /opt/rocm's
-    libamdhip64 and librccl, loaded by libwiser_hip.so (conftest loads it before
-    torch).  Printed so that the GPU log records it."""
+def test_one_runtime():
+    """The GPU suite runs the engine on the same runtime as bench.py: torch is
+    imported first in both (conftest, bench.main), so libwiser_hip.so binds to
+    the libamdhip64 / librccl torch mapped, and there is only that one.
+    Printed so that the GPU log records it (bench.py prints it as "runtime")."""
     from wiser_amd import _capi
     info = _capi.runtime_info()
     print(info)
-    assert "/opt/rocm" in info.split("libamdhip64=")[1].split()[0], info
-    assert "/opt/rocm" in info.split("librccl=")[1], info
+    hip = info.split("libamdhip64=")[1].split()[0]
+    maps = open("/proc/self/maps").read()
+    loaded = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert loaded == {os.path.realpath(hip)} or loaded == {hip}, (info, loaded)
