@@ -570,9 +570,15 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     t = time.time()
 
     def share_id(x):   # rank 0's RCCL id to every rank, over the launcher's gloo group
+        if dist is None:   # (one rank: --mode shard at N = 1, a rehearsal of this path)
+            return x
         box = [x]
         dist.broadcast_object_list(box, src=0)
         return box[0]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
     S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
     full = None
@@ -624,10 +630,12 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         if hb:
             S.step(hb, hq, 64 * hq)
             fill = max(fill, S.max_fill(hb))
-    mx = torch.tensor([float(fill)])
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    if dist is not None:
+        mx = torch.tensor([float(fill)])
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        fill = int(mx.item())
     max_hq = max(1, max(st[1] for st in steps))
-    slot = slot_for_fill(int(mx.item()), max_hq)
+    slot = slot_for_fill(fill, max_hq)
 
     def step(i, fetch=False):
         hb, hq, _, cb, _ = steps[i % nb]
@@ -655,11 +663,11 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         w.sync(full)
     lat = []
     for i in range(nb):
-        dist.barrier()
+        barrier()
         t0 = time.perf_counter()
         step(i, fetch=True)
         lat.append((time.perf_counter() - t0) * 1e3)
-    dist.barrier()
+    barrier()
     w.sync(S.engine)
     if full:
         w.sync(full)
@@ -767,7 +775,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    mode = a.mode if world > 1 else "replica"
+    # (N = 1: replica, or --mode shard to rehearse the sharded path with one rank)
+    mode = a.mode if world > 1 else ("shard" if a.mode == "shard" else "replica")
     # One HIP runtime per process, the same as the GPU test suite's: torch loads
     # first (it maps its libamdhip64 / librccl), then libwiser_hip.so binds to
     # those sonames; torch itself is only the launcher's rendezvous (N > 1)
