@@ -192,7 +192,7 @@ def test_native_rccl_step_one_rank(synth_small):
     b = w.ResidentBatch(eng, len(qs), 10)
     b.upload(arr)
     for _ in range(3):
-        S.step(b, len(qs), 16 * len(qs))
+        S.step(b, len(qs), 64 * len(qs))
     hits, nh = S.fetch_owned(b, len(qs))
     assert S.max_fill(b) > 0
     o = OracleVacuum(d)
