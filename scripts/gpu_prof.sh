@@ -31,3 +31,8 @@ cat "$O/calib_bytes.txt"
 python3 "$R/scripts/pmc_bytes.py" "$P/pmc" lean_kernel,segment_kernel "$O/pmc_segment.json"
 python3 "$R/scripts/pmc_bytes.py" "$P/pmc" > "$O/pmc_all_kernels.txt"
 echo done
+# the sharded path rehearsed with one rank: where a step's time goes
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/shard" -o shard -- \
+    python3 "$R/bench.py" --mode shard --no-cpu --no-extra --steps 300 > "$O/shard_stats.json" 2> "$O/shard_stats.err"
+find "$P/shard" -name "*kernel_stats.csv" -exec cp {} "$O/shard_kernel_stats.csv" \;
+echo "shard stats ok"
