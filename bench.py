@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "queries/sec + p50 lat, 2-term AND BM25 top-10 on Wikipedia, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_PROFILE = "r02_p_pmc_segment.json"   # scripts/gpu_prof.sh, the C2 replica leg
 CPU_SHARE = min(16, os.cpu_count() or 1)   # host threads per GPU on the box (its CPU share)
 
 
@@ -844,18 +845,20 @@ def main():
     if rank == 0 and world == 1 and not a.no_extra:
         extra = extra_legs(a, idx, local, threads)
 
-    traffic = traffic_x1 = None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_segment.json")
-    # (measured on the C2 workload: attached to C2 lines only).  traffic applies
-    # the guide's x2 FETCH_SIZE correction to every read; it is calibrated only
-    # for wide streaming reads, so the uncorrected figure is given beside it.
-    if os.path.exists(pmc) and not (a.vacuum_dir or a.linedoc):
+    traffic = traffic_fetch = None
+    pmc = os.path.join(ROOT, "profiles", PMC_PROFILE)
+    # Fabric bytes per launch of the segment phase (lean_kernel + segment_kernel),
+    # from TCC_EA0 request counts by size (scripts/pmc_bytes.py; the formula is
+    # checked against known streaming kernels in profiles/r02_p_calib_bytes.txt,
+    # where FETCH_SIZE reads half the bytes on gfx950).  Measured on the C2
+    # replica workload, so attached to C2 replica lines only.
+    if os.path.exists(pmc) and not (a.vacuum_dir or a.linedoc) and not sharded:
         try:
             pm = json.load(open(pmc))
-            traffic = pm.get("hbm_bytes_per_launch")
-            traffic_x1 = pm["read_bytes_per_launch"] / 2 + pm["write_bytes_per_launch"]
+            traffic = pm["hbm_bytes_per_launch"]
+            traffic_fetch = pm["per_launch"]["FETCH_SIZE"] * 1024
         except Exception:
-            traffic = traffic_x1 = None
+            traffic = traffic_fetch = None
 
     if rank == 0:
         out = {
@@ -876,7 +879,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "traffic_fetch_uncorrected": traffic_x1,
+                         "traffic_source": PMC_PROFILE if traffic else None,
+                         "traffic_fetch_size_raw": traffic_fetch,
                          # the segment phase: lean_kernel with the general
                          # segment_kernel beside it on a second stream (one batch
                          # at a time, HIP events fork -> join)
