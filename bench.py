@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 METRIC = "queries/sec + p50 lat, 2-term AND BM25 top-10 on Wikipedia, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_PROFILE = "r02_p_pmc_segment.json"   # scripts/gpu_prof.sh, the C2 replica leg
+DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
 CPU_SHARE = min(16, os.cpu_count() or 1)   # host threads per GPU on the box (its CPU share)
 
 
@@ -675,6 +676,7 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     t0 = time.perf_counter()
     for s in range(a.steps):
         step(s)
+    DIAG["host_enqueue_ms_per_step"] = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     w.sync(S.engine)
     if full:
         w.sync(full)
@@ -747,6 +749,7 @@ def run_replica(a, idx, lines, rank, world, local, dist, threads):
     t0 = time.perf_counter()
     for s in range(a.steps):
         batches[s % nb].run()
+    DIAG["host_enqueue_ms_per_step"] = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     w.sync(eng)
     el = time.perf_counter() - t0
     # every batch's last run: the device error flags (capacity, limits) must be
@@ -897,6 +900,8 @@ def main():
             "parity_checked_queries": checked,
         }
         out["runtime"] = runtime
+        # host time to enqueue the timed steps: close to ms_per_step = launch-bound
+        out["host_enqueue_ms_per_step"] = round(DIAG.get("host_enqueue_ms_per_step", 0.0), 4)
         if sharded:
             out["exchange"] = {"kind": "RCCL grouped send/recv per peer over xGMI (wsr_shard_step), "
                                        "fixed slots, no host round trip inside a step",

@@ -267,13 +267,30 @@ int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner
 int wsr_owner_replay_fixed(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
                            int64_t slot, const int32_t* d_rcounts, const void* d_recv);
 
+/* ---- fused fixed-slot exchange --------------------------------------
+ * wsr_shard_emit runs the batch (plan + segment kernels) and, as each query's
+ * last work item finishes, reduces its events and appends them to its owner's
+ * slot of d_send (n_owners slots of `slot` 16-byte events) at an offset taken
+ * from the owner's fill counter; d_meta (device, 2 x nq int32) receives
+ * {count, offset} per query (count -1: the slot was full, error flag set).
+ * Nothing runs between the segment kernels and the exchange.  The owner side:
+ * d_rmeta = n_shards x nq_owned {count, offset} pairs (shard-major), d_recv =
+ * n_shards slots; results of [q0, q0 + nq_owned) as wsr_owner_replay_fixed.
+ * wsr_shard_fill after wsr_shard_emit / wsr_shard_step reads the fill counters. */
+int wsr_shard_emit(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners, int64_t slot,
+                   int32_t* d_meta, void* d_send);
+int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                          int64_t slot, const int32_t* d_rmeta, const void* d_recv);
+
 /* ---- native RCCL exchange (one process per GPU; a C++ host needs no Python):
  * rank 0 makes the id, every rank opens the communicator with it (the id
  * travels by the caller's own rendezvous), then each step is one call:
- * wsr_batch_run_events + wsr_shard_pack_fixed + grouped ncclSend / ncclRecv of
- * counts and slots with every peer over xGMI + wsr_owner_replay_fixed, all
- * enqueued on the batch's stream; rank r's owned queries are
- * [r * q_per_owner, (r + 1) * q_per_owner) of a batch of world * q_per_owner. */
+ * wsr_shard_emit on the batch's stream, then, on the communicator's stream,
+ * one group of ncclSend / ncclRecv with every peer over xGMI ({count, offset}
+ * pairs and the event slot) and wsr_owner_replay_meta.  Nothing waits on the
+ * host; wsr_batch_fetch* / wsr_batch_ready join the exchange.  Rank r's owned
+ * queries are [r * q_per_owner, (r + 1) * q_per_owner) of a batch of
+ * world * q_per_owner. */
 #define WSR_COMM_ID_BYTES 128
 typedef struct wsr_comm wsr_comm;
 int wsr_comm_unique_id(uint8_t* id /* WSR_COMM_ID_BYTES */);

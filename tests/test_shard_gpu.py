@@ -173,9 +173,108 @@ def test_fixed_slot_overflow_is_loud(synth_small):
         _run_sharded_fixed(d, qs, 10, 2, slot=4)
 
 
+def _run_sharded_emit(index_dir, queries, k, world, slot):
+    """The fused exchange of wsr_shard_step with the RCCL transfer done by
+    copies on one device: wsr_shard_emit per shard (segment kernels append
+    reduced events to the owners' slots), then wsr_owner_replay_meta per owner."""
+    import torch
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd._capi import check, lib
+    from wiser_amd.shard import index_doc_count, shard_range
+    qpr = len(queries) // world
+    queries = queries[:qpr * world]
+    n = index_doc_count(index_dir)
+    engs, batches, metas, sends = [], [], [], []
+    try:
+        for r in range(world):
+            e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
+            e.Load()
+            engs.append(e)
+            arr = (_capi.Query * len(queries))()
+            for i, q in enumerate(queries):
+                arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
+            b = w.ResidentBatch(e, len(queries), k)
+            batches.append(b)
+            b.upload(arr)
+            meta = torch.full((len(queries), 2), -7, dtype=torch.int32, device="cuda")
+            send = torch.zeros((world * slot, 2), dtype=torch.int64, device="cuda")
+            check(lib.wsr_shard_emit(e._h, b._b, qpr, world, slot, C.c_void_p(meta.data_ptr()),
+                                     C.c_void_p(send.data_ptr())))
+            check(lib.wsr_sync(e._h))
+            fill = (C.c_int64 * world)()
+            check(lib.wsr_shard_fill(e._h, b._b, world, fill))
+            assert all(0 <= f for f in fill)
+            metas.append(meta)
+            sends.append(send)
+        out = []
+        for o in range(world):
+            rmeta = torch.stack([metas[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
+            recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
+            e, b = engs[o], batches[o]
+            check(lib.wsr_owner_replay_meta(e._h, b._b, o * qpr, qpr, world, slot,
+                                            C.c_void_p(rmeta.data_ptr()), C.c_void_p(recv.data_ptr())))
+            hits = (_capi.Hit * (qpr * k))()
+            nh = (C.c_int32 * qpr)()
+            rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
+            if rc:
+                raise _capi.WiserError(rc, lib.wsr_last_error().decode())
+            for i in range(qpr):
+                out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
+        return queries, out
+    finally:
+        for b in batches:
+            b.close()
+        for e in engs:
+            e.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_fused_emit_exchange_equals_oracle(synth_small, world):
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_emit.log")
+    w.gen_two_term_log(d, log, n_queries=960, seed=15)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    o = OracleVacuum(d)
+    qpr = len(qs) // world
+    qs2, got = _run_sharded_emit(d, qs, 10, world, slot=64 * qpr)
+    for q, g in zip(qs2, got):
+        assert g == o.search(q, 10)[0], (world, q)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fused_emit_wide_k(synth_small, world):
+    """k > 64: the fused emission keeps every survivor of a wide query; the
+    owner replays them with the heap in LDS (owner_replay_meta_kernel<true>)."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_emit_wide.log")
+    w.gen_two_term_log(d, log, n_queries=240, seed=16)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    o = OracleVacuum(d)
+    qpr = len(qs) // world
+    qs2, got = _run_sharded_emit(d, qs, 200, world, slot=4096 * qpr)
+    for q, g in zip(qs2, got):
+        assert g == o.search(q, 200)[0], (world, q)
+
+
+def test_fused_emit_overflow_is_loud(synth_small):
+    import wiser_amd as w  # noqa: F401
+    from wiser_amd import _capi
+    d, _ = synth_small
+    head = [f"t{i:07d}" for i in range(8)]
+    qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
+    with pytest.raises(_capi.WiserError, match="exchange slot"):
+        _run_sharded_emit(d, qs, 10, 2, slot=4)
+
+
 def test_native_rccl_step_one_rank(synth_small):
-    """wsr_shard_step (RCCL communicator, grouped send/recv, replay on the batch
-    stream) with a communicator of one rank: equal to the oracle."""
+    """wsr_shard_step (fused emission, RCCL communicator, grouped send/recv,
+    owner replay on the communicator's stream) with a communicator of one rank,
+    several steps in flight on two batches: equal to the oracle."""
     import wiser_amd as w
     from wiser_amd import _capi
     from wiser_amd.shard import NativeShardedSearcher
@@ -189,16 +288,28 @@ def test_native_rccl_step_one_rank(synth_small):
     arr = (_capi.Query * len(qs))()
     for i, q in enumerate(qs):
         arr[i] = eng.resolve(w.SearchQuery(q, n_results=10))[0]
-    b = w.ResidentBatch(eng, len(qs), 10)
-    b.upload(arr)
-    for _ in range(3):
-        S.step(b, len(qs), 64 * len(qs))
-    hits, nh = S.fetch_owned(b, len(qs))
-    assert S.max_fill(b) > 0
+    half = len(qs) // 2
+    parts = [qs[:half], qs[half:2 * half]]
+    bs = []
+    for p, part in enumerate(parts):
+        b = w.ResidentBatch(eng, half, 10)
+        b.upload((_capi.Query * half)(*arr[p * half:(p + 1) * half]))
+        bs.append(b)
+    for _ in range(3):   # consecutive steps of two batches in flight
+        for b in bs:
+            S.step(b, half, 64 * half)
     o = OracleVacuum(d)
-    for i, q in enumerate(qs):
-        assert [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] == o.search(q, 10)[0], q
-    b.close()
+    for b, part in zip(bs, parts):
+        hits, nh = S.fetch_owned(b, half)
+        assert S.max_fill(b) > 0
+        for i, q in enumerate(part):
+            assert [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] == o.search(q, 10)[0], q
+    # an overflowing slot fails the fetch loudly
+    S.step(bs[0], half, 2)
+    with pytest.raises(_capi.WiserError, match="exchange slot"):
+        S.fetch_owned(bs[0], half)
+    for b in bs:
+        b.close()
     S.close()
 
 

@@ -118,6 +118,8 @@ _sigs = {
     "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_close": (None, [_P]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
+    "wsr_shard_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
+    "wsr_owner_replay_meta": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,

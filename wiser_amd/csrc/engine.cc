@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <cstdlib>
@@ -140,6 +141,10 @@ struct wsr_batch {
   uint64_t x_slots = 0;     // slot capacity * pairs the two event buffers were sized for
   int x_pairs = 0;
   hipEvent_t xev[2] = {nullptr, nullptr};   // pack done -> comm stream; exchange done -> replay
+  bool x_pending = false;   // a shard step's exchange + owner replay (xev[1]) not yet joined
+  bool x_fused = false;     // the last exchange was a wsr_shard_step (fill counters after d_ctr)
+  int32_t* d_xmeta = nullptr;    // fused shard step: per query {count, offset}, owner-major
+  int32_t* d_xrmeta = nullptr;   // ... received, shard-major
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
@@ -494,7 +499,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_plan, sizeof(QueryPlan) * max_q));
     HIP_OK(hipMalloc(&b->d_desc, sizeof(QueryDesc) * max_q));
     HIP_OK(hipMalloc(&b->d_part, sizeof(PlanPart) * ((max_q + kPlanThreads - 1) / kPlanThreads + 1)));
-    HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * kNumCounters));
+    HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * (kNumCounters + kMaxOwners)));   // + shard fill counters
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
@@ -527,7 +532,8 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase),
                   static_cast<void*>(b->d_xcount), static_cast<void*>(b->d_xrcount),
-                  static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv)})
+                  static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv),
+                  static_cast<void*>(b->d_xmeta), static_cast<void*>(b->d_xrmeta)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
@@ -606,6 +612,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     if (ev_need > b->ev_cap) {
       if (b->d_events) HIP_OK(hipFree(b->d_events));
       b->ev_cap = ev_need + ev_need / 4 + 4096;
@@ -643,19 +650,41 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   return WSR_OK;
 }
 
-static int batch_run(wsr_handle* h, wsr_batch* b, bool replay);
+// Shard emission of a batch run (wsr_shard_step): owners, queries per owner,
+// slot, and the send / meta buffers the segment kernels append to.
+struct ShardEmit {
+  int owners;
+  int32_t qpr;
+  uint64_t slot;
+  Event* send;
+  int32_t* meta;
+};
+
+static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* se = nullptr);
 
 int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, true); }
 int wsr_batch_run_events(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, false); }
 
-static int batch_run(wsr_handle* h, wsr_batch* b, bool replay) {
+static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* se) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
-    HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * kNumCounters, st));
-    const bool fused = replay && h->fuse_replay;
+    // the previous shard step's exchange and owner replay (on the communicator's
+    // stream) read this batch's buffers and write its results
+    if (b->x_pending) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));
+    b->x_pending = false;
+    HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * (kNumCounters + (se ? se->owners : 0)), st));
+    const bool fused = (replay && h->fuse_replay) || se;
     FusedReplay fr{fused ? b->d_qdone : nullptr, b->d_hits, b->stride, b->d_nhits};
+    if (se) {
+      fr.x_send = se->send;
+      fr.x_meta = se->meta;
+      fr.x_fill = b->d_ctr + kNumCounters;
+      fr.x_err = b->d_ctr + kCtrError;
+      fr.x_slot = se->slot;
+      fr.x_qpr = se->qpr;
+    }
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
@@ -706,6 +735,7 @@ int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits)
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
@@ -725,6 +755,7 @@ int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
@@ -756,7 +787,8 @@ void wsr_pinned_free(void* p) {
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   if (!b->ran) return 0;
-  const hipError_t e = hipEventQuery(b->ev[3]);   // recorded after the batch's last kernel
+  hipError_t e = hipEventQuery(b->ev[3]);   // recorded after the batch's last kernel
+  if (e == hipSuccess && b->x_pending) e = hipEventQuery(b->xev[1]);   // and a shard step's replay
   if (e == hipSuccess) return 1;
   if (e == hipErrorNotReady) return 0;
   return fail(WSR_E_HIP, hipGetErrorString(e));
@@ -767,6 +799,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
@@ -910,8 +943,9 @@ int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n
     hipStream_t st = b->st;
     if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
     if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
-    if (n_owners > 1024) return fail(WSR_E_LIMIT, "more than 1024 owners");
+    if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
     HIP_OK(hipMemsetAsync(b->d_otot, 0, sizeof(int64_t) * n_owners, st));
+    b->x_fused = false;
     HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
     HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
     HIP_OK(hipMemcpyAsync(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost, st));
@@ -931,6 +965,7 @@ int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send) {
     HIP_OK(launch_pack_events(b->d_plan, b->nq, b->d_events, b->d_scount, b->d_soff,
                               static_cast<Event*>(d_send), b->st));
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -973,12 +1008,13 @@ int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32
   if (!h || !b || !b->ran || !d_counts || !d_send || q_per_owner <= 0 || n_owners <= 0 || slot <= 0 ||
       static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
     return fail(WSR_E_INVALID, "bad shard_pack_fixed arguments");
-  if (n_owners > 1024) return fail(WSR_E_LIMIT, "more than 1024 owners");
+  if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
     if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
     if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
+    b->x_fused = false;
     HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
     HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
     HIP_OK(launch_pack_fixed(b->d_plan, b->nq, b->d_events, d_counts, b->d_soff, q_per_owner,
@@ -991,12 +1027,19 @@ int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32
 }
 
 int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals) {
-  if (!h || !b || !b->d_otot || !owner_totals || n_owners <= 0 || n_owners > 1024)
-    return fail(WSR_E_INVALID, "call wsr_shard_pack_fixed first");
+  if (!h || !b || !(b->d_otot || b->x_fused) || !owner_totals || n_owners <= 0 || n_owners > kMaxOwners)
+    return fail(WSR_E_INVALID, "call wsr_shard_pack_fixed or wsr_shard_step first");
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
-    HIP_OK(hipMemcpy(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (b->x_fused) {   // the segment kernels' per-owner fill counters
+      std::vector<uint32_t> fill(n_owners);
+      HIP_OK(hipMemcpy(fill.data(), b->d_ctr + kNumCounters, sizeof(uint32_t) * n_owners, hipMemcpyDeviceToHost));
+      for (int i = 0; i < n_owners; ++i) owner_totals[i] = fill[i];
+    } else {
+      HIP_OK(hipMemcpy(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost));
+    }
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -1041,7 +1084,17 @@ struct wsr_comm {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   int world = 0, rank = 0, device = 0;
+  // WSR_HOST_TIMING=1: host time per phase of wsr_shard_step (enqueue only),
+  // printed to stderr when the communicator closes
+  bool timing = false;
+  uint64_t steps = 0, t_ns[4] = {0, 0, 0, 0};   // run, (unused), rccl, replay
 };
+
+static uint64_t now_ns() {
+  return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now().time_since_epoch())
+                                   .count());
+}
 
 int wsr_comm_unique_id(uint8_t* id) {
   if (!id) return fail(WSR_E_INVALID, "null argument");
@@ -1062,40 +1115,105 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   std::memcpy(&u, id, sizeof u);
   const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
   if (r != ncclSuccess) return fail(WSR_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // the exchange stream waits on every step's segment kernels: at high
+  // priority it gets a hardware queue of its own, so its waits do not hold up
+  // batch streams that share a queue with it (+3 % on the one-rank rehearsal,
+  // profiles/r02_v_shard_variants.txt; WSR_COMM_PRIORITY=0 turns it off)
+  int lo_prio = 0, hi_prio = 0;
+  const bool prio = env_number("WSR_COMM_PRIORITY", 1) != 0 &&
+                    hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+  if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
+            : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     (void)ncclCommDestroy(c->comm);
     return fail(WSR_E_HIP, "hipStreamCreate failed");
   }
   c->world = world;
   c->rank = rank;
   c->device = device;
+  const char* ht = std::getenv("WSR_HOST_TIMING");
+  c->timing = ht && *ht && *ht != '0';
   *out = c.release();
   return WSR_OK;
 }
 
 void wsr_comm_close(wsr_comm* c) {
   if (!c) return;
+  if (c->timing && c->steps)
+    std::fprintf(stderr, "wsr_shard_step host us/step over %llu steps: run %.1f rccl %.1f replay %.1f\n",
+                 static_cast<unsigned long long>(c->steps), c->t_ns[0] / 1e3 / c->steps,
+                 c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
+int wsr_shard_emit(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners, int64_t slot,
+                   int32_t* d_meta, void* d_send) {
+  if (!h || !b || !d_meta || !d_send || q_per_owner <= 0 || n_owners <= 0 || slot <= 0 ||
+      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
+    return fail(WSR_E_INVALID, "bad shard_emit arguments");
+  if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
+  if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
+  const ShardEmit se{n_owners, q_per_owner, static_cast<uint64_t>(slot), static_cast<Event*>(d_send), d_meta};
+  const int rc = batch_run(h, b, false, &se);
+  if (rc == WSR_OK) b->x_fused = true;
+  return rc;
+}
+
+static int owner_replay_meta_on(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                                int64_t slot, const int32_t* d_rmeta, const void* d_recv, hipStream_t st) {
+  if (!h || !b || n_shards <= 0 || n_shards > kMaxOwners || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq ||
+      slot <= 0 || (nq_owned && (!d_rmeta || !d_recv)))
+    return fail(WSR_E_INVALID, "bad owner_replay_meta arguments");
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(launch_owner_replay_meta(b->d_q, q0, nq_owned, n_shards, d_rmeta, static_cast<uint64_t>(slot),
+                                    static_cast<const Event*>(d_recv), b->d_hits, b->stride, b->d_nhits,
+                                    b->d_ctr, b->has_wide, st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
+                          int64_t slot, const int32_t* d_rmeta, const void* d_recv) {
+  if (!b) return fail(WSR_E_INVALID, "null argument");
+  return owner_replay_meta_on(h, b, q0, nq_owned, n_shards, slot, d_rmeta, d_recv, b->st);
+}
+
+// One step of a doc-range sharded batch, all of it enqueued, nothing waited on:
+//   batch stream: wsr_shard_emit (plan + segment kernels; the worker that
+//     finishes a query reduces its events into the owner's slot);
+//   communicator stream (joined by xev[0]): one RCCL group of send/recv per
+//     peer -- the {count, offset} pairs and the event slot -- then the owner
+//     replay of this rank's queries; xev[1] marks the end.
+// The batch stream never waits on the exchange inside a step, so the next
+// batches' kernels run under it; the next run of this batch waits for xev[1]
+// (long past by then), and the fetches join it.
 int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
   if (!h || !b || !c || q_per_owner <= 0 || slot <= 0 ||
       static_cast<int64_t>(q_per_owner) * c->world != b->nq)
     return fail(WSR_E_INVALID, "bad shard_step arguments (the batch must hold world * q_per_owner queries)");
-  int rc = batch_run(h, b, false);
-  if (rc) return rc;
   const int W = c->world;
+  if (W > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners ranks");
+  uint64_t t0 = c->timing ? now_ns() : 0;
+  auto lap = [&](int i) {
+    if (!c->timing) return;
+    const uint64_t t = now_ns();
+    c->t_ns[i] += t - t0;
+    t0 = t;
+  };
   try {
     HIP_OK(hipSetDevice(h->device));
     const uint64_t need = static_cast<uint64_t>(slot) * W;
-    if (!b->d_xcount) {
-      HIP_OK(hipMalloc(&b->d_xcount, sizeof(int32_t) * b->max_q));
-      HIP_OK(hipMalloc(&b->d_xrcount, sizeof(int32_t) * b->max_q));
+    if (!b->d_xmeta) {
+      HIP_OK(hipMalloc(&b->d_xmeta, sizeof(int32_t) * 2 * b->max_q));
+      HIP_OK(hipMalloc(&b->d_xrmeta, sizeof(int32_t) * 2 * b->max_q));
     }
     if (need > b->x_slots || W != b->x_pairs) {
+      if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));
       if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
       if (b->d_xrecv) HIP_OK(hipFree(b->d_xrecv));
       b->d_xsend = b->d_xrecv = nullptr;
@@ -1104,41 +1222,46 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
       b->x_slots = need;
       b->x_pairs = W;
     }
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  rc = wsr_shard_pack_fixed(h, b, q_per_owner, W, slot, b->d_xcount, b->d_xsend);
-  if (rc) return rc;
-  // counts and event slots, every pair at once (xGMI is point to point: one
-  // send / receive per peer, no ring)
-  auto nc = [](ncclResult_t r, const char* what) {
-    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
-  };
-  try {
     if (!b->xev[0]) {
       HIP_OK(hipEventCreateWithFlags(&b->xev[0], hipEventDisableTiming));
       HIP_OK(hipEventCreateWithFlags(&b->xev[1], hipEventDisableTiming));
     }
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  int rc = wsr_shard_emit(h, b, q_per_owner, W, slot, b->d_xmeta, b->d_xsend);
+  if (rc) return rc;
+  lap(0);
+  // xGMI is point to point: one send / receive per peer and buffer, no ring
+  auto nc = [](ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+  };
+  try {
     HIP_OK(hipEventRecord(b->xev[0], b->st));
     HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
     nc(ncclGroupStart(), "ncclGroupStart");
     for (int p = 0; p < W; ++p) {
-      nc(ncclSend(b->d_xcount + static_cast<size_t>(p) * q_per_owner, q_per_owner, ncclInt32, p, c->comm,
-                  c->stream), "ncclSend counts");
-      nc(ncclRecv(b->d_xrcount + static_cast<size_t>(p) * q_per_owner, q_per_owner, ncclInt32, p, c->comm,
-                  c->stream), "ncclRecv counts");
+      nc(ncclSend(b->d_xmeta + static_cast<size_t>(p) * 2 * q_per_owner, 2 * static_cast<size_t>(q_per_owner),
+                  ncclInt32, p, c->comm, c->stream), "ncclSend meta");
+      nc(ncclRecv(b->d_xrmeta + static_cast<size_t>(p) * 2 * q_per_owner, 2 * static_cast<size_t>(q_per_owner),
+                  ncclInt32, p, c->comm, c->stream), "ncclRecv meta");
       nc(ncclSend(b->d_xsend + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
                   c->comm, c->stream), "ncclSend events");
       nc(ncclRecv(b->d_xrecv + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
                   c->comm, c->stream), "ncclRecv events");
     }
     nc(ncclGroupEnd(), "ncclGroupEnd");
-    HIP_OK(hipEventRecord(b->xev[1], c->stream));
-    HIP_OK(hipStreamWaitEvent(b->st, b->xev[1], 0));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
-  return wsr_owner_replay_fixed(h, b, c->rank * q_per_owner, q_per_owner, W, slot, b->d_xrcount, b->d_xrecv);
+  lap(2);
+  rc = owner_replay_meta_on(h, b, c->rank * q_per_owner, q_per_owner, W, slot, b->d_xrmeta, b->d_xrecv, c->stream);
+  if (rc) return rc;
+  if (hipEventRecord(b->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
+  b->x_pending = true;
+  lap(3);
+  ++c->steps;
+  return WSR_OK;
 }
 
 int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
@@ -1147,6 +1270,7 @@ int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, w
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     if (ctr[kCtrError])
@@ -1207,6 +1331,7 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                                     static_cast<size_t>(kStatStride) * rows);
   try {
     HIP_OK(hipStreamSynchronize(b->st));
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());

@@ -58,6 +58,7 @@ constexpr int kStatStride = 16;  // + section cycles: 4 dequeue/setup, 5 driver,
 constexpr int kStatStride = 4;
 #endif
 enum { kErrLimit = 1, kErrCapacity = 2, kErrExchange = 4 };
+constexpr int kMaxOwners = 1024;   // doc-range shards (ranks) of one exchange
 
 #ifndef WSR_SEG_COST
 #define WSR_SEG_COST 63
@@ -86,11 +87,25 @@ constexpr float kItemFixedCost = 4.0f;
 // query's last item replays it (q_done: per-query completed items, zeroed by
 // the plan kernel).  q_done == nullptr: no fusion (separate replay launch, or
 // doc-range shard mode where events are exchanged first).
+//
+// Fused shard emission (wsr_shard_step, x_send != nullptr): the worker that
+// completes a query's last item reduces the query's events to those of a heap
+// run from empty over this shard (EventFilter; every survivor for k > kMaxK),
+// appends them to the owner's slot of the send buffer at an offset taken from
+// the owner's fill counter, and records {count, offset} for the query
+// (count -1 and kErrExchange when the slot is full).  No reduce, scan or pack
+// launch is left between the segment kernels and the exchange.
 struct FusedReplay {
   uint32_t* q_done;
   HitDev* hits;
   int hit_stride;
   int32_t* n_hits;
+  Event* x_send;        // owner o's slot at x_send + o * x_slot
+  int32_t* x_meta;      // per query {count, offset in the owner's slot}
+  uint32_t* x_fill;     // per owner: events appended (zeroed before the batch)
+  uint32_t* x_err;      // error flags word
+  uint64_t x_slot;
+  int32_t x_qpr;        // queries per owner
 };
 
 // Plan pass 1 -> pass 2: per plan workgroup (kPlanThreads queries), its items
@@ -150,6 +165,11 @@ hipError_t launch_pack_fixed(const QueryPlan* plan, int nq, const Event* events,
 hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
                                      uint64_t* roff, uint64_t slot, const Event* recv, HitDev* hits,
                                      int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st);
+// owner side of the fused exchange: meta[(g * nq + i) * 2] = {count, offset}
+// sent by shard g for owned query i, its events at recv + g * slot + offset
+hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* meta,
+                                    uint64_t slot, const Event* recv, HitDev* hits, int hit_stride,
+                                    int32_t* n_hits, uint32_t* counters, bool any_wide, hipStream_t st);
 // resident 64-thread segment workgroups per CU
 int segment_kernel_occupancy();
 

@@ -486,6 +486,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     if (fr.q_done) {
       fr.q_done[i] = 0;
       if (p.n_items == 0) fr.n_hits[i] = 0;   // no item will replay an empty query
+      if (p.n_items == 0 && fr.x_meta) {      // ... nor emit it: no events for its owner
+        fr.x_meta[2 * i] = 0;
+        fr.x_meta[2 * i + 1] = 0;
+      }
     }
   }
   // the workgroup's items per key and event capacity (pass 2 scans them)
@@ -1086,6 +1090,65 @@ __global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restri
   sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
 }
 
+// Fused shard emission (FusedReplay::x_send): the query's events, reduced as
+// shard_reduce_kernel does (compacted in place, coherent: other workers wrote
+// them), then appended to the owner's slot and described in x_meta.
+__device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan* plan, int qi, Event* events,
+                                             const uint32_t* ev_cnt, const FusedReplay& fr, uint32_t* s_off) {
+  const uint32_t l = threadIdx.x & 63;
+  const QueryPlan P = plan[qi];
+  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+  Event* out = events + P.ev_base;
+  uint32_t n = 0;
+  // writes land at out[n], below every event not yet read (see shard_reduce_kernel)
+  auto emit = [&](double sv, int32_t dv) {
+    if (l == 0) {
+      Event e;
+      e.score = sv;
+      e.doc = dv;
+      e.pad = 0;
+      store_event_coherent(&out[n], e);
+    }
+    ++n;
+  };
+  auto count_of = [&](uint32_t r) { return load_count<true>(ev_cnt + P.item_base + r); };
+  auto base_of = [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; };
+  if (k > static_cast<uint32_t>(kMaxK)) {
+    PassFilter F;
+    consume_stream<true>(F, P.n_items, count_of, base_of, s_off, emit);
+  } else {
+    EventFilter F;
+    F.k = k;
+    consume_stream<true>(F, P.n_items, count_of, base_of, s_off, emit);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  const uint32_t o = static_cast<uint32_t>(qi) / static_cast<uint32_t>(fr.x_qpr);
+  uint32_t off = 0;
+  if (l == 0 && n) off = atomicAdd(&fr.x_fill[o], n);
+  off = uni(off);
+  int32_t cnt = static_cast<int32_t>(n);
+  if (static_cast<uint64_t>(off) + n > fr.x_slot) {
+    cnt = -1;
+    if (l == 0) atomicOr(fr.x_err, static_cast<uint32_t>(kErrExchange));
+  } else {
+    Event* dst = fr.x_send + static_cast<uint64_t>(o) * fr.x_slot + off;
+    for (uint32_t i = l; i < n; i += 64) {
+      double sc;
+      int32_t dc;
+      load_event<true>(&out[i], &sc, &dc);
+      Event e;
+      e.score = sc;
+      e.doc = dc;
+      e.pad = 0;
+      dst[i] = e;
+    }
+  }
+  if (l == 0) {
+    fr.x_meta[2 * qi] = cnt;
+    fr.x_meta[2 * qi + 1] = static_cast<int32_t>(off);
+  }
+}
+
 // ------------------------------------------------------ item plumbing --
 // Next work item of a persistent worker over items [lo, hi), split into
 // kQueueShards round-robin shards (relative index i in shard i % kQueueShards),
@@ -1167,17 +1230,22 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
   // them with sc1 loads.  A release / acquire pair at agent scope would add a
   // buffer_wbl2 / buffer_inv of the whole L2 to every item.)
   if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the segments
-  if (fr.q_done && uni(static_cast<uint32_t>(qs[qi].k)) <= static_cast<uint32_t>(kMaxK)) {
+  // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the
+  // segments; in a shard step every query is emitted here
+  if (fr.q_done && (fr.x_send || uni(static_cast<uint32_t>(qs[qi].k)) <= static_cast<uint32_t>(kMaxK))) {
     __builtin_amdgcn_s_waitcnt(0);
     block_sync<kWave>();
     uint32_t old = 0;
     if (l == 0)
       old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = uni(old);
-    if (old + 1 == n_items)
-      replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
-                        fr.n_hits, s_off);
+    if (old + 1 == n_items) {
+      if (fr.x_send)
+        shard_emit_call(qs, plan, static_cast<int>(qi), const_cast<Event*>(events), ev_cnt, fr, s_off);
+      else
+        replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
+                          fr.n_hits, s_off);
+    }
   }
 }
 
@@ -2455,6 +2523,54 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
+// Owner side of the fused exchange (wsr_shard_step): meta[(g * nq + i) * 2] =
+// {count, offset} shard g sent for owned query i (count -1: the sender's slot
+// overflowed: flagged, read as empty); its events at recv + g * slot + offset.
+// kWide: the queries with k > kMaxK, heap in LDS (a separate instance, so the
+// common one reserves no LDS for it).
+template <bool kWide>
+__global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
+                                                               int n_shards, const int32_t* __restrict__ meta,
+                                                               uint64_t slot, const Event* __restrict__ recv,
+                                                               HitDev* __restrict__ hits, int hit_stride,
+                                                               int32_t* __restrict__ n_hits,
+                                                               uint32_t* __restrict__ counters) {
+  __shared__ uint32_t s_off[64];
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  const int gq = q0 + qi;
+  const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
+  if ((k > static_cast<uint32_t>(kMaxK)) != kWide) return;
+  const uint32_t l = threadIdx.x & 63;
+  if (l < static_cast<uint32_t>(n_shards) && meta[(static_cast<int64_t>(l) * nq + qi) * 2] < 0)
+    atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
+  auto count_of = [&](uint32_t g) {
+    const int32_t c = meta[(static_cast<int64_t>(g) * nq + qi) * 2];
+    return static_cast<uint32_t>(c > 0 ? c : 0);
+  };
+  auto base_of = [&](uint32_t g) {
+    return recv + g * slot + static_cast<uint32_t>(meta[(static_cast<int64_t>(g) * nq + qi) * 2 + 1]);
+  };
+  if constexpr (kWide) {
+    __shared__ double s_hs[kMaxKWide];
+    __shared__ int32_t s_hd[kMaxKWide];
+    LdsHeapSink sink;
+    sink.hs = s_hs;
+    sink.hd = s_hd;
+    sink.k = k;
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, s_off, [](double, int32_t) {});
+    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+  } else {
+    EventFilter F;
+    F.k = k;
+    HeapSink sink;
+    sink.k = k;
+    consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of, s_off,
+                   [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+  }
+}
+
 // Fixed-slot exchange (no host round trip): owner o's events from this shard
 // go to send[o * slot ...] in query order; a query whose events would pass the
 // slot's end is not copied, its count becomes -1 and the error flag is set (the
@@ -2633,6 +2749,18 @@ hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_sha
   hipLaunchKernelGGL(scan_rows_kernel, dim3(n_shards), dim3(1024), 0, st, rcount, nq, roff, counters);
   hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount, roff,
                      static_cast<const uint64_t*>(nullptr), slot, recv, hits, hit_stride, n_hits);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* meta,
+                                    uint64_t slot, const Event* recv, HitDev* hits, int hit_stride,
+                                    int32_t* n_hits, uint32_t* counters, bool any_wide, hipStream_t st) {
+  if (nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(owner_replay_meta_kernel<false>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta, slot,
+                     recv, hits, hit_stride, n_hits, counters);
+  if (any_wide)
+    hipLaunchKernelGGL(owner_replay_meta_kernel<true>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
+                       slot, recv, hits, hit_stride, n_hits, counters);
   return hipGetLastError();
 }
 
