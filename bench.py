@@ -274,6 +274,7 @@ def c3_leg(a, local, threads):
     eng = w.VacuumEngine(d, device=local, threads=threads, positions=False)
     eng.Load()
     out["load_s"] = round(time.time() - t, 1)
+    out["image"] = eng.image_info()
     items = [(l.split(), False) for l in open(qlog).read().splitlines()]
     leg = run_leg(eng, d, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 2)
     eng.close()
@@ -812,6 +813,7 @@ def main():
     parallelism = f"docshard{world}" if sharded else f"replicas{world}"
     global_batch = a.batch * world
     acc = kernel_accounting(eng, batches)
+    image = eng.image_info()
     nbk = len(batches)
     seg_avg_ms = acc["seg"] / nbk
     achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
@@ -900,6 +902,7 @@ def main():
             "parity_checked_queries": checked,
         }
         out["runtime"] = runtime
+        out["image"] = image   # HBM bytes of the engine image the value ran on
         # host time to enqueue the timed steps: close to ms_per_step = launch-bound
         out["host_enqueue_ms_per_step"] = round(DIAG.get("host_enqueue_ms_per_step", 0.0), 4)
         if sharded:

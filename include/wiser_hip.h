@@ -137,6 +137,18 @@ typedef struct wsr_batch_stats {
                                 general segment_kernel) */
 } wsr_batch_stats;
 
+/* HBM bytes of an engine's image, per buffer. */
+typedef struct wsr_image_info {
+  uint64_t total_bytes;
+  uint64_t blob_bytes;    /* docid + tf spans, byte-exact from my.vacuum */
+  uint64_t dense_bytes;   /* rank bitmaps of the dense lists */
+  uint64_t tf8_bytes;     /* their 1-byte tfs */
+  uint64_t plen_bytes;    /* per-posting doc-length codes */
+  uint64_t dir_bytes;     /* list heads, block directory, decoded tails, doc lengths */
+  uint64_t pos_bytes;     /* position boxes (positions = 1) */
+  uint32_t n_lists, dense_lists;
+} wsr_image_info;
+
 const char* wsr_last_error(void);
 const char* wsr_version(void);
 /* the HIP runtime this process runs the engine on: hipRuntimeGetVersion and
@@ -146,6 +158,7 @@ int wsr_runtime_info(char* buf, int32_t cap);
 /* ---- engine ---------------------------------------------------------- */
 int wsr_open(const char* vacuum_dir, const wsr_open_opts* opts, wsr_handle** out);
 void wsr_close(wsr_handle* h);
+int wsr_image_info_get(wsr_handle* h, wsr_image_info* out);
 int wsr_term_count(wsr_handle* h, int32_t* out);
 int wsr_n_docs(wsr_handle* h, int32_t* out);
 /* list id (or -1) and document frequency (0 if absent) of one term */

@@ -115,3 +115,19 @@ def test_one_runtime():
     maps = open("/proc/self/maps").read()
     loaded = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert loaded == {os.path.realpath(hip)} or loaded == {hip}, (info, loaded)
+
+
+def test_image_info(c3_small):
+    """wsr_image_info_get: the per-buffer HBM bytes of an image add up, the
+    blob holds at least the file's docid + tf spans, and dense lists exist."""
+    import wiser_amd as w
+    d, _, st = c3_small
+    eng = w.VacuumEngine(d, positions=False)
+    eng.Load()
+    info = eng.image_info()
+    eng.close()
+    parts = ("blob_bytes", "dense_bytes", "tf8_bytes", "plen_bytes", "dir_bytes", "pos_bytes")
+    assert info["total_bytes"] == sum(info[p] for p in parts)
+    assert info["pos_bytes"] <= 8 * len(parts)   # positions off: only the 1-element placeholders
+    assert 0 < info["dense_lists"] < info["n_lists"]
+    assert info["blob_bytes"] < st.vacuum_bytes

@@ -52,6 +52,12 @@ class BatchStats(C.Structure):
                 ("lean_ms", C.c_double)]
 
 
+class ImageInfo(C.Structure):
+    _fields_ = [("total_bytes", C.c_uint64), ("blob_bytes", C.c_uint64), ("dense_bytes", C.c_uint64),
+                ("tf8_bytes", C.c_uint64), ("plen_bytes", C.c_uint64), ("dir_bytes", C.c_uint64),
+                ("pos_bytes", C.c_uint64), ("n_lists", C.c_uint32), ("dense_lists", C.c_uint32)]
+
+
 class ServeStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("seconds", C.c_double), ("qps", C.c_double),
                 ("p50_ms", C.c_double), ("p99_ms", C.c_double), ("batches", C.c_uint64),
@@ -83,6 +89,7 @@ _sigs = {
     "wsr_runtime_info": (C.c_int, [C.c_char_p, C.c_int32]),
     "wsr_open": (C.c_int, [C.c_char_p, C.POINTER(OpenOpts), C.POINTER(_P)]),
     "wsr_close": (None, [_P]),
+    "wsr_image_info_get": (C.c_int, [_P, C.POINTER(ImageInfo)]),
     "wsr_term_count": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "wsr_n_docs": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "wsr_lookup": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

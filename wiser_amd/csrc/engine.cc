@@ -47,10 +47,11 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 template <class T, class A>
-void dev_upload(T** dst, const std::vector<T, A>& src) {
+uint64_t dev_upload(T** dst, const std::vector<T, A>& src) {
   const size_t n = std::max<size_t>(src.size(), 1) * sizeof(T);
   HIP_OK(hipMalloc(reinterpret_cast<void**>(dst), n));
   if (!src.empty()) HIP_OK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return n;
 }
 
 // tuning knobs read once per wsr_open (unset or unparsable: the default)
@@ -92,6 +93,7 @@ struct wsr_handle {
   uint32_t* d_pos_start = nullptr;
   bool positions = false;
   uint32_t dense_lists = 0;
+  wsr_image_info info{};            // HBM bytes of the image's buffers
   bool fuse_replay = true;
   bool seg_floor = true;
   std::vector<ListDev> lists;       // host copy of the directory heads
@@ -160,6 +162,14 @@ extern "C" {
 const char* wsr_last_error(void) { return g_err.c_str(); }
 const char* wsr_version(void) { return "wiser-hip 0.2 (gfx950)"; }
 
+int wsr_image_info_get(wsr_handle* h, wsr_image_info* out) {
+  if (!h || !out) return fail(WSR_E_INVALID, "null argument");
+  *out = h->info;
+  out->total_bytes = out->blob_bytes + out->dense_bytes + out->tf8_bytes + out->plen_bytes + out->dir_bytes +
+                     out->pos_bytes;
+  return WSR_OK;
+}
+
 int wsr_runtime_info(char* buf, int32_t cap) {
   if (!buf || cap <= 0) return fail(WSR_E_INVALID, "null argument");
   int ver = 0;
@@ -209,11 +219,11 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->positions = opts && opts->positions;
     HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions, dense_budget);
     if (h->positions) {
-      dev_upload(&h->d_pos_blob, img.pos_blob);
-      dev_upload(&h->d_pos_lists, img.pos_lists);
-      dev_upload(&h->d_pos_pk, img.pos_pk);
-      dev_upload(&h->d_pos_tail, img.pos_tail);
-      dev_upload(&h->d_pos_start, img.pos_start);
+      h->info.pos_bytes += dev_upload(&h->d_pos_blob, img.pos_blob);
+      h->info.pos_bytes += dev_upload(&h->d_pos_lists, img.pos_lists);
+      h->info.pos_bytes += dev_upload(&h->d_pos_pk, img.pos_pk);
+      h->info.pos_bytes += dev_upload(&h->d_pos_tail, img.pos_tail);
+      h->info.pos_bytes += dev_upload(&h->d_pos_start, img.pos_start);
       h->args.pos_blob = h->d_pos_blob;
       h->args.pos_lists = h->d_pos_lists;
       h->args.pos_pk = reinterpret_cast<const uint2*>(h->d_pos_pk);
@@ -222,24 +232,26 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
       std::vector<uint8_t>().swap(img.pos_blob);
       std::vector<uint32_t>().swap(img.pos_start);
     }
-    dev_upload(&h->d_dense, img.dense);
-    dev_upload(&h->d_tf8, img.tf8);
+    h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
+    h->info.tf8_bytes = dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
+    h->info.dense_lists = img.dense_lists;
+    h->info.n_lists = static_cast<uint32_t>(img.lists.size());
     h->args.dense = h->d_dense;
     h->args.tf8 = h->d_tf8;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
     h->args.and_wpb = static_cast<float>(env_number("WSR_AND_WPB", 0.0));
-    dev_upload(&h->d_blob, img.blob);
-    dev_upload(&h->d_plen, img.plen);
+    h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
+    h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
-    dev_upload(&h->d_tails, img.tails);
+    h->info.dir_bytes += dev_upload(&h->d_tails, img.tails);
     h->args.tails = h->d_tails;
-    dev_upload(&h->d_lists, img.lists);
-    dev_upload(&h->d_blocks, img.blocks);
-    dev_upload(&h->d_last, img.blk_last);
-    dev_upload(&h->d_meta, img.blk_meta);
-    dev_upload(&h->d_c4, h->idx.char4_lengths());
+    h->info.dir_bytes += dev_upload(&h->d_lists, img.lists);
+    h->info.dir_bytes += dev_upload(&h->d_blocks, img.blocks);
+    h->info.dir_bytes += dev_upload(&h->d_last, img.blk_last);
+    h->info.dir_bytes += dev_upload(&h->d_meta, img.blk_meta);
+    h->info.dir_bytes += dev_upload(&h->d_c4, h->idx.char4_lengths());
     std::vector<double> cache(h->idx.bm25_cache(), h->idx.bm25_cache() + 256);
     dev_upload(&h->d_cache, cache);
     h->lists = img.lists;

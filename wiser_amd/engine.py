@@ -118,6 +118,12 @@ class VacuumEngine:
         except Exception:
             pass
 
+    def image_info(self) -> Dict[str, int]:
+        """HBM bytes of this engine's image per buffer (wsr_image_info_get)."""
+        i = _capi.ImageInfo()
+        check(lib.wsr_image_info_get(self._h, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in _capi.ImageInfo._fields_}
+
     def TermCount(self) -> int:
         n = C.c_int32()
         check(lib.wsr_term_count(self._h, C.byref(n)))
