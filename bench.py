@@ -818,7 +818,9 @@ def main():
     seg_avg_ms = acc["seg"] / nbk
     achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
     if dist:
-        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=not sharded)
+        # both forms count the queries each rank completed (its own 4096 per
+        # step: owned heavy + light, or its replica's): the value is their sum
+        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=True)
     qps = queries / el
     for b in batches:
         b.close()
