@@ -607,6 +607,7 @@ class VacuumIter {
   int term_freq() { return static_cast<int>(tf_.at(doc_.posting_index())); }
   void advance() { doc_.advance(); }
   void skip_forward(uint32_t d) { doc_.skip_forward(d); }
+  void skip_to(int posting) { doc_.skip_to(posting); }   // DocIdIterator::SkipTo (flash_iterators.h:170-179)
   // AssignPositionBegin (:1002-1005)
   PosBagIter* position_begin() { pos_->skip_to(doc_.posting_index()); return pos_.get(); }
   int posting_index() const { return doc_.posting_index(); }
@@ -1433,6 +1434,31 @@ int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* t
       if (n < cap) { docs[n] = it.doc_id(); tfs[n] = it.term_freq(); }
       ++n;
       it.advance();
+    }
+    return n;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+// The doc-id iterator of a term's list driven op by op (tests_11.cc:218-424,
+// tests_12.cc:33-270): ops[2i] = 0 Advance, 1 SkipTo(posting arg), 2
+// SkipForward(doc arg); after each op out[3i..3i+2] = {PostingIndex, Value (-1
+// at the end), IsEnd}.  Returns n, or -1 (unknown term / error).
+int orc_vacuum_docid_ops(orc_vacuum* h, const char* term, const int64_t* ops, int n, int64_t* out) {
+  auto f = h->tip.find(term);
+  if (f == h->tip.end()) { g_err = "unknown term"; return -1; }
+  try {
+    VacuumIter it(h->map, f->second);
+    for (int i = 0; i < n; ++i) {
+      const int64_t op = ops[2 * i], arg = ops[2 * i + 1];
+      if (op == 0) it.advance();
+      else if (op == 1) it.skip_to(static_cast<int>(arg));
+      else it.skip_forward(static_cast<uint32_t>(arg));
+      out[3 * i] = it.posting_index();
+      out[3 * i + 1] = it.is_end() ? -1 : it.doc_id();
+      out[3 * i + 2] = it.is_end() ? 1 : 0;
     }
     return n;
   } catch (const std::exception& e) {

@@ -48,6 +48,9 @@ int orc_vacuum_n_docs(orc_vacuum* h);
 int orc_vacuum_df(orc_vacuum* h, const char* term);
 /* iterate a whole list through DocIdIterator / TermFreqIterator */
 int orc_vacuum_list(orc_vacuum* h, const char* term, uint32_t* docs, uint32_t* tfs, int cap);
+/* doc-id iterator ops (0 Advance, 1 SkipTo posting, 2 SkipForward doc) ->
+ * {PostingIndex, Value or -1, IsEnd} per op */
+int orc_vacuum_docid_ops(orc_vacuum* h, const char* term, const int64_t* ops, int n, int64_t* out);
 /* VacuumEngine::Search: returns n entries (<= k), fills docs/scores and doc_freqs
  * (doc_freqs filled only when every term exists, as the reference). */
 int orc_vacuum_search(orc_vacuum* h, const char* const* terms, int n_terms, int k,

@@ -74,6 +74,8 @@ for name, res, args in [
     ("orc_highlight", C.c_int, [_I32P, _I32P, C.c_int, C.c_int, C.c_char_p, C.c_char_p, C.c_int]),
     ("orc_docstore_get", C.c_int64, [_P, C.c_int, C.c_char_p, C.c_int64]),
     ("orc_vacuum_offsets", C.c_int, [_P, C.c_char_p, C.c_int, _I32P, C.c_int]),
+    ("orc_vacuum_docid_ops", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64), C.c_int,
+                                       C.POINTER(C.c_int64)]),
 ]:
     f = getattr(lib, name)
     f.restype = res
@@ -143,6 +145,20 @@ class OracleVacuum:
         if m < 0:
             raise RuntimeError(_err())
         return list(d[:m]), list(t[:m])
+
+    def docid_ops(self, term, ops):
+        """Drive the term's DocIdIterator: ops = [("advance",), ("skip_to", posting),
+        ("skip_forward", doc)] -> [(PostingIndex, Value or None, IsEnd)] after each."""
+        code = {"advance": 0, "skip_to": 1, "skip_forward": 2}
+        flat = []
+        for op in ops:
+            flat += [code[op[0]], op[1] if len(op) > 1 else 0]
+        arr = (C.c_int64 * max(len(flat), 1))(*flat)
+        out = (C.c_int64 * max(3 * len(ops), 1))()
+        if lib.orc_vacuum_docid_ops(self.h, term.encode(), arr, len(ops), out) < 0:
+            raise RuntimeError(_err())
+        return [(out[3 * i], None if out[3 * i + 1] < 0 else out[3 * i + 1], bool(out[3 * i + 2]))
+                for i in range(len(ops))]
 
     def search(self, terms, k, phrase=False):
         """-> ([(doc, score)], doc_freqs); phrase = SearchQuery::is_phrase"""

@@ -1,13 +1,15 @@
-"""The round-2 reference KATs on the GPU (see test_ref_kats.py for the CPU side):
-tests_18.cc:178-255 phrase engine with bloom filters, tests_14.cc:163-219 tfs /
-decoded blocks, tests_16.cc:45-75 query-log parsing by the product's own text
-path (wsr_resolve_text)."""
+"""The round-2 reference KATs on the GPU (see test_ref_kats.py and
+test_iter_kats.py for the CPU side): tests_18.cc:178-255 phrase engine with
+bloom filters, tests_14.cc:163-219 tfs / decoded blocks, tests_16.cc:45-75
+query-log parsing by the product's own text path (wsr_resolve_text), and the
+doc-id iterator lists of tests_11.cc:218-424 / tests_12.cc:33-270."""
 import ctypes as C
 import os
 
 import pytest
 
 from conftest import DATA
+from test_iter_kats import iter_indexes  # noqa: F401  (fixture)
 from test_ref_kats import ref_phrases, toy_bloom  # noqa: F401  (fixture)
 
 pytestmark = pytest.mark.gpu
@@ -65,3 +67,33 @@ def test_tests_16_log_through_resolve_text(built, indexes):
     assert q[1].n_terms == 3 and q[1].flags == 0
     assert [eng.lookup(t)[0] for t in ("nightt", "rain", "nashvil")] == list(q[1].list_ids[:3])
     eng.close()
+
+
+def test_iter_kat_lists_on_gpu(iter_indexes):  # noqa: F811
+    """tests_11.cc:218-424 / tests_12.cc:33-270 lists (test_iter_kats.py) on the
+    device: every block decoded equals the KAT values (the pack / VInts boundary
+    at 127 / 128 included), and the intersections and single-term top-k with
+    k up to the whole list (all ties) equal the oracle."""
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    from test_iter_kats import SPECS
+    for name, (_, lists) in SPECS.items():
+        d = iter_indexes[name]
+        eng = w.VacuumEngine(d, positions=False)
+        eng.Load()
+        o = OracleVacuum(d)
+        for t, docs in lists.items():
+            lid, df = eng.lookup(t)
+            assert df == len(docs)
+            got = []
+            for blk in range((df + 127) // 128):
+                got += eng.decode_block(lid, blk, 0)
+            assert got == docs, (name, t)
+        terms = sorted(lists)
+        qs = [[t] for t in terms] + [[a, b] for a in terms for b in terms if a != b]
+        for k in (10, 1024):
+            res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
+            for q, r in zip(qs, res):
+                assert [(e.doc_id, e.doc_score) for e in r.entries] == o.search(q, k)[0], (name, q, k)
+        o.close()
+        eng.close()

@@ -61,6 +61,20 @@ def test_bm25_kat():
     assert fmt3(lib.orc_tfnorm_lossy(8 / 3.0, 1, lib.orc_char4_encode(2))) == "1.11"
 
 
+def test_score_terms_in_doc_kat():
+    """tests_2.cc:162-245: CalcDocScoreForOneQuery over the 3-doc engine
+    (avg length 8/3): wisconsin on a 2-token doc 1.09, hello 0.149,
+    hello + world 0.672 (idf summed in query order)."""
+    avg = (2 + 2 + 4) / 3.0
+    s1 = 0.0 + lib.orc_es_idf(3, 1) * lib.orc_es_tfnorm(1, 2, avg)
+    assert fmt3(s1) == "1.09"
+    s2 = 0.0 + lib.orc_es_idf(3, 3) * lib.orc_es_tfnorm(1, 2, avg)
+    assert fmt3(s2) == "0.149"
+    s3 = (0.0 + lib.orc_es_idf(3, 3) * lib.orc_es_tfnorm(1, 2, avg)) + \
+        lib.orc_es_idf(3, 2) * lib.orc_es_tfnorm(1, 2, avg)
+    assert fmt3(s3) == "0.672"
+
+
 def test_varint_kat():
     # tests_15.cc:311-324 (64-bit varint round trip)
     b = O.varint_encode(3748449232)
