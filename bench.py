@@ -79,10 +79,12 @@ def parse():
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
-    p.add_argument("--heavy-blocks", type=int, default=64,
+    p.add_argument("--heavy-blocks", type=int, default=-1,
                    help="N>1 shards: queries whose driver list has at least this many 128-posting "
                         "blocks run on every shard (RCCL exchange); the others run whole on the "
-                        "rank's full-index image (0: every query is sharded)")
+                        "rank's full-index image (0: every query is sharded; -1, the default: "
+                        "max(64, 63 * N), so that each shard's part of a sharded query is at "
+                        "least one full work item)")
     return p.parse_args()
 
 
@@ -585,7 +587,11 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
 
     S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
     full = None
-    if a.heavy_blocks > 0:
+    # per-item fixed work is large (profiles/r02_x_item_size.txt: items of 16
+    # blocks run at half the rate of 63), so a query is split over the shards
+    # only when every shard still gets at least one full item of it
+    heavy_blocks = a.heavy_blocks if a.heavy_blocks >= 0 else max(64, 63 * world)
+    if heavy_blocks > 0:
         full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
         full.Load()
     log(f"rank {rank}: shard {S.doc_range}{' + full image' if full else ''} loaded in {time.time()-t:.1f}s")
@@ -595,14 +601,14 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     df = {}
 
     def is_heavy(q):
-        if a.heavy_blocks <= 0:
+        if heavy_blocks <= 0:
             return True
         ds = []
         for x in q:
             if x not in df:
                 df[x] = S.engine.lookup(x)[1]   # global df, as every image keeps
             ds.append(df[x])
-        return bool(ds) and min(ds) > 0 and min(math.ceil(d / 128) for d in ds) >= a.heavy_blocks
+        return bool(ds) and min(ds) > 0 and min(math.ceil(d / 128) for d in ds) >= heavy_blocks
 
     # every rank builds the same global heavy batches from the same log split
     steps = []   # per batch index: (heavy ResidentBatch or None, q_per_owner, heavy chunk,
@@ -693,12 +699,14 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
                   for s in range(a.steps))
     S.slot = slot
     S.heavy_share = sum(st[1] for st in steps) / max(1, nb * B)
+    S.heavy_blocks = heavy_blocks
     batches = [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]]
     eng = full if (full and any(st[3] for st in steps)) else S.engine
 
     class Closer:
         slot = S.slot
         heavy_share = S.heavy_share
+        heavy_blocks = S.heavy_blocks
 
         def close(self):
             for hb, _, _, cb, _ in steps:
@@ -910,7 +918,9 @@ def main():
         if sharded:
             out["exchange"] = {"kind": "RCCL grouped send/recv per peer over xGMI (wsr_shard_step), "
                                        "fixed slots, no host round trip inside a step",
-                               "slot_events": getattr(S, "slot", None)}
+                               "slot_events": getattr(S, "slot", None),
+                               "heavy_blocks": getattr(S, "heavy_blocks", None),
+                               "heavy_query_share": round(getattr(S, "heavy_share", 0.0), 4)}
         if control:
             out["control"] = control
         if extra:

@@ -718,6 +718,9 @@ __device__ __forceinline__ double length_norm(uint32_t c4, double avg) {
 __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm) {
   // TfNormLossy (scoring.h:65-69) times idf (scoring.h:136-140)
   const double f = static_cast<double>(static_cast<int32_t>(tf));
+#ifdef WSR_DIAG_CHEAP_SCORE   // timing diagnostic only (wrong scores): no divide
+  return idf * (f + norm);
+#endif
   const double k1p1 = 1.2 + 1;
   const double tfn = (f * k1p1) / (f + norm);
   return idf * tfn;
@@ -1200,6 +1203,9 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
                                             const FusedReplay& fr, uint32_t* s_off) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
+#ifdef WSR_DIAG_NO_REFILTER   // diagnostic: keep every event (still exact, more of them)
+  prev_pub = nullptr;
+#endif
   if (prev_pub && ev_n > 0) {
     const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double fl_end = __longlong_as_double(static_cast<long long>(
@@ -1592,6 +1598,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         uni(static_cast<uint32_t>(fb))));
     const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     uint64_t cm = __ballot(alive && sc > flo && (pt_n < k || sc > kth));
+#ifdef WSR_DIAG_NO_TOPK   // timing diagnostic only (wrong results): no running top-k
+    cm = 0;
+#endif
     while (cm) {
       const int fl = __builtin_ctzll(cm);
       cm &= cm - 1;
