@@ -316,6 +316,11 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
 int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,
                            uint32_t* out, int32_t* count);
 
+/* Diagnostics build only (-DWSR_REPLAY_PROF): after wsr_batch_run_events,
+ * replay the batch (replay_kernel) and return 6 u32 per query: filter cycles,
+ * finish cycles, events, filter candidates, heap insertions, work items. */
+int wsr_debug_replay_profile(wsr_handle* h, wsr_batch* b, uint32_t* rows);
+
 /* Raw per-workgroup counters of the last segment launch (diagnostics):
  * n_wg rows of `stride` u32 {survivors, driver blocks, other blocks, ...;
  * section cycle counts in a -DWSR_PROFILE build}.  out may be NULL to query. */

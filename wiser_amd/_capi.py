@@ -126,6 +126,7 @@ _sigs = {
     "wsr_comm_close": (None, [_P]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
     "wsr_shard_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
+    "wsr_debug_replay_profile": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "wsr_owner_replay_meta": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

@@ -1351,6 +1351,33 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
   return WSR_OK;
 }
 
+int wsr_debug_replay_profile(wsr_handle* h, wsr_batch* b, uint32_t* rows) {
+  if (!h || !b || !rows || !b->ran) return fail(WSR_E_INVALID, "run the batch (events) first");
+  std::lock_guard<std::mutex> g(h->mu);
+  uint32_t* d = nullptr;
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(b->st));
+    HIP_OK(hipMalloc(&d, sizeof(uint32_t) * 6 * std::max(b->nq, 1)));
+    HIP_OK(hipMemset(d, 0, sizeof(uint32_t) * 6 * std::max(b->nq, 1)));
+    const hipError_t e = set_replay_prof(d);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return fail(WSR_E_INVALID, "replay profile needs a -DWSR_REPLAY_PROF build");
+    }
+    HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride, b->d_nhits,
+                         b->st));
+    HIP_OK(hipStreamSynchronize(b->st));
+    HIP_OK(set_replay_prof(nullptr));
+    HIP_OK(hipMemcpy(rows, d, sizeof(uint32_t) * 6 * b->nq, hipMemcpyDeviceToHost));
+    HIP_OK(hipFree(d));
+  } catch (const std::exception& ex) {
+    if (d) (void)hipFree(d);
+    return fail(WSR_E_HIP, ex.what());
+  }
+  return WSR_OK;
+}
+
 int wsr_debug_dense_lookup(const char* dir, uint32_t doc_lo, uint32_t doc_hi, uint32_t dense_div,
                            const char* term, const uint32_t* docs, int32_t n, int32_t* tf_out,
                            int32_t* is_dense) {

@@ -140,6 +140,9 @@ int lean_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);
+// diagnostics build (-DWSR_REPLAY_PROF): replay_kernel writes 6 words per query
+// (filter cycles, finish cycles, events, candidates, insertions, items)
+hipError_t set_replay_prof(uint32_t* rows);
 // queries with k > kMaxK (their segments emitted every survivor): heap in LDS
 hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                               const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,

@@ -616,7 +616,6 @@ struct WaveLds {
   Event evs[64];         // events buffered for one coalesced store
   double norm[256];      // Bm25Similarity cache_ (host table, scoring.h:85-90)
   uint32_t cur[kMaxTerms];  // per other slot: cursor into its block directory
-  uint32_t roff[64];     // fused replay: segment offsets of the event stream
   uint4 dblk[64];        // the driver's directory entries of the current segment
   uint32_t dmeta[64];
   uint32_t tf[128];      // cooperative decode of a VInts tf tail
@@ -828,12 +827,19 @@ struct EventFilter {
   double pt = 0.0;    // running top-k of events, lane t = rank t
   uint32_t pt_n = 0;
   uint32_t k = 0;
+#ifdef WSR_REPLAY_PROF   // diagnostics: events seen, candidates, insertions
+  uint32_t n_ev = 0, n_cand = 0, n_ins = 0;
+#endif
   // one chunk of up to 64 events, lane i = event i of the chunk
   template <class Emit>
   __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&& emit) {
     const uint32_t l = threadIdx.x & 63;
     const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     uint64_t cm = __ballot(valid && (pt_n < k || sc > kth));
+#ifdef WSR_REPLAY_PROF
+    n_ev += __popcll(__ballot(valid));
+    n_cand += __popcll(cm);
+#endif
     while (cm) {
       const int fl = __builtin_ctzll(cm);
       cm &= cm - 1;
@@ -841,6 +847,9 @@ struct EventFilter {
       const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
       const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
       if (pos < k) {
+#ifdef WSR_REPLAY_PROF
+        ++n_ins;
+#endif
         emit(sv, dv);
         const double up = wave_shr1_f64(pt);
         if (l > pos) pt = up;
@@ -852,45 +861,49 @@ struct EventFilter {
 };
 
 // The events of `nseg` segments (doc-id order), consumed as one stream in
-// chunks of 64: the segment counts are loaded 64 at a time and scanned into
-// s_off (LDS); each lane finds its event's segment by binary search there, and
-// the next chunk's loads are issued before the current chunk is filtered.
+// chunks of 64: the segment counts are loaded 64 at a time and scanned, lane r
+// holding segment r's count and offset; a chunk finds each lane's segment by
+// walking the few segments that overlap it (readlane, no memory), and the next
+// chunk's loads are issued before the current chunk is filtered.  (Round 1
+// searched an LDS copy of the offsets per lane; inside the out-of-line replay
+// those were flat accesses whose waits also waited for the in-flight event
+// loads, so every search step cost a full memory round trip.)
 // count_of(r) and base_of(r) give segment r's event count and first event.
 template <bool kCoherent = false, class Filter, class CountOf, class BaseOf, class Emit>
 __device__ __forceinline__ void consume_stream(Filter& F, uint32_t nseg, CountOf count_of,
-                                               BaseOf base_of, uint32_t* s_off, Emit&& emit) {
+                                               BaseOf base_of, Emit&& emit) {
   const uint32_t l = threadIdx.x & 63;
   for (uint32_t r0 = 0; r0 < nseg; r0 += 64) {
     const uint32_t nj = min(64u, nseg - r0);
     const uint32_t c = l < nj ? count_of(r0 + l) : 0u;
     const uint32_t inc = wave_incl_scan(c);
     const uint32_t total = uni(__builtin_amdgcn_readlane(inc, 63));
-    __builtin_amdgcn_wave_barrier();
-    s_off[l] = inc - c;
-    __builtin_amdgcn_wave_barrier();
-    auto load = [&](uint32_t g, double* sc, int32_t* dc) {
+    const uint32_t off = inc - c;   // segment l's first event in the stream
+    // chunk [g0, g0 + 64): lane l loads stream event g0 + l
+    auto load = [&](uint32_t g0, double* sc, int32_t* dc) {
       *sc = 0.0;
       *dc = 0;
-      if (g < total) {
-        uint32_t lo = 0, len = nj;   // last j with s_off[j] <= g
-        while (len > 1) {
-          const uint32_t h = len >> 1;
-          if (s_off[lo + h] <= g) { lo += h; len -= h; } else { len = h; }
-        }
-        const Event* e = base_of(r0 + lo) + (g - s_off[lo]);
-        load_event<kCoherent>(e, sc, dc);
+      const uint32_t g = g0 + l;
+      uint64_t m = __ballot(l < nj && c > 0 && off < g0 + 64u && off + c > g0);
+      uint32_t rs = 0, ro = 0;
+      while (m) {
+        const int r = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t o = __builtin_amdgcn_readlane(off, r);
+        const uint32_t cc = __builtin_amdgcn_readlane(c, r);
+        if (g >= o && g - o < cc) { rs = static_cast<uint32_t>(r); ro = o; }
       }
+      if (g < total) load_event<kCoherent>(base_of(r0 + rs) + (g - ro), sc, dc);
     };
     double sc, nsc;
     int32_t dc, ndc;
-    load(l, &sc, &dc);
+    load(0, &sc, &dc);
     for (uint32_t c0 = 0; c0 < total; c0 += 64) {
-      load(c0 + 64 + l, &nsc, &ndc);
+      load(c0 + 64, &nsc, &ndc);
       F.step(sc, dc, c0 + l < total, emit);
       sc = nsc;
       dc = ndc;
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1024,6 +1037,10 @@ struct HeapSink {
   }
 };
 
+#ifdef WSR_REPLAY_PROF
+__device__ uint32_t* g_replay_prof = nullptr;   // diagnostics build: per-query replay rows
+#endif
+
 // One wave per query: filter the events of its segments (doc-id order) and
 // apply the survivors of the filter to the heap.
 template <bool kCoherent>
@@ -1031,9 +1048,12 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
                                              const QueryPlan* __restrict__ plan, int qi,
                                              const Event* events, const uint32_t* ev_cnt,
                                              HitDev* __restrict__ hits, int hit_stride,
-                                             int32_t* __restrict__ n_hits, uint32_t* s_off) {
+                                             int32_t* __restrict__ n_hits) {
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
+#ifdef WSR_REPLAY_PROF
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
   EventFilter F;
   F.k = k;
   HeapSink sink;
@@ -1041,17 +1061,28 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
   consume_stream<kCoherent>(
       F, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
       [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
-      s_off, [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+      [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+#ifdef WSR_REPLAY_PROF
+  const uint64_t t_filter = __builtin_amdgcn_s_memtime();
+#endif
   sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
+#ifdef WSR_REPLAY_PROF
+  // (unfused replay_kernel only: one row of g_replay_prof per query)
+  if ((threadIdx.x & 63) == 0 && g_replay_prof) {
+    uint32_t* o = g_replay_prof + 6 * qi;
+    o[0] = static_cast<uint32_t>(t_filter - t_start);
+    o[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_filter);
+    o[2] = F.n_ev; o[3] = F.n_cand; o[4] = F.n_ins; o[5] = P.n_items;
+  }
+#endif
 }
 
 // out-of-line copy for the segment kernel (keeps its register allocation
 // independent of the replay code; called once per query)
 __device__ __noinline__ void replay_query_call(const QueryIn* qs, const QueryPlan* plan, int qi,
                                                const Event* events, const uint32_t* ev_cnt,
-                                               HitDev* hits, int hit_stride, int32_t* n_hits,
-                                               uint32_t* s_off) {
-  replay_query<true>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
+                                               HitDev* hits, int hit_stride, int32_t* n_hits) {
+  replay_query<true>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits);
 }
 
 __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
@@ -1060,10 +1091,9 @@ __global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ 
                                                     const uint32_t* __restrict__ ev_cnt,
                                                     HitDev* __restrict__ hits, int hit_stride,
                                                     int32_t* __restrict__ n_hits) {
-  __shared__ uint32_t s_off[64];
   const int qi = blockIdx.x;
   if (qi >= nq || qs[qi].k > kMaxK) return;   // (wide queries: wide_replay_kernel)
-  replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits, s_off);
+  replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits);
 }
 
 // Wide queries (k > kMaxK): their segments emitted every survivor; one wave
@@ -1074,7 +1104,6 @@ __global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restri
                                                          const uint32_t* __restrict__ ev_cnt,
                                                          HitDev* __restrict__ hits, int hit_stride,
                                                          int32_t* __restrict__ n_hits) {
-  __shared__ uint32_t s_off[64];
   __shared__ double s_hs[kMaxKWide];
   __shared__ int32_t s_hd[kMaxKWide];
   const int qi = blockIdx.x;
@@ -1089,7 +1118,7 @@ __global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restri
   consume_stream<false>(
       sink, P.n_items, [&](uint32_t r) { return ev_cnt[P.item_base + r]; },
       [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
-      s_off, [](double, int32_t) {});
+      [](double, int32_t) {});
   sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
 }
 
@@ -1097,7 +1126,7 @@ __global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restri
 // shard_reduce_kernel does (compacted in place, coherent: other workers wrote
 // them), then appended to the owner's slot and described in x_meta.
 __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan* plan, int qi, Event* events,
-                                             const uint32_t* ev_cnt, const FusedReplay& fr, uint32_t* s_off) {
+                                             const uint32_t* ev_cnt, const FusedReplay& fr) {
   const uint32_t l = threadIdx.x & 63;
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
@@ -1118,11 +1147,11 @@ __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan*
   auto base_of = [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; };
   if (k > static_cast<uint32_t>(kMaxK)) {
     PassFilter F;
-    consume_stream<true>(F, P.n_items, count_of, base_of, s_off, emit);
+    consume_stream<true>(F, P.n_items, count_of, base_of, emit);
   } else {
     EventFilter F;
     F.k = k;
-    consume_stream<true>(F, P.n_items, count_of, base_of, s_off, emit);
+    consume_stream<true>(F, P.n_items, count_of, base_of, emit);
   }
   __builtin_amdgcn_s_waitcnt(0);
   const uint32_t o = static_cast<uint32_t>(qi) / static_cast<uint32_t>(fr.x_qpr);
@@ -1200,7 +1229,7 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
                                             uint32_t n_items, uint32_t item,
                                             const uint64_t* prev_pub, Event* ev_out, uint32_t ev_n,
                                             const Event* events, uint32_t* ev_cnt,
-                                            const FusedReplay& fr, uint32_t* s_off) {
+                                            const FusedReplay& fr) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
 #ifdef WSR_DIAG_NO_REFILTER   // diagnostic: keep every event (still exact, more of them)
@@ -1247,10 +1276,10 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     old = uni(old);
     if (old + 1 == n_items) {
       if (fr.x_send)
-        shard_emit_call(qs, plan, static_cast<int>(qi), const_cast<Event*>(events), ev_cnt, fr, s_off);
+        shard_emit_call(qs, plan, static_cast<int>(qi), const_cast<Event*>(events), ev_cnt, fr);
       else
         replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
-                          fr.n_hits, s_off);
+                          fr.n_hits);
     }
   }
 }
@@ -2285,7 +2314,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       step(sb, sa, b + 1);
     }
     if (evb) flush_events(evb);
-    finish_item<false>(qs, plan, qi, P.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.roff);
+    finish_item<false>(qs, plan, qi, P.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
@@ -2394,7 +2423,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
                    ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
     WSR_T(1)
-    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr, S.q);
+    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
     WSR_T(2)
     item = 0xFFFFFFFFu;
   }
@@ -2422,7 +2451,6 @@ __global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restr
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const QueryPlan P = plan[qi];
-  __shared__ uint32_t s_off[64];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
   Event* out = events + P.ev_base;
   uint32_t n = 0;
@@ -2436,11 +2464,11 @@ __global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restr
   auto base_of = [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; };
   if (k > static_cast<uint32_t>(kMaxK)) {   // wide: every survivor goes to the owner
     PassFilter F;
-    consume_stream(F, P.n_items, count_of, base_of, s_off, emit);
+    consume_stream(F, P.n_items, count_of, base_of, emit);
   } else {
     EventFilter F;
     F.k = k;
-    consume_stream(F, P.n_items, count_of, base_of, s_off, emit);
+    consume_stream(F, P.n_items, count_of, base_of, emit);
   }
   if ((threadIdx.x & 63) == 0) scount[qi] = static_cast<int32_t>(n);
 }
@@ -2500,7 +2528,6 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
                                                           const Event* __restrict__ recv,
                                                           HitDev* __restrict__ hits, int hit_stride,
                                                           int32_t* __restrict__ n_hits) {
-  __shared__ uint32_t s_off[64];
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const int gq = q0 + qi;
@@ -2519,7 +2546,7 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
     sink.hs = s_hs;
     sink.hd = s_hd;
     sink.k = k;
-    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, s_off, [](double, int32_t) {});
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
     return;
   }
@@ -2527,7 +2554,7 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
   F.k = k;
   HeapSink sink;
   sink.k = k;
-  consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of, s_off,
+  consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of,
                  [&](double sv, int32_t dv) { sink.insert(sv, dv); });
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
@@ -2544,7 +2571,6 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
                                                                HitDev* __restrict__ hits, int hit_stride,
                                                                int32_t* __restrict__ n_hits,
                                                                uint32_t* __restrict__ counters) {
-  __shared__ uint32_t s_off[64];
   const int qi = blockIdx.x;
   if (qi >= nq) return;
   const int gq = q0 + qi;
@@ -2567,14 +2593,14 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
     sink.hs = s_hs;
     sink.hd = s_hd;
     sink.k = k;
-    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, s_off, [](double, int32_t) {});
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
   } else {
     EventFilter F;
     F.k = k;
     HeapSink sink;
     sink.k = k;
-    consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of, s_off,
+    consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of,
                    [&](double sv, int32_t dv) { sink.insert(sv, dv); });
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
   }
@@ -2701,6 +2727,15 @@ hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, c
   hipLaunchKernelGGL(wide_replay_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events, ev_cnt, hits,
                      hit_stride, n_hits);
   return hipGetLastError();
+}
+
+hipError_t set_replay_prof(uint32_t* rows) {
+#ifdef WSR_REPLAY_PROF
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_replay_prof), &rows, sizeof rows);
+#else
+  (void)rows;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
