@@ -37,7 +37,7 @@ _capi.check(_capi.lib.wsr_debug_replay_profile(eng._h, b._b, rows))
 r = np.frombuffer(rows, dtype=np.uint32).reshape(-1, 6).astype(np.int64)
 filt, fin, ev, cand, ins, items = r.T
 tot = filt + fin
-print(f"{'C3' if args.wiki else 'C2'} high x high, {len(hh)} queries (s_memtime ticks, 100 MHz)")
+print(f"{'C3' if args.wiki else 'C2'} high x high, {len(hh)} queries (s_memtime: core clock cycles)")
 for name, v in (("filter", filt), ("finish", fin), ("total", tot), ("events", ev), ("candidates", cand),
                 ("insertions", ins), ("items", items)):
     print(f"  {name:10s} mean {v.mean():10.1f} p50 {np.median(v):10.1f} p99 {np.percentile(v, 99):10.1f} "

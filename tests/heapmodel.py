@@ -71,3 +71,61 @@ def rank_stream(items, k):
     while h.v and len(out) < k:
         out.append(h.v[0]); h.pop()
     return out[::-1], ins
+
+
+class WaveHeapModel:
+    """The device's wave-parallel restatement of the same heap (kernels.hip
+    WaveHeap): entry i in lane i; a sift up moves, in one step, every ancestor
+    whose score is > the value one level down (they are the deepest part of the
+    chain, since scores never decrease going down); a pop first shifts the
+    root-to-hole path of 'second children' up one level, then sifts the old last
+    entry up from the hole.  Must leave the array exactly as Heap does."""
+
+    def __init__(self):
+        self.v = []
+
+    def _sift_up(self, hole, anc, val):
+        L = [x for x in anc if self.v[x][0] > val[0]]
+        if not L:
+            self.v[hole] = val
+            return
+        old = list(self.v)
+        chain = set(anc) | {hole}
+        for y in chain:
+            if y != 0 and (y - 1) // 2 in L:
+                self.v[y] = old[(y - 1) // 2]
+        self.v[min(L)] = val
+
+    @staticmethod
+    def _ancestors(h):
+        out = []
+        while h > 0:
+            h = (h - 1) // 2
+            out.append(h)
+        return out
+
+    def push(self, val):
+        self.v.append(None)
+        h = len(self.v) - 1
+        self._sift_up(h, self._ancestors(h), val)
+
+    def pop(self):
+        n = len(self.v)
+        if n > 1:
+            ln = n - 1
+            val = self.v[ln]
+            old = list(self.v)
+
+            def nxt(i):   # __adjust_heap's choice: the right child unless it is > the left
+                return 2 * i + 1 if old[2 * i + 2][0] > old[2 * i + 1][0] else 2 * i + 2
+            path, h = [0], 0
+            while h < (ln - 1) // 2:
+                h = nxt(h)
+                path.append(h)
+            if (ln & 1) == 0 and h == (ln - 2) // 2:
+                h = 2 * h + 1
+                path.append(h)
+            for a, b in zip(path, path[1:]):
+                self.v[a] = old[b]
+            self._sift_up(h, path[:-1], val)
+        self.v.pop()

@@ -767,10 +767,17 @@ __device__ __forceinline__ double shfl_f64(double v, uint32_t src) {
 // libstdc++ std::priority_queue<unique_ptr<ResultDocEntry>, vector, EntryGreater>
 // (query_processing.h:510-524): push = push_back + __push_heap, pop = __pop_heap
 // (+ __adjust_heap) + pop_back, with comp(a, b) = a.score > b.score.
-// The heap lives in the wave's registers, lane i = heap[i] (k <= 64); the
-// library's sift loops run as a scalar walk that reads single lanes
-// (v_readlane) and writes one lane by a compare-select: a few cycles per
-// step, no LDS round trips.
+// The heap lives in the wave's registers, lane i = heap[i] (k <= 64), and each
+// library operation runs as a few wave-wide steps instead of a scalar walk
+// (the same array after every operation; tests/test_heap_parallel.py checks the
+// model of this against the serial restatement):
+//  * a sift up (__push_heap) of value v from `hole`: along the hole's ancestors
+//    the scores never decrease going down, so the ancestors with score > v are
+//    the deepest part of the chain; each of them moves one level down and v
+//    lands at the shallowest (at the hole when there is none);
+//  * __adjust_heap from the root: the path of "second children" (the right
+//    child unless it is > the left) is a short uniform walk; the path shifts up
+//    one level, then the old last entry sifts up from the path's end.
 struct WaveHeap {
   double hs = 0.0;
   int32_t hd = 0;
@@ -780,40 +787,59 @@ struct WaveHeap {
   __device__ __forceinline__ int32_t doc(uint32_t i) const {
     return static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(hd), static_cast<int>(i)));
   }
-  __device__ __forceinline__ void set(uint32_t i, double vs, int32_t vd) {
-    if ((threadIdx.x & 63) == i) { hs = vs; hd = vd; }
-  }
-  // __push_heap(first, hole, 0, value)
-  __device__ __forceinline__ void push_hole(uint32_t hole, double vs, int32_t vd) {
-    while (hole > 0) {
-      const uint32_t parent = (hole - 1) >> 1;
-      const double ps = at(parent);
-      if (!(ps > vs)) break;
-      set(hole, ps, doc(parent));
-      hole = parent;
+  // __push_heap(first, hole, 0, value); anc = the hole's ancestors (bit mask)
+  __device__ __forceinline__ void sift_up(uint32_t hole, uint64_t anc, double vs, int32_t vd) {
+    const uint32_t l = threadIdx.x & 63;
+    const bool on = (anc >> l) & 1ull;
+    const uint64_t down = __ballot(on && hs > vs);   // ancestors that move one level down
+    if (down == 0) {
+      if (l == hole) { hs = vs; hd = vd; }
+      return;
     }
-    set(hole, vs, vd);
+    const uint32_t par = l ? (l - 1) >> 1 : 0u;
+    const double ps = shfl_f64(hs, par);
+    const int32_t pd = __shfl(hd, static_cast<int>(par), 64);
+    if ((on || l == hole) && l != 0 && ((down >> par) & 1ull)) { hs = ps; hd = pd; }
+    if (l == static_cast<uint32_t>(__builtin_ctzll(down))) { hs = vs; hd = vd; }
   }
-  __device__ __forceinline__ void push(double vs, int32_t vd) { push_hole(n, vs, vd); ++n; }
+  __device__ __forceinline__ void push(double vs, int32_t vd) {
+    const uint32_t h = n++;
+    uint64_t anc = 0;
+    for (uint32_t x = h; x > 0;) {
+      x = (x - 1) >> 1;
+      anc |= 1ull << x;
+    }
+    sift_up(h, anc, vs, vd);
+  }
   __device__ __forceinline__ void pop() {
     if (n > 1) {
       const uint32_t len = n - 1;
       const double vs = at(len);
       const int32_t vd = doc(len);
       // __adjust_heap(first, 0, len, value)
-      uint32_t hole = 0, child = 0;
-      while (child < (len - 1) / 2) {
-        child = 2 * (child + 1);
-        if (at(child) > at(child - 1)) --child;
-        set(hole, at(child), doc(child));
-        hole = child;
+      const uint32_t l = threadIdx.x & 63;
+      const double vl = shfl_f64(hs, min(2 * l + 1, 63u));
+      const double vr = shfl_f64(hs, min(2 * l + 2, 63u));
+      const uint32_t nxt = vr > vl ? 2 * l + 1 : 2 * l + 2;
+      uint32_t h = 0, src = l;
+      uint64_t path = 1;
+      while (h < (len - 1) / 2) {
+        const uint32_t c = __builtin_amdgcn_readlane(nxt, static_cast<int>(h));
+        if (l == h) src = c;
+        h = c;
+        path |= 1ull << h;
       }
-      if ((len & 1) == 0 && child == (len - 2) / 2) {
-        child = 2 * (child + 1);
-        set(hole, at(child - 1), doc(child - 1));
-        hole = child - 1;
+      if ((len & 1) == 0 && h == (len - 2) / 2) {
+        const uint32_t c = 2 * h + 1;
+        if (l == h) src = c;
+        h = c;
+        path |= 1ull << h;
       }
-      push_hole(hole, vs, vd);
+      const double ss = shfl_f64(hs, src);
+      const int32_t sd = __shfl(hd, static_cast<int>(src), 64);
+      hs = ss;
+      hd = sd;
+      sift_up(h, path & ~(1ull << h), vs, vd);
     }
     --n;
   }
@@ -827,19 +853,12 @@ struct EventFilter {
   double pt = 0.0;    // running top-k of events, lane t = rank t
   uint32_t pt_n = 0;
   uint32_t k = 0;
-#ifdef WSR_REPLAY_PROF   // diagnostics: events seen, candidates, insertions
-  uint32_t n_ev = 0, n_cand = 0, n_ins = 0;
-#endif
   // one chunk of up to 64 events, lane i = event i of the chunk
   template <class Emit>
   __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&& emit) {
     const uint32_t l = threadIdx.x & 63;
     const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     uint64_t cm = __ballot(valid && (pt_n < k || sc > kth));
-#ifdef WSR_REPLAY_PROF
-    n_ev += __popcll(__ballot(valid));
-    n_cand += __popcll(cm);
-#endif
     while (cm) {
       const int fl = __builtin_ctzll(cm);
       cm &= cm - 1;
@@ -847,9 +866,6 @@ struct EventFilter {
       const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl));
       const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
       if (pos < k) {
-#ifdef WSR_REPLAY_PROF
-        ++n_ins;
-#endif
         emit(sv, dv);
         const double up = wave_shr1_f64(pt);
         if (l > pos) pt = up;
@@ -1008,12 +1024,45 @@ struct LdsHeapSink {
 
 // RankDoc (query_processing.h:595-602) on the restated heap, then SortHeap
 // (query_processing.h:551-562): results leave with one coalesced store.
+// As a stream consumer (step) it needs no separate insertion filter: the
+// reference's test is the heap's own (size < k, or score > its top, the k-th
+// best), and the heap's state after any prefix of the event stream is the
+// reference heap's at that doc (only insertions change it, and every
+// insertion is an event), so an event that is not an insertion is rejected
+// here exactly as its survivor was.
 struct HeapSink {
   WaveHeap H;
   uint32_t k = 0;
+#ifdef WSR_REPLAY_PROF   // diagnostics: events seen, candidates, insertions
+  uint32_t n_ev = 0, n_cand = 0, n_ins = 0;
+#endif
   __device__ __forceinline__ void insert(double sv, int32_t dv) {
     if (H.n < k) H.push(sv, dv);
     else if (sv > H.at(0)) { H.pop(); H.push(sv, dv); }
+    else return;
+#ifdef WSR_REPLAY_PROF
+    ++n_ins;
+#endif
+  }
+  // one chunk of up to 64 events in doc order (lane order): the candidates
+  // beat the heap's top as it stands (it only grows), each applied in turn
+  template <class Emit>
+  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&&) {
+    const double top = H.n < k ? -1.0 : H.at(0);
+    uint64_t cm = __ballot(valid && sc > top);
+#ifdef WSR_REPLAY_PROF
+    n_ev += __popcll(__ballot(valid));
+    n_cand += __popcll(cm);
+#endif
+#ifdef WSR_DIAG_REPLAY_NO_HEAP   // timing diagnostic only (wrong results): stream, no heap
+    cm = 0;
+#endif
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      insert(readlane_f64(sc, fl),
+             static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl)));
+    }
   }
   __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
     const uint32_t l = threadIdx.x & 63;
@@ -1041,8 +1090,8 @@ struct HeapSink {
 __device__ uint32_t* g_replay_prof = nullptr;   // diagnostics build: per-query replay rows
 #endif
 
-// One wave per query: filter the events of its segments (doc-id order) and
-// apply the survivors of the filter to the heap.
+// One wave per query: the events of its segments (doc-id order) through the
+// restated heap (HeapSink::step: the heap's own insertion test).
 template <bool kCoherent>
 __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
                                              const QueryPlan* __restrict__ plan, int qi,
@@ -1054,14 +1103,12 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
 #ifdef WSR_REPLAY_PROF
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
-  EventFilter F;
-  F.k = k;
   HeapSink sink;
   sink.k = k;
   consume_stream<kCoherent>(
-      F, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
+      sink, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
       [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
-      [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+      [](double, int32_t) {});
 #ifdef WSR_REPLAY_PROF
   const uint64_t t_filter = __builtin_amdgcn_s_memtime();
 #endif
@@ -1072,7 +1119,7 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
     uint32_t* o = g_replay_prof + 6 * qi;
     o[0] = static_cast<uint32_t>(t_filter - t_start);
     o[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_filter);
-    o[2] = F.n_ev; o[3] = F.n_cand; o[4] = F.n_ins; o[5] = P.n_items;
+    o[2] = sink.n_ev; o[3] = sink.n_cand; o[4] = sink.n_ins; o[5] = P.n_items;
   }
 #endif
 }
@@ -2550,12 +2597,9 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
     return;
   }
-  EventFilter F;
-  F.k = k;
   HeapSink sink;
   sink.k = k;
-  consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of,
-                 [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+  consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
@@ -2596,12 +2640,9 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
   } else {
-    EventFilter F;
-    F.k = k;
     HeapSink sink;
     sink.k = k;
-    consume_stream(F, static_cast<uint32_t>(n_shards), count_of, base_of,
-                   [&](double sv, int32_t dv) { sink.insert(sv, dv); });
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
   }
 }
