@@ -60,6 +60,10 @@ def parse():
                    help="N>1: shard = doc-range shards with the RCCL event exchange (the value; "
                         "auto also measures replica as the control); replica = full index per "
                         "GPU, queries split across ranks, no collective")
+    p.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
+                   help="N>1 shards: the engine's own RCCL step (the measurement), or the same "
+                        "fused step with the transfer over the launcher's gloo group (a multi-rank "
+                        "rehearsal on one GPU; its speed is not the exchange's)")
     p.add_argument("--dist-backend", default="gloo",
                    help="the launcher's host-side group (rendezvous, RCCL id, barriers, timing "
                         "reduction); the data path is the engine's own RCCL exchange")
@@ -76,6 +80,9 @@ def parse():
     p.add_argument("--no-extra", action="store_true",
                    help="skip the secondary legs (N=1 only)")
     p.add_argument("--no-c3", action="store_true", help="skip the en-Wikipedia-shaped C3 leg")
+    p.add_argument("--legs", default="",
+                   help="comma list of secondary legs to run (default: all of end_to_end, "
+                        "c3_wiki_standin, c4_mixed_1to5, c5_phrase, serving, c1_snippets)")
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
@@ -365,9 +372,17 @@ def extra_legs(a, idx, local, threads):
     1-5 term AND queries (AOL shares) and 2-term phrase queries."""
     import wiser_amd as w
     legs = {}
-    legs["end_to_end"] = end_to_end_leg(a, idx, a.qlog, local, threads)
-    if not a.no_c3:
+    chosen = set(x for x in a.legs.split(",") if x)
+
+    def want(name):
+        return not chosen or name in chosen
+
+    if want("end_to_end"):
+        legs["end_to_end"] = end_to_end_leg(a, idx, a.qlog, local, threads)
+    if not a.no_c3 and want("c3_wiki_standin"):
         legs["c3_wiki_standin"] = c3_leg(a, local, threads)
+    if not (want("c4_mixed_1to5") or want("c5_phrase") or want("serving") or want("c1_snippets")):
+        return legs
     tag = os.path.basename(idx.rstrip("/"))
     mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
     phr = os.path.join(a.index_dir, f"phrase_{tag}_10000.log")
@@ -376,30 +391,38 @@ def extra_legs(a, idx, local, threads):
     has_pool = os.path.exists(os.path.join(idx, "phrases.txt"))
     if has_pool and not os.path.exists(phr):
         w.gen_phrase_log(idx, phr, n_queries=10000, seed=7)
-    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
-    eng.Load()
-    items = [(l.split(), False) for l in open(mixed).read().splitlines()]
-    legs["c4_mixed_1to5"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
-                                    0 if a.no_cpu else a.cpu_seconds / 4)
-    legs["c4_mixed_1to5"]["workload"] = ("20000 AND queries of 1-5 terms (AOL term-count shares, "
-                                         "gen_synthetic_log group rule, seed 7), top-10")
-    eng.close()
+    if want("c4_mixed_1to5"):
+        eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+        eng.Load()
+        items = [(l.split(), False) for l in open(mixed).read().splitlines()]
+        legs["c4_mixed_1to5"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
+                                        0 if a.no_cpu else a.cpu_seconds / 4)
+        legs["c4_mixed_1to5"]["workload"] = ("20000 AND queries of 1-5 terms (AOL term-count shares, "
+                                             "gen_synthetic_log group rule, seed 7), top-10")
+        eng.close()
     if not has_pool:   # phrase pool: synthetic indexes only
-        legs["serving"] = serving_leg(a, idx, local, threads)
-        legs["c1_snippets"] = snippet_leg(a, local, threads)
+        if want("serving"):
+            legs["serving"] = serving_leg(a, idx, local, threads)
+        if want("c1_snippets"):
+            legs["c1_snippets"] = snippet_leg(a, local, threads)
         return legs
-    t = time.time()
-    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
-    eng.Load()
-    log(f"engine with positions loaded in {time.time()-t:.1f}s")
-    items = w.read_query_log(phr)
-    legs["c5_phrase"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
-                                0 if a.no_cpu else a.cpu_seconds / 4)
-    legs["c5_phrase"]["workload"] = ("10000 two-term phrase queries drawn from the corpus's "
-                                     "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
-    eng.close()
-    legs["serving"] = serving_leg(a, idx, local, threads)
-    legs["c1_snippets"] = snippet_leg(a, local, threads)
+    if not (want("c5_phrase") or want("serving") or want("c1_snippets")):
+        return legs
+    if want("c5_phrase"):
+        t = time.time()
+        eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
+        eng.Load()
+        log(f"engine with positions loaded in {time.time()-t:.1f}s")
+        items = w.read_query_log(phr)
+        legs["c5_phrase"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
+                                    0 if a.no_cpu else a.cpu_seconds / 4)
+        legs["c5_phrase"]["workload"] = ("10000 two-term phrase queries drawn from the corpus's "
+                                         "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
+        eng.close()
+    if want("serving"):
+        legs["serving"] = serving_leg(a, idx, local, threads)
+    if want("c1_snippets"):
+        legs["c1_snippets"] = snippet_leg(a, local, threads)
     return legs
 
 
@@ -585,7 +608,11 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         if dist is not None:
             dist.barrier()
 
-    S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
+    if a.exchange == "gloo" and dist is not None:
+        from wiser_amd.shard import HostExchangeShardedSearcher
+        S = HostExchangeShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
+    else:
+        S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
     full = None
     # per-item fixed work is large (profiles/r02_x_item_size.txt: items of 16
     # blocks run at half the rate of 63), so a query is split over the shards
@@ -916,8 +943,12 @@ def main():
         # host time to enqueue the timed steps: close to ms_per_step = launch-bound
         out["host_enqueue_ms_per_step"] = round(DIAG.get("host_enqueue_ms_per_step", 0.0), 4)
         if sharded:
-            out["exchange"] = {"kind": "RCCL grouped send/recv per peer over xGMI (wsr_shard_step), "
-                                       "fixed slots, no host round trip inside a step",
+            kind = ("RCCL grouped send/recv per peer over xGMI (wsr_shard_step), fixed slots, no host "
+                    "round trip inside a step")
+            if a.exchange == "gloo" and world > 1:
+                kind = ("REHEARSAL: fused emit / owner replay with the slots moved by gloo through "
+                        "host memory (not the RCCL path's speed)")
+            out["exchange"] = {"kind": kind,
                                "slot_events": getattr(S, "slot", None),
                                "heavy_blocks": getattr(S, "heavy_blocks", None),
                                "heavy_query_share": round(getattr(S, "heavy_share", 0.0), 4)}

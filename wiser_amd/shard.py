@@ -15,8 +15,11 @@ round trip inside a step):
     packs each owner's events into a fixed slot, RCCL moves counts and slots
     with grouped send / recv over xGMI, the owner replays; all on the batch's
     HIP stream.  torch is only the launcher's rendezvous (gloo, host side).
-  * ShardedSearcher: the same fixed slots exchanged by torch.distributed
-    all_to_all (gloo on the CPU in tests, or RCCL through torch).
+  * HostExchangeShardedSearcher: the same fused device halves with the
+    transfer done by torch.distributed (gloo): the multi-rank rehearsal on one
+    GPU, where RCCL refuses two ranks;
+  * ShardedSearcher: the earlier split form (reduce, pack, replay launches)
+    exchanged by torch.distributed all_to_all (gloo on the CPU in tests).
 A slot that overflows fails the batch loudly (error flag at fetch); the slot
 size comes from the measured fill (slot_for_fill).
 """
@@ -149,6 +152,62 @@ class NativeShardedSearcher:
         if self._c:
             lib.wsr_comm_close(self._c)
             self._c = None
+        self.engine.close()
+
+
+class HostExchangeShardedSearcher:
+    """The fused step of NativeShardedSearcher with the transfer done by the
+    caller's torch.distributed group instead of RCCL: wsr_shard_emit (segments
+    append each query's reduced events to its owner's slot), an all_to_all of
+    the {count, offset} pairs and the slots, wsr_owner_replay_meta.  This is the
+    multi-rank rehearsal on ONE GPU (RCCL refuses two ranks on one device): the
+    gloo group moves host copies, so it checks the orchestration and the results,
+    not the exchange's speed.  Same step / max_fill / fetch_owned / close."""
+
+    def __init__(self, index_dir: str, rank: int, world: int, group=None, device: int = 0,
+                 threads: int = 0, positions: bool = False):
+        from .engine import VacuumEngine
+        self.rank, self.world, self.group = rank, world, group
+        self.n_docs = index_doc_count(index_dir)
+        self.doc_range = shard_range(self.n_docs, rank, world)
+        self.engine = VacuumEngine(index_dir, device=device, threads=threads,
+                                   doc_range=self.doc_range if world > 1 else None, positions=positions)
+        self.engine.Load()
+        self._keep = {}
+
+    def step(self, b, qpr: int, slot: int):
+        import torch
+        import torch.distributed as dist
+        W = self.world
+        dev = torch.device("cuda", self.engine.device)
+        meta = torch.empty((W * qpr, 2), dtype=torch.int32, device=dev)
+        send = torch.empty((W * slot, EVENT_WORDS), dtype=torch.int64, device=dev)
+        check(lib.wsr_shard_emit(self.engine._h, b._b, qpr, W, slot, C.c_void_p(meta.data_ptr()),
+                                 C.c_void_p(send.data_ptr())))
+        check(lib.wsr_sync(self.engine._h))
+        rmeta = torch.empty((W * qpr, 2), dtype=torch.int32)
+        recv = torch.empty((W * slot, EVENT_WORDS), dtype=torch.int64)
+        dist.all_to_all_single(rmeta, meta.cpu(), group=self.group)
+        dist.all_to_all_single(recv, send.cpu(), group=self.group)
+        rmeta, recv = rmeta.to(dev), recv.to(dev)
+        torch.cuda.synchronize(dev)
+        check(lib.wsr_owner_replay_meta(self.engine._h, b._b, self.rank * qpr, qpr, W, slot,
+                                        C.c_void_p(rmeta.data_ptr()), C.c_void_p(recv.data_ptr())))
+        self._keep[id(b)] = (meta, send, rmeta, recv)   # alive until the replay has run
+
+    def max_fill(self, b) -> int:
+        tot = (C.c_int64 * self.world)()
+        check(lib.wsr_shard_fill(self.engine._h, b._b, self.world, tot))
+        return max(tot)
+
+    def fetch_owned(self, b, qpr: int):
+        hits = (_capi.Hit * (qpr * b.stride))()
+        nh = (C.c_int32 * qpr)()
+        check(lib.wsr_batch_fetch_range(self.engine._h, b._b, self.rank * qpr, qpr, hits, nh))
+        return hits, nh
+
+    def close(self):
+        self._keep.clear()
         self.engine.close()
 
 
