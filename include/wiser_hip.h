@@ -297,13 +297,13 @@ int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_ow
 
 /* ---- native RCCL exchange (one process per GPU; a C++ host needs no Python):
  * rank 0 makes the id, every rank opens the communicator with it (the id
- * travels by the caller's own rendezvous), then each step is one call:
- * wsr_shard_emit on the batch's stream, then, on the communicator's stream,
- * one group of ncclSend / ncclRecv with every peer over xGMI ({count, offset}
- * pairs and the event slot) and wsr_owner_replay_meta.  Nothing waits on the
- * host; wsr_batch_fetch* / wsr_batch_ready join the exchange.  Rank r's owned
- * queries are [r * q_per_owner, (r + 1) * q_per_owner) of a batch of
- * world * q_per_owner. */
+ * travels by the caller's own rendezvous), then each step is one call: the
+ * segments emit into per-owner regions ({count, offset} pairs + the event
+ * slot) on the batch's stream, then, on the communicator's stream, one
+ * ncclAllToAll of the regions over xGMI and the owner replay.  Nothing waits
+ * on the host; wsr_batch_fetch* / wsr_batch_ready join the exchange.  Rank
+ * r's owned queries are [r * q_per_owner, (r + 1) * q_per_owner) of a batch
+ * of world * q_per_owner. */
 #define WSR_COMM_ID_BYTES 128
 typedef struct wsr_comm wsr_comm;
 int wsr_comm_unique_id(uint8_t* id /* WSR_COMM_ID_BYTES */);

@@ -134,19 +134,16 @@ struct wsr_batch {
   uint64_t* d_roff = nullptr;     // owner side per (shard, query) offsets
   uint64_t* d_rbase = nullptr;
   size_t roff_cap = 0;
-  // native fixed-slot exchange (wsr_shard_step): counts, owner-major send slots,
-  // shard-major receive slots, allocated on first use
-  int32_t* d_xcount = nullptr;
-  int32_t* d_xrcount = nullptr;
+  // native exchange (wsr_shard_step): per owner a region of {count, offset}
+  // pairs + an event slot, owner-major to send, shard-major received;
+  // allocated on first use
   Event* d_xsend = nullptr;
   Event* d_xrecv = nullptr;
-  uint64_t x_slots = 0;     // slot capacity * pairs the two event buffers were sized for
+  uint64_t x_slots = 0;     // region events * pairs the two exchange buffers were sized for
   int x_pairs = 0;
   hipEvent_t xev[2] = {nullptr, nullptr};   // pack done -> comm stream; exchange done -> replay
   bool x_pending = false;   // a shard step's exchange + owner replay (xev[1]) not yet joined
   bool x_fused = false;     // the last exchange was a wsr_shard_step (fill counters after d_ctr)
-  int32_t* d_xmeta = nullptr;    // fused shard step: per query {count, offset}, owner-major
-  int32_t* d_xrmeta = nullptr;   // ... received, shard-major
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
@@ -543,9 +540,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_pub), static_cast<void*>(b->d_ph),
                   static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase),
-                  static_cast<void*>(b->d_xcount), static_cast<void*>(b->d_xrcount),
-                  static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv),
-                  static_cast<void*>(b->d_xmeta), static_cast<void*>(b->d_xrmeta)})
+                  static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv)})
     if (p) (void)hipFree(p);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
@@ -667,9 +662,11 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
 struct ShardEmit {
   int owners;
   int32_t qpr;
-  uint64_t slot;
-  Event* send;
-  int32_t* meta;
+  uint64_t slot;         // capacity of an owner's slot (events)
+  Event* send;           // owner 0's slot; owner o's at send + o * stride
+  uint64_t stride;
+  int32_t* meta;         // owner 0's {count, offset} block; owner o's at meta + o * meta_stride
+  uint64_t meta_stride;
 };
 
 static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* se = nullptr);
@@ -695,6 +692,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
       fr.x_fill = b->d_ctr + kNumCounters;
       fr.x_err = b->d_ctr + kCtrError;
       fr.x_slot = se->slot;
+      fr.x_stride = se->stride;
+      fr.x_meta_stride = se->meta_stride;
       fr.x_qpr = se->qpr;
     }
     HIP_OK(hipEventRecord(b->ev[0], st));
@@ -1167,20 +1166,22 @@ int wsr_shard_emit(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_o
     return fail(WSR_E_INVALID, "bad shard_emit arguments");
   if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
   if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
-  const ShardEmit se{n_owners, q_per_owner, static_cast<uint64_t>(slot), static_cast<Event*>(d_send), d_meta};
+  const ShardEmit se{n_owners, q_per_owner, static_cast<uint64_t>(slot), static_cast<Event*>(d_send),
+                     static_cast<uint64_t>(slot), d_meta, 2ull * static_cast<uint64_t>(q_per_owner)};
   const int rc = batch_run(h, b, false, &se);
   if (rc == WSR_OK) b->x_fused = true;
   return rc;
 }
 
 static int owner_replay_meta_on(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                                int64_t slot, const int32_t* d_rmeta, const void* d_recv, hipStream_t st) {
+                                const int32_t* d_rmeta, uint64_t meta_stride, uint64_t stride,
+                                const void* d_recv, hipStream_t st) {
   if (!h || !b || n_shards <= 0 || n_shards > kMaxOwners || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq ||
-      slot <= 0 || (nq_owned && (!d_rmeta || !d_recv)))
+      stride == 0 || (nq_owned && (!d_rmeta || !d_recv)))
     return fail(WSR_E_INVALID, "bad owner_replay_meta arguments");
   try {
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(launch_owner_replay_meta(b->d_q, q0, nq_owned, n_shards, d_rmeta, static_cast<uint64_t>(slot),
+    HIP_OK(launch_owner_replay_meta(b->d_q, q0, nq_owned, n_shards, d_rmeta, meta_stride, stride,
                                     static_cast<const Event*>(d_recv), b->d_hits, b->stride, b->d_nhits,
                                     b->d_ctr, b->has_wide, st));
   } catch (const std::exception& e) {
@@ -1191,25 +1192,29 @@ static int owner_replay_meta_on(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t
 
 int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
                           int64_t slot, const int32_t* d_rmeta, const void* d_recv) {
-  if (!b) return fail(WSR_E_INVALID, "null argument");
-  return owner_replay_meta_on(h, b, q0, nq_owned, n_shards, slot, d_rmeta, d_recv, b->st);
+  if (!b || slot <= 0) return fail(WSR_E_INVALID, "bad owner_replay_meta arguments");
+  return owner_replay_meta_on(h, b, q0, nq_owned, n_shards, d_rmeta, 2ull * static_cast<uint64_t>(nq_owned),
+                              static_cast<uint64_t>(slot), d_recv, b->st);
 }
 
 // One step of a doc-range sharded batch, all of it enqueued, nothing waited on:
-//   batch stream: wsr_shard_emit (plan + segment kernels; the worker that
-//     finishes a query reduces its events into the owner's slot);
-//   communicator stream (joined by xev[0]): one RCCL group of send/recv per
-//     peer -- the {count, offset} pairs and the event slot -- then the owner
-//     replay of this rank's queries; xev[1] marks the end.
-// The batch stream never waits on the exchange inside a step, so the next
-// batches' kernels run under it; the next run of this batch waits for xev[1]
-// (long past by then), and the fetches join it.
+//   batch stream: the plan + segment kernels; the worker that finishes a
+//     query reduces its events into the owner's region of the send buffer;
+//   communicator stream (joined by xev[0]): one ncclAllToAll of the regions
+//     (RCCL's pairwise exchange over xGMI), then the owner replay of this
+//     rank's queries; xev[1] marks the end.
+// An owner's region is [{count, offset} of its qpr queries, padded to whole
+// events][slot of events], so one collective moves both.  The batch stream
+// never waits on the exchange inside a step, so the next batches' kernels run
+// under it; the next run of this batch waits for xev[1] (long past by then),
+// and the fetches join it.
 int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
   if (!h || !b || !c || q_per_owner <= 0 || slot <= 0 ||
       static_cast<int64_t>(q_per_owner) * c->world != b->nq)
     return fail(WSR_E_INVALID, "bad shard_step arguments (the batch must hold world * q_per_owner queries)");
   const int W = c->world;
   if (W > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners ranks");
+  if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
   uint64_t t0 = c->timing ? now_ns() : 0;
   auto lap = [&](int i) {
     if (!c->timing) return;
@@ -1217,13 +1222,12 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
     c->t_ns[i] += t - t0;
     t0 = t;
   };
+  // region of one owner: the meta block (2 int32 per query, 4 per event) + the slot
+  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
+  const uint64_t region = meta_events + static_cast<uint64_t>(slot);
   try {
     HIP_OK(hipSetDevice(h->device));
-    const uint64_t need = static_cast<uint64_t>(slot) * W;
-    if (!b->d_xmeta) {
-      HIP_OK(hipMalloc(&b->d_xmeta, sizeof(int32_t) * 2 * b->max_q));
-      HIP_OK(hipMalloc(&b->d_xrmeta, sizeof(int32_t) * 2 * b->max_q));
-    }
+    const uint64_t need = region * W;
     if (need > b->x_slots || W != b->x_pairs) {
       if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));
       if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
@@ -1241,33 +1245,26 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
-  int rc = wsr_shard_emit(h, b, q_per_owner, W, slot, b->d_xmeta, b->d_xsend);
+  const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));   // int32 per region
+  const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), b->d_xsend + meta_events, region,
+                     reinterpret_cast<int32_t*>(b->d_xsend), meta_stride};
+  int rc = batch_run(h, b, false, &se);
   if (rc) return rc;
+  b->x_fused = true;
   lap(0);
-  // xGMI is point to point: one send / receive per peer and buffer, no ring
-  auto nc = [](ncclResult_t r, const char* what) {
-    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
-  };
   try {
     HIP_OK(hipEventRecord(b->xev[0], b->st));
     HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
-    nc(ncclGroupStart(), "ncclGroupStart");
-    for (int p = 0; p < W; ++p) {
-      nc(ncclSend(b->d_xmeta + static_cast<size_t>(p) * 2 * q_per_owner, 2 * static_cast<size_t>(q_per_owner),
-                  ncclInt32, p, c->comm, c->stream), "ncclSend meta");
-      nc(ncclRecv(b->d_xrmeta + static_cast<size_t>(p) * 2 * q_per_owner, 2 * static_cast<size_t>(q_per_owner),
-                  ncclInt32, p, c->comm, c->stream), "ncclRecv meta");
-      nc(ncclSend(b->d_xsend + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
-                  c->comm, c->stream), "ncclSend events");
-      nc(ncclRecv(b->d_xrecv + static_cast<size_t>(p) * slot, static_cast<size_t>(slot) * 2, ncclUint64, p,
-                  c->comm, c->stream), "ncclRecv events");
-    }
-    nc(ncclGroupEnd(), "ncclGroupEnd");
+    const ncclResult_t r = ncclAllToAll(b->d_xsend, b->d_xrecv, region * (sizeof(Event) / sizeof(uint64_t)),
+                                        ncclUint64, c->comm, c->stream);
+    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   lap(2);
-  rc = owner_replay_meta_on(h, b, c->rank * q_per_owner, q_per_owner, W, slot, b->d_xrmeta, b->d_xrecv, c->stream);
+  rc = owner_replay_meta_on(h, b, c->rank * q_per_owner, q_per_owner, W,
+                            reinterpret_cast<const int32_t*>(b->d_xrecv), meta_stride, region,
+                            b->d_xrecv + meta_events, c->stream);
   if (rc) return rc;
   if (hipEventRecord(b->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
   b->x_pending = true;

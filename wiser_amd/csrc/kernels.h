@@ -100,12 +100,19 @@ struct FusedReplay {
   HitDev* hits;
   int hit_stride;
   int32_t* n_hits;
-  Event* x_send;        // owner o's slot at x_send + o * x_slot
-  int32_t* x_meta;      // per query {count, offset in the owner's slot}
+  Event* x_send;        // owner o's slot at x_send + o * x_stride (x_slot events)
+  int32_t* x_meta;      // {count, offset in the owner's slot} of query i of owner o at
+                        //   x_meta + o * x_meta_stride + 2 * i
   uint32_t* x_fill;     // per owner: events appended (zeroed before the batch)
   uint32_t* x_err;      // error flags word
-  uint64_t x_slot;
+  uint64_t x_slot;      // slot capacity (events)
+  uint64_t x_stride;    // events between owners' slots
+  uint64_t x_meta_stride;   // int32 between owners' meta blocks
   int32_t x_qpr;        // queries per owner
+  __device__ int32_t* meta_of(uint32_t q) const {
+    const uint32_t o = q / static_cast<uint32_t>(x_qpr);
+    return x_meta + o * x_meta_stride + 2ull * (q - o * static_cast<uint32_t>(x_qpr));
+  }
 };
 
 // Plan pass 1 -> pass 2: per plan workgroup (kPlanThreads queries), its items
@@ -170,9 +177,11 @@ hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_sha
                                      int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st);
 // owner side of the fused exchange: meta[(g * nq + i) * 2] = {count, offset}
 // sent by shard g for owned query i, its events at recv + g * slot + offset
+// (meta of shard g at meta + g * meta_stride, its events at recv + g * stride)
 hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* meta,
-                                    uint64_t slot, const Event* recv, HitDev* hits, int hit_stride,
-                                    int32_t* n_hits, uint32_t* counters, bool any_wide, hipStream_t st);
+                                    uint64_t meta_stride, uint64_t stride, const Event* recv, HitDev* hits,
+                                    int hit_stride, int32_t* n_hits, uint32_t* counters, bool any_wide,
+                                    hipStream_t st);
 // resident 64-thread segment workgroups per CU
 int segment_kernel_occupancy();
 

@@ -487,8 +487,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       fr.q_done[i] = 0;
       if (p.n_items == 0) fr.n_hits[i] = 0;   // no item will replay an empty query
       if (p.n_items == 0 && fr.x_meta) {      // ... nor emit it: no events for its owner
-        fr.x_meta[2 * i] = 0;
-        fr.x_meta[2 * i + 1] = 0;
+        int32_t* m = fr.meta_of(static_cast<uint32_t>(i));
+        m[0] = 0;
+        m[1] = 0;
       }
     }
   }
@@ -1210,7 +1211,7 @@ __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan*
     cnt = -1;
     if (l == 0) atomicOr(fr.x_err, static_cast<uint32_t>(kErrExchange));
   } else {
-    Event* dst = fr.x_send + static_cast<uint64_t>(o) * fr.x_slot + off;
+    Event* dst = fr.x_send + static_cast<uint64_t>(o) * fr.x_stride + off;
     for (uint32_t i = l; i < n; i += 64) {
       double sc;
       int32_t dc;
@@ -1223,8 +1224,9 @@ __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan*
     }
   }
   if (l == 0) {
-    fr.x_meta[2 * qi] = cnt;
-    fr.x_meta[2 * qi + 1] = static_cast<int32_t>(off);
+    int32_t* m = fr.meta_of(static_cast<uint32_t>(qi));
+    m[0] = cnt;
+    m[1] = static_cast<int32_t>(off);
   }
 }
 
@@ -2603,15 +2605,17 @@ __global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restr
   sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
 }
 
-// Owner side of the fused exchange (wsr_shard_step): meta[(g * nq + i) * 2] =
-// {count, offset} shard g sent for owned query i (count -1: the sender's slot
-// overflowed: flagged, read as empty); its events at recv + g * slot + offset.
+// Owner side of the fused exchange (wsr_shard_step): meta[g * meta_stride +
+// 2 * i] = {count, offset} shard g sent for owned query i (count -1: the
+// sender's slot overflowed: flagged, read as empty); its events at recv +
+// g * stride + offset.
 // kWide: the queries with k > kMaxK, heap in LDS (a separate instance, so the
 // common one reserves no LDS for it).
 template <bool kWide>
 __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
                                                                int n_shards, const int32_t* __restrict__ meta,
-                                                               uint64_t slot, const Event* __restrict__ recv,
+                                                               uint64_t meta_stride, uint64_t stride,
+                                                               const Event* __restrict__ recv,
                                                                HitDev* __restrict__ hits, int hit_stride,
                                                                int32_t* __restrict__ n_hits,
                                                                uint32_t* __restrict__ counters) {
@@ -2621,15 +2625,14 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
   const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
   if ((k > static_cast<uint32_t>(kMaxK)) != kWide) return;
   const uint32_t l = threadIdx.x & 63;
-  if (l < static_cast<uint32_t>(n_shards) && meta[(static_cast<int64_t>(l) * nq + qi) * 2] < 0)
+  auto meta_of = [&](uint32_t g) { return meta + g * meta_stride + 2ull * static_cast<uint32_t>(qi); };
+  if (l < static_cast<uint32_t>(n_shards) && meta_of(l)[0] < 0)
     atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
   auto count_of = [&](uint32_t g) {
-    const int32_t c = meta[(static_cast<int64_t>(g) * nq + qi) * 2];
+    const int32_t c = meta_of(g)[0];
     return static_cast<uint32_t>(c > 0 ? c : 0);
   };
-  auto base_of = [&](uint32_t g) {
-    return recv + g * slot + static_cast<uint32_t>(meta[(static_cast<int64_t>(g) * nq + qi) * 2 + 1]);
-  };
+  auto base_of = [&](uint32_t g) { return recv + g * stride + static_cast<uint32_t>(meta_of(g)[1]); };
   if constexpr (kWide) {
     __shared__ double s_hs[kMaxKWide];
     __shared__ int32_t s_hd[kMaxKWide];
@@ -2838,14 +2841,15 @@ hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_sha
 }
 
 hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* meta,
-                                    uint64_t slot, const Event* recv, HitDev* hits, int hit_stride,
-                                    int32_t* n_hits, uint32_t* counters, bool any_wide, hipStream_t st) {
+                                    uint64_t meta_stride, uint64_t stride, const Event* recv, HitDev* hits,
+                                    int hit_stride, int32_t* n_hits, uint32_t* counters, bool any_wide,
+                                    hipStream_t st) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(owner_replay_meta_kernel<false>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta, slot,
-                     recv, hits, hit_stride, n_hits, counters);
+  hipLaunchKernelGGL(owner_replay_meta_kernel<false>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
+                     meta_stride, stride, recv, hits, hit_stride, n_hits, counters);
   if (any_wide)
     hipLaunchKernelGGL(owner_replay_meta_kernel<true>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
-                       slot, recv, hits, hit_stride, n_hits, counters);
+                       meta_stride, stride, recv, hits, hit_stride, n_hits, counters);
   return hipGetLastError();
 }
 
