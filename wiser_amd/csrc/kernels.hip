@@ -365,22 +365,49 @@ __device__ __forceinline__ T wave_incl_scan_any(T x) {
   }
   return x;
 }
-// exclusive prefix of x over the workgroup's threads, and the workgroup total
-template <class T>
-__device__ __forceinline__ T block_excl_scan(T x, T* s_w /*[4]*/, T* total) {
+// Exclusive prefixes over the workgroup's threads of N u32 values and one
+// u64, and their workgroup totals, with one pair of barriers for all of them
+// (the plan kernels' per-key item counts and event capacity).
+template <int N>
+struct ScanLds {
+  uint32_t w[N][kPlanThreads / 64];
+  uint64_t w64[kPlanThreads / 64];
+};
+template <int N>
+__device__ __forceinline__ void block_excl_scan_n(const uint32_t (&x)[N], uint64_t y, uint32_t (&ex)[N],
+                                                  uint32_t (&tot)[N], uint64_t& ey, uint64_t& toty,
+                                                  ScanLds<N>& S) {
   const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const T inc = wave_incl_scan_any(x);
+  uint32_t inc[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) inc[k] = wave_incl_scan(x[k]);
+  const uint64_t incy = wave_incl_scan_any(y);
   __syncthreads();
-  if (l == 63) s_w[w] = inc;
+  if (l == 63) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) S.w[k][w] = inc[k];
+    S.w64[w] = incy;
+  }
   __syncthreads();
-  T below = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    uint32_t below = 0, t = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kPlanThreads / 64; ++i) {
+      below += i < w ? S.w[k][i] : 0u;
+      t += S.w[k][i];
+    }
+    ex[k] = below + inc[k] - x[k];
+    tot[k] = t;
+  }
+  uint64_t below = 0, t = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kPlanThreads / 64; ++i) {
-    below += i < w ? s_w[i] : T(0);
-    tot += s_w[i];
+    below += i < w ? S.w64[i] : 0ull;
+    t += S.w64[i];
   }
-  *total = tot;
-  return below + inc - x;
+  ey = below + incy - y;
+  toty = t;
 }
 
 // Pass 1, one thread per query: driver (shortest list here), segment length
@@ -392,8 +419,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
                                                          uint32_t* __restrict__ counters, FusedReplay fr,
                                                          QueryDesc* __restrict__ desc,
                                                          PlanPart* __restrict__ part) {
-  __shared__ uint32_t s_w[kPlanThreads / 64];
-  __shared__ uint64_t s_w64[kPlanThreads / 64];
+  __shared__ ScanLds<kPlanKeys> S;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   QueryPlan p{0, 0, 1, 0, 0};
   if (i < nq) {
@@ -495,15 +521,16 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
   }
   // the workgroup's items per key and event capacity (pass 2 scans them)
   const uint32_t key = plan_key(p.driver);
-  uint32_t tot;
+  uint32_t v[kPlanKeys], ex[kPlanKeys], tot[kPlanKeys];
 #pragma unroll
-  for (int k = 0; k < kPlanKeys; ++k) {
-    (void)block_excl_scan<uint32_t>(key == static_cast<uint32_t>(k) ? p.n_items : 0u, s_w, &tot);
-    if (threadIdx.x == 0) part[blockIdx.x].items[k] = tot;
+  for (int k = 0; k < kPlanKeys; ++k) v[k] = key == static_cast<uint32_t>(k) ? p.n_items : 0u;
+  uint64_t cex, ctot;
+  block_excl_scan_n<kPlanKeys>(v, static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128, ex, tot, cex, ctot, S);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < kPlanKeys; ++k) part[blockIdx.x].items[k] = tot[k];
+    part[blockIdx.x].cap = ctot;
   }
-  uint64_t ctot;
-  (void)block_excl_scan<uint64_t>(static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128, s_w64, &ctot);
-  if (threadIdx.x == 0) part[blockIdx.x].cap = ctot;
 }
 
 // Pass 2, the same workgroups: every workgroup sums the partials of all
@@ -520,37 +547,39 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
                                                         uint32_t* __restrict__ item_q,
                                                         uint64_t* __restrict__ pub,
                                                         QueryDesc* __restrict__ desc) {
-  __shared__ uint32_t s_w[kPlanThreads / 64];
-  __shared__ uint64_t s_w64[kPlanThreads / 64];
+  __shared__ ScanLds<kPlanKeys> S;
   __shared__ uint32_t s_key_all[kPlanKeys], s_key_below[kPlanKeys];
   __shared__ uint64_t s_cap_all, s_cap_below;
   const uint32_t t = threadIdx.x;
-  // partial sums of all workgroups / of the lower ones (strided over threads)
-  uint32_t all[kPlanKeys], below[kPlanKeys];
+  // partial sums of all workgroups / of the lower ones: the first wave strides
+  // over the partials and reduces across its lanes (no barrier until the end)
+  if (t < 64) {
+    uint32_t all[kPlanKeys], below[kPlanKeys];
 #pragma unroll
-  for (int k = 0; k < kPlanKeys; ++k) all[k] = below[k] = 0;
-  uint64_t call = 0, cbelow = 0;
-  for (int g = static_cast<int>(t); g < n_part; g += kPlanThreads) {
-    const PlanPart P = part[g];
-    const bool lo = g < static_cast<int>(blockIdx.x);
+    for (int k = 0; k < kPlanKeys; ++k) all[k] = below[k] = 0;
+    uint64_t call = 0, cbelow = 0;
+    for (int g = static_cast<int>(t); g < n_part; g += 64) {
+      const PlanPart P = part[g];
+      const bool lo = g < static_cast<int>(blockIdx.x);
 #pragma unroll
-    for (int k = 0; k < kPlanKeys; ++k) { all[k] += P.items[k]; below[k] += lo ? P.items[k] : 0u; }
-    call += P.cap;
-    cbelow += lo ? P.cap : 0ull;
+      for (int k = 0; k < kPlanKeys; ++k) { all[k] += P.items[k]; below[k] += lo ? P.items[k] : 0u; }
+      call += P.cap;
+      cbelow += lo ? P.cap : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kPlanKeys; ++k) {
+      all[k] = __builtin_amdgcn_readlane(wave_incl_scan(all[k]), 63);
+      below[k] = __builtin_amdgcn_readlane(wave_incl_scan(below[k]), 63);
+    }
+    call = wave_incl_scan_any(call);
+    cbelow = wave_incl_scan_any(cbelow);
+    if (t == 63) {
+#pragma unroll
+      for (int k = 0; k < kPlanKeys; ++k) { s_key_all[k] = all[k]; s_key_below[k] = below[k]; }
+      s_cap_all = call;
+      s_cap_below = cbelow;
+    }
   }
-  uint32_t tot;
-#pragma unroll
-  for (int k = 0; k < kPlanKeys; ++k) {
-    (void)block_excl_scan<uint32_t>(all[k], s_w, &tot);
-    if (t == 0) s_key_all[k] = tot;
-    (void)block_excl_scan<uint32_t>(below[k], s_w, &tot);
-    if (t == 0) s_key_below[k] = tot;
-  }
-  uint64_t ctot;
-  (void)block_excl_scan<uint64_t>(call, s_w64, &ctot);
-  if (t == 0) s_cap_all = ctot;
-  (void)block_excl_scan<uint64_t>(cbelow, s_w64, &ctot);
-  if (t == 0) s_cap_below = ctot;
   __syncthreads();
   uint32_t key_base[kPlanKeys];
   uint32_t run = 0, n_lean = 0;
@@ -567,14 +596,17 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
   QueryPlan p{0, 0, 1, 0, 0};
   if (i < nq) p = plan[i];
   const uint32_t key = plan_key(p.driver);
+  uint32_t v[kPlanKeys], ex[kPlanKeys], tot[kPlanKeys];
+#pragma unroll
+  for (int k = 0; k < kPlanKeys; ++k) v[k] = key == static_cast<uint32_t>(k) ? p.n_items : 0u;
+  const uint64_t cap = static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
+  uint64_t cex, ctot;
+  block_excl_scan_n<kPlanKeys>(v, cap, ex, tot, cex, ctot, S);
   uint32_t base = 0;
 #pragma unroll
-  for (int k = 0; k < kPlanKeys; ++k) {
-    const uint32_t ex = block_excl_scan<uint32_t>(key == static_cast<uint32_t>(k) ? p.n_items : 0u, s_w, &tot);
-    if (key == static_cast<uint32_t>(k)) base = key_base[k] + ex;
-  }
-  const uint64_t cap = static_cast<uint64_t>(p.n_items) * p.seg_blocks * 128;
-  const uint64_t cb = s_cap_below + block_excl_scan<uint64_t>(cap, s_w64, &ctot);
+  for (int k = 0; k < kPlanKeys; ++k)
+    if (key == static_cast<uint32_t>(k)) base = key_base[k] + ex[k];
+  const uint64_t cb = s_cap_below + cex;
   if (i < nq) {
     plan[i].item_base = base;
     plan[i].ev_base = cb;
