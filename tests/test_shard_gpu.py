@@ -50,6 +50,7 @@ def _run_sharded(index_dir, queries, k, world, phrase=False):
             acc += totals[g][o]
         recv = torch.cat(parts + [torch.zeros((1, 2), dtype=torch.int64, device="cuda")]).contiguous()
         e, b = engs[o], batches[o]
+        torch.cuda.synchronize()   # (torch built rcounts / recv on its own stream)
         check(lib.wsr_owner_replay(e._h, b._b, o * qpr, qpr, world, C.c_void_p(rcounts.data_ptr()),
                                    C.c_void_p(recv.data_ptr()), (C.c_uint64 * world)(*rbase)))
         hits = (_capi.Hit * (qpr * k))()
@@ -126,6 +127,7 @@ def _run_sharded_fixed(index_dir, queries, k, world, slot):
         rcounts = torch.stack([counts[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
         recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
         e, b = engs[o], batches[o]
+        torch.cuda.synchronize()   # (torch built rcounts / recv on its own stream)
         check(lib.wsr_owner_replay_fixed(e._h, b._b, o * qpr, qpr, world, slot,
                                          C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr())))
         hits = (_capi.Hit * (qpr * k))()
@@ -199,6 +201,7 @@ def _run_sharded_emit(index_dir, queries, k, world, slot):
             b.upload(arr)
             meta = torch.full((len(queries), 2), -7, dtype=torch.int32, device="cuda")
             send = torch.zeros((world * slot, 2), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()   # (the fills run on torch's stream, the emit on the batch's)
             check(lib.wsr_shard_emit(e._h, b._b, qpr, world, slot, C.c_void_p(meta.data_ptr()),
                                      C.c_void_p(send.data_ptr())))
             check(lib.wsr_sync(e._h))
@@ -212,6 +215,7 @@ def _run_sharded_emit(index_dir, queries, k, world, slot):
             rmeta = torch.stack([metas[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
             recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
             e, b = engs[o], batches[o]
+            torch.cuda.synchronize()   # (torch built rmeta / recv on its own stream)
             check(lib.wsr_owner_replay_meta(e._h, b._b, o * qpr, qpr, world, slot,
                                             C.c_void_p(rmeta.data_ptr()), C.c_void_p(recv.data_ptr())))
             hits = (_capi.Hit * (qpr * k))()

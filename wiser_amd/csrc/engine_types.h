@@ -24,7 +24,8 @@ struct ListDev {
   uint64_t tf8;       // byte offset of the list's 1-byte tf array (posting order)
   uint64_t tail;      // its last block decoded (tail_cnt doc ids, then tail_cnt tfs) in the
                       // image's tails array when that block is a VInts blob, else kNoTail
-  uint64_t pad;
+  uint32_t last;      // last doc id of its last block in the image (= blk_last of that block)
+  uint32_t pad;
 };
 static_assert(sizeof(ListDev) == 64, "ListDev layout");
 constexpr uint64_t kNoTail = ~0ull;

@@ -408,6 +408,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     ld.bm = kNoDense;
     ld.tf8 = 0;
     ld.tail = kNoTail;
+    ld.last = 0;
     ld.pad = 0;
     if (!nbl) { img.list_bytes[id] = 0; continue; }
     if (in.vtail) { ld.tail = ntail; ntail += 2ull * in.tail_cnt; }
@@ -467,6 +468,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       img.blocks[j] = BlockDev{s.rows[r].prev_doc, s.last[r], static_cast<uint32_t>(s.rows[r].doc_off - d0),
                                static_cast<uint32_t>((d1 - d0) + s.rows[r].tf_off - t0)};
       img.blk_last[j] = s.last[r];
+      if (r == r1 - 1) img.lists[id].last = s.last[r];   // (this worker's own list)
       const uint8_t* pd = file + s.rows[r].doc_off;
       const uint8_t* pf = file + s.rows[r].tf_off;
       const uint32_t bd = pd[0] == kPackMagic ? pd[1] : 0u;

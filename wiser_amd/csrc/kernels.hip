@@ -430,16 +430,24 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       ok = false;
       atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
     }
-    uint32_t nb[kMaxTerms];
+    // one round of loads: every term's block count, bitmap and last doc
+    uint32_t nb[kMaxTerms], last[kMaxTerms];
     bool dn[kMaxTerms];
 #pragma unroll
     for (int s = 0; s < kMaxTerms; ++s) {
       nb[s] = 0xFFFFFFFFu;
+      last[s] = 0xFFFFFFFFu;
       dn[s] = false;
       if (ok && s < q.n_terms) {
         const int32_t id = q.list[s];
-        if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) ok = false;
-        else { nb[s] = ix.lists[id].nblk; dn[s] = ix.lists[id].bm != kNoDense; }
+        if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) {
+          ok = false;
+        } else {
+          const ListDev& L = ix.lists[id];
+          nb[s] = L.nblk;
+          dn[s] = L.bm != kNoDense;
+          last[s] = L.last;
+        }
         if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
       }
     }
@@ -473,6 +481,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       if (lean) {
         // the lean kernel's record: driver, the most selective other list (O1),
         // the smallest last doc of the others (bases are added by plan_fill_kernel)
+        uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
+#pragma unroll
+        for (int s = 0; s < kMaxTerms; ++s) {
+          if (s >= q.n_terms || s == static_cast<int>(d)) continue;
+          min_last = last[s] < min_last ? last[s] : min_last;
+          if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
+        }
+        // (the driver's and O1's records: a second round of loads, side by side)
         const ListDev A = ix.lists[q.list[d]];
         QueryDesc D;
         D.a_base = A.base;
@@ -481,14 +497,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.a_blk0 = A.blk0;
         D.a_nblk = A.nblk;
         D.a_tail_cnt = A.tail_cnt;
-        uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
-        for (int s = 0; s < q.n_terms; ++s) {
-          if (s == static_cast<int>(d)) continue;
-          const ListDev B = ix.lists[q.list[s]];
-          const uint32_t bl = ix.blk_last[B.blk0 + B.nblk - 1];
-          min_last = bl < min_last ? bl : min_last;
-          if (B.nblk < o_nb) { o1 = s; o_nb = B.nblk; }
-        }
         D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
         if (o1 < kMaxTerms) {
           const ListDev O = ix.lists[q.list[o1]];
