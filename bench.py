@@ -920,6 +920,9 @@ def main():
             "p50_alone_ms": round(p50, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         # the same bytes over the pipelined step time (consecutive
+                         # batches overlap on the device; value's own clock)
+                         "achieved_per_step": round((acc["algo"] / nbk) / (el / a.steps) / 1e9, 1),
                          "traffic": traffic,
                          "traffic_source": PMC_PROFILE if traffic else None,
                          "traffic_fetch_size_raw": traffic_fetch,
@@ -943,8 +946,8 @@ def main():
         # host time to enqueue the timed steps: close to ms_per_step = launch-bound
         out["host_enqueue_ms_per_step"] = round(DIAG.get("host_enqueue_ms_per_step", 0.0), 4)
         if sharded:
-            kind = ("RCCL grouped send/recv per peer over xGMI (wsr_shard_step), fixed slots, no host "
-                    "round trip inside a step")
+            kind = ("one ncclAllToAll of per-owner regions ({count, offset} pairs + fixed event slot) over "
+                    "xGMI per step (wsr_shard_step), no host round trip inside a step")
             if a.exchange == "gloo" and world > 1:
                 kind = ("REHEARSAL: fused emit / owner replay with the slots moved by gloo through "
                         "host memory (not the RCCL path's speed)")

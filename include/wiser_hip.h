@@ -198,7 +198,9 @@ int wsr_batch_run(wsr_handle* h, wsr_batch* b);
 int wsr_batch_run_events(wsr_handle* h, wsr_batch* b);
 /* wait for the engine stream */
 int wsr_sync(wsr_handle* h);
-/* copy results to the host (waits for the stream) */
+/* copy results to the host: the copies are queued behind the batch's kernels,
+ * then one wait.  Fails with WSR_E_INTERNAL when the device raised an error
+ * flag (hits / n_hits then hold no meaningful results). */
 int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits);
 int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out);
 /* as wsr_batch_fetch, but only the first `cols` (<= hit stride) entries of each

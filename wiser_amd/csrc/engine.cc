@@ -112,6 +112,7 @@ struct wsr_batch {
   QueryDesc* d_desc = nullptr;     // lean queries' work records
   PlanPart* d_part = nullptr;      // plan pass 1 -> 2 partial sums, per kPlanThreads queries
   uint32_t* d_ctr = nullptr;
+  uint32_t* h_ctr = nullptr;       // pinned host copy of the counters (fetch)
   Event* d_events = nullptr;
   uint64_t ev_cap = 0;
   uint32_t* d_evcnt = nullptr;
@@ -509,6 +510,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_desc, sizeof(QueryDesc) * max_q));
     HIP_OK(hipMalloc(&b->d_part, sizeof(PlanPart) * ((max_q + kPlanThreads - 1) / kPlanThreads + 1)));
     HIP_OK(hipMalloc(&b->d_ctr, sizeof(uint32_t) * (kNumCounters + kMaxOwners)));   // + shard fill counters
+    HIP_OK(hipHostMalloc(&b->h_ctr, sizeof(uint32_t) * kNumCounters));
     HIP_OK(hipMalloc(&b->d_hits, sizeof(HitDev) * static_cast<size_t>(max_q) * stride));
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
@@ -542,6 +544,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase),
                   static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv)})
     if (p) (void)hipFree(p);
+  if (b->h_ctr) (void)hipHostFree(b->h_ctr);
   for (auto& e : b->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
   if (b->fork) (void)hipEventDestroy(b->fork);
@@ -741,46 +744,71 @@ int wsr_sync(wsr_handle* h) {
   return WSR_OK;
 }
 
-int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits) {
-  if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
+// Results of the batch's last run: the counters, hit rows and hit counts go
+// out as copies queued on the batch stream behind its kernels (and behind a
+// shard step's exchange + owner replay), then one wait -- one host round trip
+// instead of a synchronize per buffer (pinned destinations; pageable ones are
+// copied after the wait).  The error flags are checked after the
+// copies; on an error the output buffers hold whatever the run left and the
+// call fails.  cols < stride copies the first cols entries of every row.
+static bool host_pinned(const void* p) {
+  if (!p) return true;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();   // plain pageable memory: not an error of this call
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+static int batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols) {
   try {
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
-    uint32_t ctr[kNumCounters];
-    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
-    if (b->nq) {
-      if (hits) HIP_OK(hipMemcpy(hits, b->d_hits, sizeof(HitDev) * b->nq * b->stride, hipMemcpyDeviceToHost));
+    hipStream_t st = b->st;
+    if (b->x_pending) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));   // a shard step's exchange + replay
+    HIP_OK(hipMemcpyAsync(b->h_ctr, b->d_ctr, sizeof(uint32_t) * kNumCounters, hipMemcpyDeviceToHost, st));
+    if (b->nq && !(host_pinned(hits) && host_pinned(n_hits))) {
+      // pageable destinations: a queued copy into them is staged by the runtime
+      // while the stream drains (serialising concurrent callers), so wait
+      // first and copy after
+      HIP_OK(hipStreamSynchronize(st));
+      const uint32_t err = b->h_ctr[kCtrError];
+      if (err) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(err));
+      if (hits && cols == b->stride)
+        HIP_OK(hipMemcpy(hits, b->d_hits, sizeof(HitDev) * b->nq * b->stride, hipMemcpyDeviceToHost));
+      else if (hits)
+        HIP_OK(hipMemcpy2D(hits, sizeof(HitDev) * cols, b->d_hits, sizeof(HitDev) * b->stride,
+                           sizeof(HitDev) * cols, b->nq, hipMemcpyDeviceToHost));
       if (n_hits) HIP_OK(hipMemcpy(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost));
+      return WSR_OK;
     }
+    if (b->nq) {
+      if (hits && cols == b->stride)
+        HIP_OK(hipMemcpyAsync(hits, b->d_hits, sizeof(HitDev) * b->nq * b->stride, hipMemcpyDeviceToHost, st));
+      else if (hits)   // a pitched copy
+        HIP_OK(hipMemcpy2DAsync(hits, sizeof(HitDev) * cols, b->d_hits, sizeof(HitDev) * b->stride,
+                                sizeof(HitDev) * cols, b->nq, hipMemcpyDeviceToHost, st));
+      if (n_hits)
+        HIP_OK(hipMemcpyAsync(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    const uint32_t err = b->h_ctr[kCtrError];
+    if (err) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(err));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   return WSR_OK;
 }
 
+int wsr_batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits) {
+  if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
+  return batch_fetch(h, b, hits, n_hits, b->stride);
+}
+
 int wsr_batch_fetch_cols(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hits, int32_t cols) {
   if (!h || !b || !b->ran) return fail(WSR_E_INVALID, "batch has not been run");
   if (cols < 1 || cols > b->stride) return fail(WSR_E_INVALID, "cols must be in [1, hit stride]");
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
-    uint32_t ctr[kNumCounters];
-    HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    if (ctr[kCtrError]) return fail(WSR_E_INTERNAL, "device reported error flags " + std::to_string(ctr[kCtrError]));
-    if (b->nq) {
-      // the first `cols` entries of every query's row: a pitched copy
-      if (hits)
-        HIP_OK(hipMemcpy2D(hits, sizeof(HitDev) * cols, b->d_hits, sizeof(HitDev) * b->stride,
-                           sizeof(HitDev) * cols, b->nq, hipMemcpyDeviceToHost));
-      if (n_hits) HIP_OK(hipMemcpy(n_hits, b->d_nhits, sizeof(int32_t) * b->nq, hipMemcpyDeviceToHost));
-    }
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
+  return batch_fetch(h, b, hits, n_hits, cols);
 }
 
 int wsr_pinned_alloc(uint64_t bytes, void** out) {

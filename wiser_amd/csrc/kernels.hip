@@ -430,7 +430,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       ok = false;
       atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
     }
-    // one round of loads: every term's block count, bitmap and last doc
+    // one round of loads: every term's block count, bitmap and last doc (each
+    // load's predicate depends on the query record only, not on an earlier
+    // load's value, so all of them are in flight together)
     uint32_t nb[kMaxTerms], last[kMaxTerms];
     bool dn[kMaxTerms];
 #pragma unroll
@@ -438,19 +440,19 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       nb[s] = 0xFFFFFFFFu;
       last[s] = 0xFFFFFFFFu;
       dn[s] = false;
-      if (ok && s < q.n_terms) {
-        const int32_t id = q.list[s];
-        if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) {
-          ok = false;
-        } else {
-          const ListDev& L = ix.lists[id];
-          nb[s] = L.nblk;
-          dn[s] = L.bm != kNoDense;
-          last[s] = L.last;
-        }
-        if (nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
+      const int32_t id = q.list[s];
+      const bool in = s < q.n_terms;
+      if (in && (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists)) ok = false;
+      if (in && id >= 0 && static_cast<uint32_t>(id) < ix.n_lists) {
+        const ListDev& L = ix.lists[id];
+        nb[s] = L.nblk;
+        dn[s] = L.bm != kNoDense;
+        last[s] = L.last;
       }
     }
+#pragma unroll
+    for (int s = 0; s < kMaxTerms; ++s)
+      if (s < q.n_terms && nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
     if (ok) {
       uint32_t d = 0, nd = nb[0];
 #pragma unroll

@@ -110,7 +110,7 @@ def slot_for_fill(max_fill: int, qpr: int) -> int:
 
 class NativeShardedSearcher:
     """One rank of a doc-range sharded engine whose whole step runs in C++
-    (wsr_shard_step: run + pack + RCCL grouped send/recv + owner replay)."""
+    (wsr_shard_step: run with fused emission + one ncclAllToAll + owner replay)."""
 
     def __init__(self, index_dir: str, rank: int, world: int, share_id, device: int = 0,
                  threads: int = 0, positions: bool = False):
