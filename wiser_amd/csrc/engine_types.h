@@ -25,7 +25,8 @@ struct ListDev {
   uint64_t tail;      // its last block decoded (tail_cnt doc ids, then tail_cnt tfs) in the
                       // image's tails array when that block is a VInts blob, else kNoTail
   uint32_t last;      // last doc id of its last block in the image (= blk_last of that block)
-  uint32_t pad;
+  uint32_t tfmax;     // an upper bound of its tfs in the image: exact for dense lists (their tfs
+                      // are decoded at load), else the largest pack width's maximum (~0u: unknown)
 };
 static_assert(sizeof(ListDev) == 64, "ListDev layout");
 constexpr uint64_t kNoTail = ~0ull;
@@ -107,7 +108,12 @@ struct QueryDesc {
   uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16
   uint32_t o_list;      // O1's list id
   uint32_t k;           // n_results (> kMaxK: wide, every survivor is an event)
-  uint32_t pad[4];
+  // score bound of a driver posting before the other lists are probed (f32,
+  // the lean kernel's pre-probe pruning): b_id * tf / (tf + norm) is its own
+  // term (b_id = 2.2 * idf), b_iom / (b_m + norm) bounds all the other terms
+  // (b_m = their largest tfmax, b_iom = sum of 2.2 * idf over them, times b_m)
+  float b_id, b_iom, b_m;
+  uint32_t pad;
 };
 static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
 

@@ -409,7 +409,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     ld.tf8 = 0;
     ld.tail = kNoTail;
     ld.last = 0;
-    ld.pad = 0;
+    ld.tfmax = 0;
     if (!nbl) { img.list_bytes[id] = 0; continue; }
     if (in.vtail) { ld.tail = ntail; ntail += 2ull * in.tail_cnt; }
     if (in.dense) {
@@ -463,6 +463,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     if (gap) std::memset(&img.blob[ld.base + in.bytes], 0, gap);
     const uint64_t n_img = (r1 - r0 - 1) * kPackSize + in.tail_cnt;
     if (in.dense) { s.docs.resize(n_img); s.tfs.resize(n_img); }
+    uint32_t tfmax = 0;   // (ListDev::tfmax: exact where the tfs are decoded, else pack maxima)
     for (uint64_t r = r0; r < r1; ++r) {
       const uint64_t j = ld.blk0 + (r - r0);
       img.blocks[j] = BlockDev{s.rows[r].prev_doc, s.last[r], static_cast<uint32_t>(s.rows[r].doc_off - d0),
@@ -488,9 +489,13 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
       for (int i = cnt; i < kPackSize; ++i) o[i] = 0;
       const bool last_vints = in.vtail && r + 1 == nrows;
-      if (in.dense || last_vints)
+      if (in.dense || last_vints) {
         if (!host_decode_block(pf, fend, cnt, false, 0, tfs))
           throw std::runtime_error("cannot decode the tfs of '" + idx.term(id) + "'");
+        for (int i = 0; i < cnt; ++i) tfmax = std::max(tfmax, tfs[i]);
+      } else {
+        tfmax = std::max(tfmax, bf == 0 ? ~0u : bf >= 32 ? ~0u : (1u << bf) - 1u);
+      }
       if (last_vints) {   // the list's VInts tail, decoded once (the kernels read it as words)
         std::memcpy(&img.tails[ld.tail], docs, cnt * sizeof(uint32_t));
         std::memcpy(&img.tails[ld.tail + cnt], tfs, cnt * sizeof(uint32_t));
@@ -500,6 +505,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         std::memcpy(&s.tfs[(r - r0) * kPackSize], tfs, cnt * sizeof(uint32_t));
       }
     }
+    img.lists[id].tfmax = tfmax;   // (this worker's own list)
     if (in.dense) {
       // rank bitmap: per 32 docs, the postings before them and the doc mask
       DenseEnt* de = &img.dense[ld.bm];

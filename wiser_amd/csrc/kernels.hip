@@ -514,7 +514,21 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.seg = seg;
         D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16);
         D.k = static_cast<uint32_t>(q.k);
-        for (int t = 0; t < 4; ++t) D.pad[t] = 0;
+        // pre-probe score bound: the other terms' BM25 parts are at most
+        // sum(2.2 idf) * M / (M + norm) with M their largest tf bound
+        double io = 0.0;
+        uint32_t mm = 0;
+        for (int s = 0; s < q.n_terms; ++s) {
+          if (s == static_cast<int>(d)) continue;
+          const ListDev& L = ix.lists[q.list[s]];
+          io += 2.2 * L.idf;
+          mm = L.tfmax > mm ? L.tfmax : mm;
+        }
+        const float mf = o1 < kMaxTerms ? static_cast<float>(mm) : 1.0f;
+        D.b_id = static_cast<float>(2.2 * A.idf);
+        D.b_m = mf;
+        D.b_iom = static_cast<float>(io * static_cast<double>(mf));
+        D.pad = 0;
         desc[i] = D;
       }
     }
@@ -1637,6 +1651,29 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint64_t floor_bits =
       prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
   double pub_val = 0.0;
+  // Pre-probe pruning.  A driver posting whose score bound -- its own term,
+  // exact, plus QueryDesc's bound of the other terms at its doc length -- is
+  // <= the threshold known so far, max(the floor of the query's earlier items,
+  // the running k-th best), can be no event: the reference heap inserts only a
+  // strictly larger score (query_processing.h:595-602), and both only grow.
+  // Such a posting is dropped before its bitmap probe.  The bound is f32 and
+  // the threshold carries a 0.2 % margin, far above the bound's rounding, so a
+  // dropped posting's f64 score is strictly below the threshold.
+  constexpr float kPruneMargin = 0.998f;
+  const float b_id = Q.b_id, b_iom = Q.b_iom, b_m = Q.b_m;
+#ifdef WSR_NO_PRUNE   // A/B diagnostic: every posting is probed
+  const float thr_s = -1.0f;
+#else
+  float thr_s = wide ? -1.0f
+                     : static_cast<float>(__longlong_as_double(static_cast<long long>(
+                           (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
+                           uni(static_cast<uint32_t>(floor_bits))))) * kPruneMargin;
+#endif
+  auto bound = [&](uint32_t t, uint32_t c) __attribute__((always_inline)) {
+    const float nf = static_cast<float>(norm_tab[c]);
+    const float f = static_cast<float>(t);
+    return b_id * f * __builtin_amdgcn_rcpf(f + nf) + b_iom * __builtin_amdgcn_rcpf(b_m + nf);
+  };
 
   auto flush = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
@@ -1747,6 +1784,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     const double pv = kn > flo ? kn : flo;
     pub_val = pv > pub_val ? pv : pub_val;
+#ifndef WSR_NO_PRUNE
+    thr_s = static_cast<float>(pv) * kPruneMargin;
+#endif
   };
 
   // Pipeline registers, in two alternating sets: iteration j reads set X
@@ -1756,15 +1796,16 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   struct Regs {
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
     uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
+    uint32_t wc = 0;                               //   its doc-length codes (2 bytes of a word)
+    uint32_t wt0 = 0, wt1 = 0, wt2 = 0;            //   its driver tf pack words
+    uint32_t wtb = 1, wtrel = 0;                   //   (uniform: width, blob offset)
     // D: a decoded block and its loads in flight
-    uint32_t da0 = ~0u, da1 = ~0u, dcw = 0;        // docs, doc-length codes (2 bytes of a word)
-    uint32_t dt0 = 0, dt1 = 0, dt2 = 0;            // driver tf pack words
-    uint32_t dtb = 1, dtrel = 0;                   //   (uniform: width, blob offset)
+    uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
+    uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
     uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap words
     // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
-    // block or outside the image, a rank with bit 31 set is an O1 miss -- so
-    // that they take no scalar lane-mask registers across the iteration)
-    uint32_t dtl = 0;                              // uniform: the block is the VInts tail
+    // block, outside the image or pruned, a rank with bit 31 set is an O1 miss
+    // -- so that they take no scalar lane-mask registers across the iteration)
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
     uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (in flight)
@@ -1788,6 +1829,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     Y.wrel = uni(S.dblk[bi].z);
     uint32_t sh;
     pair_words(a_blob + Y.wrel + 2, Y.wbits, l, Y.w0, Y.w1, Y.w2, sh);
+    // its doc-length codes (postings 2l, 2l+1: one line per block, plen) and
+    // driver tfs, so that D can bound each posting's score before the probe
+    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
+    Y.wtb = (m >> 8) ? (m >> 8) : 1u;
+    Y.wtrel = uni(S.dblk[bi].w);
+    pair_words(a_blob + Y.wtrel + 2, Y.wtb, l, Y.wt0, Y.wt1, Y.wt2, sh);
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     LT0()
@@ -1844,12 +1891,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       Y.hx1 = h1 ? (x1 & 0x7FFFFFFFu) : 0x80000000u;
 
       Y.ha0 = X.da0; Y.ha1 = X.da1;
-      Y.hc0 = (X.dcw >> ((l & 1u) << 4)) & 0xFFu;
-      Y.hc1 = (X.dcw >> (((l & 1u) << 4) + 8)) & 0xFFu;
-      uint32_t t0, t1;
-      pair_values(X.dt0, X.dt1, X.dt2, pair_shift(X.dtrel, X.dtb), X.dtb, t0, t1);
-      Y.ht0 = X.dtl ? ttf0 : t0;
-      Y.ht1 = X.dtl ? ttf1 : t1;
+      Y.hc0 = X.dcc & 0xFFu;
+      Y.hc1 = X.dcc >> 8;
+      Y.ht0 = X.dt0;
+      Y.ht1 = X.dt1;
     }
     LT(2)
     // D(j): decode block j from X's words into Y, issue its loads
@@ -1857,7 +1902,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool live = j < bend;
       const uint32_t bi = live ? j - b0 : 0u;
       const uint32_t prev = uni(S.dblk[bi].x);
-      const uint32_t m = uni(S.dmeta[bi]);
       const uint32_t cnt = live ? ((j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
       pair_values(X.w0, X.w1, X.w2, pair_shift(X.wrel, X.wbits), X.wbits, x0, x1);
@@ -1869,17 +1913,21 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       if (tl) { a0 = tdoc0; a1 = tdoc1; }
       const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
       const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
-      const bool in0 = !single && ok0 && a0 - lo < span;
-      const bool in1 = !single && ok1 && a1 - lo < span;
+      uint32_t t0, t1;
+      pair_values(X.wt0, X.wt1, X.wt2, pair_shift(X.wtrel, X.wtb), X.wtb, t0, t1);
+      if (tl) { t0 = ttf0; t1 = ttf1; }
+      const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
+      const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
+      // pre-probe pruning (above): a dropped posting is never probed
+      const bool p0 = ok0 && bound(t0, c0) > thr_s;
+      const bool p1 = ok1 && bound(t1, c1) > thr_s;
+      const bool in0 = !single && p0 && a0 - lo < span;
+      const bool in1 = !single && p1 && a1 - lo < span;
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
-      // doc-length codes of postings 2l, 2l+1: one line per block (plen)
-      Y.dcw = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (live ? j : b0)) * 32u + (l >> 1)];
-      Y.dtb = (m >> 8) ? (m >> 8) : 1u;
-      Y.dtrel = uni(S.dblk[bi].w);
-      uint32_t sh;
-      pair_words(a_blob + Y.dtrel + 2, Y.dtb, l, Y.dt0, Y.dt1, Y.dt2, sh);
-      Y.da0 = ok0 ? a0 : ~0u; Y.da1 = ok1 ? a1 : ~0u; Y.dtl = tl ? 1u : 0u;
+      Y.dcc = c0 | (c1 << 8);
+      Y.dt0 = t0; Y.dt1 = t1;
+      Y.da0 = p0 ? a0 : ~0u; Y.da1 = p1 ? a1 : ~0u;
       if (live) ++n_dblk;
       // past the smallest last doc of the other lists nothing later can match
       if (live && __ballot((ok0 && a0 > min_last) || (ok1 && a1 > min_last))) bend = j + 1;
@@ -2428,8 +2476,12 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 // Small LDS (LeanLds per wave + one shared norm table) and a register budget
 // of WSR_LEAN_WGS workgroups per CU keep several waves per SIMD resident, which
 // is what hides the dependent loads of short items and of the probe chains.
+// 5 workgroups (the conjunctive instance: 96 VGPRs, 31.8 KB LDS, 5 waves per
+// SIMD; the phrase / bitmap-intersection instances stay LDS-bound at 2 and 4):
+// with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against 4
+// (profiles/r02_pr2_ab.txt).
 #ifndef WSR_LEAN_WGS
-#define WSR_LEAN_WGS 4
+#define WSR_LEAN_WGS 5
 #endif
 template <bool kPh, bool kAnd>
 __global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
