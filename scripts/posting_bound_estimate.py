@@ -33,6 +33,7 @@ idf = lambda df: np.log(1 + (N - df + 0.5) / (df + 0.5))  # noqa: E731
 tfn = lambda tf, nm: (tf * 2.2) / (tf + nm)  # noqa: E731
 K, SEG, WIN = 10, 63, 2048
 tot = pr_glob = pr_win = surv = surv_glob = 0
+nblk = blk_all = blk_hit = 0
 for q in [l.split() for l in open(logp)][:nq]:
     if min(o.df(t) for t in q) < 10000:
         continue
@@ -63,9 +64,13 @@ for q in [l.split() for l in open(logp)][:nq]:
             pr_glob += int((ub_g[sl] <= thr).sum())
             pr_win += int((ub_w[sl] <= thr).sum())
             surv += int(hit[sl].sum())
+            nblk += 1
+            blk_all += bool((ub_g[sl] <= thr).all())
+            blk_hit += bool(((ub_g[sl] > thr) & hit[sl]).any())
             surv_glob += int((hit[sl] & (ub_g[sl] > thr)).sum())
             v = sc[sl]
             run = np.sort(np.concatenate([run, v[v > 0]]))[::-1][:K]
 print(f"high x high driver postings {tot}: ruled out before the probe by the bound with the "
       f"list's max tf {pr_glob / tot:.3f}, with the 2048-doc window's max tf {pr_win / tot:.3f}; "
-      f"survivors scored {surv} -> {surv_glob} with the list bound")
+      f"survivors scored {surv} -> {surv_glob} with the list bound; blocks {nblk}: every posting ruled out "
+      f"{blk_all / nblk:.3f}, no survivor left {1 - blk_hit / nblk:.3f}")

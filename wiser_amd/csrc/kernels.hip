@@ -1794,11 +1794,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   // swapped.  No register holding an in-flight load is ever copied (a copy
   // would wait for the load).
   struct Regs {
+    // (the block's pack widths and blob offsets are read again from the
+    // directory in LDS where they are used, so that no scalar registers hold
+    // them across the iteration)
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
-    uint32_t wbits = 1, wrel = 0;                  //   (uniform: width, blob offset)
     uint32_t wc = 0;                               //   its doc-length codes (2 bytes of a word)
     uint32_t wt0 = 0, wt1 = 0, wt2 = 0;            //   its driver tf pack words
-    uint32_t wtb = 1, wtrel = 0;                   //   (uniform: width, blob offset)
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
@@ -1825,16 +1826,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
     const uint32_t m = uni(S.dmeta[bi]);
-    Y.wbits = (m & 0xFF) ? (m & 0xFF) : 1u;   // VInts tail: harmless dummy read
-    Y.wrel = uni(S.dblk[bi].z);
+    const uint4 e = S.dblk[bi];
     uint32_t sh;
-    pair_words(a_blob + Y.wrel + 2, Y.wbits, l, Y.w0, Y.w1, Y.w2, sh);
+    // (VInts tail: width 0 -> a harmless dummy read)
+    pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
     // its doc-length codes (postings 2l, 2l+1: one line per block, plen) and
     // driver tfs, so that D can bound each posting's score before the probe
     Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
-    Y.wtb = (m >> 8) ? (m >> 8) : 1u;
-    Y.wtrel = uni(S.dblk[bi].w);
-    pair_words(a_blob + Y.wtrel + 2, Y.wtb, l, Y.wt0, Y.wt1, Y.wt2, sh);
+    pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1, Y.wt2, sh);
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     LT0()
@@ -1900,11 +1899,16 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     // D(j): decode block j from X's words into Y, issue its loads
     {
       const bool live = j < bend;
-      const uint32_t bi = live ? j - b0 : 0u;
-      const uint32_t prev = uni(S.dblk[bi].x);
+      // (the block issue_words loaded: j < b1 there, and the values of a block
+      // past bend are discarded below)
+      const uint32_t bi = j < b1 ? j - b0 : 0u;
+      const uint4 be = S.dblk[bi];
+      const uint32_t m = uni(S.dmeta[bi]);
+      const uint32_t prev = uni(be.x);
+      const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
       const uint32_t cnt = live ? ((j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
-      pair_values(X.w0, X.w1, X.w2, pair_shift(X.wrel, X.wbits), X.wbits, x0, x1);
+      pair_values(X.w0, X.w1, X.w2, pair_shift(uni(be.z), wbits), wbits, x0, x1);
       const uint32_t sm = x0 + x1;
       const uint32_t inc = wave_incl_scan(sm);
       uint32_t a0 = prev + (inc - sm) + x0;
@@ -1914,13 +1918,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
       const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
       uint32_t t0, t1;
-      pair_values(X.wt0, X.wt1, X.wt2, pair_shift(X.wtrel, X.wtb), X.wtb, t0, t1);
+      pair_values(X.wt0, X.wt1, X.wt2, pair_shift(uni(be.w), wtb), wtb, t0, t1);
       if (tl) { t0 = ttf0; t1 = ttf1; }
       const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
       const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
       // pre-probe pruning (above): a dropped posting is never probed
-      const bool p0 = ok0 && bound(t0, c0) > thr_s;
-      const bool p1 = ok1 && bound(t1, c1) > thr_s;
+      // (branch-free: the bound of a lane past the block is computed and dropped)
+      const bool p0 = ok0 & (bound(t0, c0) > thr_s);
+      const bool p1 = ok1 & (bound(t1, c1) > thr_s);
       const bool in0 = !single && p0 && a0 - lo < span;
       const bool in1 = !single && p1 && a1 - lo < span;
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
