@@ -1229,8 +1229,15 @@ __global__ __launch_bounds__(64) void wide_replay_kernel(const QueryIn* __restri
 // Fused shard emission (FusedReplay::x_send): the query's events, reduced as
 // shard_reduce_kernel does (compacted in place, coherent: other workers wrote
 // them), then appended to the owner's slot and described in x_meta.
+// (the exchange fields come as values: a FusedReplay passed by reference would
+// be copied to every wave's stack at kernel entry, 6 KB of scratch per wave)
 __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan* plan, int qi, Event* events,
-                                             const uint32_t* ev_cnt, const FusedReplay& fr) {
+                                             const uint32_t* ev_cnt, Event* x_send, int32_t* x_meta,
+                                             uint32_t* x_fill, uint32_t* x_err, uint64_t x_slot,
+                                             uint64_t x_stride, uint64_t x_meta_stride, int32_t x_qpr) {
+  FusedReplay fr{};
+  fr.x_send = x_send; fr.x_meta = x_meta; fr.x_fill = x_fill; fr.x_err = x_err;
+  fr.x_slot = x_slot; fr.x_stride = x_stride; fr.x_meta_stride = x_meta_stride; fr.x_qpr = x_qpr;
   const uint32_t l = threadIdx.x & 63;
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
@@ -1381,7 +1388,8 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     old = uni(old);
     if (old + 1 == n_items) {
       if (fr.x_send)
-        shard_emit_call(qs, plan, static_cast<int>(qi), const_cast<Event*>(events), ev_cnt, fr);
+        shard_emit_call(qs, plan, static_cast<int>(qi), const_cast<Event*>(events), ev_cnt, fr.x_send,
+                        fr.x_meta, fr.x_fill, fr.x_err, fr.x_slot, fr.x_stride, fr.x_meta_stride, fr.x_qpr);
       else
         replay_query_call(qs, plan, static_cast<int>(qi), events, ev_cnt, fr.hits, fr.hit_stride,
                           fr.n_hits);
