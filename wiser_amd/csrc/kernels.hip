@@ -1568,6 +1568,49 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
   v1 = __builtin_amdgcn_alignbit(up ? w2 : w1, up ? w1 : w0, s2 & 31u) & mask;
 }
 
+// Coalesced form of pair_words (the lean pipeline): lane l loads dwords 2l and
+// 2l+1 of the pack's dword-aligned span, and only the lanes the pack reaches
+// (16 b + 8 bytes: the pack, its misalignment and the third word of the last
+// pair), so the load touches the pack's few lines once instead of 64
+// overlapping 12-byte gathers.  pick_words then hands each lane the three
+// words of its pair through the LDS crossbar (ds_bpermute, no LDS storage).
+// Widths up to 31 (a doc-id gap or tf of 2^31 or more never occurs: doc ids
+// and tfs are below 2^32 and deltas below the doc count).
+// Measured slower than the 12-byte gathers (main leg 25.3 M against 26.4 M
+// q/s, profiles/r02_sb_ab.txt): the eight ds_bpermute per block cost more than
+// the vector-memory work they save, so it is off (-DWSR_COALESCED_WORDS=1).
+#ifndef WSR_COALESCED_WORDS
+#define WSR_COALESCED_WORDS 0
+#endif
+#ifndef WSR_FLOOR_REFRESH   // driver blocks between floor refreshes (0: floor read once per item)
+#define WSR_FLOOR_REFRESH 0
+#endif
+__device__ __forceinline__ void pack_dwords(const uint8_t* d, uint32_t b, uint32_t l, uint32_t& r0,
+                                            uint32_t& r1) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(d, 4));
+  r0 = 0;
+  r1 = 0;
+  if (8 * l < 16 * b + 8) {
+    r0 = w[2 * l];
+    r1 = w[2 * l + 1];
+  }
+}
+
+// the words (w0, w1, w2) of the pair at bit offset bitpos of the span
+__device__ __forceinline__ void pick_words(uint32_t r0, uint32_t r1, uint32_t bitpos, uint32_t& w0,
+                                           uint32_t& w1, uint32_t& w2) {
+  const uint32_t i0 = bitpos >> 5;
+  const int src = static_cast<int>(i0 >> 1) << 2;
+  const uint32_t a0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r0)));
+  const uint32_t a1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r1)));
+  const uint32_t c0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src + 4, static_cast<int>(r0)));
+  const uint32_t c1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src + 4, static_cast<int>(r1)));
+  const bool odd = i0 & 1u;
+  w0 = odd ? a1 : a0;
+  w1 = odd ? c0 : a1;
+  w2 = odd ? c1 : c0;
+}
+
 // Segment of an item whose other lists all carry rank bitmaps (the common
 // case: a short driver against long lists).  The driver's blocks stream
 // through a software pipeline, one block per stage and iteration j:
@@ -1656,9 +1699,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   // here; the segment's own k-th best is published once, at the end; events
   // stay in LDS until 64 are pending (a chunk adds at most 64).  The final
   // re-filter in finish_item applies the floor as it stands at the end.
-  const uint64_t floor_bits =
+  uint64_t floor_bits =
       prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
   double pub_val = 0.0;
+#if WSR_FLOOR_REFRESH
+  // Floor refresh (every WSR_FLOOR_REFRESH driver blocks): the item publishes
+  // its floor as it stands (the k-th best of docs before the next item) and
+  // reads the previous item's, so the items of one query, which run at once,
+  // hand their thresholds down the chain while they run instead of at their
+  // ends.  The load is issued just before a block's pack loads, which the next
+  // iteration waits for anyway, and consumed one refresh later.
+  uint64_t floor_next = floor_bits;
+  double sent = 0.0;
+#endif
   // Pre-probe pruning.  A driver posting whose score bound -- its own term,
   // exact, plus QueryDesc's bound of the other terms at its doc length -- is
   // <= the threshold known so far, max(the floor of the query's earlier items,
@@ -1822,6 +1875,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 
   };
   Regs R0, R1;
+#if !WSR_COALESCED_WORDS
   // byte shift of a pair's first value inside its aligned dword (pair_words)
   auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
     const uint32_t bit = 2 * l * bits;
@@ -1829,22 +1883,56 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                        (bit >> 3);
     return ((a & 3u) << 3) + (bit & 7u);
   };
+#endif
   const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
     const uint32_t m = uni(S.dmeta[bi]);
     const uint4 e = S.dblk[bi];
-    uint32_t sh;
     // (VInts tail: width 0 -> a harmless dummy read)
+#if WSR_COALESCED_WORDS
+    pack_dwords(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1);
+#else
+    uint32_t sh;
     pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
+#endif
     // its doc-length codes (postings 2l, 2l+1: one line per block, plen) and
     // driver tfs, so that D can bound each posting's score before the probe
     Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
+#if WSR_COALESCED_WORDS
+    pack_dwords(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1);
+#else
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1, Y.wt2, sh);
+#endif
+  };
+  // the bit offset of lane l's pair in its pack's dword-aligned span
+  auto span_bit = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
+    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + rel + 2;
+    return ((a & 3u) << 3) + 2 * l * bits;
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     LT0()
+#if WSR_FLOOR_REFRESH
+    if (((j - b0) % WSR_FLOOR_REFRESH) == WSR_FLOOR_REFRESH - 1 && !wide) {
+      const uint64_t fb = (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_next >> 32))) << 32) |
+                          uni(static_cast<uint32_t>(floor_next));
+      if (fb > floor_bits) {
+        floor_bits = fb;
+#ifndef WSR_NO_PRUNE
+        const float t = static_cast<float>(__longlong_as_double(static_cast<long long>(fb))) * kPruneMargin;
+        thr_s = t > thr_s ? t : thr_s;
+#endif
+      }
+      if (my_pub && pub_val > sent) {
+        if (l == 0)
+          __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sent = pub_val;
+      }
+      if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     // W(j+1): the doc-id words of block j+1
     issue_words(j + 1, Y);
     LT(0)
@@ -1916,7 +2004,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
       const uint32_t cnt = live ? ((j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
+#if WSR_COALESCED_WORDS
+      uint32_t pw0, pw1, pw2;
+      const uint32_t bp = span_bit(uni(be.z), wbits);
+      pick_words(X.w0, X.w1, bp, pw0, pw1, pw2);
+      pair_values(pw0, pw1, pw2, bp & 31u, wbits, x0, x1);
+#else
       pair_values(X.w0, X.w1, X.w2, pair_shift(uni(be.z), wbits), wbits, x0, x1);
+#endif
       const uint32_t sm = x0 + x1;
       const uint32_t inc = wave_incl_scan(sm);
       uint32_t a0 = prev + (inc - sm) + x0;
@@ -1926,7 +2021,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
       const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
       uint32_t t0, t1;
+#if WSR_COALESCED_WORDS
+      const uint32_t tp = span_bit(uni(be.w), wtb);
+      pick_words(X.wt0, X.wt1, tp, pw0, pw1, pw2);
+      pair_values(pw0, pw1, pw2, tp & 31u, wtb, t0, t1);
+#else
       pair_values(X.wt0, X.wt1, X.wt2, pair_shift(uni(be.w), wtb), wtb, t0, t1);
+#endif
       if (tl) { t0 = ttf0; t1 = ttf1; }
       const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
       const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
