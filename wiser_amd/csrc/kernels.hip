@@ -1582,8 +1582,12 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 #ifndef WSR_COALESCED_WORDS
 #define WSR_COALESCED_WORDS 0
 #endif
-#ifndef WSR_FLOOR_REFRESH   // driver blocks between floor refreshes (0: floor read once per item)
-#define WSR_FLOOR_REFRESH 0
+// driver blocks between floor refreshes (0: floor read once per item).  At 8:
+// events per 4,096 C2 queries 160 k -> 98 k (high x high 584 k -> 356 k), the
+// most events of one query 3,378 -> 1,111, main leg 26.37 -> 26.53 M q/s
+// (4 is no better; profiles/r02_sc_ab.txt)
+#ifndef WSR_FLOOR_REFRESH
+#define WSR_FLOOR_REFRESH 8
 #endif
 __device__ __forceinline__ void pack_dwords(const uint8_t* d, uint32_t b, uint32_t l, uint32_t& r0,
                                             uint32_t& r1) {
@@ -1970,8 +1974,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     {
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
-      const bool h0 = X.da0 != ~0u && (single || (q0 < span && ((X.de0.y >> s0) & 1u)));
-      const bool h1 = X.da1 != ~0u && (single || (q1 < span && ((X.de1.y >> s1) & 1u)));
+      // (bitwise, not short-circuit: the compiler would branch on each term)
+      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & (((X.de0.y >> s0) & 1u) != 0u)));
+      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & (((X.de1.y >> s1) & 1u) != 0u)));
       const uint32_t x0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
       const uint32_t x1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
       uint32_t w;
@@ -2018,8 +2023,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       uint32_t a1 = a0 + x1;
       const bool tl = live && dtail && j == b1 - 1;
       if (tl) { a0 = tdoc0; a1 = tdoc1; }
-      const bool ok0 = 2 * l < cnt && a0 - lo < hi_rel;
-      const bool ok1 = 2 * l + 1 < cnt && a1 - lo < hi_rel;
+      const bool ok0 = (2 * l < cnt) & (a0 - lo < hi_rel);
+      const bool ok1 = (2 * l + 1 < cnt) & (a1 - lo < hi_rel);
       uint32_t t0, t1;
 #if WSR_COALESCED_WORDS
       const uint32_t tp = span_bit(uni(be.w), wtb);
@@ -2035,8 +2040,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       // (branch-free: the bound of a lane past the block is computed and dropped)
       const bool p0 = ok0 & (bound(t0, c0) > thr_s);
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
-      const bool in0 = !single && p0 && a0 - lo < span;
-      const bool in1 = !single && p1 && a1 - lo < span;
+      const bool in0 = !single & p0 & (a0 - lo < span);
+      const bool in1 = !single & p1 & (a1 - lo < span);
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
       Y.dcc = c0 | (c1 << 8);
@@ -2044,7 +2049,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       Y.da0 = p0 ? a0 : ~0u; Y.da1 = p1 ? a1 : ~0u;
       if (live) ++n_dblk;
       // past the smallest last doc of the other lists nothing later can match
-      if (live && __ballot((ok0 && a0 > min_last) || (ok1 && a1 > min_last))) bend = j + 1;
+      const uint64_t past = __ballot((ok0 & (a0 > min_last)) | (ok1 & (a1 > min_last)));
+      if (live & (past != 0)) bend = j + 1;
     }
     LT(3)
   };
