@@ -1586,6 +1586,14 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // events per 4,096 C2 queries 160 k -> 98 k (high x high 584 k -> 356 k), the
 // most events of one query 3,378 -> 1,111, main leg 26.37 -> 26.53 M q/s
 // (4 is no better; profiles/r02_sc_ab.txt)
+// Gathers of the bitmap probe and of O1's tf bytes only on the lanes that need
+// them (exec-masked) instead of every lane reading a dummy word
+#ifndef WSR_MASKED_GATHERS
+#define WSR_MASKED_GATHERS 0
+#endif
+#ifndef WSR_OOB_GATHERS
+#define WSR_OOB_GATHERS 0
+#endif
 #ifndef WSR_FLOOR_REFRESH
 #define WSR_FLOOR_REFRESH 8
 #endif
@@ -1889,6 +1897,17 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   };
 #endif
   const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
+#if WSR_OOB_GATHERS
+  // Buffer views of O1's bitmap and tf bytes: a lane with nothing to fetch
+  // gives an offset past the view's end, so its load returns 0 without a
+  // memory access (the wave's other lanes still load; no branch, no exec
+  // change, so the pipeline's wait counts are the same on every path).
+  constexpr uint32_t kOob = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t r_bm =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(o_bm), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_tf8 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(__builtin_align_down(o_tf8, 4)), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
+#endif
 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
@@ -1983,8 +2002,18 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #ifdef WSR_DIAG_NO_TF8   // timing diagnostic only (wrong tfs): no O1 tf gathers
       Y.hf0 = 0x01010101u; Y.hf1 = 0x01010101u; (void)w;
 #else
+#if WSR_OOB_GATHERS
+      (void)w;
+      Y.hf0 = __builtin_amdgcn_raw_buffer_load_b32(r_tf8, (h0 & !single) ? ((x0 + tf8_mis) & ~3u) : kOob, 0, 0);
+      Y.hf1 = __builtin_amdgcn_raw_buffer_load_b32(r_tf8, (h1 & !single) ? ((x1 + tf8_mis) & ~3u) : kOob, 0, 0);
+#elif WSR_MASKED_GATHERS
+      // (only the hits' lanes gather: the others keep a stale word, never read)
+      if (h0 & !single) Y.hf0 = byte_word(o_tf8 + x0, &w);
+      if (h1 & !single) Y.hf1 = byte_word(o_tf8 + x1, &w);
+#else
       Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? x0 : 0u), &w);
       Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? x1 : 0u), &w);
+#endif
 #endif
       // (ranks are < 2^31; a single-term item's are unused)
       Y.hx0 = h0 ? (x0 & 0x7FFFFFFFu) : 0x80000000u;
@@ -2042,8 +2071,22 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
+#if WSR_OOB_GATHERS
+      {
+        const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in0 ? ((a0 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
+        const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in1 ? ((a1 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
+        Y.de0 = make_uint2(v0[0], v0[1]);
+        Y.de1 = make_uint2(v1[0], v1[1]);
+      }
+#elif WSR_MASKED_GATHERS
+      // (only the postings that passed the bound probe: a pruned lane keeps a
+      // stale word, which H never reads -- its doc is ~0u or outside the span)
+      if (in0) Y.de0 = o_bm[(a0 - lo) / kDenseDocs];
+      if (in1) Y.de1 = o_bm[(a1 - lo) / kDenseDocs];
+#else
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
+#endif
       Y.dcc = c0 | (c1 << 8);
       Y.dt0 = t0; Y.dt1 = t1;
       Y.da0 = p0 ? a0 : ~0u; Y.da1 = p1 ? a1 : ~0u;
