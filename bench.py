@@ -867,6 +867,7 @@ def main():
     # every batch ran there (replicas), else one batch at a time
     iso_ms = acc["seg"] / nbk
     seg_avg_ms = DIAG.get("timed_seg_ms", iso_ms)
+    seg_src = "timed region" if "timed_seg_ms" in DIAG else "one batch at a time"
     lean_avg_ms = DIAG.get("timed_lean_ms", acc["lean"] / nbk)
     achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
     if dist:
@@ -950,8 +951,7 @@ def main():
                          "kernel": "lean_kernel||segment_kernel",
                          "algo_bytes_per_launch": int(acc["algo"] / nbk),
                          "avg_launch_ms": round(seg_avg_ms, 4),
-                         "launch_ms_source": ("timed region" if "timed_seg_ms" in DIAG
-                                              else "one batch at a time"),
+                         "launch_ms_source": seg_src,
                          "lean_kernel_ms": round(lean_avg_ms, 4),
                          "isolated_launch_ms": round(iso_ms, 4),
                          "isolated_frac": round((acc["algo"] / nbk) / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
