@@ -929,7 +929,14 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
   // through the term index (VacuumInvertedIndex::FindIteratorsSolid,
   // vacuum_engine.h:89-99)
   int32_t n = 0;
-  std::string term;
+  // the terms are parsed first and looked up together (find_many: the
+  // dictionary's cache misses overlap)
+  std::vector<const char*> tp;
+  std::vector<uint32_t> tn;
+  std::vector<int32_t*> dst;
+  tp.reserve(static_cast<size_t>(max_q) * 2);
+  tn.reserve(static_cast<size_t>(max_q) * 2);
+  dst.reserve(static_cast<size_t>(max_q) * 2);
   for (int64_t at = 0; at < len;) {
     int64_t e = at;
     while (e < len && text[e] != '\n') ++e;
@@ -950,14 +957,18 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
       if (j > i) {
         if (w.n_terms >= WSR_MAX_TERMS)
           return fail(WSR_E_LIMIT, "query " + std::to_string(n) + ": more than WSR_MAX_TERMS terms");
-        term.assign(text + i, static_cast<size_t>(j - i));
-        w.list_ids[w.n_terms++] = h->idx.find(term);
+        tp.push_back(text + i);
+        tn.push_back(static_cast<uint32_t>(j - i));
+        dst.push_back(&w.list_ids[w.n_terms++]);
       }
       i = j;
     }
     for (int t = w.n_terms; t < WSR_MAX_TERMS; ++t) w.list_ids[t] = -1;
     ++n;
   }
+  std::vector<int32_t> ids(tp.size());
+  h->idx.find_many(tp.data(), tn.data(), tp.size(), ids.data());
+  for (size_t i = 0; i < ids.size(); ++i) *dst[i] = ids[i];
   *nq_out = n;
   return WSR_OK;
 }

@@ -24,9 +24,83 @@ VacuumIndex::~VacuumIndex() {
   if (map_) ::munmap(map_, map_len_);
 }
 
-int32_t VacuumIndex::find(const std::string& term) const {
-  auto it = lookup_.find(term);
-  return it == lookup_.end() ? -1 : it->second;
+namespace {
+// FNV-1a, 64-bit
+inline uint64_t term_hash(const char* p, size_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<uint8_t>(p[i])) * 0x100000001b3ull;
+  return h ^ (h >> 29);
+}
+inline bool same(const std::string& t, const char* p, size_t n) {
+  return t.size() == n && std::memcmp(t.data(), p, n) == 0;
+}
+}  // namespace
+
+int32_t VacuumIndex::find(const std::string& term) const { return find(term.data(), term.size()); }
+
+int32_t VacuumIndex::find(const char* p, size_t n) const {
+  if (tslot_.empty()) return -1;
+  const uint64_t h = term_hash(p, n);
+  const uint32_t tag = static_cast<uint32_t>(h >> 32);
+  for (uint64_t i = h & tmask_;; i = (i + 1) & tmask_) {
+    const uint64_t e = tslot_[i];
+    if (e == 0) return -1;
+    if (static_cast<uint32_t>(e >> 32) == tag) {
+      const int32_t id = static_cast<int32_t>(static_cast<uint32_t>(e)) - 1;
+      if (same(terms_[id], p, n)) return id;
+    }
+  }
+}
+
+void VacuumIndex::find_many(const char* const* p, const uint32_t* n, size_t cnt, int32_t* out) const {
+  if (tslot_.empty()) {
+    for (size_t i = 0; i < cnt; ++i) out[i] = -1;
+    return;
+  }
+  constexpr size_t G = 32;
+  uint64_t h[G];
+  int32_t cand[G];
+  for (size_t g0 = 0; g0 < cnt; g0 += G) {
+    const size_t m = std::min(G, cnt - g0);
+    for (size_t i = 0; i < m; ++i) {   // hashes; prefetch the home slots
+      h[i] = term_hash(p[g0 + i], n[g0 + i]);
+      __builtin_prefetch(&tslot_[h[i] & tmask_]);
+    }
+    for (size_t i = 0; i < m; ++i) {   // first tag match; prefetch its string
+      const uint32_t tag = static_cast<uint32_t>(h[i] >> 32);
+      cand[i] = -1;
+      for (uint64_t s = h[i] & tmask_;; s = (s + 1) & tmask_) {
+        const uint64_t e = tslot_[s];
+        if (e == 0) break;
+        if (static_cast<uint32_t>(e >> 32) == tag) {
+          cand[i] = static_cast<int32_t>(static_cast<uint32_t>(e)) - 1;
+          __builtin_prefetch(&terms_[cand[i]]);
+          break;
+        }
+      }
+    }
+    for (size_t i = 0; i < m; ++i) {   // confirm (a tag collision falls back to the full probe)
+      const int32_t c = cand[i];
+      out[g0 + i] = (c >= 0 && same(terms_[c], p[g0 + i], n[g0 + i])) ? c
+                    : (c < 0 ? -1 : find(p[g0 + i], n[g0 + i]));
+    }
+  }
+}
+
+int32_t VacuumIndex::insert_term(const char* p, size_t n, int32_t id) {
+  const uint64_t h = term_hash(p, n);
+  const uint32_t tag = static_cast<uint32_t>(h >> 32);
+  for (uint64_t i = h & tmask_;; i = (i + 1) & tmask_) {
+    const uint64_t e = tslot_[i];
+    if (e == 0) {
+      tslot_[i] = (static_cast<uint64_t>(tag) << 32) | static_cast<uint32_t>(id + 1);
+      return id;
+    }
+    if (static_cast<uint32_t>(e >> 32) == tag) {
+      const int32_t old = static_cast<int32_t>(static_cast<uint32_t>(e)) - 1;
+      if (same(terms_[old], p, n)) return old;
+    }
+  }
 }
 
 void VacuumIndex::open(const std::string& dir) {
@@ -137,21 +211,25 @@ void VacuumIndex::open(const std::string& dir) {
         throw std::runtime_error("posting list of '" + all.substr(ents[bad].at, ents[bad].len) +
                                  "' has a wrong magic byte or a bad doc freq");
     }
-    lookup_.reserve(ents.size());
+    uint64_t cap = 16;
+    while (cap < 2 * ents.size()) cap <<= 1;
+    tslot_.assign(cap, 0);
+    tmask_ = cap - 1;
     terms_.reserve(ents.size());
     off_.reserve(ents.size());
     df_.reserve(ents.size());
     for (const Ent& e : ents) {
-      std::string term = all.substr(e.at, e.len);
       const uint64_t off = e.off, df = e.df;
-      auto ins = lookup_.emplace(term, static_cast<int32_t>(terms_.size()));
-      if (!ins.second) { // later entries win, as htrie_map assignment does
-        const int32_t id = ins.first->second;
+      const int32_t next = static_cast<int32_t>(terms_.size());
+      // (the candidate string must be in terms_ for the table's compare)
+      terms_.emplace_back(all, e.at, e.len);
+      const int32_t id = insert_term(terms_.back().data(), terms_.back().size(), next);
+      if (id != next) { // later entries win, as htrie_map assignment does
+        terms_.pop_back();
         off_[id] = off;
         df_[id] = static_cast<uint32_t>(df);
         continue;
       }
-      terms_.push_back(term);
       off_.push_back(off);
       df_.push_back(static_cast<uint32_t>(df));
     }

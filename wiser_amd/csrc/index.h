@@ -45,6 +45,11 @@ class VacuumIndex {
 
   int32_t n_lists() const { return static_cast<int32_t>(terms_.size()); }
   int32_t find(const std::string& term) const;  // -1 when absent
+  int32_t find(const char* p, size_t n) const;
+  // n terms at once (the batch path): hashes first, then the table slots and
+  // the candidate strings prefetched a group at a time, so the lookups' cache
+  // misses overlap instead of running one after another
+  void find_many(const char* const* p, const uint32_t* n, size_t cnt, int32_t* out) const;
   const std::string& term(int32_t id) const { return terms_[id]; }
   uint32_t df(int32_t id) const { return df_[id]; }
   uint64_t list_offset(int32_t id) const { return off_[id]; }
@@ -65,7 +70,13 @@ class VacuumIndex {
 
  private:
   std::vector<std::string> terms_;
-  std::unordered_map<std::string, int32_t> lookup_;
+  // term -> id: open addressing, linear probing, one 8-byte slot per entry
+  // (high half: the hash's high 32 bits, low half: id + 1; 0 = empty), at most
+  // half full.  (A std::unordered_map lookup costs two dependent cache misses;
+  // this one, one for the slot and one for the string compare.)
+  std::vector<uint64_t> tslot_;
+  uint64_t tmask_ = 0;
+  int32_t insert_term(const char* p, size_t n, int32_t id);   // existing id, or id when new
   std::vector<uint64_t> off_;
   std::vector<uint32_t> df_;
   std::vector<double> idf_;
