@@ -92,6 +92,11 @@ def parse():
                         "rank's full-index image (0: every query is sharded; -1, the default: "
                         "max(64, 63 * N), so that each shard's part of a sharded query is at "
                         "least one full work item)")
+    p.add_argument("--shard-every", type=int, default=0,
+                   help="N>1 shards: the heavy queries of this many consecutive steps go through "
+                        "one sharded step (a heavy batch every that many steps; 0, the default: "
+                        "enough steps for about 1024 heavy queries per rank, at most the log's "
+                        "batches)")
     return p.parse_args()
 
 
@@ -649,21 +654,39 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
             ds.append(df[x])
         return bool(ds) and min(ds) > 0 and min(math.ceil(d / 128) for d in ds) >= heavy_blocks
 
+    # Heavy queries of `every` consecutive steps go through one sharded step (at
+    # the first step of the group): a sharded step has a large fixed host cost
+    # (its own plan and segment launches, the RCCL call, the owner replay), so
+    # with few heavy queries per step (0.7 % of the log at N = 8) a step per
+    # batch makes the loop host-bound (profiles/r02_sm_shard_every.txt: 0.22 ms
+    # of host time per 0.15 ms step); grouped, heavy batches keep ~1024 queries
+    # per rank and the light batches run every step.
+    def heavy_of(j, g):
+        chunk = lines[g * per_rank + j * B: g * per_rank + (j + 1) * B]
+        return [q for q in chunk if is_heavy(q)]
+    every = a.shard_every
+    if every <= 0:
+        per_step = max(1, sum(len(heavy_of(j, rank)) for j in range(nb)) // nb)
+        every = max(1, min(nb, -(-1024 // per_step)))
+        if dist is not None:   # one cadence for every rank (the collective pairs up)
+            ev = torch.tensor([float(every)])
+            dist.all_reduce(ev, op=dist.ReduceOp.MAX)
+            every = int(ev.item())
+    every = max(1, min(every, nb))
     # every rank builds the same global heavy batches from the same log split
     steps = []   # per batch index: (heavy ResidentBatch or None, q_per_owner, heavy chunk,
                  #                   cheap ResidentBatch or None, cheap chunk)
     for j in range(nb):
-        parts = []
-        for g in range(world):
-            chunk = lines[g * per_rank + j * B: g * per_rank + (j + 1) * B]
-            parts.append([q for q in chunk if is_heavy(q)])
-        hq = max(len(p) for p in parts)
-        hb, hchunk = None, []
-        if hq:
-            for p in parts:
-                hchunk += p + [[]] * (hq - len(p))   # (an empty query: an empty result)
-            hb = w.ResidentBatch(S.engine, hq * world, a.k)
-            hb.upload(resolve(S.engine, hchunk, a.k))
+        hb, hq, hchunk = None, 0, []
+        if j % every == 0:
+            group = range(j, min(nb, j + every))
+            parts = [sum((heavy_of(jj, g) for jj in group), []) for g in range(world)]
+            hq = max(len(p) for p in parts)
+            if hq:
+                for p in parts:
+                    hchunk += p + [[]] * (hq - len(p))   # (an empty query: an empty result)
+                hb = w.ResidentBatch(S.engine, hq * world, a.k)
+                hb.upload(resolve(S.engine, hchunk, a.k))
         mine = lines[rank * per_rank + j * B: rank * per_rank + (j + 1) * B]
         cheap = [q for q in mine if not is_heavy(q)]
         cb = None
@@ -739,6 +762,7 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
     S.slot = slot
     S.heavy_share = sum(st[1] for st in steps) / max(1, nb * B)
     S.heavy_blocks = heavy_blocks
+    S.every = every
     batches = [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]]
     eng = full if (full and any(st[3] for st in steps)) else S.engine
 
@@ -746,6 +770,7 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         slot = S.slot
         heavy_share = S.heavy_share
         heavy_blocks = S.heavy_blocks
+        every = S.every
 
         def close(self):
             for hb, _, _, cb, _ in steps:
@@ -976,6 +1001,7 @@ def main():
             out["exchange"] = {"kind": kind,
                                "slot_events": getattr(S, "slot", None),
                                "heavy_blocks": getattr(S, "heavy_blocks", None),
+                               "shard_every": getattr(S, "every", None),
                                "heavy_query_share": round(getattr(S, "heavy_share", 0.0), 4)}
         if control:
             out["control"] = control
