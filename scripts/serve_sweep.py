@@ -13,7 +13,7 @@ lines = [l.split() for l in open(os.path.join(idx, "two_term_100000.log")).read(
 arr = (_capi.Query * len(lines))()
 for i, t in enumerate(lines):
     arr[i] = eng.resolve(w.SearchQuery(t, n_results=10))[0]
-for c, d, win in [(16, 256, 1000), (16, 256, 200), (8, 512, 1000), (4, 1024, 1000), (16, 16, 50), (4, 64, 100)]:
+for c, d, win in [(4, 1024, 1000), (4, 1024, 500), (4, 1024, 250), (4, 1024, 100), (4, 2048, 250), (8, 512, 250), (4, 64, 100), (4, 64, 30)]:
     srv = w.Server(eng, max_batch=4096, window_us=win)
     st = srv.bench(arr, n_clients=c, depth=d, seconds=2.0)
     srv.close()

@@ -9,8 +9,9 @@
 // On the GPU one query is far too little work, so the dispatcher thread here
 // collects requests for a short window (or until a batch is full), runs them
 // as one resident batch (wsr_batch_*), and hands each caller its own entries.
-// Two batches alternate, so the next batch is collected and uploaded while the
-// previous one runs.
+// Up to four batches are in flight: the dispatcher collects, uploads and
+// launches, a completer thread retires them in launch order and hands out the
+// results, so the next batch is launched while earlier ones run and return.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -78,24 +79,34 @@ struct Slot {
 }  // namespace
 
 struct wsr_server {
+  // batches in flight at once: the dispatcher fills and launches, a completer
+  // thread retires them in launch order, so launching never waits for a
+  // result hand-off
+  static constexpr int kSlots = 4;
   wsr_handle* h = nullptr;
   int max_batch = 4096;
   std::chrono::microseconds window{200};
-  std::mutex mu;
-  std::condition_variable cv_work;   // dispatcher: requests arrived / stop
+  std::mutex mu;                     // queue, slot states, stop, idle
+  std::condition_variable cv_work;   // dispatcher: requests arrived / a slot freed / stop
   std::deque<Req*> queue;
   bool stop = false;
-  bool idle = false;                 // dispatcher asleep on cv_work (no batch in flight)
-  std::thread worker;
-  Slot slots[2];
-  // fetch buffers of one batch, page-locked so the result copies are DMA'd
+  bool idle = false;                 // dispatcher asleep on cv_work with nothing to launch
+  int n_busy = 0;
+  std::thread worker, completer;
+  Slot slots[kSlots];
+  std::mutex fmu;                    // the launched batches, oldest first
+  std::condition_variable cv_done;
+  std::deque<Slot*> inflight;
+  bool fstop = false;
+  // fetch buffers of one batch (completer only), page-locked so the result
+  // copies are DMA'd
   wsr_hit* hits = nullptr;
   int32_t* nh = nullptr;
-  std::vector<wsr_query> qbuf;
+  std::vector<wsr_query> qbuf;       // dispatcher only
   std::atomic<uint64_t> batches{0}, queries{0};
 
   void complete(Slot& s) {
-    int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
+    int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);   // (waits for the batch)
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
       r->rc = rc;
@@ -107,56 +118,70 @@ struct wsr_server {
       r->signal();
     }
     s.reqs.clear();
-    s.busy = false;
   }
 
-  // Dispatch policy: with the GPU idle, whatever is queued runs at once (the
-  // latency of a lone query is one batch); with one batch running, the next
-  // fills until max_batch or until its oldest request has waited `window`,
-  // then runs beside it; with two running, the older one is completed first.
+  // Completer: retires launched batches in order and frees their slots.
+  void retire() {
+    for (;;) {
+      Slot* s = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(fmu);
+        cv_done.wait(lk, [&] { return !inflight.empty() || fstop; });
+        if (inflight.empty()) return;
+        s = inflight.front();
+        inflight.pop_front();
+      }
+      complete(*s);
+      bool wake;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        s->busy = false;
+        --n_busy;
+        wake = idle;
+      }
+      if (wake) cv_work.notify_one();
+    }
+  }
+
+  // Dispatch policy: with no batch in flight, whatever is queued runs at once
+  // (the latency of a lone query is one batch); with batches in flight, the
+  // next one fills until max_batch or until its oldest request has waited
+  // `window`; with every slot in flight, it waits for the completer.
   void run() {
     uint64_t seq = 0;
     for (;;) {
-      for (auto& s : slots)   // retire finished batches, oldest first (a HIP error
-        if (s.busy && wsr_batch_ready(h, s.b) != 0) complete(s);   // too: the fetch reports it)
-      Slot* oldest = nullptr;
-      int n_busy = 0;
-      for (auto& s : slots)
-        if (s.busy) { ++n_busy; if (!oldest || s.seq < oldest->seq) oldest = &s; }
       std::vector<Req*> take;
+      Slot* slot = nullptr;
       {
         std::unique_lock<std::mutex> lk(mu);
-        if (queue.empty()) {
-          if (stop && !n_busy) break;
-          if (n_busy) {
-            lk.unlock();
-            std::this_thread::sleep_for(std::chrono::microseconds(10));
-          } else if (!stop) {
-            idle = true;
-            cv_work.wait(lk);
-            idle = false;
+        for (;;) {
+          if (queue.empty() && stop) break;
+          if (!queue.empty() && n_busy < kSlots) {
+            if (n_busy > 0 && !stop && static_cast<int>(queue.size()) < max_batch) {
+              const auto due = queue.front()->t_enq + window;
+              if (Clock::now() < due) {   // (submit wakes us early when the batch fills)
+                idle = true;
+                cv_work.wait_until(lk, due);
+                idle = false;
+                continue;
+              }
+            }
+            break;
           }
-          continue;
+          idle = true;
+          cv_work.wait(lk);
+          idle = false;
         }
-        if (n_busy == 2) {
-          lk.unlock();
-          complete(*oldest);
-          continue;
-        }
-        if (n_busy == 1 && !stop && static_cast<int>(queue.size()) < max_batch) {
-          const auto due = queue.front()->t_enq + window;
-          const auto now = Clock::now();
-          if (now < due) {
-            lk.unlock();
-            std::this_thread::sleep_for(std::min<Clock::duration>(due - now, std::chrono::microseconds(10)));
-            continue;
-          }
-        }
+        if (queue.empty()) break;   // stop, and everything was launched
         const size_t n = std::min<size_t>(queue.size(), static_cast<size_t>(max_batch));
         take.assign(queue.begin(), queue.begin() + static_cast<long>(n));
         queue.erase(queue.begin(), queue.begin() + static_cast<long>(n));
+        for (auto& sl : slots)
+          if (!sl.busy) { slot = &sl; break; }
+        slot->busy = true;
+        ++n_busy;
       }
-      Slot& s = slots[0].busy ? slots[1] : slots[0];
+      Slot& s = *slot;
       qbuf.resize(take.size());
       s.kmax = 1;
       for (size_t i = 0; i < take.size(); ++i) {
@@ -173,16 +198,26 @@ struct wsr_server {
           r->rc = wsr_search_batch(h, &r->q, 1, std::max(1, r->q.k), r->out, r->n_out);
           r->signal();
         }
+        std::lock_guard<std::mutex> g(mu);
+        s.busy = false;
+        --n_busy;
         continue;
       }
       s.reqs = std::move(take);
-      s.busy = true;
       s.seq = ++seq;
       ++batches;
       queries += s.reqs.size();
+      {
+        std::lock_guard<std::mutex> g(fmu);
+        inflight.push_back(&s);
+      }
+      cv_done.notify_one();
     }
-    for (auto& s : slots)
-      if (s.busy) complete(s);
+    {
+      std::lock_guard<std::mutex> g(fmu);
+      fstop = true;   // the completer drains what is in flight, then ends
+    }
+    cv_done.notify_one();
   }
 
   int submit(Req* r) {
@@ -197,7 +232,9 @@ struct wsr_server {
       std::lock_guard<std::mutex> g(mu);
       if (stop) return WSR_E_INVALID;
       queue.push_back(r);
-      wake = idle;   // the dispatcher sleeps only with no batch in flight
+      // the dispatcher sleeps with nothing to launch, or until a window ends:
+      // wake it for the first request, or when a batch is full
+      wake = idle && (queue.size() == 1 || static_cast<int>(queue.size()) == max_batch);
     }
     if (wake) cv_work.notify_one();
     return WSR_OK;
@@ -236,6 +273,7 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
     return WSR_E_HIP;
   }
   s->worker = std::thread([p = s.get()] { p->run(); });
+  s->completer = std::thread([p = s.get()] { p->retire(); });
   *out = s.release();
   return WSR_OK;
 }
@@ -247,7 +285,8 @@ void wsr_server_close(wsr_server* s) {
     s->stop = true;
   }
   s->cv_work.notify_all();
-  if (s->worker.joinable()) s->worker.join();
+  if (s->worker.joinable()) s->worker.join();         // launches what is queued, then stops the completer
+  if (s->completer.joinable()) s->completer.join();   // retires what is in flight
   for (auto& sl : s->slots)
     if (sl.b) wsr_batch_destroy(s->h, sl.b);
   if (s->hits) (void)hipHostFree(s->hits);
