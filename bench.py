@@ -555,7 +555,7 @@ def serving_leg(a, idx, local, threads):
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
     out = {}
-    for clients, depth, window in ((4, 1024, 1000), (8, 1024, 1000), (4, 64, 100)):
+    for clients, depth, window in ((4, 1024, 1000), (4, 64, 100)):
         srv = w.Server(eng, max_batch=a.batch, window_us=window)
         st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
         srv.close()
