@@ -1594,6 +1594,9 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 #ifndef WSR_OOB_GATHERS
 #define WSR_OOB_GATHERS 0
 #endif
+#ifndef WSR_BOUND_NO_RCP   // the pre-probe bound compared without the own term's reciprocal
+#define WSR_BOUND_NO_RCP 0
+#endif
 #ifndef WSR_FLOOR_REFRESH
 #define WSR_FLOOR_REFRESH 8
 #endif
@@ -1741,6 +1744,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                      : static_cast<float>(__longlong_as_double(static_cast<long long>(
                            (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
                            uni(static_cast<uint32_t>(floor_bits))))) * kPruneMargin;
+#endif
+#if WSR_BOUND_NO_RCP
+  // passes(t, c) == (bound(t, c) > thr_s) without the own term's reciprocal:
+  // b_id tf / (tf + nf) + o > thr  <=>  b_id tf > (thr - o) (tf + nf), as
+  // tf + nf > 0.  Rounding moves either side by a few f32 ulps of the score
+  // scale, far inside the 0.2 % threshold margin, so a dropped posting's score
+  // is still strictly below the threshold.
+  auto passes = [&](uint32_t t, uint32_t c) __attribute__((always_inline)) {
+    const float nf = static_cast<float>(norm_tab[c]);
+    const float f = static_cast<float>(t);
+    const float o = b_iom * __builtin_amdgcn_rcpf(b_m + nf);
+    return b_id * f > (thr_s - o) * (f + nf);
+  };
 #endif
   auto bound = [&](uint32_t t, uint32_t c) __attribute__((always_inline)) {
     const float nf = static_cast<float>(norm_tab[c]);
@@ -2067,8 +2083,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
       // pre-probe pruning (above): a dropped posting is never probed
       // (branch-free: the bound of a lane past the block is computed and dropped)
+#if WSR_BOUND_NO_RCP
+      const bool p0 = ok0 & passes(t0, c0);
+      const bool p1 = ok1 & passes(t1, c1);
+#else
       const bool p0 = ok0 & (bound(t0, c0) > thr_s);
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
+#endif
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
 #if WSR_OOB_GATHERS
