@@ -106,7 +106,11 @@ struct wsr_server {
   std::atomic<uint64_t> batches{0}, queries{0};
 
   void complete(Slot& s) {
-    int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);   // (waits for the batch)
+    // poll the batch's end event, so the fetch below finds it done (a blocking
+    // wait inside the fetch can sleep through the batch's end and wake late);
+    // a HIP error ends the poll too, and the fetch reports it
+    while (wsr_batch_ready(h, s.b) == 0) std::this_thread::yield();
+    int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
       r->rc = rc;
