@@ -2667,8 +2667,11 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #ifndef WSR_LEAN_WGS
 #define WSR_LEAN_WGS 5
 #endif
+#ifndef WSR_LEAN_WGS_PHRASE
+#define WSR_LEAN_WGS_PHRASE 3
+#endif
 template <bool kPh, bool kAnd>
-__global__ __launch_bounds__(64 * kLeanWaves, WSR_LEAN_WGS) void lean_kernel(
+__global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : WSR_LEAN_WGS) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
@@ -3023,8 +3026,13 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st) {
   // (a persistent grid sized for the conjunctive instance: waves of a larger
   // instance that find no room start later and find the queue drained)
-  if (ph)
+  // (phrase batches: the bitmap-intersection path only when it is on, so the
+  // default phrase instance leaves out its step buffer, as the conjunctive one)
+  if (ph && ix.and_wpb > 0.0f)
     hipLaunchKernelGGL((lean_kernel<true, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
+                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+  else if (ph)
+    hipLaunchKernelGGL((lean_kernel<true, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
                        nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   else if (ix.and_wpb > 0.0f)
     hipLaunchKernelGGL((lean_kernel<false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
