@@ -1945,11 +1945,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1, Y.wt2, sh);
 #endif
   };
+#if WSR_COALESCED_WORDS
   // the bit offset of lane l's pair in its pack's dword-aligned span
   auto span_bit = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
     const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + rel + 2;
     return ((a & 3u) << 3) + 2 * l * bits;
   };
+#endif
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     LT0()
 #if WSR_FLOOR_REFRESH
@@ -2671,7 +2673,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #define WSR_LEAN_WGS_PHRASE 3
 #endif
 template <bool kPh, bool kAnd>
-__global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : WSR_LEAN_WGS) void lean_kernel(
+__global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd ? 4 : WSR_LEAN_WGS)) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
