@@ -1585,7 +1585,8 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // driver blocks between floor refreshes (0: floor read once per item).  At 8:
 // events per 4,096 C2 queries 160 k -> 98 k (high x high 584 k -> 356 k), the
 // most events of one query 3,378 -> 1,111, main leg 26.37 -> 26.53 M q/s
-// (4 is no better; profiles/r02_sc_ab.txt)
+// (4 is no better; profiles/r02_sc_ab.txt; 16 and 32 are within the noise,
+// with 6 % and 21 % more events: profiles/r02_su_refresh_interval_ab.txt)
 // Gathers of the bitmap probe and of O1's tf bytes only on the lanes that need
 // them (exec-masked) instead of every lane reading a dummy word
 #ifndef WSR_MASKED_GATHERS
