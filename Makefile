@@ -20,8 +20,13 @@ ORAFLAGS := -O3 -DNDEBUG -std=c++17 -fPIC -ffp-contract=off -Wall -shared
 
 CLI     := wiser_amd/_lib/engine_cli
 CALIB   := wiser_amd/_lib/calib_ea
+DICT    := wiser_amd/_lib/dict_check
 
-all: $(LIB) $(ORACLE) $(CLI) $(CALIB)
+all: $(LIB) $(ORACLE) $(CLI) $(CALIB) $(DICT)
+
+# CPU check of the term dictionary (tests/test_dictionary.py)
+$(DICT): tests/cpp/dict_check.cc wiser_amd/csrc/index.h $(LIB)
+	$(CXX) -O2 -std=c++17 -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ tests/cpp/dict_check.cc -Lwiser_amd/_lib -lwiser_hip -Wl,-rpath,'$$ORIGIN'
 
 # counter calibration (profiles only): known-byte reads for rocprofv3 --pmc
 $(CALIB): scripts/calib_ea.hip
