@@ -1601,6 +1601,9 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 #ifndef WSR_FLOOR_REFRESH
 #define WSR_FLOOR_REFRESH 8
 #endif
+#ifndef WSR_PUBLISH_EVERY   // driver blocks between publishes (a multiple of WSR_FLOOR_REFRESH)
+#define WSR_PUBLISH_EVERY WSR_FLOOR_REFRESH
+#endif
 __device__ __forceinline__ void pack_dwords(const uint8_t* d, uint32_t b, uint32_t l, uint32_t& r0,
                                             uint32_t& r1) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(d, 4));
@@ -1966,12 +1969,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         thr_s = t > thr_s ? t : thr_s;
 #endif
       }
-      if (my_pub && pub_val > sent) {
+#ifndef WSR_DIAG_NO_PUBLISH   // diagnostic: the refresh reads floors but never publishes
+      if (my_pub && pub_val > sent && ((j - b0) % WSR_PUBLISH_EVERY) == WSR_PUBLISH_EVERY - 1) {
         if (l == 0)
           __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sent = pub_val;
       }
+#endif
       if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
