@@ -1601,6 +1601,9 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 #ifndef WSR_FLOOR_REFRESH
 #define WSR_FLOOR_REFRESH 8
 #endif
+#ifndef WSR_STAGE_ORDER   // 1: the lean pipeline's stages run W, D, C, H instead of W, C, H, D
+#define WSR_STAGE_ORDER 0
+#endif
 #ifndef WSR_PUBLISH_EVERY   // driver blocks between publishes (a multiple of WSR_FLOOR_REFRESH)
 #define WSR_PUBLISH_EVERY WSR_FLOOR_REFRESH
 #endif
@@ -1956,33 +1959,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     return ((a & 3u) << 3) + 2 * l * bits;
   };
 #endif
-  auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    LT0()
-#if WSR_FLOOR_REFRESH
-    if (((j - b0) % WSR_FLOOR_REFRESH) == WSR_FLOOR_REFRESH - 1 && !wide) {
-      const uint64_t fb = (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_next >> 32))) << 32) |
-                          uni(static_cast<uint32_t>(floor_next));
-      if (fb > floor_bits) {
-        floor_bits = fb;
-#ifndef WSR_NO_PRUNE
-        const float t = static_cast<float>(__longlong_as_double(static_cast<long long>(fb))) * kPruneMargin;
-        thr_s = t > thr_s ? t : thr_s;
-#endif
-      }
-#ifndef WSR_DIAG_NO_PUBLISH   // diagnostic: the refresh reads floors but never publishes
-      if (my_pub && pub_val > sent && ((j - b0) % WSR_PUBLISH_EVERY) == WSR_PUBLISH_EVERY - 1) {
-        if (l == 0)
-          __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sent = pub_val;
-      }
-#endif
-      if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
-    // W(j+1): the doc-id words of block j+1
-    issue_words(j + 1, Y);
-    LT(0)
+  auto stage_C = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // C(j-2): compaction of block j-2 (its H fields are in X)
     if (j >= b0 + 2) {
       const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
@@ -2011,7 +1988,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #pragma nounroll
       for (int c = 0; c < 2 && qtail - qhead >= 64; ++c) score_chunk(64);
     }
-    LT(1)
+  };
+  auto stage_H = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // H(j-1): block j-1 (D fields in X): O1 hits, its driver tfs and length
     // codes extracted, into Y's H fields
     {
@@ -2049,7 +2027,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       Y.ht0 = X.dt0;
       Y.ht1 = X.dt1;
     }
-    LT(2)
+  };
+  auto stage_D = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // D(j): decode block j from X's words into Y, issue its loads
     {
       const bool live = j < bend;
@@ -2124,7 +2103,51 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint64_t past = __ballot((ok0 & (a0 > min_last)) | (ok1 & (a1 > min_last)));
       if (live & (past != 0)) bend = j + 1;
     }
+  };
+  auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
+    LT0()
+#if WSR_FLOOR_REFRESH
+    if (((j - b0) % WSR_FLOOR_REFRESH) == WSR_FLOOR_REFRESH - 1 && !wide) {
+      const uint64_t fb = (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_next >> 32))) << 32) |
+                          uni(static_cast<uint32_t>(floor_next));
+      if (fb > floor_bits) {
+        floor_bits = fb;
+#ifndef WSR_NO_PRUNE
+        const float t = static_cast<float>(__longlong_as_double(static_cast<long long>(fb))) * kPruneMargin;
+        thr_s = t > thr_s ? t : thr_s;
+#endif
+      }
+#ifndef WSR_DIAG_NO_PUBLISH   // diagnostic: the refresh reads floors but never publishes
+      if (my_pub && pub_val > sent && ((j - b0) % WSR_PUBLISH_EVERY) == WSR_PUBLISH_EVERY - 1) {
+        if (l == 0)
+          __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sent = pub_val;
+      }
+#endif
+      if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+    // W(j+1): the doc-id words of block j+1
+    issue_words(j + 1, Y);
+    LT(0)
+#if WSR_STAGE_ORDER
+    // (D, C, then H: the probes D issues get almost two iterations before H
+    // reads them, instead of the tail of one)
+    stage_D(X, Y, j);
     LT(3)
+    stage_C(X, Y, j);
+    LT(1)
+    stage_H(X, Y, j);
+    LT(2)
+#else
+    stage_C(X, Y, j);
+    LT(1)
+    stage_H(X, Y, j);
+    LT(2)
+    stage_D(X, Y, j);
+    LT(3)
+#endif
   };
   if (kAnd && and_path) {
     // Bitmap intersection: the segment's doc span, 32 docs per word, one word
