@@ -84,6 +84,7 @@ struct wsr_handle {
   double* d_cache = nullptr;
   DenseEnt* d_dense = nullptr;
   uint8_t* d_tf8 = nullptr;
+  uint8_t* d_wmax = nullptr;
   uint8_t* d_plen = nullptr;
   uint32_t* d_tails = nullptr;
   uint8_t* d_pos_blob = nullptr;    // positions (opened with wsr_open_opts::positions)
@@ -231,12 +232,14 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
       std::vector<uint32_t>().swap(img.pos_start);
     }
     h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
+    h->info.dense_bytes += dev_upload(&h->d_wmax, img.wmax);   // (the window maxima with the bitmaps)
     h->info.tf8_bytes = dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
     h->info.dense_lists = img.dense_lists;
     h->info.n_lists = static_cast<uint32_t>(img.lists.size());
     h->args.dense = h->d_dense;
     h->args.tf8 = h->d_tf8;
+    h->args.wmax = h->d_wmax;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
     h->args.and_wpb = static_cast<float>(env_number("WSR_AND_WPB", 0.0));
@@ -301,6 +304,7 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8),
+                  static_cast<void*>(h->d_wmax),
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),

@@ -33,6 +33,8 @@ constexpr uint64_t kNoTail = ~0ull;
 
 constexpr uint64_t kNoDense = ~0ull;
 constexpr uint32_t kDenseDocs = 32;   // doc ids per DenseEnt
+constexpr uint32_t kWinEnts = 64;     // DenseEnts per tf-maximum window (2,048 docs); every
+                                      // list's bitmap starts at a multiple of it
 constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 
 // Dense lists (df >= span / dense_div) also carry a rank bitmap of their doc

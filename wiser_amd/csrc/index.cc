@@ -356,7 +356,9 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   // doc ids a bitmap covers: the image's range clipped to the doc-length records
   const uint64_t span_end = std::min<uint64_t>(doc_hi, static_cast<uint64_t>(std::max(idx.n_docs(), 0)));
   const uint32_t span = span_end > doc_lo ? static_cast<uint32_t>(span_end - doc_lo) : 0u;
-  const uint64_t n_ent = (static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs;
+  // (whole tf-maximum windows, so that every list's bitmap starts at a multiple of kWinEnts)
+  const uint64_t n_ent = ((static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs + kWinEnts - 1) /
+                         kWinEnts * kWinEnts;
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
   struct Info {            // pass 1: the list's share of the image
     uint32_t r0 = 0, r1 = 0;   // image rows [r0, r1); r0 >= r1: no docs in the image
@@ -513,6 +515,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.tails.resize(ntail);
   img.dense.resize(ne);
   img.tf8.resize(ntf8);
+  img.wmax.resize(ne / kWinEnts);
 
   lap("pass 2 (offsets, allocation)");
   // ---- pass 3: fill in place
@@ -599,6 +602,15 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       }
       uint8_t* t8 = &img.tf8[ld.tf8];
       for (uint64_t j = 0; j < n_img; ++j) t8[j] = static_cast<uint8_t>(s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape);
+      // largest tf per 2,048-doc window (the lean kernel's pre-probe bound)
+      uint8_t* wm = &img.wmax[ld.bm / kWinEnts];
+      std::memset(wm, 0, n_ent / kWinEnts);
+      const uint64_t n_win = n_ent / kWinEnts;
+      for (uint64_t j = 0; j < n_img; ++j) {   // (docs past the span have no bitmap bit either)
+        if (s.docs[j] < doc_lo) continue;
+        const uint64_t wi = (s.docs[j] - doc_lo) / (static_cast<uint64_t>(kDenseDocs) * kWinEnts);
+        if (wi < n_win) wm[wi] = std::max(wm[wi], t8[j]);
+      }
     }
     if (positions) {
       // The list's position cozy box (flash_engine_dumper.h:78-104): the bag of

@@ -119,6 +119,8 @@ struct HostImage {
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
   big_vector<DenseEnt> dense;   // rank bitmaps of the dense lists
   big_vector<uint8_t> tf8;      // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
+  big_vector<uint8_t> wmax;     // per dense list and 2,048-doc window (64 bitmap entries): its
+                                // largest tf, 255 = 255 or more (entry ListDev::bm / 64 + window)
   uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
   uint32_t dense_lists = 0;
   big_vector<uint32_t> tails;   // decoded VInts last blocks (ListDev::tail)

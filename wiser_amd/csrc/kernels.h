@@ -37,6 +37,7 @@ struct IndexArgs {
   const uint2* pos_pk;      // per full pack: byte offset from PosDev::base, bit width
   const uint32_t* pos_tail; // decoded VInts remainders
   const uint32_t* pos_start;// bag start entry of every posting, 128 slots per image block
+  const uint8_t* wmax;      // per dense list and 2,048-doc window: its largest tf (HostImage::wmax)
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,

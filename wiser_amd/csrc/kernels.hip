@@ -528,7 +528,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.b_id = static_cast<float>(2.2 * A.idf);
         D.b_m = mf;
         D.b_iom = static_cast<float>(io * static_cast<double>(mf));
-        D.pad = 0;
+        // bit 0: a two-term lean query, whose other-term bound may use O1's
+        // per-window tf maxima instead of its list maximum (lean_segment)
+        D.pad = (q.n_terms == 2 && o1 < kMaxTerms) ? 1u : 0u;
         desc[i] = D;
       }
     }
@@ -1601,6 +1603,9 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 #ifndef WSR_FLOOR_REFRESH
 #define WSR_FLOOR_REFRESH 8
 #endif
+#ifndef WSR_WIN_BOUND   // the pre-probe bound with O1's per-window tf maxima (two-term queries)
+#define WSR_WIN_BOUND 0
+#endif
 #ifndef WSR_STAGE_ORDER   // 1: the lean pipeline's stages run W, D, C, H instead of W, C, H, D
 #define WSR_STAGE_ORDER 0
 #endif
@@ -1743,7 +1748,26 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   // the threshold carries a 0.2 % margin, far above the bound's rounding, so a
   // dropped posting's f64 score is strictly below the threshold.
   constexpr float kPruneMargin = 0.998f;
-  const float b_id = Q.b_id, b_iom = Q.b_iom, b_m = Q.b_m;
+  const float b_id = Q.b_id;
+  float b_iom = Q.b_iom, b_m = Q.b_m;
+#if WSR_WIN_BOUND
+  // Windowed other-term bound (two-term queries): per driver block, O1's
+  // largest tf over the 2,048-doc windows the block's doc range touches
+  // replaces its list maximum (255 in a window: 255 or more, use the list's).
+  const bool win = (Q.pad & 1u) != 0u && ix.wmax != nullptr;
+  const float io = b_m > 0.0f ? b_iom / b_m : 0.0f;   // 2.2 idf of O1
+  const float m_list = b_m;
+  const uint8_t* o_wm = win ? ix.wmax + Q.o_bm / kWinEnts : reinterpret_cast<const uint8_t*>(ix.blk_last);
+  const uint32_t wm_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_wm) & 3u);
+  // the windows [w0, w1] of a block (directory entry e), clipped to the span
+  auto win_range = [&](const uint4& e, uint32_t& w0, uint32_t& w1) __attribute__((always_inline)) {
+    const uint32_t first = uni(e.x) > lo ? uni(e.x) - lo : 0u;
+    const uint32_t last = uni(e.y) - lo < span ? uni(e.y) - lo : (span ? span - 1 : 0u);
+    w0 = first / (kDenseDocs * kWinEnts);
+    w1 = last / (kDenseDocs * kWinEnts);
+    if (w1 < w0) w1 = w0;
+  };
+#endif
 #ifdef WSR_NO_PRUNE   // A/B diagnostic: every posting is probed
   const float thr_s = -1.0f;
 #else
@@ -1896,6 +1920,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
     uint32_t wc = 0;                               //   its doc-length codes (2 bytes of a word)
     uint32_t wt0 = 0, wt1 = 0, wt2 = 0;            //   its driver tf pack words
+#if WSR_WIN_BOUND
+    uint32_t wm = 0;                               //   O1's window tf maxima (a raw dword per lane)
+#endif
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
@@ -1946,6 +1973,14 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     // its doc-length codes (postings 2l, 2l+1: one line per block, plen) and
     // driver tfs, so that D can bound each posting's score before the probe
     Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
+#if WSR_WIN_BOUND
+    {
+      uint32_t w0, w1;
+      win_range(e, w0, w1);
+      Y.wm = *reinterpret_cast<const uint32_t*>(
+          __builtin_align_down(o_wm + (win ? min(w0 + l, w1) : 0u), 4));
+    }
+#endif
 #if WSR_COALESCED_WORDS
     pack_dwords(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1);
 #else
@@ -2068,6 +2103,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       if (tl) { t0 = ttf0; t1 = ttf1; }
       const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
       const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
+#if WSR_WIN_BOUND
+      if (win) {   // (wave-uniform)
+        uint32_t w0, w1;
+        win_range(be, w0, w1);
+        const uint32_t idx = min(w0 + l, w1);
+        uint32_t v = (X.wm >> (((wm_mis + idx) & 3u) << 3)) & 0xFFu;
+        if (w1 - w0 >= 64u) v = 255u;   // (wider than a wave: the list maximum)
+        const uint32_t m = umax(wave_excl_max(v), v);
+        const uint32_t mm = uni(__builtin_amdgcn_readlane(m, 63));
+        b_m = mm >= 255u ? m_list : static_cast<float>(mm);
+        b_iom = io * b_m;
+      }
+#endif
       // pre-probe pruning (above): a dropped posting is never probed
       // (branch-free: the bound of a lane past the block is computed and dropped)
 #if WSR_BOUND_NO_RCP
