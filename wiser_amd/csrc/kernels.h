@@ -68,8 +68,10 @@ constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; b
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
 // phrase queries: every survivor also runs the position check, so an item of
 // kSegCost blocks is longer; smaller items keep the queue's tail balanced
+// (5: the 5-block phrase items of the round-1 tuning, now that a bitmap probe
+// round no longer adds to an item's cost, WSR_DENSE_COST)
 #ifndef WSR_SEG_COST_PHRASE
-#define WSR_SEG_COST_PHRASE 8
+#define WSR_SEG_COST_PHRASE 5
 #endif
 constexpr int kSegCostPhrase = WSR_SEG_COST_PHRASE;
 static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSegCost");

@@ -281,8 +281,12 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
 // Other list B is probed through its rank bitmap when it has one and is at
 // least dense_ratio times as long as the driver (then a block decode per
 // probe would mostly decode postings nobody asks for).
+// (0: a lean item is kSegCost driver blocks, 63; with the pre-probe bound and
+// the floor refresh, longer items prune more and carry less fixed work per
+// block: main leg 26.6 -> 28.0 M q/s against 0.5, i.e. 42-block items, and
+// 27.9 M at 0.25: profiles/r02_sy_item_size_ab.txt)
 #ifndef WSR_DENSE_COST
-#define WSR_DENSE_COST 0.5f
+#define WSR_DENSE_COST 0.0f
 #endif
 constexpr float kDenseCost = WSR_DENSE_COST;   // plan cost of a bitmap probe round, in block decodes
 
