@@ -207,7 +207,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // en-Wikipedia-shaped C3 corpus this halves the mixed batch against 128,
     // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
     // caps the bitmaps' HBM, longest lists first)
-    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 1024));
+    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048));
     const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 32) * 1e9);
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
     // replay inside the segment kernel (WSR_FUSE_REPLAY=0: separate launch)
