@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "queries/sec + p50 lat, 2-term AND BM25 top-10 on Wikipedia, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_PROFILE = "r02_fp5_pmc_segment.json"   # scripts/gpu_prof.sh, the C2 replica leg
+PMC_PROFILE = "r02_fp6_pmc_segment.json"   # scripts/gpu_prof.sh, the C2 replica leg
 DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
 CPU_SHARE = min(16, os.cpu_count() or 1)   # host threads per GPU on the box (its CPU share)
 
