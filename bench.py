@@ -1,24 +1,29 @@
 #!/usr/bin/env python3
 """Throughput bench: 2-term AND + BM25 top-10 over a Vacuum index on MI355X.
 
-Workload (BASELINE.json configs[1], SURVEY.md 8d "C2"): 1M synthetic Zipf docs
-(V=500k, s=1.07, lognormal lengths, seed 0x5EED2026) written in the reference's
-Vacuum layout by the build's writer; 100k two-term queries drawn by the
-gen_synthetic_log.py:191-214 rule (seed 7); batches of 4096 queries per GPU;
-k = 10.  The English-Wikipedia index of configs[2..4] is not available offline.
+Workload (BASELINE.json metric "... on Wikipedia", configs[2], SURVEY.md 8d
+"C3"): no en-Wikipedia dump exists offline, so the index is the Wikipedia-shaped
+stand-in written by the build's writer in the reference's Vacuum layout: 5.5 M
+docs, 5.64 M terms with the df histogram of the reference's en-Wikipedia index
+(tools/gen_synthetic_log.py:8-16), 0.81 G postings; 100k two-term queries drawn
+by the gen_synthetic_log.py:191-214 rule (seed 7); batches of 4096 queries per
+GPU; k = 10.  (--workload c2: configs[1], 1 M synthetic Zipf docs; at N = 1 it
+also runs as the `c2_synthetic_1m` leg.  --vacuum-dir: a real dump.)
 
 A step = one batch through the engine with the batch's resolved queries
 already resident in HBM:
-  N = 1          plan + segment + replay kernels over the whole index;
-  N > 1 (shard, the value)  every rank holds the doc-id range [N*r/W, N*(r+1)/W)
-                 and takes 4096 queries per step; the heavy ones (driver list >=
-                 --heavy-blocks blocks) run on every shard, their events move
-                 through fixed slots by the engine's own RCCL send/recv over
-                 xGMI (wsr_shard_step) and each owner replays its queries; the
-                 light ones run whole on the rank's full-index image (per-GPU
-                 work ~constant: weak scaling);
-  N > 1 (replica, the control) full index per GPU, 4096 queries per rank.
-value = queries completed by all ranks / max-over-ranks wall time.
+  N = 1     plan + segment + replay kernels over the whole index;
+  N > 1     three forms measured in one run, each rank 4096 queries per step:
+            hybrid (the value): queries whose driver list has >= --heavy-blocks
+              blocks run on every doc-range shard (rank r holds doc ids
+              [N*r/W, N*(r+1)/W)), their events move through fixed slots by the
+              engine's own RCCL all-to-all over xGMI (wsr_shard_step) and each
+              owner replays its queries; the others run whole on the rank's
+              full-index image;
+            docshard: the same with every query sharded (--heavy-blocks 0, the
+              north_star layout an index larger than one GPU needs);
+            replica (control): full index per GPU, no collective.
+value = queries completed by all ranks / max-over-ranks wall time (weak scaling).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -26,6 +31,7 @@ value = queries completed by all ranks / max-over-ranks wall time.
 import argparse
 import ctypes as C
 import json
+import math
 import os
 import statistics
 import sys
@@ -36,9 +42,46 @@ sys.path.insert(0, ROOT)
 
 METRIC = "queries/sec + p50 lat, 2-term AND BM25 top-10 on Wikipedia, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PMC_PROFILE = "r02_fp6_pmc_segment.json"   # scripts/gpu_prof.sh, the C2 replica leg
+# Per-launch fabric bytes of the segment phase (scripts/gpu_prof.sh,
+# scripts/pmc_bytes.py), one profile per workload: attached to lines of that
+# workload only, with the file named in roofline.traffic_source.
+PMC_PROFILES = {"c3": "r03_pmc_segment_c3.json", "c2": "r03_pmc_segment_c2.json"}
 DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
-CPU_SHARE = min(16, os.cpu_count() or 1)   # host threads per GPU on the box (its CPU share)
+
+
+def cpu_share():
+    """Host CPUs this process may use: sched_getaffinity, the cgroup quota
+    (cpu.max, v2; cfs_quota_us / period, v1) and the pool's documented per-GPU
+    share (OMP_NUM_THREADS is set to it on the GPU box).  -> dict"""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    eff = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    hint = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(hint) if hint.isdigit() and int(hint) > 0 else None
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "effective_cpus": eff,
+            "pool_share": share}
+
+
+CPUS = cpu_share()
+# host threads per GPU for builds, loads and the snippet stage: the pool's share
+# when it is stated, else the effective CPUs (at most 16)
+HOST_THREADS = max(1, min(CPUS["pool_share"] or 16, CPUS["effective_cpus"]))
 
 
 def log(msg):
@@ -51,15 +94,18 @@ def parse():
     p.add_argument("--steps", type=int, default=3000,
                    help="timed steps (batches); the default makes the timed region >= 0.5 s")
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--docs", type=int, default=1_000_000)
-    p.add_argument("--vocab", type=int, default=500_000)
+    p.add_argument("--workload", choices=["c3", "c2"], default="c3",
+                   help="c3 (default): the en-Wikipedia-shaped stand-in (BASELINE configs[2]); "
+                        "c2: 1M synthetic Zipf docs (configs[1])")
+    p.add_argument("--docs", type=int, default=1_000_000, help="C2 docs")
+    p.add_argument("--vocab", type=int, default=500_000, help="C2 vocabulary")
     p.add_argument("--queries", type=int, default=100_000)
     p.add_argument("--batch", type=int, default=4096, help="queries per GPU per step")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--mode", choices=["auto", "shard", "replica"], default="auto",
-                   help="N>1: shard = doc-range shards with the RCCL event exchange (the value; "
-                        "auto also measures replica as the control); replica = full index per "
-                        "GPU, queries split across ranks, no collective")
+                   help="N>1: auto = hybrid doc-range shards (the value) + every-query doc-range "
+                        "shards + replicas (control), all in one run; shard = the sharded forms only; "
+                        "replica = full index per GPU, queries split across ranks, no collective")
     p.add_argument("--exchange", choices=["rccl", "gloo"], default="rccl",
                    help="N>1 shards: the engine's own RCCL step (the measurement), or the same "
                         "fused step with the transfer over the launcher's gloo group (a multi-rank "
@@ -70,24 +116,24 @@ def parse():
     p.add_argument("--index-dir", default=os.environ.get("WISER_BENCH_DIR", "/tmp/wiser_bench"))
     p.add_argument("--vacuum-dir", default=None,
                    help="configs[2]: an existing Vacuum dump (my.vacuum, my.tip, my.doc_length), "
-                        "e.g. the reference's en-Wikipedia index, instead of the C2 corpus")
+                        "e.g. the reference's en-Wikipedia index, instead of the stand-in")
     p.add_argument("--linedoc", default=None,
                    help="configs[2]: build the index from this linedoc first (--format)")
     p.add_argument("--format", default="WITH_POSITIONS", choices=["WITH_POSITIONS", "TOKEN_ONLY"])
     p.add_argument("--cpu-seconds", type=float, default=16.0,
-                   help="bounded CPU-baseline sample (oracle, 1 thread), rank 0 at N=1")
+                   help="bounded CPU-baseline sample (oracle), rank 0 at N=1, split over the "
+                        "thread counts measured")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the secondary legs (N=1 only)")
-    p.add_argument("--no-c3", action="store_true", help="skip the en-Wikipedia-shaped C3 leg")
     p.add_argument("--legs", default="",
-                   help="comma list of secondary legs to run (default: all of end_to_end, "
-                        "c3_wiki_standin, c4_mixed_1to5, c5_phrase, serving, c1_snippets)")
+                   help="comma list of secondary legs to run (default: all of c2_synthetic_1m, "
+                        "end_to_end, c4_mixed_1to5, c5_phrase, serving, c1_snippets)")
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
     p.add_argument("--heavy-blocks", type=int, default=-1,
-                   help="N>1 shards: queries whose driver list has at least this many 128-posting "
+                   help="N>1 hybrid: queries whose driver list has at least this many 128-posting "
                         "blocks run on every shard (RCCL exchange); the others run whole on the "
                         "rank's full-index image (0: every query is sharded; -1, the default: "
                         "max(64, 63 * N), so that each shard's part of a sharded query is at "
@@ -100,12 +146,66 @@ def parse():
     return p.parse_args()
 
 
-def ensure_index(a, rank, dist):
-    """The C2 synthetic index (default), or -- configs[2] -- an existing Vacuum
-    dump (--vacuum-dir, e.g. the reference's en-Wikipedia dump) or one built here
-    from a linedoc (--linedoc); the two-term log is generated over its df table
-    by the gen_synthetic_log.py:191-214 rule, in --index-dir."""
+def c3_dir(a):
+    return os.path.join(a.index_dir, f"c3_wiki_{a.c3_docs}_{a.c3_term_scale:g}")
+
+
+def ensure_c3(a):
+    """The C3 stand-in and its 100k two-term log (built once per box, ~35 s)."""
     import wiser_amd as w
+    d = c3_dir(a)
+    qlog = os.path.join(d, "two_term_100000.log")
+    info = None
+    if not os.path.exists(os.path.join(d, "READY")):
+        os.makedirs(d, exist_ok=True)
+        t = time.time()
+        st = w.build_wiki_standin(d, n_docs=a.c3_docs, term_scale=a.c3_term_scale, threads=HOST_THREADS)
+        w.gen_two_term_log(d, qlog, n_queries=100000, seed=7)
+        open(os.path.join(d, "READY"), "w").write("ok")
+        info = {"docs": st.n_docs, "terms": st.n_terms, "postings": st.n_postings,
+                "vacuum_bytes": st.vacuum_bytes, "avg_length": round(st.avg_length, 2),
+                "build_s": round(time.time() - t, 1)}
+        log(f"C3 stand-in built: {info}")
+    return d, qlog, info
+
+
+def ensure_c2(a):
+    import wiser_amd as w
+    idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
+    qlog = os.path.join(idx, f"two_term_{a.queries}.log")
+    if not os.path.exists(os.path.join(idx, "READY")):
+        os.makedirs(idx, exist_ok=True)
+        t = time.time()
+        st = w.build_synthetic(idx, n_docs=a.docs, vocab=a.vocab, threads=HOST_THREADS)
+        w.gen_two_term_log(idx, qlog, n_queries=a.queries, seed=7)
+        open(os.path.join(idx, "READY"), "w").write("ok")
+        log(f"built index {st.n_docs} docs {st.n_terms} terms {st.n_postings} postings "
+            f"{st.vacuum_bytes/1e9:.2f} GB in {time.time()-t:.1f}s")
+    return idx, qlog
+
+
+def workload_text(a, idx, n_lines):
+    if a.vacuum_dir or a.linedoc:
+        return (f"Vacuum index {idx}: {n_lines} two-term AND queries (gen_synthetic_log.py:191-214 "
+                f"rule, seed 7), {a.batch} queries per GPU per step, top-{a.k}")
+    if a.workload == "c2":
+        return (f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), {n_lines} two-term AND "
+                f"queries (gen_synthetic_log rule, seed 7), {a.batch} queries per GPU per step, "
+                f"top-{a.k}")
+    return (f"C3 stand-in (en-Wikipedia-shaped): {a.c3_docs} docs, the en-Wikipedia df histogram "
+            f"x {a.c3_term_scale:g} (gen_synthetic_log.py:8-16), {n_lines} two-term AND queries "
+            f"(:191-214 rule, seed 7), {a.batch} queries per GPU per step, top-{a.k}, "
+            "device-resident")
+
+
+def ensure_index(a, rank, dist):
+    """The headline index and its two-term log: the C3 stand-in (default), C2,
+    or -- configs[2] proper -- an existing Vacuum dump (--vacuum-dir, e.g. the
+    reference's en-Wikipedia dump) or one built here from a linedoc (--linedoc);
+    the log is generated over the index's df table by the
+    gen_synthetic_log.py:191-214 rule."""
+    import wiser_amd as w
+    built = None
     if a.vacuum_dir or a.linedoc:
         idx = a.vacuum_dir
         if a.linedoc:
@@ -120,22 +220,18 @@ def ensure_index(a, rank, dist):
                 log(f"built index {st.n_docs} docs {st.n_terms} terms from {a.linedoc} "
                     f"in {time.time()-t:.1f}s")
             w.gen_two_term_log(idx, qlog, n_queries=a.queries, seed=7)
-        if dist:
-            dist.barrier()
-        return idx, qlog
-    idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
-    qlog = os.path.join(idx, f"two_term_{a.queries}.log")
-    if rank == 0 and not os.path.exists(os.path.join(idx, "READY")):
-        os.makedirs(idx, exist_ok=True)
-        t = time.time()
-        st = w.build_synthetic(idx, n_docs=a.docs, vocab=a.vocab, threads=min(16, os.cpu_count()))
-        w.gen_two_term_log(idx, qlog, n_queries=a.queries, seed=7)
-        open(os.path.join(idx, "READY"), "w").write("ok")
-        log(f"built index {st.n_docs} docs {st.n_terms} terms {st.n_postings} postings "
-            f"{st.vacuum_bytes/1e9:.2f} GB in {time.time()-t:.1f}s")
+    elif a.workload == "c3":
+        idx, qlog = c3_dir(a), os.path.join(c3_dir(a), "two_term_100000.log")
+        if rank == 0:
+            idx, qlog, built = ensure_c3(a)
+    else:
+        idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
+        qlog = os.path.join(idx, f"two_term_{a.queries}.log")
+        if rank == 0:
+            idx, qlog = ensure_c2(a)
     if dist:
         dist.barrier()
-    return idx, qlog
+    return idx, qlog, built
 
 
 def resolve(eng, chunk, k):
@@ -160,38 +256,54 @@ def check_against_oracle(idx, chunk, hits, nh, k, n, phrase=False):
 
 
 def cpu_rate(idx, lines, k, seconds, threads, phrases=None):
-    """(queries, seconds) of the oracle over the head of a log, bounded in time."""
+    """(queries, seconds) of the oracle over the log (cycled), `threads`
+    persistent C++ workers sharing the read-only index for a bounded time."""
     from oracle.oracle import OracleVacuum
     orc = OracleVacuum(idx)
-    step = 64 * threads
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:   # the log is cycled when it runs out
-        at = done % len(lines)
-        orc.search_lines(lines[at:at + step], k, threads=threads,
-                         phrases=phrases[at:at + step] if phrases else None)
-        done += len(lines[at:at + step])
-    cel = time.perf_counter() - t0
-    orc.close()
-    return done, cel
+    try:
+        return orc.bench_lines(lines, k, threads, seconds, phrases=phrases)
+    finally:
+        orc.close()
 
 
-def cpu_baseline(idx, lines, k, seconds):
-    """the CPU restatement (built -O3 -DNDEBUG like the reference,
-    CMakeLists.txt:6,12) on the box's host cores: 1 thread, the box's CPU share
-    per GPU, and nproc threads (std::thread workers over the shared read-only
-    index, as the reference's gRPC threads share one engine,
-    grpc_server_impl.h:260-263).  value = the nproc run."""
-    nproc = os.cpu_count() or 1
-    d1, c1 = cpu_rate(idx, lines, k, seconds / 3, 1)
-    ds, cs = cpu_rate(idx, lines, k, seconds / 3, CPU_SHARE)
-    dn, cn = cpu_rate(idx, lines, k, seconds / 3, nproc)
-    return {"value": round(dn / cn, 1), "unit": "queries/s", "cores": nproc, "kind": "port",
-            "sample": f"{dn} queries of the same log (cycled from its start), oracle "
-                      f"restatement of VacuumEngine::Search (-O3 -DNDEBUG), {nproc} threads (nproc), "
-                      f"{cn:.1f}s; {CPU_SHARE} threads: {ds} in {cs:.1f}s; 1 thread: {d1} in {c1:.1f}s",
-            "single_thread": round(d1 / c1, 1), "share_threads": CPU_SHARE,
-            "share_value": round(ds / cs, 1), "nproc": nproc, "build": "-O3 -DNDEBUG",
-            "cpu_model": cpu_model()}
+def cpu_thread_counts():
+    """1 thread, the pool's per-GPU share, the effective CPUs, the affinity set."""
+    xs = [1, CPUS["pool_share"] or 0, CPUS["effective_cpus"], CPUS["affinity"]]
+    return sorted(set(x for x in xs if x and x >= 1))
+
+
+def cpu_baseline(idx, lines, k, seconds, what):
+    """SURVEY 8d: the CPU restatement of VacuumEngine::Search (oracle/oracle.cc,
+    -O3 -DNDEBUG like the reference, CMakeLists.txt:6,12) on the box's host
+    cores, workers sharing the read-only index as the reference's gRPC threads
+    share one engine (grpc_server_impl.h:260-263).  Timed at 1 thread, the
+    pool's per-GPU share, the effective CPU count and the affinity set; `value`
+    is the fastest of them and `cores` its thread count."""
+    counts = cpu_thread_counts()
+    runs = {}
+    for t in counts:
+        d, c = cpu_rate(idx, lines, k, seconds / len(counts), t)
+        runs[t] = (d, c)
+    best = max(runs, key=lambda t: runs[t][0] / runs[t][1])
+    d, c = runs[best]
+    out = {"value": round(d / c, 1), "unit": "queries/s", "cores": best, "kind": "port",
+           "sample": (f"{d} queries of {what} (the log cycled), oracle restatement of "
+                      f"VacuumEngine::Search (-O3 -DNDEBUG), {best} persistent worker threads over "
+                      f"the shared index, {c:.1f}s"),
+           "by_threads": {str(t): round(runs[t][0] / runs[t][1], 1) for t in counts},
+           "single_thread": round(runs[1][0] / runs[1][1], 1),
+           "effective_cpus": CPUS["effective_cpus"], "affinity_cpus": CPUS["affinity"],
+           "nproc": CPUS["nproc"], "cgroup_quota_cpus": CPUS["cgroup_quota_cpus"],
+           "pool_share": CPUS["pool_share"],
+           "build": "-O3 -DNDEBUG", "cpu_model": cpu_model(),
+           "timing": "one C call per thread count: workers started and parked before the clock, "
+                     "results to preallocated arrays (orc_vacuum_bench_lines)"}
+    top = max(counts)
+    if top > best:
+        out["note"] = (f"{top} threads ({runs[top][0] / runs[top][1]:.0f} q/s) are slower than {best}: "
+                       "the box's cores beyond its per-GPU share are not this job's to use "
+                       f"(pool share {CPUS['pool_share']}, nproc {CPUS['nproc']})")
+    return out
 
 
 def cpu_model():
@@ -202,6 +314,17 @@ def cpu_model():
     except OSError:
         pass
     return None
+
+
+def roofline_of(acc, nbk, launch_ms, source):
+    """Algorithmic bytes per launch (wsr_list_bytes) over the
+    segment phase's launch duration."""
+    algo = acc["algo"] / nbk
+    ach = algo / (launch_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "algo_bytes_per_launch": int(algo),
+            "avg_launch_ms": round(launch_ms, 4), "launch_ms_source": source,
+            "kernel": "lean_kernel||segment_kernel"}
 
 
 def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
@@ -245,57 +368,52 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
             b.run()
     w.sync(eng)
     el = time.perf_counter() - t0
+    seg = [b.stats() for b in batches]   # each batch's last run: inside the timed loop
+    timed_seg = sum(st.segment_ms for st in seg) / len(seg)
     for b in batches:   # device error flags of every batch's last run (fetch raises)
         b.fetch()
     nq = len(items) * passes
     for b in batches:
         b.close()
+    nbk = len(batches)
     out = {"value": round(nq / el, 1), "unit": "queries/s", "queries": len(items),
-           "batch": batch, "passes": passes, "p50_ms": round(statistics.median(lat), 3),
-           "segment_ms_per_batch": round(acc["seg"] / len(batches), 4),
-           "survivors_per_batch": int(acc["surv"] / len(batches)),
+           "batch": batch, "passes": passes, "ms_per_batch": round(el / (passes * nbk) * 1e3, 4),
+           "p50_alone_ms": round(statistics.median(lat), 3),
+           "segment_ms_per_batch": round(acc["seg"] / nbk, 4),
+           "survivors_per_batch": int(acc["surv"] / nbk),
+           "driver_blocks_per_batch": int(acc["dblk"] / nbk),
+           "roofline": roofline_of(acc, nbk, timed_seg, "timed region"),
            "parity_checked_queries": checked}
     if cpu_seconds:
         lines = [t for t, _ in items]
         phr = [p for _, p in items]
-        d, c = cpu_rate(idx, lines, k, cpu_seconds, CPU_SHARE, phrases=phr)
-        out["cpu_baseline"] = {"value": round(d / c, 1), "cores": CPU_SHARE, "kind": "port",
-                               "sample": f"{d} queries of the leg's log (cycled), {c:.1f}s"}
+        d, c = cpu_rate(idx, lines, k, cpu_seconds, HOST_THREADS, phrases=phr)
+        out["cpu_baseline"] = {"value": round(d / c, 1), "cores": HOST_THREADS, "kind": "port",
+                               "sample": f"{d} queries of the leg's log (cycled), {HOST_THREADS} "
+                                         f"persistent workers, {c:.1f}s"}
     return out
 
 
-def c3_leg(a, local, threads):
-    """BASELINE configs[2] ("C3") stand-in, one GPU: no en-Wikipedia dump exists
-    offline, so the index is the writer's Wikipedia-shaped corpus (df histogram
-    of tools/gen_synthetic_log.py:8-16, 5.64 M terms, 5.5 M docs; writer.h
-    WikiSpec) and the log is 100k two-term queries by the :191-214 rule over its
-    df table; batches of 4096, top-10, device-resident, as the main leg."""
+def c2_leg(a, local, threads):
+    """BASELINE configs[1] ("C2"), one GPU: 1M synthetic Zipf docs (V=500k,
+    s=1.07), its 100k two-term log, batches of 4096, top-10, device-resident."""
     import wiser_amd as w
-    d = os.path.join(a.index_dir, f"c3_wiki_{a.c3_docs}_{a.c3_term_scale:g}")
-    qlog = os.path.join(d, "two_term_100000.log")
-    out = {}
-    if not os.path.exists(os.path.join(d, "READY")):
-        os.makedirs(d, exist_ok=True)
-        t = time.time()
-        st = w.build_wiki_standin(d, n_docs=a.c3_docs, term_scale=a.c3_term_scale, threads=threads)
-        w.gen_two_term_log(d, qlog, n_queries=100000, seed=7)
-        open(os.path.join(d, "READY"), "w").write("ok")
-        out["index"] = {"docs": st.n_docs, "terms": st.n_terms, "postings": st.n_postings,
-                        "vacuum_bytes": st.vacuum_bytes, "avg_length": round(st.avg_length, 2),
-                        "build_s": round(time.time() - t, 1)}
-        log(f"C3 stand-in built: {out['index']}")
+    idx, qlog = ensure_c2(a)
     t = time.time()
-    eng = w.VacuumEngine(d, device=local, threads=threads, positions=False)
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
     eng.Load()
-    out["load_s"] = round(time.time() - t, 1)
-    out["image"] = eng.image_info()
+    load_s = round(time.time() - t, 1)
+    image = eng.image_info()
     items = [(l.split(), False) for l in open(qlog).read().splitlines()]
-    leg = run_leg(eng, d, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 2)
+    leg = run_leg(eng, idx, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 4)
     eng.close()
-    leg.update(out)
-    leg["workload"] = (f"C3 stand-in: {a.c3_docs} docs, en-Wikipedia df histogram x {a.c3_term_scale:g} "
-                       "(gen_synthetic_log.py:8-16), 100000 two-term AND queries (:191-214 rule, "
-                       "seed 7), top-10, batches of 4096, device-resident")
+    leg.update({"load_s": load_s, "image": image,
+                "workload": (f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), 100000 two-term "
+                             "AND queries (gen_synthetic_log rule, seed 7), top-10, batches of 4096, "
+                             "device-resident")})
+    pmc = load_pmc("c2")
+    if pmc:
+        leg["roofline"].update(pmc)
     return leg
 
 
@@ -366,15 +484,18 @@ def end_to_end_leg(a, idx, qlog, local, threads):
     eng.close()
     best = max(out.values(), key=lambda x: x["value"])
     out.update({"value": best["value"], "unit": "queries/s", "p50_ms": best["p50_ms"], "p99_ms": best["p99_ms"],
-                "workload": ("C2 log as text, batches of 4096: wsr_search_text = term lookup + upload + "
+                "workload": ("the headline log as text, batches of 4096: wsr_search_text = term lookup + upload + "
                              "run + results to host memory; client threads submit batches back to back, "
                              "latency submit -> host results per batch under that load")})
     return out
 
 
-def extra_legs(a, idx, local, threads):
-    """BASELINE configs[3] / [4] analogues on the C2 index, one GPU: mixed
-    1-5 term AND queries (AOL shares) and 2-term phrase queries."""
+def extra_legs(a, idx, qlog, local, threads):
+    """The other legs of one N = 1 run: C2 (configs[1]) as a leg of its own,
+    then over the headline index: the whole Search chain from strings
+    (end_to_end), mixed 1-5 term AND (configs[3]'s query mix), two-term
+    phrases (configs[4]; on the headline index when it has a phrase pool, else
+    on C2), single-query serving, and C1 with snippets (configs[0])."""
     import wiser_amd as w
     legs = {}
     chosen = set(x for x in a.legs.split(",") if x)
@@ -382,52 +503,49 @@ def extra_legs(a, idx, local, threads):
     def want(name):
         return not chosen or name in chosen
 
+    c2_idx = None
+    if want("c2_synthetic_1m") and not (a.workload == "c2" and not (a.vacuum_dir or a.linedoc)):
+        legs["c2_synthetic_1m"] = c2_leg(a, local, threads)
     if want("end_to_end"):
-        legs["end_to_end"] = end_to_end_leg(a, idx, a.qlog, local, threads)
-    if not a.no_c3 and want("c3_wiki_standin"):
-        legs["c3_wiki_standin"] = c3_leg(a, local, threads)
-    if not (want("c4_mixed_1to5") or want("c5_phrase") or want("serving") or want("c1_snippets")):
-        return legs
+        legs["end_to_end"] = end_to_end_leg(a, idx, qlog, local, threads)
     tag = os.path.basename(idx.rstrip("/"))
-    mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
-    phr = os.path.join(a.index_dir, f"phrase_{tag}_10000.log")
-    if not os.path.exists(mixed):
-        w.gen_mixed_log(idx, mixed, n_queries=20000, seed=7)
-    has_pool = os.path.exists(os.path.join(idx, "phrases.txt"))
-    if has_pool and not os.path.exists(phr):
-        w.gen_phrase_log(idx, phr, n_queries=10000, seed=7)
     if want("c4_mixed_1to5"):
+        mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
+        if not os.path.exists(mixed):
+            w.gen_mixed_log(idx, mixed, n_queries=20000, seed=7)
         eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
         eng.Load()
         items = [(l.split(), False) for l in open(mixed).read().splitlines()]
         legs["c4_mixed_1to5"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
                                         0 if a.no_cpu else a.cpu_seconds / 4)
-        legs["c4_mixed_1to5"]["workload"] = ("20000 AND queries of 1-5 terms (AOL term-count shares, "
-                                             "gen_synthetic_log group rule, seed 7), top-10")
+        legs["c4_mixed_1to5"]["workload"] = (f"{tag}: 20000 AND queries of 1-5 terms (AOL term-count "
+                                             "shares, gen_synthetic_log group rule, seed 7), top-10")
         eng.close()
-    if not has_pool:   # phrase pool: synthetic indexes only
-        if want("serving"):
-            legs["serving"] = serving_leg(a, idx, local, threads)
-        if want("c1_snippets"):
-            legs["c1_snippets"] = snippet_leg(a, local, threads)
-        return legs
-    if not (want("c5_phrase") or want("serving") or want("c1_snippets")):
-        return legs
     if want("c5_phrase"):
+        pidx = idx
+        if not os.path.exists(os.path.join(idx, "phrases.txt")):
+            pidx = c2_idx = ensure_c2(a)[0]   # (the pool of a synthetic corpus)
+        ptag = os.path.basename(pidx.rstrip("/"))
+        phr = os.path.join(a.index_dir, f"phrase_{ptag}_10000.log")
+        if not os.path.exists(phr):
+            w.gen_phrase_log(pidx, phr, n_queries=10000, seed=7)
         t = time.time()
-        eng = w.VacuumEngine(idx, device=local, threads=threads, positions=True)
+        eng = w.VacuumEngine(pidx, device=local, threads=threads, positions=True)
         eng.Load()
-        log(f"engine with positions loaded in {time.time()-t:.1f}s")
+        load_s = round(time.time() - t, 1)
         items = w.read_query_log(phr)
-        legs["c5_phrase"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
+        legs["c5_phrase"] = run_leg(eng, pidx, items, a.k, a.batch, 4, a.check,
                                     0 if a.no_cpu else a.cpu_seconds / 4)
-        legs["c5_phrase"]["workload"] = ("10000 two-term phrase queries drawn from the corpus's "
-                                         "unique-term bigrams (gen_synthetic_log.py:216-265), top-10")
+        legs["c5_phrase"]["load_s"] = load_s
+        legs["c5_phrase"]["image"] = eng.image_info()
+        legs["c5_phrase"]["workload"] = (f"{ptag}: 10000 two-term phrase queries from the corpus's "
+                                         "phrase pool (gen_synthetic_log.py:216-265), top-10")
         eng.close()
     if want("serving"):
-        legs["serving"] = serving_leg(a, idx, local, threads)
+        legs["serving"] = serving_leg(a, idx, qlog, local, threads)
     if want("c1_snippets"):
         legs["c1_snippets"] = snippet_leg(a, local, threads)
+    del c2_idx
     return legs
 
 
@@ -458,10 +576,10 @@ def snippet_leg(a, local, threads):
     terms = distinct + [rng.choice(distinct) for _ in range(10000)]
     eng = w.VacuumEngine(d, device=local, threads=threads, positions=False)
     eng.Load()
-    eng.snippet_threads = CPU_SHARE
+    eng.snippet_threads = HOST_THREADS
     from wiser_amd import _capi
     # native path timed: the batch's GPU top-k (wsr_search_batch), then the
-    # snippet stage of its entries on CPU_SHARE threads (wsr_snippets_batch)
+    # snippet stage of its entries on HOST_THREADS threads (wsr_snippets_batch)
     batches = []
     for i in range(0, len(terms), a.batch):
         chunk = terms[i:i + a.batch]
@@ -482,7 +600,7 @@ def snippet_leg(a, local, threads):
             _capi.check(_capi.lib.wsr_search_batch(eng._h, arr, nq, a.k, hits, nh))
             t1 = time.perf_counter()
             if snip:
-                _capi.check(_capi.lib.wsr_snippets_batch(eng._h, arr, nq, hits, nh, a.k, 3, CPU_SHARE,
+                _capi.check(_capi.lib.wsr_snippets_batch(eng._h, arr, nq, hits, nh, a.k, 3, HOST_THREADS,
                                                          sbuf, cap, ends, C.byref(total)))
                 n += sum(nh)
             t_topk += t1 - t0
@@ -502,7 +620,7 @@ def snippet_leg(a, local, threads):
     if bad:
         raise SystemExit(f"c1 snippet leg: {bad} queries differ from the oracle")
     out = {"value": round(len(terms) / el, 1), "unit": "queries/s", "queries": len(terms),
-           "snippets": n_snip, "snippets_per_s": round(n_snip / t_snip, 1), "snippet_threads": CPU_SHARE,
+           "snippets": n_snip, "snippets_per_s": round(n_snip / t_snip, 1), "snippet_threads": HOST_THREADS,
            "topk_ms_per_batch": round(1e3 * t_topk / len(batches), 3),
            "snippet_ms_per_batch": round(1e3 * t_snip / len(batches), 3),
            "parity_checked_queries": min(a.check, len(terms)),
@@ -540,17 +658,17 @@ def snippet_leg(a, local, threads):
     return out
 
 
-def serving_leg(a, idx, local, threads):
+def serving_leg(a, idx, qlog, local, threads):
     """Single-query serving through the micro-batcher (wsr_server_*): 4 client
     threads keep 1024 (or 64) queries each in flight (the reference client's
-    threads, grpc_client_impl.h:557-620) over the C2 log; latency = submit ->
+    threads, grpc_client_impl.h:557-620) over the headline log; latency = submit ->
     result.  The clients share the box's 16-core CPU share with the dispatcher,
     so few client threads with deep windows load it best."""
     import wiser_amd as w
     from wiser_amd import _capi
     eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
     eng.Load()
-    lines = [l.split() for l in open(a.qlog).read().splitlines()]
+    lines = [l.split() for l in open(qlog).read().splitlines()]
     arr = (_capi.Query * len(lines))()
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
@@ -568,13 +686,16 @@ def serving_leg(a, idx, local, threads):
 
 
 def timed_launch_stats(batches, steps):
-    """Segment-phase launch durations of the timed region itself: every batch's
-    HIP events (recorded on its own stream, fork -> join) of its last run inside
-    the timed loop, with consecutive batches overlapping as they ran there (the
-    durations a rocprofv3 kernel trace of the same command averages)."""
-    if steps < len(batches):
+    """Segment-phase launch durations of the timed region itself: the HIP
+    events (recorded on each batch's own stream, fork -> join) of every batch's
+    last run inside the timed loop, with consecutive batches overlapping as they
+    ran there (the durations a rocprofv3 kernel trace of the same command
+    averages).  With fewer steps than batches only the batches the timed loop
+    ran count (the others last ran one at a time, before it)."""
+    ran = batches[:min(steps, len(batches))]
+    if not ran:
         return
-    seg = [b.stats() for b in batches]
+    seg = [b.stats() for b in ran]
     DIAG["timed_seg_ms"] = sum(st.segment_ms for st in seg) / len(seg)
     DIAG["timed_lean_ms"] = sum(st.lean_ms for st in seg) / len(seg)
 
@@ -599,19 +720,11 @@ def kernel_accounting(eng, batches):
     return acc
 
 
-def run_shard(a, idx, lines, rank, world, local, dist, threads):
-    """Doc-range shards, the N > 1 value.  Every rank holds the
-    doc-id range [N*r/W, N*(r+1)/W) and takes its own 4096 queries per step.
-    Heavy queries (driver list of >= --heavy-blocks blocks, where the work is)
-    run on every rank over its range: wsr_shard_step packs each owner's events
-    into a fixed slot, RCCL moves counts and slots between all pairs, and the
-    owner replays its queries; the rest run whole on the rank's full-index
-    image with no collective (--heavy-blocks 0: every query is sharded).
-    Returns (queries, seconds, p50 ms, batches, engine, checked, closer)."""
-    import math
-    import torch
+def open_shard_engines(a, idx, rank, world, local, dist, threads, need_full):
+    """This rank's doc-range shard image (with the engine's RCCL communicator)
+    and, for the hybrid and replica forms, the full-index image."""
     import wiser_amd as w
-    from wiser_amd.shard import NativeShardedSearcher, slot_for_fill
+    from wiser_amd.shard import NativeShardedSearcher
     t = time.time()
 
     def share_id(x):   # rank 0's RCCL id to every rank, over the launcher's gloo group
@@ -621,24 +734,36 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         dist.broadcast_object_list(box, src=0)
         return box[0]
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     if a.exchange == "gloo" and dist is not None:
         from wiser_amd.shard import HostExchangeShardedSearcher
         S = HostExchangeShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
     else:
         S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
     full = None
-    # per-item fixed work is large (profiles/r02_x_item_size.txt: items of 16
-    # blocks run at half the rate of 63), so a query is split over the shards
-    # only when every shard still gets at least one full item of it
-    heavy_blocks = a.heavy_blocks if a.heavy_blocks >= 0 else max(64, 63 * world)
-    if heavy_blocks > 0:
+    if need_full:
         full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
         full.Load()
     log(f"rank {rank}: shard {S.doc_range}{' + full image' if full else ''} loaded in {time.time()-t:.1f}s")
+    return S, full
+
+
+def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
+    """Doc-range shards.  Every rank holds the doc-id range
+    [N*r/W, N*(r+1)/W) (S) and takes its own 4096 queries per step.  Heavy
+    queries (driver list of >= heavy_blocks blocks, where the work is) run on
+    every rank over its range: wsr_shard_step packs each owner's events into a
+    fixed slot, one RCCL all-to-all moves counts and slots between all pairs,
+    and the owner replays its queries; the rest run whole on the rank's
+    full-index image (full) with no collective (heavy_blocks 0: every query is
+    sharded, full unused).  Returns a dict of the run and its batches."""
+    import torch
+    import wiser_amd as w
+    from wiser_amd.shard import slot_for_fill
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
     B = a.batch
     per_rank = len(lines) // world
     nb = max(1, per_rank // B)
@@ -718,20 +843,23 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
             return (S.fetch_owned(hb, hq) if hb else None), (cb.fetch() if cb else None)
         return None
 
+    def sync_all():
+        w.sync(S.engine)
+        if full:
+            w.sync(full)
+
     checked = 0
     if a.check:   # every rank takes part in the collectives; rank 0 checks
         (hres, cres) = step(0, fetch=True)
         if rank == 0:
             hb, hq, hchunk, cb, cheap = steps[0]
             if hres:
-                checked += check_against_oracle(idx, hchunk[:hq], hres[0], hres[1], a.k, a.check)
+                checked += check_against_oracle(S.engine.engine_dir_path, hchunk[:hq], hres[0], hres[1], a.k, a.check)
             if cres:
-                checked += check_against_oracle(idx, cheap, cres[0], cres[1], a.k, a.check)
-    for s in range(a.warmup):
-        step(s)
-    w.sync(S.engine)
-    if full:
-        w.sync(full)
+                checked += check_against_oracle(S.engine.engine_dir_path, cheap, cres[0], cres[1], a.k, a.check)
+    for s_ in range(a.warmup):
+        step(s_)
+    sync_all()
     lat = []
     for i in range(nb):
         barrier()
@@ -739,16 +867,12 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         step(i, fetch=True)
         lat.append((time.perf_counter() - t0) * 1e3)
     barrier()
-    w.sync(S.engine)
-    if full:
-        w.sync(full)
+    sync_all()
     t0 = time.perf_counter()
-    for s in range(a.steps):
-        step(s)
-    DIAG["host_enqueue_ms_per_step"] = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
-    w.sync(S.engine)
-    if full:
-        w.sync(full)
+    for s_ in range(a.steps):
+        step(s_)
+    host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
+    sync_all()
     el = time.perf_counter() - t0
     for hb, hq, _, cb, _ in steps:   # error flags (a slot overflow among them) of every last step
         if hb:
@@ -756,42 +880,27 @@ def run_shard(a, idx, lines, rank, world, local, dist, threads):
         if cb:
             cb.fetch()
     # every rank completes its own 4096 queries per step (heavy owned + cheap)
-    queries = sum(len(steps[s % nb][4]) + sum(1 for q in steps[s % nb][2][rank * steps[s % nb][1]:
-                                                                       (rank + 1) * steps[s % nb][1]] if q)
-                  for s in range(a.steps))
-    S.slot = slot
-    S.heavy_share = sum(st[1] for st in steps) / max(1, nb * B)
-    S.heavy_blocks = heavy_blocks
-    S.every = every
-    batches = [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]]
-    eng = full if (full and any(st[3] for st in steps)) else S.engine
+    queries = sum(len(steps[s_ % nb][4]) + sum(1 for q in steps[s_ % nb][2][rank * steps[s_ % nb][1]:
+                                                                          (rank + 1) * steps[s_ % nb][1]] if q)
+                  for s_ in range(a.steps))
+    share = sum(st[1] for st in steps) / max(1, nb * B)
 
-    class Closer:
-        slot = S.slot
-        heavy_share = S.heavy_share
-        heavy_blocks = S.heavy_blocks
-        every = S.every
-
-        def close(self):
-            for hb, _, _, cb, _ in steps:
-                for x in (hb, cb):
-                    if x and x not in batches:
-                        x.close()
-            S.close()
-            if full:
-                full.close()
-    return queries, el, statistics.median(lat), batches, eng, checked, Closer()
+    def close():
+        for hb, _, _, cb, _ in steps:
+            for x in (hb, cb):
+                if x:
+                    x.close()
+    return {"queries": queries, "el": el, "p50": statistics.median(lat), "checked": checked,
+            "slot": slot, "heavy_share": share, "heavy_blocks": heavy_blocks, "every": every,
+            "host_ms": host_ms,
+            "batches": [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]],
+            "engine": full if (full and any(st[3] for st in steps)) else S.engine, "close": close}
 
 
-def run_replica(a, idx, lines, rank, world, local, dist, threads):
-    """Full index per GPU; the log is split across ranks, 4096 queries per
-    rank per step, consecutive batches in flight on per-batch streams."""
+def run_replica(a, eng, idx, lines, rank, world, dist):
+    """Full index per GPU (eng); the log is split across ranks, 4096 queries
+    per rank per step, consecutive batches in flight on per-batch streams."""
     import wiser_amd as w
-    t = time.time()
-    # the conjunctive workload never reads positions: the image leaves them out
-    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
-    eng.Load()
-    log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
     per_rank = (len(lines) + world - 1) // world
     mine = lines[rank * per_rank:(rank + 1) * per_rank] or lines[:a.batch]
     batches, chunks = [], []
@@ -822,7 +931,7 @@ def run_replica(a, idx, lines, rank, world, local, dist, threads):
     t0 = time.perf_counter()
     for s in range(a.steps):
         batches[s % nb].run()
-    DIAG["host_enqueue_ms_per_step"] = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
+    host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     w.sync(eng)
     el = time.perf_counter() - t0
     timed_launch_stats(batches, a.steps)
@@ -831,7 +940,12 @@ def run_replica(a, idx, lines, rank, world, local, dist, threads):
     for b in batches:
         b.fetch()
     queries = sum(batches[s % nb].nq for s in range(a.steps))
-    return queries, el, statistics.median(lat), batches, eng, checked, None
+
+    def close():
+        for b in batches:
+            b.close()
+    return {"queries": queries, "el": el, "p50": statistics.median(lat), "checked": checked,
+            "host_ms": host_ms, "batches": batches, "engine": eng, "close": close}
 
 
 def reduce_timing(dist, el, queries, p50, on_gpu, summed):
@@ -845,6 +959,27 @@ def reduce_timing(dist, el, queries, p50, on_gpu, summed):
     sm = tt.clone()
     dist.all_reduce(sm, op=dist.ReduceOp.SUM)
     return mx[0].item(), (sm[1].item() if summed else queries), mx[2].item()
+
+
+def load_pmc(workload):
+    """Per-launch fabric bytes of the segment phase (lean_kernel +
+    segment_kernel) from TCC_EA0 request counts by size (scripts/pmc_bytes.py;
+    the formula is checked against known streaming kernels in the same
+    profile run's calib_bytes file, where FETCH_SIZE reads half the bytes on
+    gfx950), measured on this workload's replica leg."""
+    name = PMC_PROFILES.get(workload)
+    path = os.path.join(ROOT, "profiles", name) if name else None
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        pm = json.load(open(path))
+        out = {"traffic": pm["hbm_bytes_per_launch"], "traffic_source": name,
+               "traffic_fetch_size_raw": pm["per_launch"].get("FETCH_SIZE", 0.0) * 1024}
+        if "algo_bytes_per_launch" in pm:   # the profiled run's own algorithmic bytes
+            out["traffic_over_algo"] = round(pm["hbm_bytes_per_launch"] / pm["algo_bytes_per_launch"], 3)
+        return out
+    except Exception:
+        return None
 
 
 def main():
@@ -862,7 +997,7 @@ def main():
         import torch
     except ImportError:
         torch = None
-    import wiser_amd  # noqa: F401
+    import wiser_amd as w
     from wiser_amd import _capi
     runtime = _capi.runtime_info()
     if world > 1:
@@ -873,113 +1008,113 @@ def main():
         # host-side group (gloo): rendezvous, the RCCL id, barriers and the
         # max-over-ranks timing; the data path is the engine's own RCCL exchange
         dist.init_process_group(a.dist_backend)
-    on_gpu = False
 
-    idx, qlog = ensure_index(a, rank, dist)
-    a.qlog = qlog
+    idx, qlog, built = ensure_index(a, rank, dist)
     lines = [l.split() for l in open(qlog).read().splitlines()]
-    threads = min(16, os.cpu_count())
+    threads = HOST_THREADS
+    wkey = "dump" if (a.vacuum_dir or a.linedoc) else a.workload
 
-    sharded = mode in ("auto", "shard")
-    runner = run_shard if sharded else run_replica
-    queries, el, p50, batches, eng, checked, S = runner(a, idx, lines, rank, world, local, dist, threads)
-    parallelism = f"docshard{world}" if sharded else f"replicas{world}"
-    global_batch = a.batch * world
-    acc = kernel_accounting(eng, batches)
-    image = eng.image_info()
-    nbk = len(batches)
-    # the launch duration of the roofline: measured over the timed region when
-    # every batch ran there (replicas), else one batch at a time
+    forms = {}      # N > 1: every form measured, reduced over ranks
+    full = S = None
+    t = time.time()
+    if mode == "replica":
+        full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+        full.Load()
+        log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
+    else:
+        hb_default = max(64, 63 * world)
+        S, full = open_shard_engines(a, idx, rank, world, local, dist, threads,
+                                     need_full=(a.heavy_blocks != 0 or a.mode == "auto"))
+    load_s = round(time.time() - t, 1)
+
+    def reduced(r):
+        el, q, p50 = r["el"], r["queries"], r["p50"]
+        if dist:
+            el, q, p50 = reduce_timing(dist, el, q, p50, False, summed=True)
+        return {"value": round(q / el, 1), "ms_per_step": round(el / a.steps * 1e3, 4),
+                "p50_alone_ms": round(p50, 3), "queries": int(q), "seconds": round(el, 5)}
+
+    if mode == "replica":
+        main_run = run_replica(a, full, idx, lines, rank, world, dist)
+        parallelism = f"replicas{world}"
+    else:
+        # the value: hybrid (--heavy-blocks default) or the form asked for
+        hb = a.heavy_blocks if a.heavy_blocks >= 0 else hb_default
+        main_run = run_shard(a, S, full, hb, lines, rank, world, dist)
+        share = main_run["heavy_share"]
+        parallelism = (f"docshard{world}" if hb == 0 else
+                       f"hybrid-docshard{world} ({100 * share:.2f}% of queries sharded)")
+    acc = kernel_accounting(main_run["engine"], main_run["batches"])
+    image = main_run["engine"].image_info()
+    nbk = len(main_run["batches"])
     iso_ms = acc["seg"] / nbk
     seg_avg_ms = DIAG.get("timed_seg_ms", iso_ms)
     seg_src = "timed region" if "timed_seg_ms" in DIAG else "one batch at a time"
     lean_avg_ms = DIAG.get("timed_lean_ms", acc["lean"] / nbk)
-    achieved = (acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9
-    if dist:
-        # both forms count the queries each rank completed (its own 4096 per
-        # step: owned heavy + light, or its replica's): the value is their sum
-        el, queries, p50 = reduce_timing(dist, el, queries, p50, on_gpu, summed=True)
-    qps = queries / el
-    for b in batches:
-        b.close()
+    mres = reduced(main_run)
+    checked = main_run["checked"]
+    host_ms = main_run["host_ms"]
+    main_run["close"]()
+    if world > 1 and a.mode == "auto":
+        # the other forms, from the same images: every query doc-range sharded
+        # (the north_star layout), and replicas (control, no collective)
+        if a.heavy_blocks != 0:
+            r = run_shard(a, S, full, 0, lines, rank, world, dist)
+            forms["docshard"] = {**reduced(r), "parallelism": f"docshard{world}", "slot_events": r["slot"],
+                                 "shard_every": r["every"],
+                                 "note": "every query on every shard, one ncclAllToAll per sharded step"}
+            r["close"]()
+        r = run_replica(a, full, idx, lines, rank, world, dist)
+        forms["replica"] = {**reduced(r), "parallelism": f"replicas{world}",
+                            "note": "control: the full index on every GPU, each rank its own 4096 "
+                                    "queries, no collective"}
+        r["close"]()
+    shard_bytes = S.engine.image_info()["total_bytes"] if S is not None else None
+    full_bytes = full.image_info()["total_bytes"] if full is not None else None
     if S is not None:
-        S.close()   # (the shard searcher and, hybrid, the full image and its batches)
-    else:
-        eng.close()
-
-    # auto at N > 1: the doc-range sharded path carries the value (SURVEY 8e,
-    # north_star); full-index replicas, queries split across ranks with no
-    # collective, are measured the same way beside it as the control
-    control = None
-    if dist and a.mode == "auto":
-        rq, rel, rp50, rb, reng, _, _ = run_replica(a, idx, lines, rank, world, local, dist, threads)
-        rel, rq, rp50 = reduce_timing(dist, rel, rq, rp50, on_gpu, summed=True)
-        control = {"value": round(rq / rel, 1), "ms_per_step": round(rel / a.steps * 1e3, 4),
-                   "global_batch": a.batch * world, "p50_alone_ms": round(rp50, 3),
-                   "parallelism": f"replicas{world}",
-                   "note": "control: the full index on every GPU, each rank its own 4096 queries, "
-                           "no collective"}
-        for b in rb:
-            b.close()
-        reng.close()
+        S.close()
+    if full is not None:
+        full.close()
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds)
+        cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds, "the headline workload's log")
     extra = None
     if rank == 0 and world == 1 and not a.no_extra:
-        extra = extra_legs(a, idx, local, threads)
-
-    traffic = traffic_fetch = None
-    pmc = os.path.join(ROOT, "profiles", PMC_PROFILE)
-    # Fabric bytes per launch of the segment phase (lean_kernel + segment_kernel),
-    # from TCC_EA0 request counts by size (scripts/pmc_bytes.py; the formula is
-    # checked against known streaming kernels in profiles/r02_p_calib_bytes.txt,
-    # where FETCH_SIZE reads half the bytes on gfx950).  Measured on the C2
-    # replica workload, so attached to C2 replica lines only.
-    if os.path.exists(pmc) and not (a.vacuum_dir or a.linedoc) and not sharded:
-        try:
-            pm = json.load(open(pmc))
-            traffic = pm["hbm_bytes_per_launch"]
-            traffic_fetch = pm["per_launch"]["FETCH_SIZE"] * 1024
-        except Exception:
-            traffic = traffic_fetch = None
+        extra = extra_legs(a, idx, qlog, local, threads)
 
     if rank == 0:
+        roof = roofline_of(acc, nbk, seg_avg_ms, seg_src)
+        roof.update({"traffic": None, "traffic_source": None})
+        if mode == "replica":
+            pmc = load_pmc(wkey)
+            if pmc:
+                roof.update(pmc)
+        roof.update({
+            # the same bytes over the pipelined step time (consecutive batches
+            # overlap on the device; value's own clock)
+            "achieved_per_step": round((acc["algo"] / nbk) / (mres["seconds"] / a.steps) / 1e9, 1),
+            # the segment phase: lean_kernel with the general segment_kernel
+            # beside it on a second stream (HIP events fork -> join on the
+            # batch's stream; isolated: one batch at a time, nothing overlapping)
+            "lean_kernel_ms": round(lean_avg_ms, 4),
+            "isolated_launch_ms": round(iso_ms, 4),
+            "isolated_frac": round((acc["algo"] / nbk) / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "algo_bytes_rule": "SURVEY 8d: per query the docid+tf span bytes of every term's list "
+                               "(wsr_list_bytes) + 1 B per survivor + 12 B per result"})
         out = {
-            "metric": METRIC, "value": round(qps, 1), "unit": "queries/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 4),
+            "metric": METRIC, "value": mres["value"], "unit": "queries/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": mres["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32/f64",
             "data": "synthetic",
-            "config": {"workload": (f"C2: {a.docs} synthetic Zipf docs (V={a.vocab}, s=1.07), "
-                                    if not (a.vacuum_dir or a.linedoc) else
-                                    f"C3: Vacuum index {idx}, ") +
-                                   f"{len(lines)} two-term AND queries (gen_synthetic_log rule, "
-                                   f"seed 7), {a.batch} queries per GPU per step, top-{a.k}",
-                       "global_batch": global_batch, "parallelism": parallelism, "k": a.k},
+            "config": {"workload": workload_text(a, idx, len(lines)), "global_batch": a.batch * world,
+                       "parallelism": parallelism, "k": a.k},
             # p50 at the operating point: the end-to-end leg (strings in, results in host
             # memory, batches overlapped); p50_alone_ms: one resident batch by itself
-            "p50_ms": (extra["end_to_end"]["p50_ms"] if extra and "end_to_end" in extra else round(p50, 3)),
-            "p50_alone_ms": round(p50, 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         # the same bytes over the pipelined step time (consecutive
-                         # batches overlap on the device; value's own clock)
-                         "achieved_per_step": round((acc["algo"] / nbk) / (el / a.steps) / 1e9, 1),
-                         "traffic": traffic,
-                         "traffic_source": PMC_PROFILE if traffic else None,
-                         "traffic_fetch_size_raw": traffic_fetch,
-                         # the segment phase: lean_kernel with the general
-                         # segment_kernel beside it on a second stream (HIP events
-                         # fork -> join on the batch's stream, over the timed region;
-                         # isolated_launch_ms: one batch at a time, nothing overlapping)
-                         "kernel": "lean_kernel||segment_kernel",
-                         "algo_bytes_per_launch": int(acc["algo"] / nbk),
-                         "avg_launch_ms": round(seg_avg_ms, 4),
-                         "launch_ms_source": seg_src,
-                         "lean_kernel_ms": round(lean_avg_ms, 4),
-                         "isolated_launch_ms": round(iso_ms, 4),
-                         "isolated_frac": round((acc["algo"] / nbk) / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "p50_ms": (extra["end_to_end"]["p50_ms"] if extra and "end_to_end" in extra
+                       else mres["p50_alone_ms"]),
+            "p50_alone_ms": mres["p50_alone_ms"],
+            "roofline": roof,
             "cpu_baseline": cpu,
             "kernel_ms_per_batch": {"plan": round(acc["plan"] / nbk, 4),
                                     "segment": round(iso_ms, 4),
@@ -990,21 +1125,25 @@ def main():
         }
         out["runtime"] = runtime
         out["image"] = image   # HBM bytes of the engine image the value ran on
+        out["load_s"] = load_s
+        if built:
+            out["index_build"] = built
         # host time to enqueue the timed steps: close to ms_per_step = launch-bound
-        out["host_enqueue_ms_per_step"] = round(DIAG.get("host_enqueue_ms_per_step", 0.0), 4)
-        if sharded:
+        out["host_enqueue_ms_per_step"] = round(host_ms, 4)
+        if mode != "replica":
             kind = ("one ncclAllToAll of per-owner regions ({count, offset} pairs + fixed event slot) over "
-                    "xGMI per step (wsr_shard_step), no host round trip inside a step")
+                    "xGMI per sharded step (wsr_shard_step), no host round trip inside a step")
             if a.exchange == "gloo" and world > 1:
                 kind = ("REHEARSAL: fused emit / owner replay with the slots moved by gloo through "
                         "host memory (not the RCCL path's speed)")
-            out["exchange"] = {"kind": kind,
-                               "slot_events": getattr(S, "slot", None),
-                               "heavy_blocks": getattr(S, "heavy_blocks", None),
-                               "shard_every": getattr(S, "every", None),
-                               "heavy_query_share": round(getattr(S, "heavy_share", 0.0), 4)}
-        if control:
-            out["control"] = control
+            out["exchange"] = {"kind": kind, "slot_events": main_run["slot"],
+                               "heavy_blocks": main_run["heavy_blocks"],
+                               "shard_every": main_run["every"],
+                               "heavy_query_share": round(main_run["heavy_share"], 4)}
+            out["hbm_per_rank"] = {"shard_image_bytes": shard_bytes, "full_image_bytes": full_bytes,
+                                   "total_bytes": (shard_bytes or 0) + (full_bytes or 0)}
+        if forms:
+            out["forms"] = forms
         if extra:
             out["legs"] = extra
         print(json.dumps(out), flush=True)

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <fcntl.h>
@@ -1645,6 +1646,65 @@ int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads,
     for (auto& t : ts) t.join();
   }
   return nq;
+}
+
+// CPU baseline timing (bench.py cpu_baseline): `threads` workers share the
+// read-only index, as the reference's gRPC threads share one engine
+// (grpc_server_impl.h:260-263).  The log is parsed once, the workers are
+// started and parked before the clock starts, each query's results go to the
+// worker's own preallocated arrays, and the workers take queries from one
+// shared counter (the log cycled) until the main thread stops them after
+// `seconds`.  Nothing is spawned, parsed or converted inside the interval.
+int orc_vacuum_bench_lines(orc_vacuum* h, const char* text, int k, int threads, double seconds,
+                           int64_t* done_out, double* elapsed_out) {
+  struct Q { std::vector<std::string> terms; std::vector<const char*> ptr; bool phrase; };
+  std::vector<Q> qs;
+  for (auto& raw : explode(text, '\n')) {
+    std::string line = raw;
+    const bool phrase = line.size() >= 2 && line.front() == '"' && line.back() == '"';
+    if (phrase) line = line.substr(1, line.size() - 2);
+    Q q;
+    q.terms = explode(line, ' ');
+    q.terms.erase(std::remove(q.terms.begin(), q.terms.end(), std::string()), q.terms.end());
+    if (q.terms.empty()) continue;
+    for (auto& s : q.terms) q.ptr.push_back(s.c_str());
+    q.phrase = phrase;
+    qs.push_back(std::move(q));
+  }
+  if (qs.empty() || threads < 1 || k < 1) return -1;
+  std::atomic<int64_t> next{0};
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false}, stop{false};
+  std::vector<int64_t> done(threads, 0);
+  auto work = [&](int t) {
+    std::vector<int32_t> docs(k);
+    std::vector<double> scores(k);
+    ready.fetch_add(1);
+    while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+    int64_t n = 0;
+    while (!stop.load(std::memory_order_relaxed)) {
+      const Q& q = qs[static_cast<size_t>(next.fetch_add(1, std::memory_order_relaxed) %
+                                          static_cast<int64_t>(qs.size()))];
+      orc_vacuum_search_phrase(h, q.ptr.data(), static_cast<int>(q.ptr.size()), k, q.phrase,
+                               docs.data(), scores.data(), nullptr);
+      ++n;
+    }
+    done[t] = n;
+  };
+  std::vector<std::thread> ts;
+  for (int i = 0; i < threads; ++i) ts.emplace_back(work, i);
+  while (ready.load() < threads) std::this_thread::yield();
+  const auto t0 = std::chrono::steady_clock::now();
+  go.store(true, std::memory_order_release);
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  stop.store(true);
+  for (auto& t : ts) t.join();
+  const auto t1 = std::chrono::steady_clock::now();
+  int64_t total = 0;
+  for (int64_t n : done) total += n;
+  *done_out = total;
+  *elapsed_out = std::chrono::duration<double>(t1 - t0).count();
+  return 0;
 }
 
 // QqMemEngineDelta::LoadLocalDocuments / AddDocument (qq_mem_engine.h:271-305):

@@ -89,6 +89,11 @@ int orc_vacuum_offsets(orc_vacuum* h, const char* term, int posting, int32_t* ou
  * Outputs are nq*k arrays plus n per query.  threads >= 1.  Returns nq. */
 int orc_vacuum_search_lines(orc_vacuum* h, const char* text, int k, int threads,
                             int32_t* docs, double* scores, int32_t* n_out, int max_q);
+/* CPU-baseline timing: `threads` persistent workers run the log's queries
+ * (cycled) for `seconds`; no spawn, parse or result conversion inside the
+ * interval.  Outputs the queries completed and the interval.  Returns 0. */
+int orc_vacuum_bench_lines(orc_vacuum* h, const char* text, int k, int threads, double seconds,
+                           int64_t* done_out, double* elapsed_out);
 
 /* ---- QqMem (in-memory, varint postings) engine restatement ----------- */
 orc_qqmem* orc_qqmem_load(const char* linedoc, int64_t n_rows, const char* format);

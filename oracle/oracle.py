@@ -50,6 +50,8 @@ for name, res, args in [
                                    _I32P, C.c_int]),
     ("orc_vacuum_search_lines", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, _I32P, _F64P, _I32P,
                                           C.c_int]),
+    ("orc_vacuum_bench_lines", C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, C.c_double,
+                                         C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     ("orc_qqmem_load", _P, [C.c_char_p, C.c_int64, C.c_char_p]),
     ("orc_qqmem_close", None, [_P]),
     ("orc_qqmem_term_count", C.c_int, [_P]),
@@ -225,6 +227,19 @@ class OracleVacuum:
         nout = (C.c_int32 * nq)()
         lib.orc_vacuum_search_lines(self.h, text, k, threads, docs, scores, nout, nq)
         return [[(docs[q * k + i], scores[q * k + i]) for i in range(nout[q])] for q in range(nq)]
+
+
+    def bench_lines(self, lines, k, threads, seconds, phrases=None):
+        """(queries, seconds): `threads` persistent C++ workers over the log
+        (cycled) for `seconds` (orc_vacuum_bench_lines)."""
+        def fmt(i, t):
+            q = " ".join(t)
+            return f'"{q}"' if phrases is not None and phrases[i] else q
+        text = "\n".join(fmt(i, t) for i, t in enumerate(lines)).encode()
+        done, el = C.c_int64(), C.c_double()
+        if lib.orc_vacuum_bench_lines(self.h, text, k, threads, seconds, C.byref(done), C.byref(el)) != 0:
+            raise RuntimeError("orc_vacuum_bench_lines failed")
+        return done.value, el.value
 
 
 class OracleQqMem:

@@ -7,8 +7,10 @@ rest; write = 64 x WRREQ_64B + 32 x the rest.  scripts/calib_ea.hip checks the
 formula on known byte counts (stream) and gives bytes per line of the engine's
 gather shapes.
 
-Usage: pmc_bytes.py PMC_DIR [KERNEL[,KERNEL...] OUT_JSON]
-Without kernels: prints every kernel's per-dispatch averages.
+Usage: pmc_bytes.py PMC_DIR [KERNEL[,KERNEL...] OUT_JSON [BENCH_JSON]]
+Without kernels: prints every kernel's per-dispatch averages.  BENCH_JSON: the
+bench line of a profiled pass; its workload and algorithmic bytes per launch
+are recorded beside the counter bytes.
 """
 import csv
 import glob
@@ -62,5 +64,13 @@ if __name__ == "__main__":
            "hbm_bytes_per_launch": tot.get("read_bytes", 0.0) + tot.get("write_bytes", 0.0),
            "formula": "read = 128*RDREQ_128B + 32*RDREQ_32B + 64*(RDREQ - both); "
                       "write = 64*WRREQ_64B + 32*(WRREQ - WRREQ_64B) (TCC_EA0, all channels)"}
+    if len(sys.argv) > 4:
+        try:
+            b = json.loads(open(sys.argv[4]).read().strip().splitlines()[-1])
+            res["algo_bytes_per_launch"] = b["roofline"]["algo_bytes_per_launch"]
+            res["workload"] = b["config"]["workload"]
+            res["traffic_over_algo"] = res["hbm_bytes_per_launch"] / res["algo_bytes_per_launch"]
+        except (OSError, ValueError, KeyError, IndexError):
+            pass
     json.dump(res, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(res, indent=1))

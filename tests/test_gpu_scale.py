@@ -4,7 +4,9 @@ by bench.py, C3 never run):
     2,048 queries of its logged two-term workload, bit for bit against the oracle;
   * C3 stand-in (configs[2]): the en-Wikipedia-shaped corpus (df histogram of
     gen_synthetic_log.py:8-16) at 1/10 of its terms over 500k docs, its
-    two-term log, bit for bit;
+    two-term log, bit for bit; and at its full size (5.5 M docs, 5.64 M terms,
+    the bench's headline index): 2,048 queries spread over the whole 100k log,
+    and 2,048 mixed 1-5 term queries (configs[3]'s mix), bit for bit;
   * the whole Search chain from query strings (wsr_search_text).
 """
 import os
@@ -34,20 +36,34 @@ def c3_small(built, tmp_path_factory):
     return d, log, st
 
 
-def _check_log(d, log, nq, k=10, stride=7):
+@pytest.fixture(scope="module")
+def c3_full(built, tmp_path_factory):
+    """The bench's headline index: the stand-in at its full size (~35 s)."""
+    import wiser_amd as w
+    d = str(tmp_path_factory.mktemp("c3full"))
+    st = w.build_wiki_standin(d, n_docs=5_500_000, term_scale=1.0, threads=min(16, os.cpu_count()))
+    log = os.path.join(d, "two_term_100000.log")
+    w.gen_two_term_log(d, log, n_queries=100_000, seed=7)
+    return d, log, st
+
+
+def _check_log(d, log, nq, k=10, stride=7, eng=None):
     import wiser_amd as w
     from oracle.oracle import OracleVacuum
     lines = [l.split() for l in open(log).read().splitlines()]
     # spread over the whole log: every stride-th query
     qs = lines[::stride][:nq]
-    eng = w.VacuumEngine(d, positions=False)
-    eng.Load()
+    own = eng is None
+    if own:
+        eng = w.VacuumEngine(d, positions=False)
+        eng.Load()
     res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
     orc = OracleVacuum(d)
     want = orc.search_lines(qs, k, threads=min(16, os.cpu_count()))
     bad = [(q, [(e.doc_id, e.doc_score) for e in r.entries][:3], x[:3])
            for q, r, x in zip(qs, res, want) if [(e.doc_id, e.doc_score) for e in r.entries] != x]
-    eng.close()
+    if own:
+        eng.close()
     orc.close()
     assert not bad, bad[:3]
     return sum(1 for x in want if x)
@@ -70,6 +86,36 @@ def test_c3_standin_logged_queries(c3_small):
     d, log, st = c3_small
     assert st.n_terms > 500_000
     _check_log(d, log, 2048, stride=5)
+
+
+@pytest.fixture(scope="module")
+def c3_full_engine(c3_full):
+    import wiser_amd as w
+    eng = w.VacuumEngine(c3_full[0], positions=False)
+    eng.Load()
+    yield eng
+    eng.close()
+
+
+def test_c3_full_size_logged_queries(c3_full, c3_full_engine):
+    """configs[2] at the headline size: 2,048 queries, every 48th of the 100k
+    log (so all of it is sampled), top-10, bit for bit against the oracle."""
+    d, log, st = c3_full
+    assert st.n_docs == 5_500_000 and st.n_terms > 5_000_000
+    nonempty = _check_log(d, log, 2048, stride=48, eng=c3_full_engine)
+    assert nonempty > 100
+
+
+def test_c3_full_size_mixed_1to5(c3_full, c3_full_engine):
+    """configs[3]'s query mix (1-5 AND terms, AOL shares) over the full-size
+    stand-in, 2,048 queries, top-10, bit for bit."""
+    import wiser_amd as w
+    d, _, _ = c3_full
+    mixed = os.path.join(d, "mixed_20000.log")
+    w.gen_mixed_log(d, mixed, n_queries=20_000, seed=7)
+    lens = [len(l.split()) for l in open(mixed).read().splitlines()]
+    assert set(lens) == {1, 2, 3, 4, 5}
+    _check_log(d, mixed, 2048, stride=9, eng=c3_full_engine)
 
 
 def test_search_text_chain(c3_small):
