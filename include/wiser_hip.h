@@ -42,17 +42,18 @@
 extern "C" {
 #endif
 
-#define WSR_MAX_TERMS 16        /* terms of a conjunctive query */
+#define WSR_MAX_TERMS 16        /* terms held in wsr_query.list_ids (more: wsr_query.more_ids) */
+#define WSR_MAX_QUERY_TERMS 1024 /* terms of a conjunctive query (AOL's longest query has 245) */
 #define WSR_MAX_PHRASE_TERMS 8  /* terms of a phrase query (the reference's cap, query_processing.h:695) */
 #define WSR_MAX_K 1024          /* n_results (k > 64 keeps the replay's heap in LDS) */
-#define WSR_SERVER_MAX_K 64     /* n_results through the micro-batcher (wsr_server_*) */
+#define WSR_SERVER_MAX_K WSR_MAX_K  /* n_results through the micro-batcher (wsr_server_*) */
 
 enum {
   WSR_OK = 0,
   WSR_E_INVALID = -1,   /* bad argument */
   WSR_E_IO = -2,        /* missing / malformed index files */
   WSR_E_HIP = -3,       /* HIP runtime error (no device, out of memory, ...) */
-  WSR_E_LIMIT = -4,     /* n_terms > WSR_MAX_TERMS (phrase: WSR_MAX_PHRASE_TERMS) or k > WSR_MAX_K */
+  WSR_E_LIMIT = -4,     /* n_terms > WSR_MAX_QUERY_TERMS (phrase: WSR_MAX_PHRASE_TERMS) or k > WSR_MAX_K */
   WSR_E_INTERNAL = -5
 };
 
@@ -72,11 +73,15 @@ typedef struct wsr_open_opts {
 typedef struct wsr_query {
   int32_t n_terms;
   int32_t k;          /* n_results; 0 => empty result */
-  int32_t list_ids[WSR_MAX_TERMS];
+  int32_t list_ids[WSR_MAX_TERMS];   /* terms 0 .. min(n_terms, 16) - 1 */
   int32_t flags;      /* WSR_QUERY_PHRASE: SearchQuery::is_phrase (types.h:205-256) --
                          a doc is ranked only if the terms occur at consecutive
                          positions (QueryProcessor::HandleTheFoundDoc,
                          query_processing.h:854-912); needs positions at wsr_open */
+  const int32_t* more_ids;   /* n_terms > WSR_MAX_TERMS: list ids of terms 16 .. n_terms - 1
+                                (caller's memory, read during the call that takes the
+                                query; the reference's conjunctive processor has no
+                                term cap, query_processing.h:710-728,810-852) */
 } wsr_query;
 #define WSR_QUERY_PHRASE 1
 
@@ -179,7 +184,9 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t hit_
  * query_pool.h:319-378): one query per line, terms separated by spaces, a
  * line in double quotes is a phrase query.  Every term is resolved through the
  * term index (VacuumInvertedIndex::FindIteratorsSolid, vacuum_engine.h:89-99);
- * q[0..*nq) receives the queries (k results each). */
+ * q[0..*nq) receives the queries (k results each).  The more_ids of a query
+ * with more than WSR_MAX_TERMS terms point into storage owned by the calling
+ * thread, valid until that thread's next wsr_resolve_text call. */
 int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t max_q,
                      wsr_query* q, int32_t* nq);
 /* The whole Search chain from strings: wsr_resolve_text, then wsr_search_batch
@@ -219,7 +226,9 @@ int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_
  * engine (grpc_server_impl.h:260-263,382-389).  wsr_server_search() may be
  * called from any number of threads; a dispatcher thread coalesces the calls
  * that arrive within window_us (or until max_batch are queued) into one GPU
- * batch, two batches alternating.  Each call blocks until its own result. */
+ * batch; up to four batches are in flight, each on its own streams, and a
+ * completer thread retires them in launch order and hands every caller its
+ * result.  Each call blocks until its own result. */
 typedef struct wsr_server wsr_server;
 typedef struct wsr_serve_stats {
   uint64_t queries;      /* completed in the run */
@@ -230,7 +239,7 @@ typedef struct wsr_serve_stats {
 } wsr_serve_stats;
 int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_server** out);
 void wsr_server_close(wsr_server* s);
-/* one query (k <= WSR_SERVER_MAX_K): hits receives n_hits <= k entries */
+/* one query (k <= WSR_SERVER_MAX_K = WSR_MAX_K): hits receives n_hits <= k entries */
 int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t* n_hits);
 /* closed-loop load (the reference client's threads, grpc_client_impl.h:557-620):
  * n_clients threads keep `depth` queries each in flight, drawn round-robin from
@@ -312,6 +321,22 @@ int wsr_comm_unique_id(uint8_t* id /* WSR_COMM_ID_BYTES */);
 int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device, wsr_comm** out);
 void wsr_comm_close(wsr_comm* c);
 int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot);
+/* wsr_shard_step's two device halves with the transfer left to the caller (a
+ * multi-rank rehearsal on one GPU, where RCCL refuses two ranks, or a host
+ * exchange): the engine's own region buffers, in the exact layout the step's
+ * ncclAllToAll moves -- world regions of *region_bytes (wsr_shard_step_regions);
+ * region o = the {count, offset} pairs of owner o's q_per_owner queries,
+ * padded to whole 16-byte events, then owner o's slot of `slot` events.
+ * wsr_shard_step_emit runs the batch with fused emission and copies the send
+ * regions to host_send (world * region_bytes); the caller delivers region o of
+ * every rank g to rank o as its region g; wsr_shard_step_replay copies those
+ * (host_recv, world * region_bytes) to the device and replays this rank's
+ * owned queries on the batch's stream. */
+int wsr_shard_step_regions(int32_t q_per_owner, int64_t slot, uint64_t* region_bytes);
+int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                        void* host_send);
+int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
+                          int64_t slot, const void* host_recv);
 
 /* Decode one block of a list on the device (test hook for the decoder):
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */

@@ -94,24 +94,28 @@ class VacuumHipEngine {
 
   std::vector<SearchResult> SearchBatch(const std::vector<SearchQuery>& qs) {
     std::vector<wsr_query> in(qs.size());
+    std::vector<std::vector<int32_t>> more(qs.size());   // terms past WSR_MAX_TERMS
     std::vector<std::vector<int>> freqs(qs.size());
     std::vector<bool> empty(qs.size(), false);
     int stride = 1;
     for (size_t i = 0; i < qs.size(); ++i) {
       const SearchQuery& q = qs[i];
-      if (q.terms.size() > WSR_MAX_TERMS || q.n_results > WSR_MAX_K)
+      if (q.terms.size() > WSR_MAX_QUERY_TERMS || q.n_results > WSR_MAX_K)
         throw std::runtime_error("query over the engine limits");
       wsr_query& w = in[i];
+      w.more_ids = nullptr;
       w.k = q.n_results < 0 ? 0 : q.n_results;
       w.flags = (q.is_phrase && q.terms.size() > 1) ? WSR_QUERY_PHRASE : 0;
       bool missing = q.terms.empty();
       for (size_t t = 0; t < q.terms.size(); ++t) {
         int32_t id, df;
         check(wsr_lookup(h_, q.terms[t].c_str(), &id, &df));
-        w.list_ids[t] = id;
+        if (t < WSR_MAX_TERMS) w.list_ids[t] = id;
+        else more[i].push_back(id);
         if (id < 0) missing = true;
         freqs[i].push_back(df);
       }
+      if (!more[i].empty()) w.more_ids = more[i].data();
       empty[i] = missing || w.k == 0;
       w.n_terms = empty[i] ? 0 : static_cast<int32_t>(q.terms.size());
       if (w.k > stride) stride = w.k;

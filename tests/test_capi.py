@@ -53,14 +53,16 @@ def test_struct_layouts(built, tmp_path):
     from wiser_amd import _capi
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "wiser_hip.h"\n'
-                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(wsr_query),'
-                   ' offsetof(wsr_query, flags), sizeof(wsr_hit), sizeof(wsr_open_opts),'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(wsr_query),'
+                   ' offsetof(wsr_query, flags), offsetof(wsr_query, more_ids), sizeof(wsr_hit),'
+                   ' sizeof(wsr_open_opts),'
                    ' offsetof(wsr_open_opts, positions), sizeof(wsr_batch_stats),'
                    ' sizeof(wsr_build_stats)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
-    assert got == [C.sizeof(_capi.Query), _capi.Query.flags.offset, C.sizeof(_capi.Hit),
+    assert got == [C.sizeof(_capi.Query), _capi.Query.flags.offset, _capi.Query.more_ids.offset,
+                   C.sizeof(_capi.Hit),
                    C.sizeof(_capi.OpenOpts), _capi.OpenOpts.positions.offset,
                    C.sizeof(_capi.BatchStats), C.sizeof(_capi.BuildStats)]
-    assert C.sizeof(_capi.Query) == 76 and C.sizeof(_capi.Hit) == 16
+    assert C.sizeof(_capi.Query) == 88 and C.sizeof(_capi.Hit) == 16

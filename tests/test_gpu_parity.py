@@ -222,7 +222,7 @@ def test_limits_fail_loudly(gpu_indexes):
     with pytest.raises(NotImplementedError):
         eng.Search(w.SearchQuery(["hello"], n_results=1025))
     with pytest.raises(NotImplementedError):
-        eng.Search(w.SearchQuery(["hello"] * 17))
+        eng.Search(w.SearchQuery(["hello"] * 1025))
 
 
 @pytest.mark.parametrize("mode", sorted(DENSE_MODES))
@@ -280,8 +280,10 @@ def test_wide_k(synth_small, mode):
 
 @pytest.mark.parametrize("mode", ["blocks", "dense", "dense_all"])
 def test_many_terms(synth_small, mode):
-    """Conjunctive queries of 9 to 16 terms (at most 8 before); the
-    phrase cap stays 8 (query_processing.h:695) and a longer phrase is refused."""
+    """Conjunctive queries of 9 to 16 terms inline, and of 17 to 40 terms
+    through the batch's term table (the reference's processor
+    has no term cap, query_processing.h:710-728,810-852); the phrase cap stays
+    8 (query_processing.h:695) and a longer phrase is refused."""
     from oracle.oracle import OracleVacuum
     import wiser_amd as w
     from wiser_amd import _capi
@@ -290,8 +292,13 @@ def test_many_terms(synth_small, mode):
     orc = OracleVacuum(d)
     head = [f"t{i:07d}" for i in range(24)]
     rng = random.Random(6)
-    qs = [rng.sample(head, n) for n in (9, 10, 12, 12, 14, 16, 16) for _ in range(6)]
+    head = [f"t{i:07d}" for i in range(48)]
+    qs = [rng.sample(head[:24], n) for n in (9, 10, 12, 12, 14, 16, 16) for _ in range(6)]
     qs += [head[:12] + head[:4]]   # duplicates: each occurrence scores
+    # past the inline 16: 17, 24 and 40 terms (the driver among the last ones
+    # too), and a 40-term query of repeated head words
+    qs += [rng.sample(head, n) for n in (17, 24, 24, 40) for _ in range(5)]
+    qs += [head[:6] * 4, (head[:3] * 8) + head[40:42], head[:20] + head[:20]]
     for k in (10, 100):
         res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
         for q, r in zip(qs, res):
@@ -300,6 +307,16 @@ def test_many_terms(synth_small, mode):
     assert nonempty > 10
     with pytest.raises(_capi.WiserError, match="LIMIT"):
         eng.SearchBatch([w.SearchQuery(head[:9], is_phrase=True)])
-    with pytest.raises(NotImplementedError):
-        eng.SearchBatch([w.SearchQuery(head[:17])])
+    # mixed with short queries in one batch, through the text path as well
+    long_q = [q for q in qs if len(q) > 16]
+    text = "\n".join(" ".join(q) for q in long_q + qs[:5]).encode()
+    import ctypes as C
+    n = len(long_q) + 5
+    hits = (_capi.Hit * (n * 10))()
+    nh = (C.c_int32 * n)()
+    nq = C.c_int32()
+    _capi.check(_capi.lib.wsr_search_text(eng._h, text, len(text), 10, 10, n, hits, nh, C.byref(nq)))
+    assert nq.value == n
+    for i, q in enumerate(long_q + qs[:5]):
+        assert [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] == orc.search(q, 10)[0]
     eng.close()

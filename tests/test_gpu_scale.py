@@ -177,3 +177,29 @@ def test_image_info(c3_small):
     assert info["pos_bytes"] <= 8 * len(parts)   # positions off: only the 1-element placeholders
     assert 0 < info["dense_lists"] < info["n_lists"]
     assert info["blob_bytes"] < st.vacuum_bytes
+
+
+def test_c5_full_size_phrases(c3_full):
+    """configs[4]'s phrase queries over the full-size stand-in (its phrase
+    pool, gen_synthetic_log.py:216-265 shape): 2,048 phrase queries, top-10,
+    bit for bit against the oracle's PhraseQueryProcessor2 restatement, and a
+    good share of them must find docs."""
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    d, _, _ = c3_full
+    log = os.path.join(d, "phrase_10000.log")
+    w.gen_phrase_log(d, log, n_queries=10_000, seed=7)
+    items = w.read_query_log(log)
+    assert all(ph and len(t) == 2 for t, ph in items)
+    qs = [t for t, _ in items][::4][:2048]
+    eng = w.VacuumEngine(d, positions=True)
+    eng.Load()
+    res = eng.SearchBatch([w.SearchQuery(q, n_results=10, is_phrase=True) for q in qs])
+    eng.close()
+    orc = OracleVacuum(d)
+    want = orc.search_lines(qs, 10, threads=min(16, os.cpu_count()), phrases=[True] * len(qs))
+    orc.close()
+    bad = [(q, [(e.doc_id, e.doc_score) for e in r.entries][:3], x[:3])
+           for q, r, x in zip(qs, res, want) if [(e.doc_id, e.doc_score) for e in r.entries] != x]
+    assert not bad, bad[:3]
+    assert sum(1 for x in want if x) > len(qs) // 2

@@ -25,7 +25,10 @@ def test_concurrent_search_matches_oracle(synth_small):
     rng = random.Random(9)
     head = [f"t{i:07d}" for i in range(40)]
     qs += [rng.sample(head, rng.randint(1, 4)) for _ in range(300)]
-    items = [(q, i % 3 == 0 and len(q) > 1, [1, 5, 10, 64][i % 4]) for i, q in enumerate(qs)]
+    # k up to the batch limit (64 was the server's cap) and
+    # queries past the 16 inline terms
+    qs += [rng.sample(head, rng.randint(17, 30)) for _ in range(20)]
+    items = [(q, i % 3 == 0 and 1 < len(q) <= 8, [1, 5, 10, 64, 100, 300][i % 6]) for i, q in enumerate(qs)]
     got = [None] * len(items)
     errors = []
 

@@ -332,3 +332,88 @@ def test_fixed_slot_wide_k(synth_small, world):
     qs2, got = _run_sharded_fixed(d, qs, 200, world, slot=4096 * qpr)
     for q, g in zip(qs2, got):
         assert g == o.search(q, 200)[0], (world, q)
+
+
+def _run_step_regions(index_dir, queries, k, world, slot):
+    """wsr_shard_step's own buffers at W > 1: every shard runs
+    wsr_shard_step_emit (fused emission into the engine's region buffer, owner
+    o's {count, offset} block inside region o, region stride = meta + slot), the
+    regions are moved exactly as ncclAllToAll moves them (region o of rank g ->
+    region g of rank o), and wsr_shard_step_replay replays each owner."""
+    import numpy as np
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd._capi import check, lib
+    from wiser_amd.shard import index_doc_count, shard_range
+    qpr = len(queries) // world
+    queries = queries[:qpr * world]
+    n = index_doc_count(index_dir)
+    rb = C.c_uint64()
+    check(lib.wsr_shard_step_regions(qpr, slot, C.byref(rb)))
+    words = rb.value // 8
+    engs, batches, sends = [], [], []
+    try:
+        for r in range(world):
+            e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
+            e.Load()
+            engs.append(e)
+            arr = (_capi.Query * len(queries))()
+            for i, q in enumerate(queries):
+                arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
+            b = w.ResidentBatch(e, len(queries), k)
+            batches.append(b)
+            b.upload(arr)
+            send = np.full(world * words, -7, dtype=np.int64)
+            check(lib.wsr_shard_step_emit(e._h, b._b, world, qpr, slot, C.c_void_p(send.ctypes.data)))
+            sends.append(send.reshape(world, words))
+        out = []
+        for o in range(world):
+            recv = np.ascontiguousarray(np.stack([sends[g][o] for g in range(world)]))
+            e, b = engs[o], batches[o]
+            check(lib.wsr_shard_step_replay(e._h, b._b, o, world, qpr, slot, C.c_void_p(recv.ctypes.data)))
+            hits = (_capi.Hit * (qpr * k))()
+            nh = (C.c_int32 * qpr)()
+            rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
+            if rc:
+                raise _capi.WiserError(rc, lib.wsr_last_error().decode())
+            for i in range(qpr):
+                out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
+        return queries, out
+    finally:
+        for b in batches:
+            b.close()
+        for e in engs:
+            e.close()
+
+
+@pytest.mark.parametrize("world,k", [(2, 10), (3, 10), (8, 10), (3, 200)])
+def test_step_regions_equal_oracle(synth_small, world, k):
+    """The native step's region layout (in-region meta, region stride, one
+    all-to-all of whole regions) at W = 2, 3, 8, narrow and wide k."""
+    from oracle.oracle import OracleVacuum
+    import wiser_amd as w
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_regions.log")
+    w.gen_two_term_log(d, log, n_queries=960, seed=17)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    if k > 64:
+        qs = qs[:240]
+    o = OracleVacuum(d)
+    qpr = len(qs) // world
+    # an odd q_per_owner pads the meta block to whole events
+    if qpr % 2 == 0:
+        qpr -= 1
+    qs = qs[:qpr * world]
+    qs2, got = _run_step_regions(d, qs, k, world, slot=(4096 if k > 64 else 64) * qpr)
+    for q, g in zip(qs2, got):
+        assert g == o.search(q, k)[0], (world, k, q)
+
+
+def test_step_regions_overflow_is_loud(synth_small):
+    import wiser_amd as w  # noqa: F401
+    from wiser_amd import _capi
+    d, _ = synth_small
+    head = [f"t{i:07d}" for i in range(8)]
+    qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
+    with pytest.raises(_capi.WiserError, match="exchange slot"):
+        _run_step_regions(d, qs, 10, 2, slot=4)

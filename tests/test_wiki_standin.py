@@ -59,3 +59,44 @@ def test_deterministic(tiny, tmp_path):
     w.build_wiki_standin(d2, n_docs=20_000, term_scale=0.002, threads=2)
     for f in ("my.vacuum", "my.tip", "my.doc_length"):
         assert open(os.path.join(d, f), "rb").read() == open(os.path.join(d2, f), "rb").read(), f
+
+
+def test_phrase_pool_and_positions(tiny):
+    """The stand-in's phrase pool (gen_synthetic_log.py:216-252 shape: pairs,
+    no term in two) and position bags: every bag is tf distinct sorted
+    positions below the doc's length; a pair's second word follows its first
+    in a share of the docs that hold both, so phrase queries find docs."""
+    from oracle.oracle import OracleVacuum
+    d, st = tiny
+    pairs = [l.split() for l in open(os.path.join(d, "phrases.txt")).read().splitlines()]
+    assert len(pairs) > 10
+    flat = [t for p in pairs for t in p]
+    assert len(flat) == len(set(flat)) and all(len(p) == 2 and p[0] != p[1] for p in pairs)
+    orc = OracleVacuum(d)
+    n = orc.n_docs()
+    lens = [0] * n
+    for i in range(st.n_terms):
+        docs, tfs = orc.postings(f"w{i:08d}")
+        for x, t in zip(docs, tfs):
+            lens[x] += t
+    both = adjacent = 0
+    for a, b in pairs[:40]:
+        da, _ = orc.postings(a)
+        db, tb = orc.postings(b)
+        assert orc.df(b) == len(db)
+        pos_a = {}
+        for j, x in enumerate(da):
+            p = orc.positions(a, j)
+            assert p == sorted(set(p)) and all(0 <= v < lens[x] for v in p)
+            pos_a[x] = p
+        for j, x in enumerate(db):
+            p = orc.positions(b, j)
+            assert len(p) == tb[j] and p == sorted(set(p)) and all(0 <= v < lens[x] for v in p)
+            if x in pos_a:
+                both += 1
+                adjacent += any(v + 1 in p for v in pos_a[x])
+        got, _ = orc.search([a, b], 10, phrase=True)
+        assert all(x in pos_a for x, _ in got)
+    # b's docs share half of the smaller list with a; 60 % of those are phrases
+    assert both > 100 and 0.45 < adjacent / both < 0.8, (both, adjacent)
+    orc.close()

@@ -15,10 +15,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WISER_HIP_LIB") or os.path.join(HERE, "_lib", "libwiser_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "wiser_hip.h")
 
-MAX_TERMS = 16
+MAX_TERMS = 16            # terms held in Query.list_ids (more: Query.more_ids)
+MAX_QUERY_TERMS = 1024
 MAX_PHRASE_TERMS = 8
 MAX_K = 1024
-SERVER_MAX_K = 64
+SERVER_MAX_K = MAX_K
 
 WSR_OK = 0
 E_INVALID, E_IO, E_HIP, E_LIMIT, E_INTERNAL = -1, -2, -3, -4, -5
@@ -36,7 +37,7 @@ class OpenOpts(C.Structure):
 
 class Query(C.Structure):
     _fields_ = [("n_terms", C.c_int32), ("k", C.c_int32), ("list_ids", C.c_int32 * MAX_TERMS),
-                ("flags", C.c_int32)]
+                ("flags", C.c_int32), ("more_ids", C.POINTER(C.c_int32))]
 
 
 class Hit(C.Structure):
@@ -126,6 +127,9 @@ _sigs = {
     "wsr_comm_close": (None, [_P]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
     "wsr_shard_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
+    "wsr_shard_step_regions": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint64)]),
+    "wsr_shard_step_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
+    "wsr_shard_step_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_debug_replay_profile": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "wsr_owner_replay_meta": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,

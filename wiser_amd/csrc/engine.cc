@@ -34,10 +34,27 @@ using namespace wiser;
 namespace {
 thread_local std::string g_err;
 
+// the list ids of a query in query order (list_ids, then more_ids)
+std::vector<int32_t> query_terms(const wsr_query& q) {
+  std::vector<int32_t> t(q.n_terms > 0 ? static_cast<size_t>(q.n_terms) : 0u);
+  for (int i = 0; i < q.n_terms; ++i) t[i] = i < WSR_MAX_TERMS ? q.list_ids[i] : q.more_ids[i - WSR_MAX_TERMS];
+  return t;
+}
+
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+}  // namespace
+
+namespace wiser {
+// (server.cc: a request failed on the dispatcher thread; its caller's thread
+// gets the message)
+void set_last_error(const std::string& msg) { g_err = msg; }
+}  // namespace wiser
+
+namespace {
 
 #define HIP_OK(expr)                                                                   \
   do {                                                                                 \
@@ -108,7 +125,8 @@ struct wsr_handle {
 
 struct wsr_batch {
   int max_q = 0, stride = 0, nq = 0;
-  QueryIn* d_q = nullptr;
+  QueryIn* d_q = nullptr;          // QueryIn[nq], then the term table of queries over kMaxTerms
+  size_t q_cap = 0;                // bytes of d_q
   QueryPlan* d_plan = nullptr;
   QueryDesc* d_desc = nullptr;     // lean queries' work records
   PlanPart* d_part = nullptr;      // plan pass 1 -> 2 partial sums, per kPlanThreads queries
@@ -349,10 +367,11 @@ int copy_out(const std::string& s, char* out, int32_t cap, int32_t* len) {
 }
 
 int check_snippet_query(const VacuumIndex& idx, const DocStore& docs, const wsr_query* q) {
-  if (q->n_terms < 1 || q->n_terms > WSR_MAX_TERMS) return fail(WSR_E_LIMIT, "bad term count");
+  if (q->n_terms < 1 || q->n_terms > WSR_MAX_QUERY_TERMS) return fail(WSR_E_LIMIT, "bad term count");
+  if (q->n_terms > WSR_MAX_TERMS && !q->more_ids) return fail(WSR_E_INVALID, "more_ids missing");
   if (!docs.is_open()) return fail(WSR_E_INVALID, "the index has no doc store (my.fdx / my.fdt)");
-  for (int i = 0; i < q->n_terms; ++i)
-    if (q->list_ids[i] < 0 || q->list_ids[i] >= idx.n_lists())
+  for (int32_t id : query_terms(*q))
+    if (id < 0 || id >= idx.n_lists())
       return fail(WSR_E_INVALID, "a query term is not in the index (no result entries)");
   return WSR_OK;
 }
@@ -363,7 +382,8 @@ int snippet_of(const VacuumIndex& idx, const SkipRowCache& rows, const DocStore&
   const int rc = check_snippet_query(idx, docs, q);
   if (rc != WSR_OK) return rc;
   try {
-    return copy_out(make_snippet(idx, rows, docs, q->list_ids, q->n_terms,
+    const std::vector<int32_t> ids = query_terms(*q);
+    return copy_out(make_snippet(idx, rows, docs, ids.data(), q->n_terms,
                                  (q->flags & WSR_QUERY_PHRASE) != 0, doc, n_passages),
                     out, cap, len);
   } catch (const std::exception& e) {
@@ -409,8 +429,9 @@ int wsr_snippets_batch(wsr_handle* h, const wsr_query* q, int32_t nq, const wsr_
     for (size_t w; (w = next.fetch_add(1)) < work.size();) {
       const int32_t i = work[w].first, j = work[w].second;
       try {
+        const std::vector<int32_t> ids = query_terms(q[i]);
         out[static_cast<size_t>(i) * stride + j] =
-            make_snippet(h->idx, *h->rows, h->docs, q[i].list_ids, q[i].n_terms,
+            make_snippet(h->idx, *h->rows, h->docs, ids.data(), q[i].n_terms,
                          (q[i].flags & WSR_QUERY_PHRASE) != 0, hits[static_cast<size_t>(i) * stride + j].doc_id,
                          n_passages);
       } catch (const std::exception& e) {
@@ -509,7 +530,8 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipSetDevice(h->device));
     b->max_q = max_q;
     b->stride = stride;
-    HIP_OK(hipMalloc(&b->d_q, sizeof(QueryIn) * max_q));
+    b->q_cap = sizeof(QueryIn) * max_q;
+    HIP_OK(hipMalloc(&b->d_q, b->q_cap));
     HIP_OK(hipMalloc(&b->d_plan, sizeof(QueryPlan) * max_q));
     HIP_OK(hipMalloc(&b->d_desc, sizeof(QueryDesc) * max_q));
     HIP_OK(hipMalloc(&b->d_part, sizeof(PlanPart) * ((max_q + kPlanThreads - 1) / kPlanThreads + 1)));
@@ -560,8 +582,10 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
 
 int wsr_check_query(wsr_handle* h, const wsr_query* q) {
   if (!h || !q) return fail(WSR_E_INVALID, "null argument");
-  if (q->n_terms > WSR_MAX_TERMS || q->k > WSR_MAX_K)
+  if (q->n_terms > WSR_MAX_QUERY_TERMS || q->k > WSR_MAX_K)
     return fail(WSR_E_LIMIT, "n_terms or k over the limit");
+  if (q->n_terms > WSR_MAX_TERMS && !q->more_ids)
+    return fail(WSR_E_INVALID, "a query of more than WSR_MAX_TERMS terms needs more_ids");
   if ((q->flags & WSR_QUERY_PHRASE) && q->n_terms > WSR_MAX_PHRASE_TERMS)
     return fail(WSR_E_LIMIT, "a phrase query has at most WSR_MAX_PHRASE_TERMS terms");
   if (q->flags & ~WSR_QUERY_PHRASE) return fail(WSR_E_INVALID, "unknown flags");
@@ -576,12 +600,14 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // (no handle lock: the handle's image is read-only after wsr_open and the
   // batch belongs to the caller, so threads with their own batches pipeline)
   std::vector<QueryIn> in(nq);
+  std::vector<int32_t> ext;   // term lists of queries over kMaxTerms, after the QueryIn array
   uint64_t ev_need = 0, items_need = 0, algo = 0;
   // the device's class rule (plan_query_kernel), restated to size the two
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
   bool has_phrase = false, has_wide = false;
+  std::vector<int32_t> ids;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
     if (s.k > b->stride)
@@ -595,34 +621,39 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
     d.flags = phrase ? kQueryPhrase : 0;
+    d.ext = 0;
+    ids = query_terms(s);
+    for (int t = 0; t < kMaxTerms; ++t) d.list[t] = t < d.n_terms ? ids[t] : -1;
+    if (d.n_terms > kMaxTerms) {
+      d.ext = static_cast<uint32_t>((sizeof(QueryIn) * static_cast<size_t>(nq)) / sizeof(int32_t) + ext.size());
+      ext.insert(ext.end(), ids.begin(), ids.end());
+    }
     uint32_t nbmin = 0xFFFFFFFFu;
     bool ok = d.n_terms > 0 && d.k > 0;
-    for (int t = 0; t < WSR_MAX_TERMS; ++t) {
-      d.list[t] = t < d.n_terms ? s.list_ids[t] : -1;
-      if (t < d.n_terms) {
-        const int32_t id = s.list_ids[t];
-        if (id < 0 || id >= static_cast<int32_t>(h->lists.size())) { ok = false; continue; }
-        nbmin = std::min(nbmin, h->lists[id].nblk);
-      }
+    for (int t = 0; t < d.n_terms; ++t) {
+      const int32_t id = ids[t];
+      if (id < 0 || id >= static_cast<int32_t>(h->lists.size())) { ok = false; continue; }
+      nbmin = std::min(nbmin, h->lists[id].nblk);
     }
     if (ok && nbmin > 0) {
       ev_need += (static_cast<uint64_t>(nbmin) + kSegCostMax) * 128;
       items_need += nbmin;
       int drv = 0;
       for (int t = 1; t < d.n_terms; ++t)
-        if (h->lists[d.list[t]].nblk < h->lists[d.list[drv]].nblk) drv = t;
+        if (h->lists[ids[t]].nblk < h->lists[ids[drv]].nblk) drv = t;
       bool lean = true;
       for (int t = 0; t < d.n_terms; ++t) {
-        const ListDev& L = h->lists[d.list[t]];
+        const ListDev& L = h->lists[ids[t]];
         if (t != drv && !(L.bm != kNoDense &&
                           static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin)))
           lean = false;
       }
       (lean ? lean_need : gen_need) += nbmin;
-      for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[d.list[t]];
+      for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[ids[t]];
       algo += 12ull * d.k;
     }
   }
+  const size_t q_bytes = sizeof(QueryIn) * static_cast<size_t>(nq) + sizeof(int32_t) * ext.size();
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
@@ -647,7 +678,16 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch *
                                      (static_cast<size_t>(std::max(h->gen_cap, 1)) +
                                       static_cast<size_t>(std::max(h->lean_wgs, 1)) * kLeanWaves)));
+    if (q_bytes > b->q_cap) {   // (the term table of long queries follows the QueryIn array)
+      if (b->d_q) HIP_OK(hipFree(b->d_q));
+      b->d_q = nullptr;
+      b->q_cap = q_bytes + q_bytes / 4;
+      HIP_OK(hipMalloc(&b->d_q, b->q_cap));
+    }
     if (nq) HIP_OK(hipMemcpy(b->d_q, in.data(), sizeof(QueryIn) * nq, hipMemcpyHostToDevice));
+    if (!ext.empty())
+      HIP_OK(hipMemcpy(reinterpret_cast<char*>(b->d_q) + sizeof(QueryIn) * nq, ext.data(),
+                       sizeof(int32_t) * ext.size(), hipMemcpyHostToDevice));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -937,7 +977,12 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
   // dictionary's cache misses overlap)
   std::vector<const char*> tp;
   std::vector<uint32_t> tn;
-  std::vector<int32_t*> dst;
+  // (query, slot) of every parsed term; ids land in list_ids, or past 16 in
+  // this thread's overflow table (more_ids), once every term is looked up
+  std::vector<std::pair<int32_t, int32_t>> dst;
+  thread_local std::vector<int32_t> overflow;
+  std::vector<size_t> more_at(static_cast<size_t>(max_q), 0);
+  size_t n_more = 0;
   tp.reserve(static_cast<size_t>(max_q) * 2);
   tn.reserve(static_cast<size_t>(max_q) * 2);
   dst.reserve(static_cast<size_t>(max_q) * 2);
@@ -954,16 +999,18 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
     std::memset(&w, 0, sizeof w);
     if (z - a >= 2 && text[a] == '"' && text[z - 1] == '"') { w.flags = WSR_QUERY_PHRASE; ++a; --z; }
     w.k = k;
+    more_at[n] = n_more;
     for (int64_t i = a; i < z;) {
       while (i < z && text[i] == ' ') ++i;
       int64_t j = i;
       while (j < z && text[j] != ' ') ++j;
       if (j > i) {
-        if (w.n_terms >= WSR_MAX_TERMS)
-          return fail(WSR_E_LIMIT, "query " + std::to_string(n) + ": more than WSR_MAX_TERMS terms");
+        if (w.n_terms >= WSR_MAX_QUERY_TERMS)
+          return fail(WSR_E_LIMIT, "query " + std::to_string(n) + ": more than WSR_MAX_QUERY_TERMS terms");
         tp.push_back(text + i);
         tn.push_back(static_cast<uint32_t>(j - i));
-        dst.push_back(&w.list_ids[w.n_terms++]);
+        dst.emplace_back(n, w.n_terms++);
+        if (w.n_terms > WSR_MAX_TERMS) ++n_more;
       }
       i = j;
     }
@@ -972,7 +1019,14 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
   }
   std::vector<int32_t> ids(tp.size());
   h->idx.find_many(tp.data(), tn.data(), tp.size(), ids.data());
-  for (size_t i = 0; i < ids.size(); ++i) *dst[i] = ids[i];
+  overflow.assign(n_more, -1);
+  for (size_t i = 0; i < ids.size(); ++i) {
+    const int32_t qi = dst[i].first, slot = dst[i].second;
+    if (slot < WSR_MAX_TERMS) q[qi].list_ids[slot] = ids[i];
+    else overflow[more_at[qi] + (slot - WSR_MAX_TERMS)] = ids[i];
+  }
+  for (int32_t i = 0; i < n; ++i)
+    if (q[i].n_terms > WSR_MAX_TERMS) q[i].more_ids = overflow.data() + more_at[i];
   *nq_out = n;
   return WSR_OK;
 }
@@ -1251,23 +1305,21 @@ int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_ow
 // never waits on the exchange inside a step, so the next batches' kernels run
 // under it; the next run of this batch waits for xev[1] (long past by then),
 // and the fetches join it.
-int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
-  if (!h || !b || !c || q_per_owner <= 0 || slot <= 0 ||
-      static_cast<int64_t>(q_per_owner) * c->world != b->nq)
+// An owner's region: the meta block (2 int32 per query, 4 per event, so the
+// qpr pairs take ceil(qpr / 2) events) followed by the slot.
+static uint64_t region_events_of(int32_t q_per_owner, int64_t slot) {
+  return (static_cast<uint64_t>(q_per_owner) + 1) / 2 + static_cast<uint64_t>(slot);
+}
+
+// First half of a shard step: size the region buffers and run the batch with
+// fused emission into the send regions (owner o's region at o * region).
+static int step_emit(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot) {
+  if (!h || !b || W < 1 || q_per_owner <= 0 || slot <= 0 || static_cast<int64_t>(q_per_owner) * W != b->nq)
     return fail(WSR_E_INVALID, "bad shard_step arguments (the batch must hold world * q_per_owner queries)");
-  const int W = c->world;
   if (W > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners ranks");
   if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
-  uint64_t t0 = c->timing ? now_ns() : 0;
-  auto lap = [&](int i) {
-    if (!c->timing) return;
-    const uint64_t t = now_ns();
-    c->t_ns[i] += t - t0;
-    t0 = t;
-  };
-  // region of one owner: the meta block (2 int32 per query, 4 per event) + the slot
   const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
-  const uint64_t region = meta_events + static_cast<uint64_t>(slot);
+  const uint64_t region = region_events_of(q_per_owner, slot);
   try {
     HIP_OK(hipSetDevice(h->device));
     const uint64_t need = region * W;
@@ -1291,10 +1343,37 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
   const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));   // int32 per region
   const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), b->d_xsend + meta_events, region,
                      reinterpret_cast<int32_t*>(b->d_xsend), meta_stride};
-  int rc = batch_run(h, b, false, &se);
+  const int rc = batch_run(h, b, false, &se);
+  if (rc == WSR_OK) b->x_fused = true;
+  return rc;
+}
+
+// Second half: the owner replay of this rank's queries over the receive
+// regions (region g = what shard g sent this owner), on stream st.
+static int step_replay(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, int64_t slot,
+                       hipStream_t st) {
+  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
+  const uint64_t region = region_events_of(q_per_owner, slot);
+  const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));
+  return owner_replay_meta_on(h, b, rank * q_per_owner, q_per_owner, W,
+                              reinterpret_cast<const int32_t*>(b->d_xrecv), meta_stride, region,
+                              b->d_xrecv + meta_events, st);
+}
+
+int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
+  if (!c) return fail(WSR_E_INVALID, "null communicator");
+  const int W = c->world;
+  uint64_t t0 = c->timing ? now_ns() : 0;
+  auto lap = [&](int i) {
+    if (!c->timing) return;
+    const uint64_t t = now_ns();
+    c->t_ns[i] += t - t0;
+    t0 = t;
+  };
+  int rc = step_emit(h, b, W, q_per_owner, slot);
   if (rc) return rc;
-  b->x_fused = true;
   lap(0);
+  const uint64_t region = region_events_of(q_per_owner, slot);
   try {
     HIP_OK(hipEventRecord(b->xev[0], b->st));
     HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
@@ -1305,15 +1384,49 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
     return fail(WSR_E_HIP, e.what());
   }
   lap(2);
-  rc = owner_replay_meta_on(h, b, c->rank * q_per_owner, q_per_owner, W,
-                            reinterpret_cast<const int32_t*>(b->d_xrecv), meta_stride, region,
-                            b->d_xrecv + meta_events, c->stream);
+  rc = step_replay(h, b, c->rank, W, q_per_owner, slot, c->stream);
   if (rc) return rc;
   if (hipEventRecord(b->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
   b->x_pending = true;
   lap(3);
   ++c->steps;
   return WSR_OK;
+}
+
+int wsr_shard_step_regions(int32_t q_per_owner, int64_t slot, uint64_t* region_bytes) {
+  if (q_per_owner <= 0 || slot <= 0 || !region_bytes) return fail(WSR_E_INVALID, "bad arguments");
+  *region_bytes = region_events_of(q_per_owner, slot) * sizeof(Event);
+  return WSR_OK;
+}
+
+int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                        void* host_send) {
+  if (!host_send) return fail(WSR_E_INVALID, "null host buffer");
+  const int rc = step_emit(h, b, world, q_per_owner, slot);
+  if (rc) return rc;
+  try {
+    HIP_OK(hipMemcpyAsync(host_send, b->d_xsend, sizeof(Event) * region_events_of(q_per_owner, slot) * world,
+                          hipMemcpyDeviceToHost, b->st));
+    HIP_OK(hipStreamSynchronize(b->st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
+                          int64_t slot, const void* host_recv) {
+  if (!h || !b || !host_recv || world < 1 || rank < 0 || rank >= world || !b->x_fused ||
+      b->x_pairs != world || region_events_of(q_per_owner, slot) * world > b->x_slots)
+    return fail(WSR_E_INVALID, "call wsr_shard_step_emit with the same world, q_per_owner and slot first");
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipMemcpyAsync(b->d_xrecv, host_recv, sizeof(Event) * region_events_of(q_per_owner, slot) * world,
+                          hipMemcpyHostToDevice, b->st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return step_replay(h, b, rank, world, q_per_owner, slot, b->st);
 }
 
 int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,

@@ -6,7 +6,8 @@
 
 namespace wiser {
 
-constexpr int kMaxTerms = 16;        // terms per conjunctive query
+constexpr int kMaxTerms = 16;        // terms held inline in a QueryIn (and the plan's one-round loads)
+constexpr int kMaxQueryTerms = 1024; // terms per conjunctive query (past kMaxTerms: QueryIn::ext)
 constexpr int kMaxPhraseTerms = 8;   // terms per phrase query (the reference's cap, query_processing.h:695)
 constexpr int kMaxK = 64;            // n_results of the wave top-k: running top-k and heap in one wave's lanes
 constexpr int kMaxKWide = 1024;      // n_results per query; k > kMaxK: every survivor is an event and the
@@ -62,8 +63,10 @@ struct QueryIn {
   int32_t k;                // n_results (0 => empty result)
   int32_t list[kMaxTerms];  // list ids in query order; -1 => term missing => empty
   int32_t flags;            // kQueryPhrase: SearchQuery::is_phrase (types.h:205-256)
+  uint32_t ext;             // n_terms > kMaxTerms: all n_terms list ids are at
+                            // reinterpret_cast<const int32_t*>(batch's QueryIn array) + ext
 };
-static_assert(sizeof(QueryIn) == 76, "QueryIn layout");
+static_assert(sizeof(QueryIn) == 80, "QueryIn layout");
 constexpr int32_t kQueryPhrase = 1;
 
 // Positions of one posting list in the image (phrase queries).  The list's
@@ -107,7 +110,7 @@ struct QueryDesc {
   uint32_t a_blk0, a_nblk, a_tail_cnt;
   uint32_t min_last;    // smallest last doc id over the other lists
   uint32_t item_base, n_items, seg;
-  uint32_t slots;       // driver slot | O1 slot << 8 (kMaxTerms: single term) | n_terms << 16
+  uint32_t slots;       // driver slot | O1 slot << 16 (kNoSlot: single term)
   uint32_t o_list;      // O1's list id
   uint32_t k;           // n_results (> kMaxK: wide, every survivor is an event)
   // score bound of a driver posting before the other lists are probed (f32,
@@ -115,9 +118,12 @@ struct QueryDesc {
   // term (b_id = 2.2 * idf), b_iom / (b_m + norm) bounds all the other terms
   // (b_m = their largest tfmax, b_iom = sum of 2.2 * idf over them, times b_m)
   float b_id, b_iom, b_m;
-  uint32_t pad;
+  uint32_t nt;          // n_terms | kDescWinBound (bit 31: a two-term query whose other-term
+                        // bound may use O1's per-window tf maxima)
 };
 static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
+constexpr uint32_t kNoSlot = 0xFFFFu;
+constexpr uint32_t kDescWinBound = 0x80000000u;
 
 // A heap-insertion event: a survivor that a top-k heap run from empty over its
 // segment inserts (query_processing.h:595-602).

@@ -48,8 +48,11 @@ struct IndexArgs {
 enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16, kQueueShards = 8,
        kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
-// QueryPlan::driver = driver slot | cost bucket << 8 | kPlanLean
+// QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean
+constexpr uint32_t kPlanSlotMask = 0x7FFu;   // (kMaxQueryTerms <= 2048)
+constexpr int kPlanBucketShift = 12;
 constexpr uint32_t kPlanLean = 1u << 16;
+static_assert(kMaxQueryTerms <= static_cast<int>(kPlanSlotMask) + 1, "driver slot field");
 constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
 // per-workgroup statistics written by the segment kernel (no atomics):
 // stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
@@ -81,7 +84,7 @@ static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSeg
 #endif
 constexpr int kSegCostGeneral = WSR_SEG_COST_GENERAL;
 static_assert(kSegCostGeneral <= kSegCost, "the event workspace is sized for kSegCost");
-// item cost classes for the longest-first queue order (QueryPlan::driver >> 8);
+// item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5
 constexpr float kItemFixedCost = 4.0f;

@@ -347,6 +347,13 @@ __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev
   return true;
 }
 
+// A query's list ids in query order: inline up to kMaxTerms, else in the
+// batch's term table after the QueryIn array (QueryIn::ext, int32 units from qs).
+__device__ __forceinline__ const int32_t* qlist_of(const QueryIn* qs, int qi) {
+  const QueryIn* q = qs + qi;
+  return q->n_terms <= kMaxTerms ? q->list : reinterpret_cast<const int32_t*>(qs) + q->ext;
+}
+
 // ----------------------------------------------------------------- plan --
 // Item order: class-major (lean items first, then general ones), then cost
 // bucket-major, heaviest bucket first (query order inside a bucket, a query's
@@ -354,7 +361,7 @@ __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev
 // the short ones fill the tail (longest-first list scheduling).
 constexpr int kPlanKeys = 2 * kCostBuckets;
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
-  const uint32_t bucket = (drv >> 8) & 0xFFu;
+  const uint32_t bucket = (drv >> kPlanBucketShift) & 0xFu;
   return ((drv & kPlanLean) ? 0u : static_cast<uint32_t>(kCostBuckets)) + (kCostBuckets - 1 - bucket);
 }
 
@@ -428,51 +435,76 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
   QueryPlan p{0, 0, 1, 0, 0};
   if (i < nq) {
     const QueryIn q = qs[i];
-    bool ok = q.n_terms > 0 && q.k > 0;
-    if (q.n_terms > kMaxTerms || q.k > kMaxKWide ||
-        (q.n_terms > kMaxPhraseTerms && (q.flags & kQueryPhrase))) {
+    const int32_t* ql = qlist_of(qs, i);
+    const int nt = q.n_terms;
+    bool ok = nt > 0 && q.k > 0;
+    if (nt > kMaxQueryTerms || q.k > kMaxKWide || (nt > kMaxPhraseTerms && (q.flags & kQueryPhrase))) {
       ok = false;
       atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrLimit));
     }
-    // one round of loads: every term's block count, bitmap and last doc (each
-    // load's predicate depends on the query record only, not on an earlier
-    // load's value, so all of them are in flight together)
-    uint32_t nb[kMaxTerms], last[kMaxTerms];
-    bool dn[kMaxTerms];
+    // Driver (fewest blocks here), cost, class, O1 (the most selective other
+    // list) and the smallest last doc of the others.  Up to kMaxTerms terms:
+    // one round of loads, every term's block count, bitmap and last doc in
+    // registers (each load's predicate depends on the query record only, so
+    // all of them are in flight together); longer queries: plain loops.
+    uint32_t d = 0, nd = 0xFFFFFFFFu, o1 = kNoSlot, min_last = 0xFFFFFFFFu;
+    float cost = 1.0f;
+    bool lean = true;
+    if (nt <= kMaxTerms) {
+      uint32_t nb[kMaxTerms], last[kMaxTerms];
+      bool dn[kMaxTerms];
 #pragma unroll
-    for (int s = 0; s < kMaxTerms; ++s) {
-      nb[s] = 0xFFFFFFFFu;
-      last[s] = 0xFFFFFFFFu;
-      dn[s] = false;
-      const int32_t id = q.list[s];
-      const bool in = s < q.n_terms;
-      if (in && (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists)) ok = false;
-      if (in && id >= 0 && static_cast<uint32_t>(id) < ix.n_lists) {
-        const ListDev& L = ix.lists[id];
-        nb[s] = L.nblk;
-        dn[s] = L.bm != kNoDense;
-        last[s] = L.last;
+      for (int s = 0; s < kMaxTerms; ++s) {
+        nb[s] = 0xFFFFFFFFu;
+        last[s] = 0xFFFFFFFFu;
+        dn[s] = false;
+        const int32_t id = q.list[s];
+        const bool in = s < nt;
+        if (in && (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists)) ok = false;
+        if (in && id >= 0 && static_cast<uint32_t>(id) < ix.n_lists) {
+          const ListDev& L = ix.lists[id];
+          nb[s] = L.nblk;
+          dn[s] = L.bm != kNoDense;
+          last[s] = L.last;
+        }
       }
-    }
 #pragma unroll
-    for (int s = 0; s < kMaxTerms; ++s)
-      if (s < q.n_terms && nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
-    if (ok) {
-      uint32_t d = 0, nd = nb[0];
+      for (int s = 0; s < kMaxTerms; ++s)
+        if (s < nt && nb[s] == 0) ok = false;  // no docs of this list in this shard: empty AND
+      nd = nb[0];
 #pragma unroll
       for (int s = 1; s < kMaxTerms; ++s) if (nb[s] < nd) { d = s; nd = nb[s]; }
-      float cost = 1.0f;
+      uint32_t o_nb = 0xFFFFFFFFu;
 #pragma unroll
-      for (int s = 0; s < kMaxTerms; ++s)
-        if (s < q.n_terms && s != static_cast<int>(d))
-          cost += use_dense(ix, dn[s], nb[s], nd) ? kDenseCost
-                                                  : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
-      const bool ph = q.n_terms > 1 && (q.flags & kQueryPhrase);
-      // lean class: every other list is probed through its bitmap (or none)
-      bool lean = true;
-#pragma unroll
-      for (int s = 0; s < kMaxTerms; ++s)
-        if (s < q.n_terms && s != static_cast<int>(d) && !use_dense(ix, dn[s], nb[s], nd)) lean = false;
+      for (int s = 0; s < kMaxTerms; ++s) {
+        if (s >= nt || s == static_cast<int>(d)) continue;
+        const bool dense = use_dense(ix, dn[s], nb[s], nd);
+        cost += dense ? kDenseCost : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+        if (!dense) lean = false;
+        min_last = last[s] < min_last ? last[s] : min_last;
+        if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
+      }
+    } else if (ok) {
+      for (int s = 0; s < nt; ++s) {
+        const int32_t id = ql[s];
+        if (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists) { ok = false; break; }
+        const uint32_t n = ix.lists[id].nblk;
+        if (n == 0) ok = false;
+        if (n < nd) { d = s; nd = n; }
+      }
+      uint32_t o_nb = 0xFFFFFFFFu;
+      for (int s = 0; ok && s < nt; ++s) {
+        if (s == static_cast<int>(d)) continue;
+        const ListDev& L = ix.lists[ql[s]];
+        const bool dense = use_dense(ix, L.bm != kNoDense, L.nblk, nd);
+        cost += dense ? kDenseCost : fminf(static_cast<float>(L.nblk) / nd, 64.0f);
+        if (!dense) lean = false;
+        min_last = L.last < min_last ? L.last : min_last;
+        if (L.nblk < o_nb) { o1 = s; o_nb = L.nblk; }
+      }
+    }
+    if (ok) {
+      const bool ph = nt > 1 && (q.flags & kQueryPhrase);
       uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : lean ? kSegCost : kSegCostGeneral) / cost);
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
@@ -481,21 +513,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       const uint32_t ic = static_cast<uint32_t>(item_cost);
       const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
       const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-      p.driver = d | (bucket << 8) | (lean ? kPlanLean : 0u);
+      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u);
       p.seg_blocks = seg;
       p.n_items = (nd + seg - 1) / seg;
       if (lean) {
-        // the lean kernel's record: driver, the most selective other list (O1),
-        // the smallest last doc of the others (bases are added by plan_fill_kernel)
-        uint32_t o1 = kMaxTerms, o_nb = 0xFFFFFFFFu, min_last = 0xFFFFFFFFu;
-#pragma unroll
-        for (int s = 0; s < kMaxTerms; ++s) {
-          if (s >= q.n_terms || s == static_cast<int>(d)) continue;
-          min_last = last[s] < min_last ? last[s] : min_last;
-          if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
-        }
+        // the lean kernel's record (bases are added by plan_fill_kernel)
         // (the driver's and O1's records: a second round of loads, side by side)
-        const ListDev A = ix.lists[q.list[d]];
+        const ListDev A = ix.lists[ql[d]];
         QueryDesc D;
         D.a_base = A.base;
         D.a_tail = A.tail;
@@ -504,10 +528,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.a_nblk = A.nblk;
         D.a_tail_cnt = A.tail_cnt;
         D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
-        if (o1 < kMaxTerms) {
-          const ListDev O = ix.lists[q.list[o1]];
+        if (o1 != kNoSlot) {
+          const ListDev O = ix.lists[ql[o1]];
           D.o_bm = O.bm; D.o_tf8 = O.tf8; D.o_idf = O.idf;
-          D.o_list = static_cast<uint32_t>(q.list[o1]);
+          D.o_list = static_cast<uint32_t>(ql[o1]);
         }
         D.min_last = min_last;
         D.a_bm = A.bm;
@@ -516,25 +540,25 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.item_base = 0;
         D.n_items = p.n_items;
         D.seg = seg;
-        D.slots = d | (o1 << 8) | (static_cast<uint32_t>(q.n_terms) << 16);
+        D.slots = d | (o1 << 16);
         D.k = static_cast<uint32_t>(q.k);
         // pre-probe score bound: the other terms' BM25 parts are at most
         // sum(2.2 idf) * M / (M + norm) with M their largest tf bound
         double io = 0.0;
         uint32_t mm = 0;
-        for (int s = 0; s < q.n_terms; ++s) {
+        for (int s = 0; s < nt; ++s) {
           if (s == static_cast<int>(d)) continue;
-          const ListDev& L = ix.lists[q.list[s]];
+          const ListDev& L = ix.lists[ql[s]];
           io += 2.2 * L.idf;
           mm = L.tfmax > mm ? L.tfmax : mm;
         }
-        const float mf = o1 < kMaxTerms ? static_cast<float>(mm) : 1.0f;
+        const float mf = o1 != kNoSlot ? static_cast<float>(mm) : 1.0f;
         D.b_id = static_cast<float>(2.2 * A.idf);
         D.b_m = mf;
         D.b_iom = static_cast<float>(io * static_cast<double>(mf));
-        // bit 0: a two-term lean query, whose other-term bound may use O1's
-        // per-window tf maxima instead of its list maximum (lean_segment)
-        D.pad = (q.n_terms == 2 && o1 < kMaxTerms) ? 1u : 0u;
+        // a two-term lean query's other-term bound may use O1's per-window tf
+        // maxima instead of its list maximum (lean_segment, WSR_WIN_BOUND)
+        D.nt = static_cast<uint32_t>(nt) | ((nt == 2 && o1 != kNoSlot) ? kDescWinBound : 0u);
         desc[i] = D;
       }
     }
@@ -678,7 +702,7 @@ struct WaveLds {
   uint32_t dtt[128];     //   and tfs
   Event evs[64];         // events buffered for one coalesced store
   double norm[256];      // Bm25Similarity cache_ (host table, scoring.h:85-90)
-  uint32_t cur[kMaxTerms];  // per other slot: cursor into its block directory
+  uint32_t cur[kMaxTerms];  // per other slot (the first kMaxTerms): cursor into its block directory
   uint4 dblk[64];        // the driver's directory entries of the current segment
   uint32_t dmeta[64];
   uint32_t tf[128];      // cooperative decode of a VInts tf tail
@@ -1683,7 +1707,7 @@ struct LeanLdsT {
 #endif
 };
 
-// o1 == kMaxTerms: single-term query, every posting of the driver survives.
+// o1 == kNoSlot: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
 template <bool kPh, bool kAnd>
@@ -1700,12 +1724,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                                              uint32_t* prof) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
-  const uint32_t d = Q.slots & 0xFFu, o1 = (Q.slots >> 8) & 0xFFu;
-  const uint32_t nt = (Q.slots >> 16) & 0xFFu, k = Q.k;
+  const uint32_t d = Q.slots & 0xFFFFu, o1 = Q.slots >> 16;
+  const uint32_t nt = Q.nt & 0xFFFFu, k = Q.k;
   // k > kMaxK: every survivor is an event; the replay's heap in LDS decides
   const bool wide = k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
-  const bool single = o1 >= kMaxTerms;
+  const bool single = o1 == kNoSlot;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
   const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
                              : reinterpret_cast<const uint2*>(ix.dense + Q.o_bm);
@@ -1758,7 +1782,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   // Windowed other-term bound (two-term queries): per driver block, O1's
   // largest tf over the 2,048-doc windows the block's doc range touches
   // replaces its list maximum (255 in a window: 255 or more, use the list's).
-  const bool win = (Q.pad & 1u) != 0u && ix.wmax != nullptr;
+  const bool win = (Q.nt & kDescWinBound) != 0u && ix.wmax != nullptr;
   const float io = b_m > 0.0f ? b_iom / b_m : 0.0f;   // 2.2 idf of O1
   const float m_list = b_m;
   const uint8_t* o_wm = win ? ix.wmax + Q.o_bm / kWinEnts : reinterpret_cast<const uint8_t*>(ix.blk_last);
@@ -2324,9 +2348,9 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     if (item >= total) break;
     const uint32_t qi = uni(item_q[item]);   // written by plan_fill_kernel
     const QueryPlan P = plan[qi];
-    const int32_t* qlist = qs[qi].list;
+    const int32_t* qlist = qlist_of(qs, static_cast<int>(qi));
     const uint32_t r = item - P.item_base;
-    const uint32_t d = uni(P.driver & 0xFFu);
+    const uint32_t d = uni(P.driver & kPlanSlotMask);
     const uint32_t nt = uni(static_cast<uint32_t>(qs[qi].n_terms));
     const uint32_t k = uni(static_cast<uint32_t>(qs[qi].k));
     const bool wide = k > static_cast<uint32_t>(kMaxK);   // every survivor is an event
@@ -2358,18 +2382,20 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     __syncthreads();
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     bool done = false;   // some other list has no doc >= the next driver doc
-    uint32_t fo = kMaxTerms;   // first other slot in query order
-#pragma unroll
-    for (uint32_t s = 0; s < kMaxTerms; ++s) {
-      if (s < nt && s != d) {
+    uint32_t fo = kNoSlot;   // first other slot in query order
+    // (cursors into the block directories of the first kMaxTerms slots live in
+    // LDS; a slot past them, in the rare longer query, finds its block from
+    // the segment's first doc at every driver block instead)
+    for (uint32_t s = 0; s < nt; ++s) {
+      if (s != d) {
         const ListDev B = ix.lists[qlist[s]];
-        if (fo == kMaxTerms) fo = s;
+        if (fo == kNoSlot) fo = s;
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
           // probed through its bitmap: no cursor, only its end matters
           if (first_doc > ix.blk_last[B.blk0 + B.nblk - 1]) done = true;
         } else {
           const uint32_t c0 = uni(find_block(ix.blk_last + B.blk0, 0, B.nblk, first_doc));
-          if (l == 0) S.cur[s] = c0;
+          if (l == 0 && s < kMaxTerms) S.cur[s] = c0;
           if (c0 >= B.nblk) done = true;
         }
       }
@@ -2377,7 +2403,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     // the first other list's bitmap entries are fetched one block ahead
     ListDev F = A;
     bool fo_dense = false;
-    if (fo < kMaxTerms) {
+    if (fo != kNoSlot) {
       F = ix.lists[qlist[fo]];
       fo_dense = use_dense(ix, F.bm != kNoDense, F.nblk, A.nblk);
     }
@@ -2544,7 +2570,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           continue;
         }
         const uint32_t* last = ix.blk_last + B.blk0;
-        const uint32_t c = uni(S.cur[s]);
+        const uint32_t c = s < kMaxTerms ? uni(S.cur[s])
+                                         : uni(find_block(last, 0, B.nblk, uni(S.dblk[b - b0].x) + (b > 0 ? 1u : 0u)));
         // directory window cur..cur+63 into LDS (one coalesced round)
         const uint32_t wn = min(kWin, B.nblk - c);
         uint32_t wl = 0;
@@ -2651,7 +2678,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         if (al1) s1 += bm25_term(B.idf, t1, nrm1);
         rec(s, (B.blk0 + j0) * 128u + p0, (B.blk0 + j1) * 128u + p1, t0, t1);
         // advance the cursor to the furthest block queried (docs only increase)
-        if (l == 0 && nd && jlast > c) S.cur[s] = jlast;
+        if (l == 0 && nd && jlast > c && s < kMaxTerms) S.cur[s] = jlast;
         WSR_T(3)
       }
       if (__ballot(al0 || al1) == 0) return;
@@ -2831,8 +2858,8 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd 
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
     if (!done && b0 < b1)
-      lean_segment<kPh, kAnd>(ix, S, norm, Q, qs[qi].list,
-                   kPh && ((Q.slots >> 16) & 0xFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
+      lean_segment<kPh, kAnd>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
+                   kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
                    ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
     WSR_T(1)
@@ -2990,8 +3017,8 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
   if ((k > static_cast<uint32_t>(kMaxK)) != kWide) return;
   const uint32_t l = threadIdx.x & 63;
   auto meta_of = [&](uint32_t g) { return meta + g * meta_stride + 2ull * static_cast<uint32_t>(qi); };
-  if (l < static_cast<uint32_t>(n_shards) && meta_of(l)[0] < 0)
-    atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
+  for (uint32_t g = l; g < static_cast<uint32_t>(n_shards); g += 64)   // (up to kMaxOwners shards)
+    if (meta_of(g)[0] < 0) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
   auto count_of = [&](uint32_t g) {
     const int32_t c = meta_of(g)[0];
     return static_cast<uint32_t>(c > 0 ? c : 0);

@@ -32,6 +32,10 @@
 
 #include "../../include/wiser_hip.h"
 
+namespace wiser {
+void set_last_error(const std::string& msg);   // engine.cc
+}
+
 namespace {
 
 using Clock = std::chrono::steady_clock;
@@ -47,8 +51,16 @@ struct Req {
   wsr_hit* out = nullptr;
   int32_t* n_out = nullptr;
   int rc = WSR_OK;
+  std::string err;   // wsr_last_error() of the thread the request failed on
   std::atomic<int> done{kPending};
-  void reset() { out = nullptr; n_out = nullptr; rc = WSR_OK; done.store(kPending, std::memory_order_relaxed); }
+  void reset() {
+    out = nullptr; n_out = nullptr; rc = WSR_OK; err.clear();
+    done.store(kPending, std::memory_order_relaxed);
+  }
+  void fail_with(int code) {
+    rc = code;
+    if (code != WSR_OK) err = wsr_last_error();
+  }
   void signal() {
     if (done.exchange(kDone, std::memory_order_acq_rel) == kSleeping)
       syscall(SYS_futex, reinterpret_cast<int*>(&done), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
@@ -108,12 +120,18 @@ struct wsr_server {
   void complete(Slot& s) {
     // poll the batch's end event, so the fetch below finds it done (a blocking
     // wait inside the fetch can sleep through the batch's end and wake late);
-    // a HIP error ends the poll too, and the fetch reports it
-    while (wsr_batch_ready(h, s.b) == 0) std::this_thread::yield();
+    // a HIP error ends the poll too, and the fetch reports it.  Yield for the
+    // first 100 us, then back off to short sleeps, so that a long batch does
+    // not keep a host core busy beside the clients and the dispatcher.
+    const auto spin_until = Clock::now() + std::chrono::microseconds(100);
+    while (wsr_batch_ready(h, s.b) == 0) {
+      if (Clock::now() < spin_until) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
-      r->rc = rc;
+      r->fail_with(rc);
       if (rc == WSR_OK) {
         const int32_t n = nh[i];
         std::memcpy(r->out, &hits[i * static_cast<size_t>(s.kmax)], sizeof(wsr_hit) * static_cast<size_t>(n));
@@ -199,7 +217,7 @@ struct wsr_server {
         // query: the batch is retried one request at a time, and only the
         // requests that fail on their own get an error
         for (Req* r : take) {
-          r->rc = wsr_search_batch(h, &r->q, 1, std::max(1, r->q.k), r->out, r->n_out);
+          r->fail_with(wsr_search_batch(h, &r->q, 1, std::max(1, r->q.k), r->out, r->n_out));
           r->signal();
         }
         std::lock_guard<std::mutex> g(mu);
@@ -306,7 +324,9 @@ int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t*
   r.n_out = n_hits;
   int rc = s->submit(&r);
   if (rc != WSR_OK) return rc;
-  return s->wait(&r);
+  rc = s->wait(&r);
+  if (rc != WSR_OK) wiser::set_last_error(r.err);   // (it failed on the dispatcher's or completer's thread)
+  return rc;
 }
 
 int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_clients,

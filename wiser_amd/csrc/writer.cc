@@ -698,6 +698,14 @@ uint32_t powerlaw_df(std::mt19937_64& g, double lo, double hi) {
   const double f = std::floor(x);
   return static_cast<uint32_t>(f < lo ? lo : (f >= hi ? hi - 1 : f));
 }
+
+// splitmix64: the stand-in's per-(term, doc) position stream
+uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 }  // namespace
 
 BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
@@ -730,16 +738,33 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
       verb[d] = static_cast<float>(std::exp(0.6 * z));
     }
   }
-  std::unique_ptr<std::atomic<uint32_t>[]> len(new std::atomic<uint32_t>[N]);
-  for (int64_t d = 0; d < N; ++d) len[d].store(0, std::memory_order_relaxed);
+  // 3) phrase pool (the stand-in for tools/gen_synthetic_log.py:216-252
+  //    find_all_unique_phrases over an English phrase list): pairs (a, b) of
+  //    distinct terms with df in [1e3, 1e6), no term in two pairs.  As a real
+  //    phrase's two words, b co-occurs with a: half of the smaller list's size
+  //    of b's docs are drawn from a's docs (b's df is kept), and in 60 % of
+  //    the docs holding both, b occurs right after a's first occurrence.
+  std::vector<int64_t> partner(V, -1);   // b -> a
+  std::vector<std::pair<int64_t, int64_t>> pool;
+  {
+    std::vector<int64_t> cand;
+    for (int64_t v = 0; v < V; ++v)
+      if (dfs[v] >= 1000 && dfs[v] < 1000000 && dfs[v] < static_cast<uint64_t>(N) / 2) cand.push_back(v);
+    std::mt19937_64 g(sp.seed ^ 0x0000000000000007ull);
+    for (size_t i = cand.size(); i > 1; --i) std::swap(cand[i - 1], cand[g() % i]);
+    for (size_t i = 0; i + 1 < cand.size(); i += 2) {
+      pool.emplace_back(cand[i], cand[i + 1]);
+      partner[cand[i + 1]] = cand[i];
+    }
+  }
+  constexpr double kPhraseRate = 0.6;
 
-  // one term's postings, from its own seed (independent of the thread count)
-  auto make_list = [&](int64_t id, TermPostings* tp) {
-    std::mt19937_64 g(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(id + 1)));
-    const uint32_t df = dfs[id];
-    std::vector<uint32_t>& docs = tp->docs;
+  // df distinct uniform doc ids, sorted: by rejection for rare terms, by
+  // selection sampling (Knuth's algorithm S) for common ones
+  auto uniform_docs = [&](uint32_t df, std::mt19937_64& g, std::vector<uint32_t>* out) {
+    std::vector<uint32_t>& docs = *out;
+    docs.clear();
     if (static_cast<int64_t>(df) * 16 < N) {
-      // rare term: distinct uniform ids by rejection
       while (docs.size() < df) {
         const size_t need = df - docs.size();
         for (size_t i = 0; i < need; ++i) docs.push_back(static_cast<uint32_t>(g() % static_cast<uint64_t>(N)));
@@ -747,54 +772,60 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
         docs.erase(std::unique(docs.begin(), docs.end()), docs.end());
       }
     } else {
-      // common term: selection sampling (Knuth's algorithm S), exactly df ids
       docs.reserve(df);
       uint64_t need = df;
       for (int64_t d = 0; d < N && need; ++d)
         if (static_cast<double>(N - d) * unit(g) < static_cast<double>(need)) { docs.push_back(static_cast<uint32_t>(d)); --need; }
     }
+  };
+  // one term's docs and tfs, from its own seed (independent of the thread count)
+  auto make_list = [&](int64_t id, std::vector<uint32_t>* docs_out, std::vector<uint32_t>* tfs_out) {
+    std::mt19937_64 g(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(id + 1)));
+    const uint32_t df = dfs[id];
+    std::vector<uint32_t>& docs = *docs_out;
+    docs.clear();
+    const int64_t a = partner[id];
+    if (a >= 0) {
+      // a phrase's second word: c of its docs come from a's docs, the rest
+      // are uniform (distinct from them)
+      std::vector<uint32_t> ad;
+      std::mt19937_64 ga(sp.seed ^ 0xA5A5A5A5A5A5A5A5ull ^ static_cast<uint64_t>(id));
+      {
+        // (a is never a pool b itself, so this does not recurse)
+        std::mt19937_64 gg(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(a + 1)));
+        uniform_docs(dfs[a], gg, &ad);
+      }
+      const uint32_t c = std::min<uint32_t>(df, static_cast<uint32_t>(ad.size())) / 2;
+      // c of a's docs (partial Fisher-Yates), then uniform docs not yet taken
+      for (uint32_t i = 0; i < c; ++i) std::swap(ad[i], ad[i + ga() % (ad.size() - i)]);
+      docs.assign(ad.begin(), ad.begin() + c);
+      std::sort(docs.begin(), docs.end());
+      while (docs.size() < df) {
+        const size_t have = docs.size();
+        for (size_t i = have; i < df; ++i) docs.push_back(static_cast<uint32_t>(g() % static_cast<uint64_t>(N)));
+        std::sort(docs.begin(), docs.end());
+        docs.erase(std::unique(docs.begin(), docs.end()), docs.end());
+      }
+      if (docs.size() > df) docs.resize(df);   // (never: unique keeps at most df)
+    } else {
+      uniform_docs(df, g, &docs);
+    }
     const double base = 0.3 + 5.0 * static_cast<double>(df) / static_cast<double>(N);
-    const uint32_t p0 = static_cast<uint32_t>(id % 61);
-    tp->tfs.resize(docs.size());
+    tfs_out->resize(docs.size());
     for (size_t i = 0; i < docs.size(); ++i) {
       const double lam = base * verb[docs[i]];
       const double t = 1.0 + std::floor(-std::log(unit(g)) * lam);
-      const uint32_t tf = static_cast<uint32_t>(t > 60000.0 ? 60000.0 : t);
-      tp->tfs[i] = tf;
-      len[docs[i]].fetch_add(tf, std::memory_order_relaxed);
-      // bag: tf consecutive positions from p0 (delta coded: p0, 1, 1, ...) and
-      // their offset pairs [9p, 9p + 7] (delta coded inside the bag)
-      tp->pos_vals.push_back(p0);
-      tp->off_vals.push_back(9 * p0);
-      tp->off_vals.push_back(7);
-      for (uint32_t r = 1; r < tf; ++r) {
-        tp->pos_vals.push_back(1);
-        tp->off_vals.push_back(2);
-        tp->off_vals.push_back(7);
-      }
-      tp->pos_sizes.push_back(tf);
-      tp->off_sizes.push_back(2 * tf);
+      (*tfs_out)[i] = static_cast<uint32_t>(t > 60000.0 ? 60000.0 : t);
     }
   };
 
-  VacuumFileWriter w(out_dir);
-  BuildStats st;
-  const int64_t BATCH = 16384;
-  for (int64_t b0 = 0; b0 < V; b0 += BATCH) {
-    const int64_t b1 = std::min(V, b0 + BATCH);
-    std::vector<std::unique_ptr<EncodedList>> enc(b1 - b0);
+  auto run_parallel = [&](int64_t b0, int64_t b1, auto&& fn) {
     std::atomic<int64_t> next{b0};
     std::atomic<bool> failed{false};
     std::string err;
     auto work = [&] {
       try {
-        for (int64_t v; (v = next++) < b1 && !failed;) {
-          TermPostings tp;
-          make_list(v, &tp);
-          auto el = std::make_unique<EncodedList>();
-          encode_list(tp, el.get());
-          enc[v - b0] = std::move(el);
-        }
+        for (int64_t v; (v = next++) < b1 && !failed;) fn(v);
       } catch (const std::exception& ex) {
         if (!failed.exchange(true)) err = ex.what();
       }
@@ -803,13 +834,108 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
     for (int i = 0; i < threads; ++i) ts.emplace_back(work);
     for (auto& t : ts) t.join();
     if (failed) throw std::runtime_error(err);
+  };
+
+  // 4) doc lengths = the sum of each doc's tfs (pass 1: lists without positions)
+  std::unique_ptr<std::atomic<uint32_t>[]> lenA(new std::atomic<uint32_t>[N]);
+  for (int64_t d = 0; d < N; ++d) lenA[d].store(0, std::memory_order_relaxed);
+  run_parallel(0, V, [&](int64_t v) {
+    thread_local std::vector<uint32_t> docs, tfs;
+    make_list(v, &docs, &tfs);
+    for (size_t i = 0; i < docs.size(); ++i) lenA[docs[i]].fetch_add(tfs[i], std::memory_order_relaxed);
+  });
+  std::vector<uint32_t> len(N);
+  for (int64_t d = 0; d < N; ++d) len[d] = lenA[d].load(std::memory_order_relaxed);
+  lenA.reset();
+
+  // the positions of term t in doc d: tf distinct values in [0, len[d]) from
+  // the (t, d) stream, sorted; `forced` (if < len) is one of them
+  auto positions = [&](int64_t t, uint32_t d, uint32_t tf, int64_t forced, std::vector<uint32_t>* out) {
+    const uint32_t L = len[d];
+    out->clear();
+    if (tf >= L) {   // every position of the doc
+      for (uint32_t p = 0; p < L; ++p) out->push_back(p);
+      return;
+    }
+    uint64_t st = mix64(sp.seed ^ (static_cast<uint64_t>(t) * 0xD1B54A32D192ED03ull) ^
+                        (static_cast<uint64_t>(d) << 1));
+    if (forced >= 0 && forced < L) out->push_back(static_cast<uint32_t>(forced));
+    if (tf <= 64) {
+      while (out->size() < tf) {
+        st = mix64(st);
+        const uint32_t p = static_cast<uint32_t>(st % L);
+        if (std::find(out->begin(), out->end(), p) == out->end()) out->push_back(p);
+      }
+    } else {
+      std::unordered_set<uint32_t> seen(out->begin(), out->end());
+      while (out->size() < tf) {
+        st = mix64(st);
+        const uint32_t p = static_cast<uint32_t>(st % L);
+        if (seen.insert(p).second) out->push_back(p);
+      }
+    }
+    std::sort(out->begin(), out->end());
+  };
+
+  // 5) pass 2: lists with positions, encoded in parallel batches, appended in
+  //    term-id order (lists are streamed: host memory does not grow with the corpus)
+  VacuumFileWriter w(out_dir);
+  BuildStats st;
+  const int64_t BATCH = 16384;
+  for (int64_t b0 = 0; b0 < V; b0 += BATCH) {
+    const int64_t b1 = std::min(V, b0 + BATCH);
+    std::vector<std::unique_ptr<EncodedList>> enc(b1 - b0);
+    run_parallel(b0, b1, [&](int64_t v) {
+      TermPostings tp;
+      make_list(v, &tp.docs, &tp.tfs);
+      // a phrase's second word: in kPhraseRate of the docs it shares with a,
+      // it occurs right after a's first occurrence
+      const int64_t a = partner[v];
+      std::vector<uint32_t> adocs, atfs;
+      if (a >= 0) make_list(a, &adocs, &atfs);
+      std::vector<uint32_t> pos, apos;
+      size_t ai = 0;
+      for (size_t i = 0; i < tp.docs.size(); ++i) {
+        const uint32_t d = tp.docs[i], tf = tp.tfs[i];
+        int64_t forced = -1;
+        if (a >= 0) {
+          while (ai < adocs.size() && adocs[ai] < d) ++ai;
+          if (ai < adocs.size() && adocs[ai] == d &&
+              (mix64(sp.seed ^ 0x7777ull ^ (static_cast<uint64_t>(v) << 32) ^ d) >> 11) * 0x1.0p-53 < kPhraseRate) {
+            positions(a, d, atfs[ai], -1, &apos);
+            forced = static_cast<int64_t>(apos[0]) + 1;
+          }
+        }
+        positions(v, d, tf, forced, &pos);
+        // bag: delta coded positions, offset pairs [9p, 9p + 7] delta coded
+        // inside the bag (an 8-char term and a space per token)
+        uint32_t pp = 0, po = 0;
+        for (uint32_t p : pos) {
+          tp.pos_vals.push_back(p - pp);
+          pp = p;
+          tp.off_vals.push_back(9 * p - po);
+          tp.off_vals.push_back(7);
+          po = 9 * p + 7;
+        }
+        tp.pos_sizes.push_back(tf);
+        tp.off_sizes.push_back(2 * tf);
+      }
+      auto el = std::make_unique<EncodedList>();
+      encode_list(tp, el.get());
+      enc[v - b0] = std::move(el);
+    });
     for (int64_t v = b0; v < b1; ++v) { w.add(wiki_term(v), *enc[v - b0]); st.n_postings += enc[v - b0]->df; }
   }
   w.close();
   DocLengths lens;
   lens.c4.reserve(N);
-  for (int64_t d = 0; d < N; ++d) lens.add(len[d].load(std::memory_order_relaxed));
+  for (int64_t d = 0; d < N; ++d) lens.add(len[d]);
   lens.write(out_dir);
+  {
+    std::ofstream pf(out_dir + "/phrases.txt", std::ios::trunc);
+    if (!pf) throw std::runtime_error("cannot write " + out_dir + "/phrases.txt");
+    for (const auto& pr : pool) pf << wiki_term(pr.first) << ' ' << wiki_term(pr.second) << '\n';
+  }
   st.n_docs = N;
   st.n_terms = w.terms();
   st.vacuum_bytes = static_cast<int64_t>(w.bytes());

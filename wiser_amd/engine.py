@@ -152,9 +152,11 @@ class VacuumEngine:
         return lid.value, df.value
 
     def resolve(self, query: SearchQuery):
-        """-> (wsr_query, doc_freqs or None) with the reference's empty-result rules."""
-        if len(query.terms) > _capi.MAX_TERMS:
-            raise NotImplementedError(f"more than {_capi.MAX_TERMS} terms per query")
+        """-> (wsr_query, doc_freqs or None) with the reference's empty-result rules.
+        A query of more than MAX_TERMS terms carries the rest in more_ids (ctypes
+        keeps the array alive with the Query and with every array it is copied into)."""
+        if len(query.terms) > _capi.MAX_QUERY_TERMS:
+            raise NotImplementedError(f"more than {_capi.MAX_QUERY_TERMS} terms per query")
         if query.n_results > _capi.MAX_K:
             raise NotImplementedError(f"n_results above {_capi.MAX_K}")
         q = _capi.Query()
@@ -167,8 +169,11 @@ class VacuumEngine:
             dfs.append(df)
         missing = any(i < 0 for i in ids) or not ids
         q.n_terms = 0 if (missing or q.k == 0) else len(ids)
-        for i, lid in enumerate(ids):
+        for i, lid in enumerate(ids[:_capi.MAX_TERMS]):
             q.list_ids[i] = lid
+        if len(ids) > _capi.MAX_TERMS:
+            more = (C.c_int32 * (len(ids) - _capi.MAX_TERMS))(*ids[_capi.MAX_TERMS:])
+            q.more_ids = C.cast(more, C.POINTER(C.c_int32))
         freqs = None if (missing or q.k == 0) else dfs
         return q, freqs
 
@@ -332,7 +337,7 @@ class Server:
 
     def Search(self, query: SearchQuery) -> SearchResult:
         q, freqs = self.engine.resolve(query)
-        hits = (_capi.Hit * _capi.SERVER_MAX_K)()
+        hits = (_capi.Hit * max(1, q.k))()
         n = C.c_int32()
         check(lib.wsr_server_search(self._s, C.byref(q), hits, C.byref(n)))
         r = SearchResult()

@@ -156,13 +156,15 @@ class NativeShardedSearcher:
 
 
 class HostExchangeShardedSearcher:
-    """The fused step of NativeShardedSearcher with the transfer done by the
-    caller's torch.distributed group instead of RCCL: wsr_shard_emit (segments
-    append each query's reduced events to its owner's slot), an all_to_all of
-    the {count, offset} pairs and the slots, wsr_owner_replay_meta.  This is the
-    multi-rank rehearsal on ONE GPU (RCCL refuses two ranks on one device): the
-    gloo group moves host copies, so it checks the orchestration and the results,
-    not the exchange's speed.  Same step / max_fill / fetch_owned / close."""
+    """The step of NativeShardedSearcher with the transfer done by the caller's
+    torch.distributed group instead of RCCL, over the same buffers:
+    wsr_shard_step_emit (the segments append each query's reduced events to its
+    owner's region of the engine's send buffer, which is copied to the host),
+    one all_to_all of whole regions -- the exact layout wsr_shard_step's
+    ncclAllToAll moves -- and wsr_shard_step_replay.  This is the multi-rank
+    rehearsal on ONE GPU (RCCL refuses two ranks on one device): the gloo group
+    moves host copies, so it checks the orchestration, the region layout and the
+    results, not the exchange's speed.  Same step / max_fill / fetch_owned / close."""
 
     def __init__(self, index_dir: str, rank: int, world: int, group=None, device: int = 0,
                  threads: int = 0, positions: bool = False):
@@ -179,21 +181,15 @@ class HostExchangeShardedSearcher:
         import torch
         import torch.distributed as dist
         W = self.world
-        dev = torch.device("cuda", self.engine.device)
-        meta = torch.empty((W * qpr, 2), dtype=torch.int32, device=dev)
-        send = torch.empty((W * slot, EVENT_WORDS), dtype=torch.int64, device=dev)
-        check(lib.wsr_shard_emit(self.engine._h, b._b, qpr, W, slot, C.c_void_p(meta.data_ptr()),
-                                 C.c_void_p(send.data_ptr())))
-        check(lib.wsr_sync(self.engine._h))
-        rmeta = torch.empty((W * qpr, 2), dtype=torch.int32)
-        recv = torch.empty((W * slot, EVENT_WORDS), dtype=torch.int64)
-        dist.all_to_all_single(rmeta, meta.cpu(), group=self.group)
-        dist.all_to_all_single(recv, send.cpu(), group=self.group)
-        rmeta, recv = rmeta.to(dev), recv.to(dev)
-        torch.cuda.synchronize(dev)
-        check(lib.wsr_owner_replay_meta(self.engine._h, b._b, self.rank * qpr, qpr, W, slot,
-                                        C.c_void_p(rmeta.data_ptr()), C.c_void_p(recv.data_ptr())))
-        self._keep[id(b)] = (meta, send, rmeta, recv)   # alive until the replay has run
+        rb = C.c_uint64()
+        check(lib.wsr_shard_step_regions(qpr, slot, C.byref(rb)))
+        send = torch.empty(W * rb.value // 8, dtype=torch.int64)
+        check(lib.wsr_shard_step_emit(self.engine._h, b._b, W, qpr, slot, C.c_void_p(send.data_ptr())))
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)   # region o -> rank o, equal splits
+        check(lib.wsr_shard_step_replay(self.engine._h, b._b, self.rank, W, qpr, slot,
+                                        C.c_void_p(recv.data_ptr())))
+        self._keep[(id(b), b.nq)] = (b, send, recv)   # alive until the replay has run
 
     def max_fill(self, b) -> int:
         tot = (C.c_int64 * self.world)()
@@ -249,14 +245,15 @@ class ShardedSearcher:
         on_gpu = torch.cuda.is_available()
         dev = torch.device("cuda", eng.device) if on_gpu else torch.device("cpu")
         # per batch and slot size: buffers used only in the batch's stream order
-        key = (id(b), slot)
+        key = (id(b), slot, Q, self.world)
         if key not in self._xbufs:
-            self._xbufs[key] = (
+            self._xbufs[key] = (b,) + (
                 torch.empty(Q, dtype=torch.int32, device=dev),
                 torch.empty((self.world * slot, EVENT_WORDS), dtype=torch.int64, device=dev),
                 torch.empty((self.world, qpr), dtype=torch.int32, device=dev),
                 torch.empty((self.world * slot, EVENT_WORDS), dtype=torch.int64, device=dev))
-        counts, send, rc_buf, rv_buf = self._xbufs[key]
+        _, counts, send, rc_buf, rv_buf = self._xbufs[key]
+        assert counts.numel() >= b.nq
         check(lib.wsr_shard_pack_fixed(eng._h, b._b, qpr, self.world, slot, C.c_void_p(counts.data_ptr()),
                                        C.c_void_p(send.data_ptr())))
         st = C.c_void_p()
