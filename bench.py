@@ -132,6 +132,9 @@ def parse():
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
+    p.add_argument("--max-inflight", type=int, default=0,
+                   help="timed loops: before launching step s, wait until the batch of step s-K has "
+                        "finished (K batches in flight at most; 0: no host throttle)")
     p.add_argument("--heavy-blocks", type=int, default=-1,
                    help="N>1 hybrid: queries whose driver list has at least this many 128-posting "
                         "blocks run on every shard (RCCL exchange); the others run whole on the "
@@ -928,8 +931,11 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
     if dist:
         dist.barrier()
     w.sync(eng)
+    K = a.max_inflight if a.max_inflight < nb else 0
     t0 = time.perf_counter()
     for s in range(a.steps):
+        if K and s >= K:
+            batches[(s - K) % nb].wait_ready()
         batches[s % nb].run()
     host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     w.sync(eng)

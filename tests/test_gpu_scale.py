@@ -203,3 +203,28 @@ def test_c5_full_size_phrases(c3_full):
            for q, r, x in zip(qs, res, want) if [(e.doc_id, e.doc_score) for e in r.entries] != x]
     assert not bad, bad[:3]
     assert sum(1 for x in want if x) > len(qs) // 2
+
+
+def test_c3_full_size_merge_class(c3_full):
+    """The merge class (merge_kernel: driver and O1 decoded and merged) on the
+    full-size stand-in's log: 2,048 queries, bit for bit, with every eligible
+    query merged (WSR_MERGE_RATIO huge) and at the bench's setting (8)."""
+    import wiser_amd as w
+    d, log, _ = c3_full
+    for ratio in ("1000000000", "8"):
+        saved = {k: os.environ.get(k) for k in ("WSR_MERGE_RATIO", "WSR_MERGE_MIN")}
+        os.environ["WSR_MERGE_RATIO"] = ratio
+        os.environ["WSR_MERGE_MIN"] = "1"
+        try:
+            eng = w.VacuumEngine(d, positions=False)
+            eng.Load()
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        try:
+            _check_log(d, log, 2048, stride=47, eng=eng)
+        finally:
+            eng.close()

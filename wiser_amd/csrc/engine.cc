@@ -120,6 +120,7 @@ struct wsr_handle {
   std::vector<uint32_t> meta;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
+  int merge_wgs = 0;   // merge kernel: workgroups of kMergeWaves waves
   int gen_cap = 0;     // general workgroups launched at most
 };
 
@@ -147,6 +148,7 @@ struct wsr_batch {
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   int seg_grid = 0;
   int lean_wgs = 0;
+  int merge_wgs = 0;              // 0: the batch has no merge item
   // doc-range shard exchange
   uint64_t* d_soff = nullptr;     // per query send offset (events)
   int64_t* d_otot = nullptr;      // per owner totals
@@ -168,9 +170,10 @@ struct wsr_batch {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
   // device (one's plan and first items under the other's last items); the
-  // general kernel goes to st2, forked from and joined back into st.
-  hipStream_t st = nullptr, st2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  // general kernel goes to st2 and the merge kernel to st3, forked from and
+  // joined back into st.
+  hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
   bool ran = false;
 };
 
@@ -261,6 +264,10 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
     h->args.and_wpb = static_cast<float>(env_number("WSR_AND_WPB", 0.0));
+    // merge class (merge_kernel): O1 at most WSR_MERGE_RATIO times the driver's
+    // blocks (0: off), a driver of at least WSR_MERGE_MIN blocks
+    h->args.merge_ratio = static_cast<float>(env_number("WSR_MERGE_RATIO", 0.0));
+    h->args.merge_min = static_cast<uint32_t>(env_number("WSR_MERGE_MIN", 2));
     h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
     h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
@@ -303,6 +310,9 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     int locc = lean_kernel_occupancy();
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
+    int mocc = merge_kernel_occupancy();
+    if (mocc < 1) mocc = 1;
+    h->merge_wgs = prop.multiProcessorCount * std::min(mocc, 16);
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -541,12 +551,15 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
-                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1))));
+                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1) +
+                                       kMergeWaves * std::max(h->merge_wgs, 1))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&b->st3, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&b->fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&b->join, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&b->join3, hipEventDisableTiming));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
     return fail(WSR_E_HIP, e.what());
@@ -559,6 +572,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (!b) return;
   if (b->st) (void)hipStreamSynchronize(b->st);
   if (b->st2) (void)hipStreamSynchronize(b->st2);
+  if (b->st3) (void)hipStreamSynchronize(b->st3);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_desc), static_cast<void*>(b->d_part),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
@@ -575,8 +589,10 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
   if (b->fork) (void)hipEventDestroy(b->fork);
   if (b->join) (void)hipEventDestroy(b->join);
+  if (b->join3) (void)hipEventDestroy(b->join3);
   if (b->st) (void)hipStreamDestroy(b->st);
   if (b->st2) (void)hipStreamDestroy(b->st2);
+  if (b->st3) (void)hipStreamDestroy(b->st3);
   delete b;
 }
 
@@ -604,7 +620,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   uint64_t ev_need = 0, items_need = 0, algo = 0;
   // the device's class rule (plan_query_kernel), restated to size the two
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
-  uint64_t lean_need = 0, gen_need = 0;
+  uint64_t lean_need = 0, gen_need = 0, merge_need = 0;
   const float dense_ratio = h->args.dense_ratio;
   bool has_phrase = false, has_wide = false;
   std::vector<int32_t> ids;
@@ -641,14 +657,23 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       int drv = 0;
       for (int t = 1; t < d.n_terms; ++t)
         if (h->lists[ids[t]].nblk < h->lists[ids[drv]].nblk) drv = t;
-      bool lean = true;
-      for (int t = 0; t < d.n_terms; ++t) {
+      auto dense = [&](int t) {
         const ListDev& L = h->lists[ids[t]];
-        if (t != drv && !(L.bm != kNoDense &&
-                          static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin)))
-          lean = false;
+        return L.bm != kNoDense && static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin);
+      };
+      int o1 = -1;
+      for (int t = 0; t < d.n_terms; ++t)
+        if (t != drv && (o1 < 0 || h->lists[ids[t]].nblk < h->lists[ids[o1]].nblk)) o1 = t;
+      bool lean = true, merge = o1 >= 0 && !phrase && nbmin >= h->args.merge_min &&
+                                static_cast<float>(h->lists[ids[o1]].nblk) <=
+                                    h->args.merge_ratio * static_cast<float>(nbmin);
+      for (int t = 0; t < d.n_terms; ++t) {
+        if (t == drv || dense(t)) continue;
+        lean = false;
+        if (t != o1) merge = false;
       }
-      (lean ? lean_need : gen_need) += nbmin;
+      // (the device's rule, plan_query_kernel: merge before lean and general)
+      (merge ? merge_need : lean ? lean_need : gen_need) += nbmin;
       for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[ids[t]];
       algo += 12ull * d.k;
     }
@@ -699,6 +724,11 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
       1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
+  // (merge items exist only when the merge class is on; the grid drains them all)
+  b->merge_wgs = h->args.merge_ratio > 0.0f
+                     ? static_cast<int>(std::max<uint64_t>(
+                           1, std::min<uint64_t>(h->merge_wgs, (merge_need + kMergeWaves - 1) / kMergeWaves)))
+                     : 0;
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -746,7 +776,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq,
+                       kLeanWaves * b->lean_wgs, kMergeWaves * b->merge_wgs, b->seg_grid, fr, b->d_itemq,
                        h->seg_floor ? b->d_pub : nullptr, b->d_desc, b->d_part, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
@@ -758,6 +788,13 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
                            h->seg_floor ? b->d_pub : nullptr,
                            b->has_phrase ? b->d_ph : nullptr, b->st2));
     HIP_OK(hipEventRecord(b->join, b->st2));
+    if (b->merge_wgs) {   // merge items on the third stream
+      HIP_OK(hipStreamWaitEvent(b->st3, b->fork, 0));
+      HIP_OK(launch_merge(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
+                          b->d_stats + static_cast<size_t>(kStatStride) * (b->seg_grid + kLeanWaves * b->lean_wgs),
+                          b->merge_wgs, fr, b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc, b->st3));
+      HIP_OK(hipEventRecord(b->join3, b->st3));
+    }
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
                        b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc,
@@ -765,6 +802,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
                                      : nullptr, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
+    if (b->merge_wgs) HIP_OK(hipStreamWaitEvent(st, b->join3, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
     if (replay && !fused)
       HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
@@ -885,7 +923,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
+    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs + kMergeWaves * b->merge_wgs;
     std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * rows);
     HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     uint64_t sv = 0, db = 0, ob = 0;
@@ -1488,7 +1526,8 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                        int32_t* n_wg, int32_t* stride) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
-  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;   // general workgroups, then lean waves
+  // general workgroups, then lean waves, then merge waves
+  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs + kMergeWaves * b->merge_wgs;
   if (n_wg) *n_wg = rows;
   if (stride) *stride = kStatStride;
   if (!out) return WSR_OK;

@@ -31,6 +31,10 @@ struct IndexArgs {
   float and_wpb;            // lean items of a driver with a bitmap intersect bitmaps word by
                             // word when their doc span is <= and_wpb 32-doc words per driver
                             // block (0 = never)
+  float merge_ratio;        // merge class: the most selective other list O1 has at most
+                            // merge_ratio times the driver's blocks (0 = never); O1 is then
+                            // decoded beside the driver and the two merged, not probed
+  uint32_t merge_min;       //   ... and the driver at least merge_min blocks
   // positions (phrase queries; null unless the engine was opened with them)
   const uint8_t* pos_blob;  // every list's position cozy box, byte-exact from my.vacuum
   const PosDev* pos_lists;  // indexed by list id
@@ -41,17 +45,23 @@ struct IndexArgs {
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
-// 4 error flags, 6 lean items (items [0, lean) run in lean_kernel, the rest in
+// 4 error flags, 6 end of the lean items, 8 end of the merge items (items
+// [0, lean) run in lean_kernel, [lean, merge) in merge_kernel, the rest in
 // segment_kernel); each work queue has one head per XCD-sized shard, each on
-// its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 + 16*s general), so
-// the dequeues of the persistent workers do not serialise on a single line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16, kQueueShards = 8,
-       kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
+// its own 64-byte line (kCtrHead0 + 16*s lean, kCtrMHead0 + 16*s merge,
+// kCtrGHead0 + 16*s general), so the dequeues of the persistent workers do
+// not serialise on a single line.
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrMerge = 8, kCtrHead0 = 16,
+       kQueueShards = 8,
+       kCtrMHead0 = kCtrHead0 + 16 * kQueueShards,
+       kCtrGHead0 = kCtrMHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
-// QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean
+// QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean / kPlanMerge
 constexpr uint32_t kPlanSlotMask = 0x7FFu;   // (kMaxQueryTerms <= 2048)
 constexpr int kPlanBucketShift = 12;
 constexpr uint32_t kPlanLean = 1u << 16;
+constexpr uint32_t kPlanMerge = 1u << 17;
+constexpr int kMergeWaves = 4;   // independent waves per merge_kernel workgroup
 static_assert(kMaxQueryTerms <= static_cast<int>(kPlanSlotMask) + 1, "driver slot field");
 constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
 // per-workgroup statistics written by the segment kernel (no atomics):
@@ -125,7 +135,7 @@ struct FusedReplay {
 // per item key (class, cost bucket) and its event capacity.
 constexpr int kPlanThreads = 256;
 struct PlanPart {
-  uint32_t items[2 * kCostBuckets];
+  uint32_t items[3 * kCostBuckets];
   uint64_t cap;
 };
 
@@ -136,7 +146,7 @@ constexpr int kPhraseScratch = kMaxPhraseTerms * 256;
 // plan queries (2 launches); part: per plan workgroup of kPlanThreads queries
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int merge_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
@@ -150,6 +160,13 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
                        uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st);
 int lean_kernel_occupancy();
+// merge items (QueryPlan kPlanMerge): merge_wgs workgroups of kMergeWaves waves;
+// stats of wave w at stats[w * kStatStride]
+hipError_t launch_merge(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
+                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                        int merge_wgs, const FusedReplay& fr, const uint32_t* item_q,
+                        uint64_t* pub, const QueryDesc* desc, hipStream_t st);
+int merge_kernel_occupancy();
 hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                          const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                          hipStream_t st);

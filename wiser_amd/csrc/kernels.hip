@@ -355,14 +355,15 @@ __device__ __forceinline__ const int32_t* qlist_of(const QueryIn* qs, int qi) {
 }
 
 // ----------------------------------------------------------------- plan --
-// Item order: class-major (lean items first, then general ones), then cost
-// bucket-major, heaviest bucket first (query order inside a bucket, a query's
+// Item order: class-major (lean items first, then merge items, then general
+// ones), then cost bucket-major, heaviest bucket first (query order inside a bucket, a query's
 // items consecutive), so the persistent workers take the long items first and
 // the short ones fill the tail (longest-first list scheduling).
-constexpr int kPlanKeys = 2 * kCostBuckets;
+constexpr int kPlanKeys = 3 * kCostBuckets;   // classes: lean, merge, general
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
   const uint32_t bucket = (drv >> kPlanBucketShift) & 0xFu;
-  return ((drv & kPlanLean) ? 0u : static_cast<uint32_t>(kCostBuckets)) + (kCostBuckets - 1 - bucket);
+  const uint32_t cls = (drv & kPlanLean) ? 0u : (drv & kPlanMerge) ? 1u : 2u;
+  return cls * kCostBuckets + (kCostBuckets - 1 - bucket);
 }
 
 // block-wide sums over the 256 threads of a plan workgroup (4 waves)
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     // all of them are in flight together); longer queries: plain loops.
     uint32_t d = 0, nd = 0xFFFFFFFFu, o1 = kNoSlot, min_last = 0xFFFFFFFFu;
     float cost = 1.0f;
-    bool lean = true;
+    bool lean = true, merge_ok = false;
     if (nt <= kMaxTerms) {
       uint32_t nb[kMaxTerms], last[kMaxTerms];
       bool dn[kMaxTerms];
@@ -484,6 +485,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         min_last = last[s] < min_last ? last[s] : min_last;
         if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
       }
+      // merge class: every other list but O1 has a bitmap, O1 is at most
+      // merge_ratio times as long as the driver
+      merge_ok = o1 != kNoSlot && static_cast<float>(o_nb) <= ix.merge_ratio * static_cast<float>(nd);
+#pragma unroll
+      for (int s = 0; s < kMaxTerms; ++s)
+        if (s < nt && s != static_cast<int>(d) && s != static_cast<int>(o1) && !use_dense(ix, dn[s], nb[s], nd))
+          merge_ok = false;
     } else if (ok) {
       for (int s = 0; s < nt; ++s) {
         const int32_t id = ql[s];
@@ -502,10 +510,21 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         min_last = L.last < min_last ? L.last : min_last;
         if (L.nblk < o_nb) { o1 = s; o_nb = L.nblk; }
       }
+      merge_ok = ok && o1 != kNoSlot && static_cast<float>(o_nb) <= ix.merge_ratio * static_cast<float>(nd);
+      for (int s = 0; merge_ok && s < nt; ++s) {
+        if (s == static_cast<int>(d) || s == static_cast<int>(o1)) continue;
+        const ListDev& L = ix.lists[ql[s]];
+        if (!use_dense(ix, L.bm != kNoDense, L.nblk, nd)) merge_ok = false;
+      }
     }
     if (ok) {
       const bool ph = nt > 1 && (q.flags & kQueryPhrase);
-      uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : lean ? kSegCost : kSegCostGeneral) / cost);
+      // merge class (merge_kernel): conjunctive, two or more terms, a driver of
+      // at least merge_min blocks; it takes such queries from the lean and the
+      // general class alike
+      const bool merge = merge_ok && !ph && nd >= ix.merge_min;
+      if (merge) { lean = false; cost = 1.0f; }
+      uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : (lean || merge) ? kSegCost : kSegCostGeneral) / cost);
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
       // for the per-item setup): the queue hands out heavy items first
@@ -513,10 +532,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       const uint32_t ic = static_cast<uint32_t>(item_cost);
       const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
       const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u);
+      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u) | (merge ? kPlanMerge : 0u);
       p.seg_blocks = seg;
       p.n_items = (nd + seg - 1) / seg;
-      if (lean) {
+      if (lean || merge) {
         // the lean kernel's record (bases are added by plan_fill_kernel)
         // (the driver's and O1's records: a second round of loads, side by side)
         const ListDev A = ix.lists[ql[d]];
@@ -597,7 +616,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
                                                         const PlanPart* __restrict__ part, int n_part,
                                                         uint32_t* __restrict__ counters,
                                                         uint64_t ev_capacity, uint32_t item_capacity,
-                                                        uint32_t lean_grid, uint32_t seg_grid,
+                                                        uint32_t lean_grid, uint32_t merge_grid, uint32_t seg_grid,
                                                         uint32_t* __restrict__ item_q,
                                                         uint64_t* __restrict__ pub,
                                                         QueryDesc* __restrict__ desc) {
@@ -636,12 +655,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
   }
   __syncthreads();
   uint32_t key_base[kPlanKeys];
-  uint32_t run = 0, n_lean = 0;
+  uint32_t run = 0, n_lean = 0, n_merge_end = 0;
 #pragma unroll
   for (int k = 0; k < kPlanKeys; ++k) {
     key_base[k] = run + s_key_below[k];
     run += s_key_all[k];
     if (k == kCostBuckets - 1) n_lean = run;
+    if (k == 2 * kCostBuckets - 1) n_merge_end = run;
   }
   const uint32_t total_items = run;
   const bool fits = s_cap_all <= ev_capacity && total_items <= item_capacity;
@@ -666,7 +686,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     plan[i].ev_base = cb;
     // (skipped when the plan does not fit the workspace: never written past it)
     if (fits) {
-      if (p.driver & kPlanLean) {
+      if (p.driver & (kPlanLean | kPlanMerge)) {
         desc[i].item_base = base;
         desc[i].ev_base = cb;
       }
@@ -681,6 +701,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
       if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
       counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
       counters[kCtrLean] = fits ? n_lean : 0u;
+      counters[kCtrMerge] = fits ? n_merge_end : 0u;
       counters[kCtrEvCap] = static_cast<uint32_t>(s_cap_all > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap_all);
     }
     // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
@@ -688,6 +709,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     // those first items (lean: one worker per wave; general: per workgroup).
     if (t < kQueueShards) {
       counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
+      counters[kCtrMHead0 + 16 * t] = (merge_grid + kQueueShards - 1 - t) / kQueueShards;
       counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
     }
   }
@@ -2333,10 +2355,10 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) S.norm[l + 64 * i] = ix.cache[l + 64 * i];
   const uint64_t lt = lanemask_lt();
-  // general items are [n_lean, total): the lean kernel takes the others
+  // general items are [merge end, total): the lean and merge kernels take the others
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
+  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrMerge], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0, n_oblk = 0;
   // first item: this workgroup's own index; then the shard heads
@@ -2879,6 +2901,465 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd 
   }
 }
 
+// ------------------------------------------------------------ merge path --
+// Items of the merge class: the driver and the most selective other list O1
+// are both decoded from their packs and merged, instead of probing O1's rank
+// bitmap once per driver posting.  At en-Wikipedia shape the bitmap probes of
+// two long lists touch about 46 cache lines per driver block (O1 holds ~1-3 %
+// of the docs, its bitmap 2 bits per doc), which is what bounds the lean
+// kernel there (TA/TD ~80 % busy, profiles/r03_c_pmc); O1's own blocks over
+// the same doc range are ~R x 200 bytes, streamed (R = O1's blocks per driver
+// block, at most WSR_MERGE_RATIO).  Reference: the intersection this replaces
+// is TwoTermNonPhraseQueryProcessor::Process / QueryProcessor::FindMatch
+// (query_processing.h:656-677,810-852) over DocIdIterator::SkipForward
+// (flash_iterators.h:181-227); the survivors, their scores and the events are
+// the lean kernel's, so the replay and its exactness argument are unchanged.
+//
+// Per driver block j (doc range (prev_j, last_j]): O1's blocks [lo_j, hi_j]
+// that overlap it are decoded into an LDS ring (block b at slot b % ring; a
+// block shared with block j-1 is not decoded again), each driver doc is
+// searched in them (which block by the ring's last docs, then lower_bound in
+// the block), and the hits join the lean kernel's survivor queue.  The words
+// of driver block j+1 and of up to kMergeG of its new O1 blocks are loaded
+// while block j is processed (two alternating register sets); more O1 blocks,
+// or a range wider than the ring, take a slower synchronous path.
+#ifndef WSR_MERGE_RING
+#define WSR_MERGE_RING 8
+#endif
+#ifndef WSR_MERGE_G
+#define WSR_MERGE_G 4
+#endif
+constexpr int kMergeRing = WSR_MERGE_RING;   // O1 blocks held decoded (a power of two)
+constexpr int kMergeG = WSR_MERGE_G;         // O1 blocks prefetched per driver block
+static_assert((kMergeRing & (kMergeRing - 1)) == 0 && kMergeG <= kMergeRing, "merge ring");
+constexpr uint32_t kMergeQ = 128;            // survivor queue entries (a ring)
+
+struct MergeLds {
+  uint32_t ring[kMergeRing * 128];   // O1 doc ids; entries past a block's count are ~0u
+  uint32_t rlast[kMergeRing];        // last doc id of the block in each slot
+  uint32_t q[4 * kMergeQ];           // survivors: doc, length code, driver tf, O1 posting (block << 7 | pos)
+  Event evs[64];
+  uint4 dblk[64];                    // the driver's directory entries of the segment
+  uint32_t dmeta[64];
+};
+
+__device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, const double* norm_tab,
+                                              const QueryDesc& Q, const int32_t* qlist, uint32_t b0,
+                                              uint32_t b1, bool dtail, uint32_t tdoc0, uint32_t tdoc1,
+                                              uint32_t ttf0, uint32_t ttf1, const uint64_t* prev_pub,
+                                              uint64_t* my_pub, Event* ev_out, uint32_t& ev_n, double& pt,
+                                              uint32_t& pt_n, uint32_t& n_surv, uint32_t& n_dblk) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt();
+  const uint32_t d = Q.slots & 0xFFFFu, o1 = Q.slots >> 16;
+  const uint32_t nt = Q.nt & 0xFFFFu, k = Q.k;
+  const bool wide = k > static_cast<uint32_t>(kMaxK);
+  const ListDev O = ix.lists[Q.o_list];
+  const uint32_t o_blk0 = uni(O.blk0), o_nblk = uni(O.nblk), o_tcnt = uni(O.tail_cnt);
+  const uint8_t* o_blob = ix.blob + O.base;
+  const bool o_vtail = O.tail != kNoTail;
+  const uint32_t* o_tails = ix.tails + (o_vtail ? O.tail : 0ull);
+  const uint8_t* a_blob = ix.blob + Q.a_base;
+  const uint32_t lo = in_vgpr(ix.doc_lo), hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);
+  const uint32_t min_last = Q.min_last;
+  const double idf_d = in_vgpr(Q.a_idf), idf_o = in_vgpr(Q.o_idf);
+  uint32_t* qdoc = S.q;
+  uint32_t* qc4 = S.q + kMergeQ;
+  uint32_t* qtd = S.q + 2 * kMergeQ;
+  uint32_t* qpo = S.q + 3 * kMergeQ;
+  uint32_t qhead = 0, qtail = 0, evb = 0;
+  uint64_t floor_bits =
+      prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  double pub_val = 0.0, sent = 0.0;
+
+  auto flush = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
+    __builtin_amdgcn_wave_barrier();
+    evb = 0;
+  };
+  // score survivors qhead .. qhead + n (n <= 64, lane = doc order), then the
+  // running top-k (as lean_segment's score_chunk)
+  auto score_chunk = [&](uint32_t n) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t e = (qhead + l) & (kMergeQ - 1);
+    bool alive = l < n;
+    const uint32_t doc = qdoc[e];
+    const uint32_t c4 = qc4[e];
+    const uint32_t td = qtd[e];
+    const uint32_t po = qpo[e];
+    __builtin_amdgcn_wave_barrier();
+    qhead += n;
+    // O1's tf: its pack (two dependent loads per survivor), or its decoded VInts tail
+    const uint32_t ob = alive ? po >> 7 : 0u, opos = po & 127u;
+    uint32_t to = 0;
+    if (o_vtail && ob == o_nblk - 1) {
+      to = o_tails[o_tcnt + opos];
+    } else {
+      const uint32_t tb = ix.blk_meta[o_blk0 + ob] >> 8;
+      const uint32_t trel = ix.blocks[o_blk0 + ob].tf_rel;
+      to = pack_value(o_blob + trel + 2, tb ? tb : 1u, opos);
+    }
+    const double norm = norm_tab[c4 & 255u];
+    double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
+    for (uint32_t s = 0; s < nt; ++s) {
+      if (s == d) {
+        sc += bm25_term(idf_d, alive ? td : 0u, norm);
+      } else if (s == o1) {
+        sc += bm25_term(idf_o, alive ? to : 0u, norm);
+      } else {
+        const ListDev B = ix.lists[qlist[s]];
+        uint32_t t = 0, x = 0;
+        const uint2 v = dense_load(ix, B, doc, alive);
+        alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
+        if (__ballot(alive) == 0) break;
+        sc += bm25_term(B.idf, alive ? t : 0u, norm);
+      }
+    }
+    const uint64_t am = __ballot(alive);
+    if (am == 0) return;
+    n_surv += __popcll(am);
+    if (wide) {   // all of them, in doc order (lane order), no floor
+      if (alive) {
+        Event ev;
+        ev.score = sc;
+        ev.doc = static_cast<int32_t>(doc);
+        ev.pad = 0;
+        S.evs[evb + __popcll(am & lt)] = ev;
+      }
+      ev_n += __popcll(am);
+      evb += __popcll(am);
+      flush();
+      return;
+    }
+    // the floor of the query's earlier items as it stands now (it only grows)
+    if (prev_pub) {
+      const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t fu = (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
+                          uni(static_cast<uint32_t>(fb));
+      if (fu > floor_bits) floor_bits = fu;
+    }
+    const uint64_t fb = floor_bits;
+    const double flo = __longlong_as_double(static_cast<long long>(fb));
+    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    uint64_t cm = __ballot(alive && sc > flo && (pt_n < k || sc > kth));
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const double sv = readlane_f64(sc, fl);
+      const uint32_t dv = __builtin_amdgcn_readlane(doc, fl);
+      const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
+      if (pos < k) {
+        if (l == 0) {
+          Event ev;
+          ev.score = sv;
+          ev.doc = static_cast<int32_t>(dv);
+          ev.pad = 0;
+          S.evs[evb] = ev;
+        }
+        ++ev_n;
+        ++evb;
+        const double up = wave_shr1_f64(pt);
+        if (l > pos) pt = up;
+        else if (l == pos) pt = sv;
+        pt_n = pt_n + 1 > k ? k : pt_n + 1;
+      }
+    }
+    if (evb) flush();
+    const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    const double pv = kn > flo ? kn : flo;
+    pub_val = pv > pub_val ? pv : pub_val;
+    if (my_pub && pub_val > sent) {   // hand the floor down the query's chain of items
+      if (l == 0)
+        __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      sent = pub_val;
+    }
+  };
+
+  // O1 directory window: lane l holds block wb + l (last = ~0u past the list)
+  uint32_t wb = 0, w_prev = 0, w_last = ~0u, w_doc = 0, w_meta = 0;
+  auto load_window = [&](uint32_t base) __attribute__((always_inline)) {
+    wb = base;
+    const uint32_t e = base + l;
+    w_prev = 0; w_last = ~0u; w_doc = 0; w_meta = 0;
+    if (e < o_nblk) {
+      const uint4 bd = reinterpret_cast<const uint4*>(ix.blocks)[o_blk0 + e];
+      w_prev = bd.x; w_last = bd.y; w_doc = bd.z;
+      w_meta = ix.blk_meta[o_blk0 + e];
+    }
+  };
+  // first O1 block at or after wb whose last doc is >= x (o_nblk if none);
+  // slides the window forward (callers ask in nondecreasing x)
+  auto first_ge = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
+    for (;;) {
+      const uint64_t below = __ballot(w_last < x);
+      if (~below) return min(wb + static_cast<uint32_t>(__builtin_ctzll(~below)), o_nblk);
+      if (wb + 64 >= o_nblk) return o_nblk;
+      load_window(wb + 64);
+    }
+  };
+  // the window must hold block b to decode it
+  auto cover = [&](uint32_t b) __attribute__((always_inline)) {
+    if (b < wb || b >= wb + 64) load_window(b);
+  };
+  // words of O1 block b for lane l (the VInts tail: its decoded doc ids)
+  auto o1_words = [&](uint32_t b, uint32_t& x0, uint32_t& x1, uint32_t& x2) __attribute__((always_inline)) {
+    const uint32_t i = b - wb;
+    const uint32_t bits = __builtin_amdgcn_readlane(w_meta, static_cast<int>(i)) & 0xFFu;
+    if (bits) {
+      uint32_t sh;
+      pair_words(o_blob + __builtin_amdgcn_readlane(w_doc, static_cast<int>(i)) + 2, bits, l, x0, x1, x2, sh);
+    } else {   // (only the list's last block is a VInts blob)
+      x0 = 2 * l < o_tcnt ? o_tails[2 * l] : 0u;
+      x1 = 2 * l + 1 < o_tcnt ? o_tails[2 * l + 1] : 0u;
+      x2 = 0;
+    }
+  };
+  uint32_t dec_hi = 0xFFFFFFFFu;   // the highest O1 block decoded (none yet)
+  // decode O1 block b (window-resident) from its words into its ring slot
+  auto o1_decode = [&](uint32_t b, uint32_t x0, uint32_t x1, uint32_t x2) __attribute__((always_inline)) {
+    const uint32_t i = b - wb;
+    const uint32_t m = __builtin_amdgcn_readlane(w_meta, static_cast<int>(i));
+    const uint32_t bits = m & 0xFFu;
+    const uint32_t cnt = b == o_nblk - 1 ? o_tcnt : 128u;
+    uint32_t v0, v1;
+    if (bits) {
+      const uint32_t rel = __builtin_amdgcn_readlane(w_doc, static_cast<int>(i));
+      const uint32_t bit = 2 * l * bits;
+      const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_blob)) + rel + 2 + (bit >> 3);
+      uint32_t y0, y1;
+      pair_values(x0, x1, x2, ((a & 3u) << 3) + (bit & 7u), bits, y0, y1);
+      const uint32_t sm = y0 + y1;
+      const uint32_t inc = wave_incl_scan(sm);
+      v0 = __builtin_amdgcn_readlane(w_prev, static_cast<int>(i)) + (inc - sm) + y0;
+      v1 = v0 + y1;
+    } else {
+      v0 = x0;
+      v1 = x1;
+    }
+    uint32_t* r = &S.ring[(b & (kMergeRing - 1)) * 128];
+    r[2 * l] = 2 * l < cnt ? v0 : 0xFFFFFFFFu;
+    r[2 * l + 1] = 2 * l + 1 < cnt ? v1 : 0xFFFFFFFFu;
+    if (l == 0) S.rlast[b & (kMergeRing - 1)] = __builtin_amdgcn_readlane(w_last, static_cast<int>(i));
+    dec_hi = b;
+  };
+  // lower_bound of x over ring blocks [c0, c1] (resident, c1 - c0 < ring):
+  // *blk = first block whose last >= x (c1 + 1: none), *pos = slot in it
+  auto ring_find = [&](uint32_t x, uint32_t c0, uint32_t c1, uint32_t* blk, uint32_t* pos)
+      __attribute__((always_inline)) {
+    uint32_t b = c0;
+    while (b <= c1 && S.rlast[b & (kMergeRing - 1)] < x) ++b;   // (at most the ring's blocks)
+    *blk = b;
+    if (b > c1) { *pos = 128; return; }
+    *pos = lds_lower_bound(&S.ring[(b & (kMergeRing - 1)) * 128], 128, x);
+  };
+
+  // two alternating register sets: driver block words, tf words, length codes,
+  // and the words of up to kMergeG new O1 blocks
+  struct MRegs {
+    uint32_t w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0, wc = 0;
+    uint32_t o0[kMergeG], o1w[kMergeG], o2[kMergeG];
+    uint32_t ob0 = 0, on = 0;    // prefetched O1 blocks [ob0, ob0 + on)
+  };
+  MRegs R0, R1;
+  auto issue = [&](uint32_t j, uint32_t hi_prev, MRegs& Y) __attribute__((always_inline)) {
+    const uint32_t bi = j - b0;
+    const uint32_t m = uni(S.dmeta[bi]);
+    const uint4 e = S.dblk[bi];
+    uint32_t sh;
+    pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
+    pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.t0, Y.t1, Y.t2, sh);
+    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + j) * 32u + (l >> 1)];
+    // O1 blocks this driver block will need beyond those the previous one
+    // needed (hi_prev: its last; every later block starts at or after it)
+    const uint32_t hi = first_ge(uni(e.y));
+    const uint32_t from = hi_prev == 0xFFFFFFFFu ? first_ge(j == 0 ? 0u : uni(e.x) + 1u) : hi_prev + 1;
+    Y.ob0 = from;
+    Y.on = 0;
+    if (hi < o_nblk && hi >= from && from >= wb) {
+      const uint32_t want = min(hi - from + 1, static_cast<uint32_t>(kMergeG));
+      const uint32_t n = min(want, wb + 64 - from);   // (inside the window)
+#pragma unroll
+      for (int g = 0; g < kMergeG; ++g)
+        if (static_cast<uint32_t>(g) < n) o1_words(from + g, Y.o0[g], Y.o1w[g], Y.o2[g]);
+      Y.on = n;
+    }
+  };
+
+  uint32_t bend = b1;
+  // block j with the words in X
+  auto body = [&](MRegs& X, MRegs& Y, uint32_t j) __attribute__((always_inline)) {
+    const uint32_t bi = j - b0;
+    const uint4 be = S.dblk[bi];
+    const uint32_t m = uni(S.dmeta[bi]);
+    const uint32_t a_first = j == 0 ? 0u : uni(be.x) + 1u, a_last = uni(be.y);
+    // O1 blocks overlapping this driver block
+    const uint32_t lo_j = first_ge(a_first);
+    const uint32_t hi_j = min(first_ge(a_last), o_nblk - 1);
+    // decode the prefetched O1 blocks (they start after the last decoded one)
+    for (uint32_t g = 0; g < X.on; ++g) {
+      const uint32_t b = X.ob0 + g;
+      if (dec_hi != 0xFFFFFFFFu && b <= dec_hi) continue;
+      cover(b);
+      uint32_t x0 = X.o0[0], x1 = X.o1w[0], x2 = X.o2[0];
+#pragma unroll
+      for (int gg = 1; gg < kMergeG; ++gg)
+        if (g == static_cast<uint32_t>(gg)) { x0 = X.o0[gg]; x1 = X.o1w[gg]; x2 = X.o2[gg]; }
+      o1_decode(b, x0, x1, x2);
+    }
+    // W(j+1): the next block's words and its first new O1 blocks
+    if (j + 1 < bend) issue(j + 1, hi_j, Y);
+    // D(j): the driver's doc ids, tfs and length codes
+    const uint32_t cnt = (j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u;
+    uint32_t x0, x1, t0, t1;
+    {
+      const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
+      const uint32_t bit = 2 * l * wbits;
+      const uint32_t ad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + uni(be.z) + 2 + (bit >> 3);
+      pair_values(X.w0, X.w1, X.w2, ((ad & 3u) << 3) + (bit & 7u), wbits, x0, x1);
+      const uint32_t tbit = 2 * l * wtb;
+      const uint32_t at = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + uni(be.w) + 2 + (tbit >> 3);
+      pair_values(X.t0, X.t1, X.t2, ((at & 3u) << 3) + (tbit & 7u), wtb, t0, t1);
+    }
+    const uint32_t sm = x0 + x1;
+    const uint32_t inc = wave_incl_scan(sm);
+    uint32_t a0 = uni(be.x) + (inc - sm) + x0;
+    uint32_t a1 = a0 + x1;
+    const bool tl = dtail && j == b1 - 1;
+    if (tl) { a0 = tdoc0; a1 = tdoc1; t0 = ttf0; t1 = ttf1; }
+    const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
+    const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
+    const bool ok0 = (2 * l < cnt) & (a0 - lo < hi_rel);
+    const bool ok1 = (2 * l + 1 < cnt) & (a1 - lo < hi_rel);
+    ++n_dblk;
+    if (__ballot((ok0 & (a0 > min_last)) | (ok1 & (a1 > min_last)))) bend = j + 1;
+    // S(j): search in O1's blocks [lo_j, hi_j], in ring-sized chunks
+    bool h0 = false, h1 = false;
+    uint32_t p0 = 0, p1 = 0;
+    if (lo_j < o_nblk) {
+      for (uint32_t c = lo_j; c <= hi_j;) {
+        const uint32_t ce = min(hi_j, c + kMergeRing - 1);
+        // (the slow path: blocks of the chunk not decoded yet, one at a time)
+        for (uint32_t b = (dec_hi == 0xFFFFFFFFu || dec_hi < c) ? c : dec_hi + 1; b <= ce; ++b) {
+          cover(b);
+          uint32_t y0, y1, y2;
+          o1_words(b, y0, y1, y2);
+          o1_decode(b, y0, y1, y2);
+        }
+        uint32_t bb, pp;
+        if (ok0 && !h0) {
+          ring_find(a0, c, ce, &bb, &pp);
+          if (bb <= ce && pp < 128 && S.ring[(bb & (kMergeRing - 1)) * 128 + pp] == a0) { h0 = true; p0 = (bb << 7) | pp; }
+        }
+        if (ok1 && !h1) {
+          ring_find(a1, c, ce, &bb, &pp);
+          if (bb <= ce && pp < 128 && S.ring[(bb & (kMergeRing - 1)) * 128 + pp] == a1) { h1 = true; p1 = (bb << 7) | pp; }
+        }
+        c = ce + 1;
+      }
+    }
+    // C(j): hits to the survivor queue in doc order; score every full 64
+    const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+    const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
+    const uint32_t r1 = r0 + (h0 ? 1u : 0u);
+    if (h0) {
+      const uint32_t e0 = r0 & (kMergeQ - 1);
+      qdoc[e0] = a0; qc4[e0] = c0; qtd[e0] = t0; qpo[e0] = p0;
+    }
+    if (h1) {
+      const uint32_t e1 = r1 & (kMergeQ - 1);
+      qdoc[e1] = a1; qc4[e1] = c1; qtd[e1] = t1; qpo[e1] = p1;
+    }
+    qtail += __popcll(m0) + __popcll(m1);
+#pragma nounroll
+    for (int cc = 0; cc < 2 && qtail - qhead >= 64; ++cc) score_chunk(64);
+  };
+
+  if (b0 < b1 && o_nblk) {
+    // the window starts at the first O1 block that can hold a doc of the segment
+    load_window(uni(find_block(ix.blk_last + o_blk0, 0, o_nblk, b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u)));
+    issue(b0, 0xFFFFFFFFu, R0);
+    for (uint32_t j = b0; j < bend; j += 2) {
+      body(R0, R1, j);
+      if (j + 1 >= bend) break;
+      body(R1, R0, j + 1);
+    }
+  }
+  if (qtail != qhead) score_chunk(qtail - qhead);
+  if (evb) flush();
+  if (my_pub && pub_val > sent && l == 0)
+    __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Persistent, workgroups of kMergeWaves independent waves (as lean_kernel):
+// each wave dequeues merge items [n_lean, n_merge) and runs merge_segment.
+#ifndef WSR_MERGE_WGS
+#define WSR_MERGE_WGS 4
+#endif
+__global__ __launch_bounds__(64 * kMergeWaves, WSR_MERGE_WGS) void merge_kernel(
+    IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
+    uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
+    uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
+    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc) {
+  __shared__ MergeLds SW[kMergeWaves];
+  __shared__ double norm[256];
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t w = uni(threadIdx.x >> 6);
+  for (uint32_t i = threadIdx.x; i < 256; i += 64 * kMergeWaves) norm[i] = ix.cache[i];
+  __syncthreads();
+  MergeLds& S = SW[w];
+  const uint32_t wid = blockIdx.x * kMergeWaves + w;
+  const uint32_t m_lo = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t m_hi = uni(__hip_atomic_load(&counters[kCtrMerge], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  uint32_t n_surv = 0, n_dblk = 0;
+  uint32_t shard = wid % kQueueShards, tried = 0;
+  uint32_t item = m_lo + wid;
+  for (;;) {
+    if (item >= m_hi) item = next_item(&counters[kCtrMHead0], m_lo, m_hi, shard, tried);
+    if (item >= m_hi) break;
+    const uint32_t qi = uni(item_q[item]);
+    const QueryDesc Q = desc[qi];
+    const uint32_t r = item - Q.item_base;
+    const uint32_t seg = Q.seg;
+    const uint32_t b0 = r * seg;
+    const uint32_t b1 = min(b0 + seg, Q.a_nblk);
+    Event* ev_out = events + Q.ev_base + static_cast<uint64_t>(r) * seg * 128;
+    uint64_t* my_pub = pub ? pub + item : nullptr;
+    const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
+    __builtin_amdgcn_wave_barrier();
+    if (b0 + l < b1) {
+      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + b0 + l];
+      S.dmeta[l] = ix.blk_meta[Q.a_blk0 + b0 + l];
+    }
+    const bool dtail = b0 < b1 && b1 == Q.a_nblk && Q.a_tail != kNoTail;
+    uint32_t tdoc0 = 0, tdoc1 = 0, ttf0 = 0, ttf1 = 0;
+    if (dtail) {
+      const uint32_t cnt = Q.a_tail_cnt;
+      const uint32_t* t = ix.tails + Q.a_tail;
+      if (2 * l < cnt) { tdoc0 = t[2 * l]; ttf0 = t[cnt + 2 * l]; }
+      if (2 * l + 1 < cnt) { tdoc1 = t[2 * l + 1]; ttf1 = t[cnt + 2 * l + 1]; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
+    const bool done = first_doc > Q.min_last;   // an other list ends before this segment
+    double pt = 0.0;
+    uint32_t pt_n = 0, ev_n = 0;
+    if (!done && b0 < b1)
+      merge_segment(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)), b0, b1, dtail, tdoc0, tdoc1, ttf0,
+                    ttf1, prev_pub, my_pub, ev_out, ev_n, pt, pt_n, n_surv, n_dblk);
+    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
+    item = 0xFFFFFFFFu;
+  }
+  if (l == 0) {
+    stats[wid * kStatStride + 0] = n_surv;
+    stats[wid * kStatStride + 1] = n_dblk;
+    stats[wid * kStatStride + 2] = 0;
+  }
+}
+
 // ------------------------------------------------------ doc-range shards --
 // Shard side: reduce each query's segment events to the events of a heap run
 // from empty over the whole shard (a superset of the global insertions inside
@@ -3106,14 +3587,14 @@ __global__ __launch_bounds__(1024) void scan_rows_kernel(const int32_t* __restri
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int merge_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st) {
   const int n_part = std::max(1, (nq + kPlanThreads - 1) / kPlanThreads);
   hipLaunchKernelGGL(plan_query_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, ix, q, nq, plan,
                      counters, fr, desc, part);
   hipLaunchKernelGGL(plan_fill_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, nq, plan, part, n_part,
                      counters, ev_capacity, item_capacity, static_cast<uint32_t>(lean_grid),
-                     static_cast<uint32_t>(seg_grid), item_q, pub, desc);
+                     static_cast<uint32_t>(merge_grid), static_cast<uint32_t>(seg_grid), item_q, pub, desc);
   return hipGetLastError();
 }
 
@@ -3151,6 +3632,22 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
     hipLaunchKernelGGL((lean_kernel<false, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
                        plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   return hipGetLastError();
+}
+
+hipError_t launch_merge(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
+                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
+                        int merge_wgs, const FusedReplay& fr, const uint32_t* item_q,
+                        uint64_t* pub, const QueryDesc* desc, hipStream_t st) {
+  hipLaunchKernelGGL(merge_kernel, dim3(merge_wgs), dim3(64 * kMergeWaves), 0, st, ix, q, plan, nq, counters,
+                     events, ev_cnt, stats, fr, item_q, pub, desc);
+  return hipGetLastError();
+}
+
+int merge_kernel_occupancy() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, merge_kernel, 64 * kMergeWaves, 0) != hipSuccess)
+    return 1;
+  return n;
 }
 
 int lean_kernel_occupancy() {

@@ -309,6 +309,18 @@ class ResidentBatch:
         check(lib.wsr_batch_fetch(self.engine._h, self._b, self._hits, self._nh))
         return self._hits, self._nh
 
+    def ready(self) -> bool:
+        """True once the batch's last run has finished on the device."""
+        rc = lib.wsr_batch_ready(self.engine._h, self._b)
+        if rc < 0:
+            check(rc)
+        return rc == 1
+
+    def wait_ready(self) -> None:
+        """Spin until the batch's last run has finished (a host-side throttle)."""
+        while not self.ready():
+            pass
+
     def stats(self) -> _capi.BatchStats:
         st = _capi.BatchStats()
         check(lib.wsr_batch_stats_get(self.engine._h, self._b, C.byref(st)))
