@@ -3161,8 +3161,13 @@ __device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, 
     uint32_t w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0, wc = 0;
     uint32_t o0[kMergeG], o1w[kMergeG], o2[kMergeG];
     uint32_t ob0 = 0, on = 0;    // prefetched O1 blocks [ob0, ob0 + on)
+    uint32_t lo = 0, hi = 0;     // the O1 blocks the driver block overlaps (lo = o_nblk: none)
   };
   MRegs R0, R1;
+  // W(j): the words of driver block j, the O1 range it overlaps and the words
+  // of its first new O1 blocks.  The range is found here, in block order, so
+  // the window only ever moves forward for it: lo_j and hi_j are asked in the
+  // order a_first_j <= a_last_j < a_first_j+1 ... (lo_j+1 >= hi_j).
   auto issue = [&](uint32_t j, uint32_t hi_prev, MRegs& Y) __attribute__((always_inline)) {
     const uint32_t bi = j - b0;
     const uint32_t m = uni(S.dmeta[bi]);
@@ -3171,14 +3176,15 @@ __device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, 
     pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.t0, Y.t1, Y.t2, sh);
     Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + j) * 32u + (l >> 1)];
-    // O1 blocks this driver block will need beyond those the previous one
-    // needed (hi_prev: its last; every later block starts at or after it)
-    const uint32_t hi = first_ge(uni(e.y));
-    const uint32_t from = hi_prev == 0xFFFFFFFFu ? first_ge(j == 0 ? 0u : uni(e.x) + 1u) : hi_prev + 1;
+    Y.lo = first_ge(j == 0 ? 0u : uni(e.x) + 1u);
+    Y.hi = Y.lo < o_nblk ? min(first_ge(uni(e.y)), o_nblk - 1) : o_nblk;
+    // O1 blocks this driver block needs beyond those the previous one needed
+    // (hi_prev: its last; this block's range starts at or after it)
+    const uint32_t from = hi_prev == 0xFFFFFFFFu ? Y.lo : max(hi_prev + 1, Y.lo);
     Y.ob0 = from;
     Y.on = 0;
-    if (hi < o_nblk && hi >= from && from >= wb) {
-      const uint32_t want = min(hi - from + 1, static_cast<uint32_t>(kMergeG));
+    if (Y.lo < o_nblk && from <= Y.hi && from >= wb) {
+      const uint32_t want = min(Y.hi - from + 1, static_cast<uint32_t>(kMergeG));
       const uint32_t n = min(want, wb + 64 - from);   // (inside the window)
 #pragma unroll
       for (int g = 0; g < kMergeG; ++g)
@@ -3193,10 +3199,8 @@ __device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, 
     const uint32_t bi = j - b0;
     const uint4 be = S.dblk[bi];
     const uint32_t m = uni(S.dmeta[bi]);
-    const uint32_t a_first = j == 0 ? 0u : uni(be.x) + 1u, a_last = uni(be.y);
-    // O1 blocks overlapping this driver block
-    const uint32_t lo_j = first_ge(a_first);
-    const uint32_t hi_j = min(first_ge(a_last), o_nblk - 1);
+    // O1 blocks overlapping this driver block (found by W(j))
+    const uint32_t lo_j = X.lo, hi_j = X.hi;
     // decode the prefetched O1 blocks (they start after the last decoded one)
     for (uint32_t g = 0; g < X.on; ++g) {
       const uint32_t b = X.ob0 + g;
