@@ -3265,6 +3265,9 @@ __device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, 
     }
     // C(j): hits to the survivor queue in doc order; score every full 64
     const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+    // (a block adds up to 128 hits to the < 64 queued: a queue that would
+    // overflow is scored first, as a partial chunk)
+    if (qtail - qhead + __popcll(m0) + __popcll(m1) > kMergeQ) score_chunk(qtail - qhead);
     const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
     const uint32_t r1 = r0 + (h0 ? 1u : 0u);
     if (h0) {
