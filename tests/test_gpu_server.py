@@ -99,7 +99,7 @@ def test_bad_request_fails_alone(synth_small):
         if kind == "flags":
             q.flags = 6
         elif kind == "k":
-            q.k = 1000
+            q.k = _capi.SERVER_MAX_K + 1   # (past the server's k limit)
         hits = (_capi.Hit * 1024)()
         nh = C.c_int32()
         errors[kind] = _capi.lib.wsr_server_search(srv._s, C.byref(q), hits, C.byref(nh))

@@ -21,7 +21,16 @@
 #include "writer.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <mutex>
+#include <queue>
 #include <cmath>
 #include <fstream>
 #include <map>
@@ -44,6 +53,21 @@
 namespace wiser {
 namespace {
 
+// The "begin" or "end" bloom bit arrays of a list's postings (bloom on):
+// has[i] = posting i has one (BloomFilterStore keeps none for a posting with no
+// neighbour on that side); the arrays of the postings that have one, each
+// `bytes` long, back to back in posting order.
+struct BloomBits {
+  bool on = false;
+  size_t bytes = 0;
+  std::vector<uint8_t> has;
+  std::vector<uint8_t> bits;
+  void push(const std::string& a) {
+    has.push_back(a.empty() ? 0 : 1);
+    bits.insert(bits.end(), a.begin(), a.end());
+  }
+};
+
 // ------------------------------------------------------------ term input --
 struct TermPostings {
   std::vector<uint32_t> docs;
@@ -52,7 +76,7 @@ struct TermPostings {
   std::vector<uint32_t> pos_sizes;
   std::vector<uint32_t> off_vals;   // per-bag delta coded [s0,e0,s1,e1..]
   std::vector<uint32_t> off_sizes;
-  std::vector<std::string> blm_begin, blm_end;   // per posting bloom bit arrays (bloom on)
+  BloomBits blm[2];                 // begin, end filters (bloom on)
 };
 
 // One encoded box: the bytes plus, for every skip row, where the row's first
@@ -104,7 +128,7 @@ struct EncodedList {
   uint32_t df = 0;
   std::vector<uint32_t> prev_doc;  // per row
   Box doc, tf, pos, off;
-  const std::vector<std::string>* blm[2] = {nullptr, nullptr};   // begin, end (bloom on)
+  const BloomBits* blm[2] = {nullptr, nullptr};   // begin, end (bloom on)
 };
 
 // One bloom section (flash_engine_dumper.h:620-646): the bloom skip list
@@ -114,20 +138,24 @@ struct EncodedList {
 // flash_containers.h:499-558).  `at` = offset of the section from the list
 // start; the skip list is sized with offsets 512 KB further out, as the
 // reference does, and the gap after it is padding.
-std::string bloom_section(const std::vector<std::string>& arrays, uint64_t at) {
+std::string bloom_section(const BloomBits& arrays, uint64_t at) {
   std::vector<std::string> boxes;
-  for (size_t i = 0; i < arrays.size(); i += kPackSize) {
-    const size_t n = std::min<size_t>(kPackSize, arrays.size() - i);
+  const size_t np = arrays.has.size();
+  const uint8_t* src = arrays.bits.data();
+  for (size_t i = 0; i < np; i += kPackSize) {
+    const size_t n = std::min<size_t>(kPackSize, np - i);
     std::string b;
     b.push_back(static_cast<char>(kBloomBoxMagic));
     put_varint(&b, n);
+    size_t present = 0;
     for (size_t c = 0; c < n; c += 8) {
       uint8_t bits = 0;
       for (size_t o = 0; o < 8 && c + o < n; ++o)
-        if (!arrays[i + c + o].empty()) bits |= static_cast<uint8_t>(1u << (7 - o));
+        if (arrays.has[i + c + o]) { bits |= static_cast<uint8_t>(1u << (7 - o)); ++present; }
       b.push_back(static_cast<char>(bits));
     }
-    for (size_t j = 0; j < n; ++j) b += arrays[i + j];
+    b.append(reinterpret_cast<const char*>(src), present * arrays.bytes);
+    src += present * arrays.bytes;
     boxes.push_back(std::move(b));
   }
   auto skip = [&](uint64_t first) {
@@ -149,7 +177,7 @@ std::string bloom_section(const std::vector<std::string>& arrays, uint64_t at) {
 void encode_list(const TermPostings& t, EncodedList* e) {
   const size_t n = t.docs.size();
   e->df = static_cast<uint32_t>(n);
-  if (!t.blm_end.empty()) { e->blm[0] = &t.blm_begin; e->blm[1] = &t.blm_end; }
+  if (t.blm[0].on) { e->blm[0] = &t.blm[0]; e->blm[1] = &t.blm[1]; }
   for (size_t r = 0; r * kPackSize < n; ++r)
     e->prev_doc.push_back(r == 0 ? 0 : t.docs[r * kPackSize - 1]);
   encode_box(t.docs, nullptr, n, true, &e->doc);
@@ -231,8 +259,7 @@ class VacuumFileWriter {
     if (bloom_) {
       // upper bound of both sections: every posting's array + box / skip overheads
       uint64_t ub = 0;
-      for (int i = 0; i < 2; ++i)
-        for (auto& a : *e.blm[i]) ub += a.size();
+      for (int i = 0; i < 2; ++i) ub += e.blm[i]->bits.size();
       ub += 2 * (e.df / kPackSize + 1) * (kPackSize / 8 + 2 * 10 + 4) + 64;
       const uint64_t est0 = encode_skip_list(e, skip_start + 512 * 1024, ub + 1024 * 1024).size();
       uint64_t at = skip_start + est0 + e.doc.bytes.size() + e.tf.bytes.size() - start;
@@ -362,25 +389,72 @@ std::vector<std::vector<std::pair<uint32_t, uint32_t>>> parse_offsets(const std:
   return res;
 }
 
-void add_bag_delta(std::vector<uint32_t>* vals, std::vector<uint32_t>* sizes,
-                   const std::vector<uint32_t>& raw) {
-  uint32_t prev = 0;
-  for (uint32_t x : raw) { vals->push_back(x - prev); prev = x; }
-  sizes->push_back(static_cast<uint32_t>(raw.size()));
-}
-
 }  // namespace
 
+// ----------------------------------------------- streaming linedoc writer --
+// The reference's dumper holds the whole inverted index in memory before it
+// writes (FlashEngineDumper::LoadQqMemDump / Dump, flash_engine_dumper.h:735-808).
+// This writer keeps host memory bounded by the chunk size instead:
+//   pass 1 (parallel): rows are cut into chunks; a worker parses a chunk into
+//     one record per (term, doc) and spills the chunk as a run file, terms
+//     ascending, each term's records in doc order;
+//   pass 2: a k-way merge of the runs by term concatenates a term's records
+//     run by run (= doc order), batches of terms are encoded in parallel
+//     and appended in term order.
+// The output is byte-identical to the one-map writer it replaces
+// (tests/golden/writer_sha256.json) at every chunk size and thread count.
 namespace {
-// "begin" / "end" neighbour lists of every token of a doc from its positions
-// (the fixture columns bloom_before / bloom: '!'-terminated groups of the
-// terms before / after each occurrence, testdata/iter_test_3_docs_tf_bi-bloom)
-void add_doc_blooms(const std::vector<std::string>& toks,
-                    const std::vector<std::vector<uint32_t>>& pos, const BloomShape& shape,
-                    std::map<std::string, TermPostings>* index) {
-  std::map<uint32_t, const std::string*> at;
+
+// utils::explode_strict (utils.cc:52-67) restricted to counting: the column
+// `col` of a tab-separated row, or false when the row has too few columns.
+bool column_of(const std::string& line, size_t col, size_t need, std::string* out) {
+  size_t at = 0, c = 0, begin = 0, end = std::string::npos;
+  for (;;) {
+    const size_t tab = line.find('\t', at);
+    const size_t stop = tab == std::string::npos ? line.size() : tab;
+    if (c == col) { begin = at; end = stop; }
+    ++c;
+    if (tab == std::string::npos) break;
+    at = tab + 1;
+  }
+  if (c < need) return false;
+  out->assign(line, begin, end - begin);
+  return true;
+}
+
+// One record: doc | tf | n_pos | position deltas | n_off | offset deltas
+// [| flags (1 begin, 2 end) | begin array | end array], varints.
+void put_record(std::string* o, uint32_t doc, uint32_t tf, const std::vector<uint32_t>& pos,
+                const std::vector<uint32_t>& off, const std::string* blm) {
+  put_varint(o, doc);
+  put_varint(o, tf);
+  put_varint(o, pos.size());
+  uint32_t prev = 0;
+  for (uint32_t x : pos) { put_varint(o, static_cast<uint32_t>(x - prev)); prev = x; }
+  put_varint(o, off.size());
+  prev = 0;
+  for (uint32_t x : off) { put_varint(o, static_cast<uint32_t>(x - prev)); prev = x; }
+  if (blm) {
+    o->push_back(static_cast<char>((blm[0].empty() ? 0 : 1) | (blm[1].empty() ? 0 : 2)));
+    *o += blm[0];
+    *o += blm[1];
+  }
+}
+
+struct TermRun {
+  std::string bytes;
+  uint32_t n = 0;
+};
+
+// "begin" / "end" bloom arrays of every token of a doc from its positions
+// (the fixture columns bloom_before / bloom: the terms before / after each
+// occurrence, testdata/iter_test_3_docs_tf_bi-bloom)
+void doc_blooms(const std::vector<const std::string*>& toks, const std::vector<std::vector<uint32_t>>& pos,
+                const BloomShape& shape, std::vector<std::array<std::string, 2>>* out) {
+  std::unordered_map<uint32_t, const std::string*> at;
   for (size_t t = 0; t < toks.size(); ++t)
-    for (uint32_t p : pos[t]) at[p] = &toks[t];
+    for (uint32_t p : pos[t]) at[p] = toks[t];
+  out->resize(toks.size());
   for (size_t t = 0; t < toks.size(); ++t) {
     std::vector<std::string> before, after;
     for (uint32_t p : pos[t]) {
@@ -388,11 +462,203 @@ void add_doc_blooms(const std::vector<std::string>& toks,
       auto it = at.find(p + 1);
       if (it != at.end()) after.push_back(*it->second);
     }
-    TermPostings& tp = (*index)[toks[t]];
-    tp.blm_begin.push_back(make_bloom(shape, before));
-    tp.blm_end.push_back(make_bloom(shape, after));
+    (*out)[t][0] = make_bloom(shape, before);
+    (*out)[t][1] = make_bloom(shape, after);
   }
 }
+
+struct ChunkOut {
+  std::vector<uint32_t> lens;
+  std::string path;
+  int64_t err_row = -1;
+  std::string err;
+};
+
+// Parse rows [doc0, doc0 + lines.size()) into one run file.
+void parse_chunk(const std::vector<std::string>& lines, uint32_t doc0, bool token_only, const BloomSpec& bloom,
+                 const BloomShape& shape, const std::string& path, ChunkOut* res) {
+  std::unordered_map<std::string, TermRun> runs;
+  res->lens.reserve(lines.size());
+  std::vector<std::array<std::string, 2>> blm;
+  std::vector<uint32_t> pos, flat;
+  for (size_t r = 0; r < lines.size(); ++r) {
+    const uint32_t doc = doc0 + static_cast<uint32_t>(r);
+    std::vector<std::string> items = explode_strict(lines[r], '\t');
+    if (token_only) {
+      // Body = tokens = column 2; tf = token count; positions = token ordinals;
+      // offsets = char span (end inclusive) of each occurrence in column 2.
+      const std::string& toks = items[2];
+      std::map<std::string, std::pair<std::vector<uint32_t>, std::vector<uint32_t>>> occ;
+      uint32_t ordinal = 0;
+      size_t i = 0;
+      while (i < toks.size()) {
+        if (toks[i] == ' ') { ++i; continue; }
+        size_t j = i;
+        while (j < toks.size() && toks[j] != ' ') ++j;
+        auto& o = occ[toks.substr(i, j - i)];
+        o.first.push_back(ordinal++);
+        o.second.push_back(static_cast<uint32_t>(i));
+        o.second.push_back(static_cast<uint32_t>(j - 1));
+        i = j;
+      }
+      if (bloom.on) {
+        std::vector<const std::string*> dt;
+        std::vector<std::vector<uint32_t>> dp;
+        for (auto& kv : occ) { dt.push_back(&kv.first); dp.push_back(kv.second.first); }
+        doc_blooms(dt, dp, shape, &blm);
+      }
+      size_t t = 0;
+      for (auto& kv : occ) {
+        TermRun& tr = runs[kv.first];
+        put_record(&tr.bytes, doc, static_cast<uint32_t>(kv.second.first.size()), kv.second.first,
+                   kv.second.second, bloom.on ? blm[t].data() : nullptr);
+        ++tr.n;
+        ++t;
+      }
+      res->lens.push_back(ordinal);
+    } else {
+      std::vector<std::string> toks = explode(items[2], ' ');
+      auto offsets = parse_offsets(items[3]);
+      std::vector<std::string> groups = explode(items[4], '.');
+      if (offsets.size() != toks.size() || groups.size() != toks.size()) {
+        res->err_row = doc;
+        res->err = "linedoc row " + std::to_string(doc) + ": token/offset/position column mismatch";
+        return;
+      }
+      std::unordered_set<std::string> seen;
+      std::vector<std::vector<uint32_t>> dpos(toks.size());
+      for (size_t t = 0; t < toks.size(); ++t) {
+        if (!seen.insert(toks[t]).second) {
+          res->err_row = doc;
+          res->err = "duplicate token '" + toks[t] + "' in row " + std::to_string(doc);
+          return;
+        }
+        for (auto& p : explode(groups[t], ';')) dpos[t].push_back(static_cast<uint32_t>(std::stoul(p)));
+      }
+      if (bloom.on) {
+        std::vector<const std::string*> dt;
+        for (auto& t : toks) dt.push_back(&t);
+        doc_blooms(dt, dpos, shape, &blm);
+      }
+      for (size_t t = 0; t < toks.size(); ++t) {
+        flat.clear();
+        for (auto& pr : offsets[t]) { flat.push_back(pr.first); flat.push_back(pr.second); }
+        TermRun& tr = runs[toks[t]];
+        put_record(&tr.bytes, doc, static_cast<uint32_t>(offsets[t].size()), dpos[t], flat,
+                   bloom.on ? blm[t].data() : nullptr);
+        ++tr.n;
+      }
+      res->lens.push_back(static_cast<uint32_t>(explode(items[1], ' ').size()));
+    }
+  }
+  // spill: term length | term | record count | record bytes | records, terms ascending
+  std::vector<std::pair<const std::string*, TermRun*>> order;
+  order.reserve(runs.size());
+  for (auto& kv : runs) order.emplace_back(&kv.first, &kv.second);
+  std::sort(order.begin(), order.end(), [](const auto& a, const auto& b) { return *a.first < *b.first; });
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot create run file " + path);
+  std::string head;
+  bool ok = true;
+  for (auto& e : order) {
+    head.clear();
+    put_varint(&head, e.first->size());
+    head += *e.first;
+    put_varint(&head, e.second->n);
+    put_varint(&head, e.second->bytes.size());
+    ok = ok && std::fwrite(head.data(), 1, head.size(), f) == head.size();
+    ok = ok && std::fwrite(e.second->bytes.data(), 1, e.second->bytes.size(), f) == e.second->bytes.size();
+    std::string().swap(e.second->bytes);
+  }
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok) throw std::runtime_error("cannot write run file " + path);
+  res->path = path;
+}
+
+// Sequential reader of one run file.
+class RunReader {
+ public:
+  explicit RunReader(const std::string& path) : buf_(1 << 20) {
+    f_ = std::fopen(path.c_str(), "rb");
+    if (!f_) throw std::runtime_error("cannot open run file " + path);
+    std::setvbuf(f_, buf_.data(), _IOFBF, buf_.size());
+    advance();
+  }
+  ~RunReader() { if (f_) std::fclose(f_); }
+  RunReader(const RunReader&) = delete;
+  RunReader& operator=(const RunReader&) = delete;
+  bool done() const { return done_; }
+  const std::string& term() const { return term_; }
+  // the current term's records appended to tp; then the next term
+  void take(TermPostings* tp, bool blooms, size_t bloom_bytes) {
+    payload_.resize(nbytes_);
+    if (nbytes_ && std::fread(&payload_[0], 1, nbytes_, f_) != nbytes_) throw std::runtime_error("short run file");
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(payload_.data());
+    const uint8_t* end = p + payload_.size();
+    auto next = [&]() -> uint32_t {
+      uint64_t v;
+      const int n = get_varint(p, end, &v);
+      if (n <= 0) throw std::runtime_error("corrupt run file");
+      p += n;
+      return static_cast<uint32_t>(v);
+    };
+    for (uint64_t r = 0; r < n_; ++r) {
+      tp->docs.push_back(next());
+      tp->tfs.push_back(next());
+      const uint32_t np = next();
+      for (uint32_t i = 0; i < np; ++i) tp->pos_vals.push_back(next());
+      tp->pos_sizes.push_back(np);
+      const uint32_t no = next();
+      for (uint32_t i = 0; i < no; ++i) tp->off_vals.push_back(next());
+      tp->off_sizes.push_back(no);
+      if (blooms) {
+        if (p >= end) throw std::runtime_error("corrupt run file");
+        const uint8_t fl = *p++;
+        for (int s = 0; s < 2; ++s) {
+          BloomBits& b = tp->blm[s];
+          const bool has = fl & (1u << s);
+          b.has.push_back(has ? 1 : 0);
+          if (has) {
+            if (static_cast<size_t>(end - p) < bloom_bytes) throw std::runtime_error("corrupt run file");
+            b.bits.insert(b.bits.end(), p, p + bloom_bytes);
+            p += bloom_bytes;
+          }
+        }
+      }
+    }
+    advance();
+  }
+
+ private:
+  bool read_varint(uint64_t* v) {
+    uint64_t x = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+      const int c = std::getc(f_);
+      if (c == EOF) return false;
+      x |= static_cast<uint64_t>(c & 0x7F) << sh;
+      if (!(c & 0x80)) { *v = x; return true; }
+    }
+    return false;
+  }
+  void advance() {
+    uint64_t len;
+    if (!read_varint(&len)) { done_ = true; return; }
+    term_.resize(len);
+    if (len && std::fread(&term_[0], 1, len, f_) != len) throw std::runtime_error("short run file");
+    if (!read_varint(&n_) || !read_varint(&nbytes_)) throw std::runtime_error("short run file");
+  }
+  std::vector<char> buf_;
+  FILE* f_ = nullptr;
+  std::string term_, payload_;
+  uint64_t n_ = 0, nbytes_ = 0;
+  bool done_ = false;
+};
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
 }  // namespace
 
 BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
@@ -404,92 +670,168 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
     throw std::runtime_error("unsupported linedoc format " + format);
   std::ifstream in(linedoc);
   if (!in) throw std::runtime_error("cannot open linedoc " + linedoc);
-  std::string line;
-  std::getline(in, line);  // header row
-  std::map<std::string, TermPostings> index;  // sorted term order in my.tip / my.vacuum
-  DocLengths lens;
+  const size_t need = token_only ? 3u : 5u;
+  const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+  const int threads = std::max(1, env_int("WSR_WRITER_THREADS", std::min(hw, 16)));
+  const size_t chunk_docs = static_cast<size_t>(std::max(1, env_int("WSR_WRITER_CHUNK_DOCS", 32768)));
+  ::mkdir(out_dir.c_str(), 0777);
+  const std::string run_dir = out_dir + "/.wsr_runs";
+  ::mkdir(run_dir.c_str(), 0777);
+  std::vector<std::unique_ptr<ChunkOut>> chunks;
+  auto cleanup = [&] {
+    for (auto& c : chunks) if (c && !c->path.empty()) ::unlink(c->path.c_str());
+    ::rmdir(run_dir.c_str());
+  };
+
+  // ---- pass 1: rows -> doc store (in order, this thread) + run files (workers)
+  struct Job {
+    std::vector<std::string> lines;
+    uint32_t doc0;
+    ChunkOut* out;
+    std::string path;
+  };
+  std::mutex mu;
+  std::condition_variable cv_job, cv_room;
+  std::deque<Job> jobs;
+  bool closing = false;
+  std::exception_ptr fatal;
+  auto worker = [&] {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_job.wait(lk, [&] { return closing || !jobs.empty(); });
+        if (jobs.empty()) return;
+        j = std::move(jobs.front());
+        jobs.pop_front();
+      }
+      cv_room.notify_one();
+      try {
+        parse_chunk(j.lines, j.doc0, token_only, bloom, shape, j.path, j.out);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!fatal) fatal = std::current_exception();
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int i = 0; i < threads; ++i) pool.emplace_back(worker);
   // doc store: DocInfo::Body() = column 2 for TOKEN_ONLY, column 1 otherwise
   // (engine_loader.h:63-65,91-93), added by FlashEngineDumper (flash_engine_dumper.h:717)
   DocStoreWriter store;
-  store.open(out_dir);
+  std::string line, body;
   uint32_t doc = 0;
-  while ((n_rows < 0 || doc < n_rows) && std::getline(in, line)) {
-    std::vector<std::string> items = explode_strict(line, '\t');
-    if (items.size() < (token_only ? 3u : 5u))
-      throw std::runtime_error("linedoc row " + std::to_string(doc) + " has too few columns");
-    store.add(token_only ? items[2] : items[1]);
-    if (token_only) {
-      // Body = tokens = column 2; tf = token count; positions = token ordinals;
-      // offsets = char span (end inclusive) of each occurrence in column 2.
-      const std::string& toks = items[2];
-      std::map<std::string, std::vector<uint32_t>> occ;
-      std::map<std::string, std::vector<uint32_t>> offs;
-      uint32_t ordinal = 0;
-      size_t i = 0;
-      while (i < toks.size()) {
-        if (toks[i] == ' ') { ++i; continue; }
-        size_t j = i;
-        while (j < toks.size() && toks[j] != ' ') ++j;
-        std::string t = toks.substr(i, j - i);
-        occ[t].push_back(ordinal++);
-        offs[t].push_back(static_cast<uint32_t>(i));
-        offs[t].push_back(static_cast<uint32_t>(j - 1));
-        i = j;
-      }
-      std::vector<std::string> dtoks;
-      std::vector<std::vector<uint32_t>> dpos;
-      for (auto& kv : occ) {
-        TermPostings& tp = index[kv.first];
-        tp.docs.push_back(doc);
-        tp.tfs.push_back(static_cast<uint32_t>(kv.second.size()));
-        add_bag_delta(&tp.pos_vals, &tp.pos_sizes, kv.second);
-        add_bag_delta(&tp.off_vals, &tp.off_sizes, offs[kv.first]);
-        if (bloom.on) { dtoks.push_back(kv.first); dpos.push_back(kv.second); }
-      }
-      if (bloom.on) add_doc_blooms(dtoks, dpos, shape, &index);
-      lens.add(ordinal);
-    } else {
-      std::vector<std::string> toks = explode(items[2], ' ');
-      auto offsets = parse_offsets(items[3]);
-      std::vector<std::string> groups = explode(items[4], '.');
-      if (offsets.size() != toks.size() || groups.size() != toks.size())
-        throw std::runtime_error("linedoc row " + std::to_string(doc) +
-                                 ": token/offset/position column mismatch");
-      std::unordered_set<std::string> seen;
-      std::vector<std::vector<uint32_t>> dpos;
-      for (size_t t = 0; t < toks.size(); ++t) {
-        if (!seen.insert(toks[t]).second)
-          throw std::runtime_error("duplicate token '" + toks[t] + "' in row " + std::to_string(doc));
-        std::vector<uint32_t> pos;
-        for (auto& p : explode(groups[t], ';')) pos.push_back(static_cast<uint32_t>(std::stoul(p)));
-        std::vector<uint32_t> flat;
-        for (auto& pr : offsets[t]) { flat.push_back(pr.first); flat.push_back(pr.second); }
-        TermPostings& tp = index[toks[t]];
-        tp.docs.push_back(doc);
-        tp.tfs.push_back(static_cast<uint32_t>(offsets[t].size()));
-        add_bag_delta(&tp.pos_vals, &tp.pos_sizes, pos);
-        add_bag_delta(&tp.off_vals, &tp.off_sizes, flat);
-        if (bloom.on) dpos.push_back(pos);
-      }
-      if (bloom.on) add_doc_blooms(toks, dpos, shape, &index);
-      lens.add(static_cast<uint32_t>(explode(items[1], ' ').size()));
+  int64_t col_err = -1;
+  try {
+    store.open(out_dir);
+    std::getline(in, line);  // header row
+    std::vector<std::string> cur;
+    auto submit = [&] {
+      if (cur.empty()) return;
+      chunks.push_back(std::make_unique<ChunkOut>());
+      Job j;
+      j.doc0 = doc - static_cast<uint32_t>(cur.size());
+      j.lines = std::move(cur);
+      j.out = chunks.back().get();
+      j.path = run_dir + "/run_" + std::to_string(chunks.size() - 1);
+      cur.clear();
+      std::unique_lock<std::mutex> lk(mu);
+      cv_room.wait(lk, [&] { return jobs.size() < static_cast<size_t>(threads); });
+      jobs.push_back(std::move(j));
+      lk.unlock();
+      cv_job.notify_one();
+    };
+    while ((n_rows < 0 || doc < n_rows) && std::getline(in, line)) {
+      if (!column_of(line, token_only ? 2 : 1, need, &body)) { col_err = doc; break; }
+      store.add(body);
+      cur.push_back(std::move(line));
+      ++doc;
+      if (cur.size() == chunk_docs) submit();
     }
-    ++doc;
+    submit();
+  } catch (...) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!fatal) fatal = std::current_exception();
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    closing = true;
+  }
+  cv_job.notify_all();
+  for (auto& t : pool) t.join();
+  if (fatal) { cleanup(); std::rethrow_exception(fatal); }
+  // the first bad row in doc order, as a one-pass reader would report it
+  for (auto& c : chunks)
+    if (c->err_row >= 0 && (col_err < 0 || c->err_row < col_err)) { cleanup(); throw std::runtime_error(c->err); }
+  if (col_err >= 0) {
+    cleanup();
+    throw std::runtime_error("linedoc row " + std::to_string(col_err) + " has too few columns");
   }
   store.close();
-  VacuumFileWriter w(out_dir, bloom);
-  BuildStats st;
-  for (auto& kv : index) {
-    EncodedList e;
-    encode_list(kv.second, &e);
-    w.add(kv.first, e);
-    st.n_postings += e.df;
+  DocLengths lens;
+  lens.c4.reserve(doc);
+  for (auto& c : chunks) {
+    for (uint32_t x : c->lens) lens.add(x);
+    std::vector<uint32_t>().swap(c->lens);
   }
-  w.close();
+
+  // ---- pass 2: merge the runs by term; encode batches in parallel, append in order
+  BuildStats st;
+  try {
+    VacuumFileWriter w(out_dir, bloom);
+    std::vector<std::unique_ptr<RunReader>> rd;
+    for (auto& c : chunks) rd.push_back(std::make_unique<RunReader>(c->path));
+    using Head = std::pair<std::string, size_t>;   // (term, run): runs of one term pop in run order
+    std::priority_queue<Head, std::vector<Head>, std::greater<Head>> heap;
+    for (size_t i = 0; i < rd.size(); ++i)
+      if (!rd[i]->done()) heap.emplace(rd[i]->term(), i);
+    std::vector<std::pair<std::string, TermPostings>> batch;
+    uint64_t batch_bytes = 0;
+    auto flush = [&] {
+      std::vector<EncodedList> enc(batch.size());
+      std::atomic<size_t> next{0};
+      auto work = [&] {
+        for (size_t i; (i = next++) < batch.size();) encode_list(batch[i].second, &enc[i]);
+      };
+      std::vector<std::thread> ts;
+      const int nt = static_cast<int>(std::min<size_t>(threads, batch.size()));
+      for (int i = 1; i < nt; ++i) ts.emplace_back(work);
+      work();
+      for (auto& t : ts) t.join();
+      for (size_t i = 0; i < batch.size(); ++i) {
+        w.add(batch[i].first, enc[i]);
+        st.n_postings += enc[i].df;
+      }
+      batch.clear();
+      batch_bytes = 0;
+    };
+    while (!heap.empty()) {
+      const std::string term = heap.top().first;
+      TermPostings tp;
+      if (bloom.on)
+        for (auto& b : tp.blm) { b.on = true; b.bytes = static_cast<size_t>(shape.bytes); }
+      while (!heap.empty() && heap.top().first == term) {
+        const size_t r = heap.top().second;
+        heap.pop();
+        rd[r]->take(&tp, bloom.on, static_cast<size_t>(shape.bytes));
+        if (!rd[r]->done()) heap.emplace(rd[r]->term(), r);
+      }
+      batch_bytes += 4 * (tp.docs.size() * 2 + tp.pos_vals.size() + tp.off_vals.size()) +
+                     tp.blm[0].bits.size() + tp.blm[1].bits.size();
+      batch.emplace_back(term, std::move(tp));
+      if (batch.size() >= 4096 || batch_bytes >= (64u << 20)) flush();
+    }
+    flush();
+    w.close();
+    st.n_terms = w.terms();
+    st.vacuum_bytes = static_cast<int64_t>(w.bytes());
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
   lens.write(out_dir);
   st.n_docs = doc;
-  st.n_terms = w.terms();
-  st.vacuum_bytes = static_cast<int64_t>(w.bytes());
   st.docs_char4_ge_0x80 = lens.big;
   st.avg_length = lens.avg;
   return st;
