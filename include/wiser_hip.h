@@ -66,6 +66,12 @@ typedef struct wsr_open_opts {
   uint32_t doc_hi;
   int32_t threads;    /* host threads for the load-time directory build (0 = all) */
   int32_t positions;  /* 1: also upload the position boxes (phrase queries) */
+  int32_t bloom_factor; /* CreateSearchEngine's bloom_enable_factor (engine_factory.h:33-34,
+                           reference default 1; 0 = BLOOM_NEVER_USE, types.h:54): with
+                           positions and a bloom index, phrase candidates are pruned by
+                           the two-way filters before the position check
+                           (QueryProcessor::IsPossibleToPresent, query_processing.h:873-884).
+                           Pruning only: results are the same at every factor. */
 } wsr_open_opts;
 
 /* A query with its terms already resolved by wsr_lookup (list id per term, in

@@ -50,14 +50,16 @@ inline void check(int rc) {
 
 class VacuumHipEngine {
  public:
-  explicit VacuumHipEngine(const std::string& dir, int device = 0) : dir_(dir), device_(device) {}
+  // bloom_enable_factor: CreateSearchEngine's (engine_factory.h:33-34), default 1
+  explicit VacuumHipEngine(const std::string& dir, int device = 0, int bloom_enable_factor = 1)
+      : dir_(dir), device_(device), bloom_factor_(bloom_enable_factor) {}
   ~VacuumHipEngine() { wsr_close(h_); }
   VacuumHipEngine(const VacuumHipEngine&) = delete;
   VacuumHipEngine& operator=(const VacuumHipEngine&) = delete;
 
   void Load() {
     if (h_) throw std::runtime_error("Engine is already loaded.");
-    wsr_open_opts o{device_, 0, 0, 0, 1};   // positions: phrase queries served
+    wsr_open_opts o{device_, 0, 0, 0, 1, bloom_factor_};   // positions: phrase queries served
     check(wsr_open(dir_.c_str(), &o, &h_));
   }
 
@@ -171,6 +173,7 @@ class VacuumHipEngine {
  private:
   std::string dir_;
   int device_;
+  int bloom_factor_ = 1;
   wsr_handle* h_ = nullptr;
 };
 

@@ -163,3 +163,83 @@ def test_bloom_index_loads_and_matches(bloom_indexes, name):
     for q in qs[:100]:
         assert orc.search(q, 10, phrase=True) == orc_plain.search(q, 10, phrase=True)
     eng.close()
+
+
+def _varint(b, i):
+    v = sh = 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << sh
+        sh += 7
+        if not c & 0x80:
+            return v, i
+
+
+def _blank_first_bloom_boxes(d, terms):
+    """Mark every posting of the first bloom box of `terms` (both sections) as
+    having no filter: the box's presence bitmap zeroed in place (the arrays stay
+    but nothing points at them).  The reference's reader then answers "not
+    present" for those postings (flash_iterators.h:1045-1050)."""
+    import struct
+    tip = open(os.path.join(d, "my.tip"), "rb").read()
+    offs, at = {}, 0
+    while at < len(tip):
+        n = struct.unpack_from("<I", tip, at)[0]
+        t = tip[at + 4:at + 4 + n].decode()
+        v = struct.unpack_from("<q", tip, at + 4 + n)[0]
+        offs[t] = v & ((1 << 48) - 1)
+        at += 4 + n + 8
+    vac = bytearray(open(os.path.join(d, "my.vacuum"), "rb").read())
+    for t in terms:
+        o = offs[t]
+        assert vac[o] == 0xF4
+        _, i = _varint(vac, o + 1)
+        s0, i = _varint(vac, i)
+        s1, _ = _varint(vac, i)
+        for s in (s0, s1):
+            p = o + s
+            assert vac[p] == 0xA4
+            _, p = _varint(vac, p + 1)
+            first, _ = _varint(vac, p)
+            b = o + first
+            assert vac[b] == 0xF5
+            n, q = _varint(vac, b + 1)
+            vac[q:q + (n + 7) // 8] = bytes((n + 7) // 8)
+    open(os.path.join(d, "my.vacuum"), "wb").write(bytes(vac))
+
+
+@pytest.mark.parametrize("factor", [0, 1, 3])
+def test_bloom_pruning_follows_reference(bloom_indexes, tmp_path, factor):
+    """The GPU applies IsPossibleToPresent (query_processing.h:873-884) before
+    the position check, with CreateSearchEngine's bloom_enable_factor: on an
+    index whose head terms lose the filters of their first 128 postings, the
+    reference prunes docs that do hold the phrase, and the GPU must prune
+    exactly the same ones (which side is checked depends on the factor and on
+    the lists' sizes; 0 = BLOOM_NEVER_USE)."""
+    import shutil
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    src, plain = bloom_indexes["pos"]
+    d = str(tmp_path / "tampered")
+    shutil.copytree(src, d)
+    heads = [f"w{i}" for i in range(8)]
+    _blank_first_bloom_boxes(d, heads)
+    ld = os.path.join(os.path.dirname(plain), "pos.linedoc")
+    seqs = [l.rstrip("\n").split("\t")[1].split() for l in open(ld).readlines()[1:]]
+    rng = random.Random(97)
+    qs = phrase_cases(seqs, 200, seed=97)
+    qs += [rng.sample(heads, 2) for _ in range(150)] + [rng.sample(heads, 3) for _ in range(50)]
+    eng = w.VacuumEngine(d, bloom_factor=factor)
+    eng.Load()
+    orc = OracleVacuum(d, bloom_factor=factor)
+    _check_phrase(eng, orc, qs, 10)
+    _check_phrase(eng, orc, qs, 10, phrase=False)
+    exact = OracleVacuum(d, bloom_factor=0)
+    n_diff = sum(orc.search(q, 10, phrase=True) != exact.search(q, 10, phrase=True) for q in qs)
+    if factor:
+        assert n_diff > 0, "the tampered filters must change some results for this test to bite"
+    else:
+        assert n_diff == 0
+    assert eng.image_info()["pos_bytes"] > 0
+    eng.close()

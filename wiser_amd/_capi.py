@@ -32,7 +32,7 @@ QUERY_PHRASE = 1
 
 class OpenOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("doc_lo", C.c_uint32), ("doc_hi", C.c_uint32),
-                ("threads", C.c_int32), ("positions", C.c_int32)]
+                ("threads", C.c_int32), ("positions", C.c_int32), ("bloom_factor", C.c_int32)]
 
 
 class Query(C.Structure):

@@ -7,8 +7,9 @@
 // libbloom's (src/libbloom/bloom.c:48-75,84-115) sized for a fixed number of
 // entries at a float error ratio, hashed with MurmurHash2
 // (libbloom/murmur2/MurmurHash2.c:15-64).  The query path only prunes with
-// them (QueryProcessor::IsPossibleToPresent, query_processing.h:766-884), so
-// the GPU engine, which checks positions exactly, never reads them.
+// them (QueryProcessor::IsPossibleToPresent, query_processing.h:766-884); the
+// GPU phrase path applies the same check before reading positions
+// (HostImage::blm, kernels.hip bloom_may).
 #pragma once
 
 #include <cmath>

@@ -109,6 +109,8 @@ struct wsr_handle {
   uint32_t* d_pos_pk = nullptr;
   uint32_t* d_pos_tail = nullptr;
   uint32_t* d_pos_start = nullptr;
+  uint8_t* d_blm = nullptr;
+  uint32_t* d_blm_hash = nullptr;
   bool positions = false;
   uint32_t dense_lists = 0;
   wsr_image_info info{};            // HBM bytes of the image's buffers
@@ -237,7 +239,19 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // (WSR_SEG_FLOOR=0: every segment from an empty top-k)
     h->seg_floor = env_number("WSR_SEG_FLOOR", 1) != 0;
     h->positions = opts && opts->positions;
-    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions, dense_budget);
+    const uint32_t bloom_factor = opts && opts->bloom_factor > 0 ? static_cast<uint32_t>(opts->bloom_factor) : 0u;
+    HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions, dense_budget,
+                                bloom_factor > 0);
+    if (img.has_blooms) {   // (counted with the position boxes)
+      h->info.pos_bytes += dev_upload(&h->d_blm, img.blm);
+      h->info.pos_bytes += dev_upload(&h->d_blm_hash, img.blm_hash);
+      h->args.blm = reinterpret_cast<const uint4*>(h->d_blm);
+      h->args.blm_hash = reinterpret_cast<const uint2*>(h->d_blm_hash);
+      h->args.blm_bits = img.blm_bits;
+      h->args.blm_hashes = img.blm_hashes;
+      h->args.bloom_factor = bloom_factor;
+      big_vector<uint8_t>().swap(img.blm);
+    }
     if (h->positions) {
       h->info.pos_bytes += dev_upload(&h->d_pos_blob, img.pos_blob);
       h->info.pos_bytes += dev_upload(&h->d_pos_lists, img.pos_lists);
@@ -336,7 +350,8 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
-                  static_cast<void*>(h->d_pos_start)})
+                  static_cast<void*>(h->d_pos_start), static_cast<void*>(h->d_blm),
+                  static_cast<void*>(h->d_blm_hash)})
     if (p) (void)hipFree(p);
   delete h;
 }

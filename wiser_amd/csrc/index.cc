@@ -16,6 +16,7 @@
 #include <thread>
 #include <unistd.h>
 
+#include "bloom.h"
 #include "format.h"
 
 namespace wiser {
@@ -148,20 +149,24 @@ void VacuumIndex::open(const std::string& dir) {
     // Bloom fields: has_bloom_begin, bytes, entries, f32 ratio; same for end.
     const uint8_t* q = map_ + 1;
     const uint8_t* e = map_ + std::min<uint64_t>(map_len_, kVacuumHeaderBytes);
-    uint64_t has_bloom[2] = {0, 0};
+    uint64_t has_bloom[2] = {0, 0}, bytes[2] = {0, 0}, entries[2] = {0, 0};
+    float ratio[2] = {0, 0};
     for (int s = 0; s < 2; ++s) {
-      uint64_t v;
       int l = get_varint(q, e, &has_bloom[s]); q += l;
-      l = get_varint(q, e, &v); q += l;
-      l = get_varint(q, e, &v); q += l;
+      l = get_varint(q, e, &bytes[s]); q += l;
+      l = get_varint(q, e, &entries[s]); q += l;
+      if (q + 4 <= e) std::memcpy(&ratio[s], q, 4);
       q += 4;
       if (q > e) throw std::runtime_error("my.vacuum: truncated header");
     }
     // Bloom filters (has_bloom) only add sections between the tf and the
     // position boxes of each list; every box is located through the skip
-    // rows, so the image is built the same way.  The position check of
-    // phrase queries is exact, so the filters (pruning only) are not uploaded.
+    // rows, so the image is built the same way.  Phrase images can carry
+    // them (build_image(..., blooms)) to prune before the position check.
     has_bloom_ = has_bloom[1] != 0;
+    bloom_bytes_ = static_cast<uint32_t>(bytes[1]);
+    bloom_entries_ = static_cast<uint32_t>(entries[1]);
+    bloom_ratio_ = ratio[1];
   }
   // --- my.tip (term_index.h:147-159)
   {
@@ -349,7 +354,7 @@ void for_each_list(int32_t L, int threads, F&& fn) {
 // the arrays in place.  (Millions of one-block lists -- the en-Wikipedia shape
 // -- made per-list vectors and their serial concatenation the load's cost.)
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div, bool positions, uint64_t dense_budget) {
+                      uint32_t dense_div, bool positions, uint64_t dense_budget, bool blooms) {
   const int32_t L = idx.n_lists();
   const uint8_t* file = idx.file();
   const uint8_t* fend = file + idx.file_bytes();
@@ -525,8 +530,27 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   };
   std::vector<PosPart> pos_parts(positions ? L : 0);
   if (positions) img.pos_start.assign(nb * kPackSize, 0);
+  // phrase bloom filters: shape from the header's "end" fields; one 16-byte
+  // slot per filter, so bit arrays of more than 16 bytes stay on the host
+  const BloomShape bshape(static_cast<int>(idx.bloom_entries()), idx.bloom_ratio());
+  const uint32_t bbytes = idx.bloom_bytes();
+  const bool with_blm = blooms && positions && idx.has_bloom() && bbytes >= 1 && bbytes <= 16 &&
+                        bshape.bits > 0 && static_cast<uint32_t>(bshape.bits) <= 8 * bbytes && bshape.hashes > 0;
+  if (with_blm) {
+    img.has_blooms = true;
+    img.blm_bits = static_cast<uint32_t>(bshape.bits);
+    img.blm_hashes = static_cast<uint32_t>(bshape.hashes);
+    img.blm.resize(nb * kPackSize * 32);
+    img.blm_hash.assign(2 * static_cast<size_t>(L), 0);
+  }
   for_each_list(L, threads, [&](int32_t id, int worker) {
     const Info& in = info[id];
+    if (with_blm) {   // bloom_check's two hashes of the term (the element looked up)
+      const std::string& t = idx.term(id);
+      const uint32_t a = murmurhash2(t.data(), static_cast<int>(t.size()), 0x9747b28c);
+      img.blm_hash[2 * id] = a;
+      img.blm_hash[2 * id + 1] = murmurhash2(t.data(), static_cast<int>(t.size()), a);
+    }
     if (in.r1 <= in.r0) return;
     Scratch& s = scratch[worker];
     uint32_t fcnt;
@@ -662,6 +686,57 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       for (uint64_t r = r0; r < r1; ++r)
         for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
           img.pos_start[(ld.blk0 + r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i]);
+    }
+    if (with_blm) {
+      // The list's two bloom sections (flash_engine_dumper.h:620-646): the 8
+      // reserved header bytes hold their offsets from the list start (prior,
+      // next); a section = 0xA4 | n boxes | delta offsets of the boxes, a box
+      // = 0xF5 | n | MSB-first presence bitmap | the present bit arrays
+      // (BloomSkipList / BloomBoxIterator, flash_containers.h:560-687).  Box b
+      // holds postings [128 b, 128 b + n): its arrays go to the image slots of
+      // skip row b, whose blocks this image holds when r0 <= b < r1.
+      const std::string& term = idx.term(id);
+      const uint8_t* pl = file + idx.list_offset(id);
+      uint64_t v, so[2];
+      const uint8_t* q = pl + 1;
+      int l = get_varint(q, fend, &v);
+      q += l;
+      for (int side = 0; side < 2; ++side) {
+        l = get_varint(q, fend, &so[side]);
+        if (!l) throw std::runtime_error("bad bloom section pointer in '" + term + "'");
+        q += l;
+      }
+      uint8_t* dst = &img.blm[ld.blk0 * kPackSize * 32];
+      std::memset(dst, 0, (r1 - r0) * kPackSize * 32);
+      for (int side = 0; side < 2; ++side) {
+        const uint8_t* p = pl + so[side];
+        uint64_t nbox = 0;
+        if (p >= fend || p[0] != kBloomSkipListMagic || !(l = get_varint(p + 1, fend, &nbox)) || nbox != nrows)
+          throw std::runtime_error("bad bloom skip list in '" + term + "'");
+        p += 1 + l;
+        uint64_t boff = 0;
+        for (uint64_t b = 0; b < r1; ++b) {
+          uint64_t d;
+          if (!(l = get_varint(p, fend, &d))) throw std::runtime_error("truncated bloom skip list in '" + term + "'");
+          p += l;
+          boff += d;
+          if (b < r0) continue;
+          const uint8_t* bx = pl + boff;
+          uint64_t n = 0;
+          if (bx >= fend || bx[0] != kBloomBoxMagic || !(l = get_varint(bx + 1, fend, &n)) || n > kPackSize)
+            throw std::runtime_error("bad bloom box in '" + term + "'");
+          const uint8_t* bm = bx + 1 + l;
+          const uint8_t* items = bm + (n + 7) / 8;
+          uint64_t phys = 0;
+          for (uint64_t i = 0; i < n; ++i) {
+            if (!(bm[i / 8] & (0x80u >> (i % 8)))) continue;
+            const uint8_t* a = items + phys * bbytes;
+            if (a + bbytes > fend) throw std::runtime_error("bloom box of '" + term + "' out of range");
+            std::memcpy(dst + ((b - r0) * kPackSize + i) * 32 + side * 16, a, bbytes);
+            ++phys;
+          }
+        }
+      }
     }
   });
 

@@ -66,6 +66,11 @@ class VacuumIndex {
   void rows_into(int32_t id, std::vector<SkipRow>* out) const;   // reuses out's storage
   const uint8_t* file() const { return map_; }
   bool has_bloom() const { return has_bloom_; }
+  // the filters' shape: VacuumHeader's "end" fields, the ones both bloom
+  // readers use (flash_iterators.h:826-889)
+  uint32_t bloom_bytes() const { return bloom_bytes_; }
+  uint32_t bloom_entries() const { return bloom_entries_; }
+  float bloom_ratio() const { return bloom_ratio_; }
   uint64_t file_bytes() const { return map_len_; }
 
  private:
@@ -87,6 +92,8 @@ class VacuumIndex {
   uint8_t* map_ = nullptr;
   uint64_t map_len_ = 0;
   bool has_bloom_ = false;
+  uint32_t bloom_bytes_ = 0, bloom_entries_ = 0;
+  float bloom_ratio_ = 0;
 };
 
 // Allocator whose resize() leaves trivial elements uninitialised: the image's
@@ -133,6 +140,16 @@ struct HostImage {
   std::vector<uint32_t> pos_pk;             // per full pack: byte offset, bit width (pairs)
   std::vector<uint32_t> pos_tail;
   std::vector<uint32_t> pos_start;          // bag start entry per posting slot (as plen)
+  // two-way phrase bloom filters (build_image(..., blooms = true), positions
+  // images of bloom indexes whose bit arrays fit 16 bytes): per posting slot
+  // (as plen) 32 bytes, its "prior" (begin) then its "next" (end) bit array,
+  // zero when the box bitmap marks the posting absent (an all-zero array
+  // answers "not present", as a missing one does); per list the two
+  // MurmurHash2 values of its term (bloom_check's a and b, libbloom/bloom.c:48-75)
+  bool has_blooms = false;
+  uint32_t blm_bits = 0, blm_hashes = 0;
+  big_vector<uint8_t> blm;
+  std::vector<uint32_t> blm_hash;           // (a, b) per list id
 };
 
 // Decode one block (pack or VInts) at p into out[0..cnt); delta-coded blocks
@@ -144,7 +161,8 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
 // a rank bitmap + 1-byte tf array (0 disables them); dense_budget > 0 caps the
 // bytes of all bitmaps + tf arrays (the longest lists keep theirs).
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div = 0, bool positions = false, uint64_t dense_budget = 0);
+                      uint32_t dense_div = 0, bool positions = false, uint64_t dense_budget = 0,
+                      bool blooms = false);
 
 // Host restatement of the device's dense probe (segment kernel): tf of doc in
 // list L of the image, -1 when absent or when L has no bitmap.

@@ -42,6 +42,13 @@ struct IndexArgs {
   const uint32_t* pos_tail; // decoded VInts remainders
   const uint32_t* pos_start;// bag start entry of every posting, 128 slots per image block
   const uint8_t* wmax;      // per dense list and 2,048-doc window: its largest tf (HostImage::wmax)
+  // phrase bloom filters (null / 0 unless a bloom index was opened with
+  // positions and bloom_factor > 0): per posting slot two 16-byte bit arrays
+  // (prior, next), per list its term's two hashes; bloom_factor as
+  // CheckBloomWithEnableFactor's (query_processing.h:796-807)
+  const uint4* blm;
+  const uint2* blm_hash;
+  uint32_t blm_bits, blm_hashes, bloom_factor;
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,

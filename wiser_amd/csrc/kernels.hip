@@ -1530,8 +1530,43 @@ struct PosStream {
 // every i, which is PhraseQueryProcessor2::NumOfMatches() > 0
 // (query_processing.h:264-336: the 2-term merge and the general max-adjusted
 // walk both find every such a).  One lane per survivor.
+// bloom_check (libbloom/bloom.c:48-75) of list `elem`'s term in the bit array
+// `side` (0 prior, 1 next) of posting slot `slot`: false = not present (an
+// all-zero array, as for a posting without one, answers false).  Bit x of the
+// array is bit x % 8 of byte x / 8, i.e. bit x % 32 of little-endian dword x / 32.
+__device__ __forceinline__ bool bloom_may(const IndexArgs& ix, uint32_t slot, uint32_t side, int32_t elem) {
+  const uint2 h = ix.blm_hash[elem];
+  const uint4 w = ix.blm[2 * slot + side];
+  for (uint32_t i = 0; i < ix.blm_hashes; ++i) {
+    const uint32_t x = (h.x + i * h.y) % ix.blm_bits;
+    const uint32_t q = x >> 5;
+    const uint32_t d = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+    if (!((d >> (x & 31u)) & 1u)) return false;
+  }
+  return true;
+}
+
+// QueryProcessor::IsPossibleToPresent (query_processing.h:873-884): two terms,
+// CheckBloomWithEnableFactor (:796-807) -- the shorter list's filter, by the
+// lists' full sizes; more terms, CheckBloomFallBack (:784-794) -- every term's
+// "next" filter holds the following term.
+__device__ __forceinline__ bool bloom_possible(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
+                                               const uint32_t* ph, uint32_t v) {
+  if (nt == 2) {
+    const uint64_t f = ix.bloom_factor;
+    const uint64_t s1 = ix.lists[qlist[0]].df, s2 = ix.lists[qlist[1]].df;
+    if (f * s1 <= s2) return bloom_may(ix, ph[v], 1, qlist[1]);
+    if (f * s2 < s1) return bloom_may(ix, ph[256 + v], 0, qlist[0]);
+    return true;
+  }
+  for (uint32_t i = 0; i + 1 < nt; ++i)
+    if (!bloom_may(ix, ph[i * 256 + v], 1, qlist[i + 1])) return false;
+  return true;
+}
+
 __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
                                           const uint32_t* ph, uint32_t v) {
+  if (ix.bloom_factor && !bloom_possible(ix, qlist, nt, ph, v)) return false;
   if (nt == 2) {   // ProcessTwoTerm: a merge of bag 0 against bag 1 shifted by one
     const PosDev P0 = ix.pos_lists[qlist[0]], P1 = ix.pos_lists[qlist[1]];
     PosStream s0, s1;

@@ -103,6 +103,7 @@ class VacuumEngine:
         opts.doc_lo, opts.doc_hi = (self.doc_range if self.doc_range else (0, 0))
         opts.threads = self.threads
         opts.positions = 1 if self.positions else 0
+        opts.bloom_factor = int(self.bloom_factor)
         h = C.c_void_p()
         check(lib.wsr_open(self.engine_dir_path.encode(), C.byref(opts), C.byref(h)))
         self._h = h
