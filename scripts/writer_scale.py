@@ -39,7 +39,7 @@ def main():
     files = {f: os.path.getsize(os.path.join(out, f)) for f in sorted(os.listdir(out))}
     print(json.dumps({"linedoc": os.path.basename(ld), "linedoc_bytes": os.path.getsize(ld), "format": fmt,
                       "bloom": "ratio 0.0009, 5 entries" if bloom else None,
-                      "threads": threads or "default (min(cpus, 16))", "chunk_docs": chunk or "default (32768)",
+                      "threads": threads or "default (min(cpus, 16))", "chunk_docs": chunk or "default (8192)",
                       "wall_s": round(el, 1), "peak_rss_mib": round(rss_kb / 1024, 1),
                       "host_cpus": os.cpu_count(), "index": st, "files": files}, indent=1))
 

@@ -673,7 +673,7 @@ BuildStats build_from_linedoc(const std::string& linedoc, int64_t n_rows,
   const size_t need = token_only ? 3u : 5u;
   const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
   const int threads = std::max(1, env_int("WSR_WRITER_THREADS", std::min(hw, 16)));
-  const size_t chunk_docs = static_cast<size_t>(std::max(1, env_int("WSR_WRITER_CHUNK_DOCS", 32768)));
+  const size_t chunk_docs = static_cast<size_t>(std::max(1, env_int("WSR_WRITER_CHUNK_DOCS", 8192)));
   ::mkdir(out_dir.c_str(), 0777);
   const std::string run_dir = out_dir + "/.wsr_runs";
   ::mkdir(run_dir.c_str(), 0777);
