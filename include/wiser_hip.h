@@ -242,7 +242,16 @@ typedef struct wsr_serve_stats {
   double p50_ms, p99_ms; /* per-query latency, submit -> result on the caller's thread */
   uint64_t batches;      /* GPU batches the dispatcher ran */
   double mean_batch;     /* queries per batch */
+  /* where a query's latency goes (means over the run): */
+  double queue_ms;       /* submit -> its batch launched (dispatcher) */
+  double gpu_ms;         /* batch launched -> its end event seen by the completer */
+  double handoff_ms;     /* end event seen -> the batch's last caller signalled */
 } wsr_serve_stats;
+/* Dispatch: a batch launches at once while fewer than `depth` batches are in
+ * flight (WSR_SERVER_DEPTH, default 2: one running, one queued behind it on
+ * the GPU, so batch size follows the load); with `depth` or more in flight it
+ * launches when max_batch queries wait or the oldest has waited window_us, and
+ * at most 4 batches are ever in flight. */
 int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_server** out);
 void wsr_server_close(wsr_server* s);
 /* one query (k <= WSR_SERVER_MAX_K = WSR_MAX_K): hits receives n_hits <= k entries */

@@ -62,7 +62,8 @@ class ImageInfo(C.Structure):
 class ServeStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("seconds", C.c_double), ("qps", C.c_double),
                 ("p50_ms", C.c_double), ("p99_ms", C.c_double), ("batches", C.c_uint64),
-                ("mean_batch", C.c_double)]
+                ("mean_batch", C.c_double), ("queue_ms", C.c_double), ("gpu_ms", C.c_double),
+                ("handoff_ms", C.c_double)]
 
 
 class BuildStats(C.Structure):

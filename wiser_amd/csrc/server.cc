@@ -16,6 +16,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -85,6 +86,7 @@ struct Slot {
   std::vector<Req*> reqs;
   bool busy = false;
   uint64_t seq = 0;   // launch order
+  Clock::time_point t_launch;
   int32_t kmax = 1;   // the largest k of its queries (result columns to copy)
 };
 
@@ -97,6 +99,7 @@ struct wsr_server {
   static constexpr int kSlots = 4;
   wsr_handle* h = nullptr;
   int max_batch = 4096;
+  int depth = 2;                     // batches in flight below which one launches at once
   std::chrono::microseconds window{200};
   std::mutex mu;                     // queue, slot states, stop, idle
   std::condition_variable cv_work;   // dispatcher: requests arrived / a slot freed / stop
@@ -116,6 +119,9 @@ struct wsr_server {
   int32_t* nh = nullptr;
   std::vector<wsr_query> qbuf;       // dispatcher only
   std::atomic<uint64_t> batches{0}, queries{0};
+  // latency breakdown (ns): submit -> launch summed over queries; launch ->
+  // end event seen and end event -> last signal summed over batches
+  std::atomic<uint64_t> queue_ns{0}, gpu_ns{0}, handoff_ns{0};
 
   void complete(Slot& s) {
     // poll the batch's end event, so the fetch below finds it done (a blocking
@@ -128,6 +134,7 @@ struct wsr_server {
       if (Clock::now() < spin_until) std::this_thread::yield();
       else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
+    const auto t_ready = Clock::now();
     int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
@@ -140,6 +147,9 @@ struct wsr_server {
       r->signal();
     }
     s.reqs.clear();
+    const auto t_done = Clock::now();
+    gpu_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t_ready - s.t_launch).count());
+    handoff_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t_done - t_ready).count());
   }
 
   // Completer: retires launched batches in order and frees their slots.
@@ -165,10 +175,13 @@ struct wsr_server {
     }
   }
 
-  // Dispatch policy: with no batch in flight, whatever is queued runs at once
-  // (the latency of a lone query is one batch); with batches in flight, the
-  // next one fills until max_batch or until its oldest request has waited
-  // `window`; with every slot in flight, it waits for the completer.
+  // Dispatch policy: with fewer than `depth` batches in flight, whatever is
+  // queued runs at once (a lone query waits for one batch; under load the GPU
+  // always has the next batch queued behind the running one, and a batch
+  // holds what arrived while the one before it ran, so its size follows the
+  // load); with more in flight, the next one fills until max_batch or until
+  // its oldest request has waited `window`; with every slot in flight, it
+  // waits for the completer.
   void run() {
     uint64_t seq = 0;
     for (;;) {
@@ -179,7 +192,7 @@ struct wsr_server {
         for (;;) {
           if (queue.empty() && stop) break;
           if (!queue.empty() && n_busy < kSlots) {
-            if (n_busy > 0 && !stop && static_cast<int>(queue.size()) < max_batch) {
+            if (n_busy >= depth && !stop && static_cast<int>(queue.size()) < max_batch) {
               const auto due = queue.front()->t_enq + window;
               if (Clock::now() < due) {   // (submit wakes us early when the batch fills)
                 idle = true;
@@ -204,6 +217,13 @@ struct wsr_server {
         ++n_busy;
       }
       Slot& s = *slot;
+      s.t_launch = Clock::now();
+      {
+        uint64_t w = 0;
+        for (Req* r : take)
+          w += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(s.t_launch - r->t_enq).count());
+        queue_ns += w;
+      }
       qbuf.resize(take.size());
       s.kmax = 1;
       for (size_t i = 0; i < take.size(); ++i) {
@@ -278,6 +298,7 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
   s->h = h;
   s->max_batch = max_batch;
   s->window = std::chrono::microseconds(window_us);
+  if (const char* e = std::getenv("WSR_SERVER_DEPTH")) s->depth = std::max(1, std::min(wsr_server::kSlots, std::atoi(e)));
   for (auto& sl : s->slots) {
     int rc = wsr_batch_create(h, max_batch, WSR_SERVER_MAX_K, &sl.b);
     if (rc != WSR_OK) {
@@ -336,6 +357,7 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
   std::vector<std::vector<float>> lat(static_cast<size_t>(n_clients));
   std::atomic<uint64_t> done{0};
   const uint64_t b0 = s->batches.load(), q0 = s->queries.load();
+  const uint64_t w0 = s->queue_ns.load(), g0 = s->gpu_ns.load(), h0 = s->handoff_ns.load();
   const auto t_start = Clock::now();
   const auto t_end = t_start + std::chrono::duration_cast<Clock::duration>(
                                    std::chrono::duration<double>(seconds));
@@ -395,7 +417,11 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
   st->p50_ms = pct(0.50);
   st->p99_ms = pct(0.99);
   st->batches = s->batches.load() - b0;
-  st->mean_batch = st->batches ? static_cast<double>(s->queries.load() - q0) / st->batches : 0.0;
+  const uint64_t nq_run = s->queries.load() - q0;
+  st->mean_batch = st->batches ? static_cast<double>(nq_run) / st->batches : 0.0;
+  st->queue_ms = nq_run ? static_cast<double>(s->queue_ns.load() - w0) * 1e-6 / nq_run : 0.0;
+  st->gpu_ms = st->batches ? static_cast<double>(s->gpu_ns.load() - g0) * 1e-6 / st->batches : 0.0;
+  st->handoff_ms = st->batches ? static_cast<double>(s->handoff_ns.load() - h0) * 1e-6 / st->batches : 0.0;
   return first_rc.load();
 }
 
