@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
 #include <sys/syscall.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "../../include/wiser_hip.h"
@@ -47,8 +48,6 @@ using Clock = std::chrono::steady_clock;
 constexpr int kPending = 0, kDone = 1, kSleeping = 2;
 
 struct Req {
-  wsr_query q;
-  Clock::time_point t_enq;
   wsr_hit* out = nullptr;
   int32_t* n_out = nullptr;
   int rc = WSR_OK;
@@ -81,14 +80,32 @@ struct Req {
 };
 static_assert(sizeof(std::atomic<int>) == sizeof(int), "futex word");
 
+// One submitted query in the ring: the query itself (so the dispatcher copies
+// a batch from consecutive entries instead of chasing every caller's stack),
+// its caller's request, its submit time; seq = index + 1 once it is published.
+struct alignas(64) Entry {
+  wsr_query q;
+  Req* r;
+  int64_t t_enq;   // steady-clock ns
+  std::atomic<uint64_t> seq{0};
+};
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
 struct Slot {
   wsr_batch* b = nullptr;
   std::vector<Req*> reqs;
-  bool busy = false;
+  std::atomic<bool> busy{false};
   uint64_t seq = 0;   // launch order
-  Clock::time_point t_launch;
+  int64_t t_launch = 0;
   int32_t kmax = 1;   // the largest k of its queries (result columns to copy)
 };
+
+// What the dispatcher sleeps for (wsr_server::sleeping): a waker clears it
+// with one compare-exchange, so one thread makes the futex call.
+constexpr int kAwake = 0, kWantWork = 1, kWantFull = 2, kWantSlot = 3;
 
 }  // namespace
 
@@ -97,16 +114,23 @@ struct wsr_server {
   // thread retires them in launch order, so launching never waits for a
   // result hand-off
   static constexpr int kSlots = 4;
+  static constexpr uint64_t kRing = 1u << 16;   // submitted, not yet batched queries
   wsr_handle* h = nullptr;
   int max_batch = 4096;
   int depth = 2;                     // batches in flight below which one launches at once
-  std::chrono::microseconds window{200};
-  std::mutex mu;                     // queue, slot states, stop, idle
-  std::condition_variable cv_work;   // dispatcher: requests arrived / a slot freed / stop
-  std::deque<Req*> queue;
-  bool stop = false;
-  bool idle = false;                 // dispatcher asleep on cv_work with nothing to launch
-  int n_busy = 0;
+  int64_t window_ns = 200000;
+  // submission ring (multi-producer, one consumer): a caller claims index
+  // tail++, fills entry index % kRing and publishes it; the dispatcher takes
+  // published entries in index order and advances `consumed`.  No lock on the
+  // submit path: one fetch-add, and a futex wake only when the dispatcher
+  // sleeps waiting for exactly what this submit brings.
+  std::unique_ptr<Entry[]> ring;
+  alignas(64) std::atomic<uint64_t> tail{0};
+  alignas(64) std::atomic<uint64_t> consumed{0};
+  alignas(64) std::atomic<uint32_t> wake_word{0};   // futex word: bumped to wake the dispatcher
+  std::atomic<int> sleeping{kAwake};
+  alignas(64) std::atomic<int> n_busy{0};
+  std::atomic<bool> stop{false};
   std::thread worker, completer;
   Slot slots[kSlots];
   std::mutex fmu;                    // the launched batches, oldest first
@@ -123,18 +147,48 @@ struct wsr_server {
   // end event seen and end event -> last signal summed over batches
   std::atomic<uint64_t> queue_ns{0}, gpu_ns{0}, handoff_ns{0};
 
+  void wake(int reason_mask) {
+    int s = sleeping.load(std::memory_order_seq_cst);
+    if (s != kAwake && ((1 << s) & reason_mask) && sleeping.compare_exchange_strong(s, kAwake)) {
+      wake_word.fetch_add(1, std::memory_order_seq_cst);
+      syscall(SYS_futex, reinterpret_cast<uint32_t*>(&wake_word), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    }
+  }
+
+  // Sleep for `why` unless the state the decision was made on (ww: the wake
+  // word read before it, tail_seen / busy_seen) changed meanwhile.  With the
+  // flag set first (seq_cst) a submitter / the completer either sees it and
+  // wakes us, or made its change before our re-check below.
+  void doze(int why, uint32_t ww, uint64_t tail_seen, int busy_seen, int64_t timeout_ns) {
+    sleeping.store(why, std::memory_order_seq_cst);
+    if (tail.load(std::memory_order_seq_cst) != tail_seen || n_busy.load(std::memory_order_seq_cst) != busy_seen ||
+        stop.load(std::memory_order_seq_cst)) {
+      sleeping.store(kAwake);
+      return;
+    }
+    timespec ts{}, *tp = nullptr;
+    if (timeout_ns >= 0) {
+      ts.tv_sec = timeout_ns / 1000000000;
+      ts.tv_nsec = timeout_ns % 1000000000;
+      tp = &ts;
+    }
+    syscall(SYS_futex, reinterpret_cast<uint32_t*>(&wake_word), FUTEX_WAIT_PRIVATE, ww, tp, nullptr, 0);
+    sleeping.store(kAwake);
+  }
+
   void complete(Slot& s) {
     // poll the batch's end event, so the fetch below finds it done (a blocking
     // wait inside the fetch can sleep through the batch's end and wake late);
     // a HIP error ends the poll too, and the fetch reports it.  Yield for the
-    // first 100 us, then back off to short sleeps, so that a long batch does
-    // not keep a host core busy beside the clients and the dispatcher.
-    const auto spin_until = Clock::now() + std::chrono::microseconds(100);
+    // first millisecond (batches take 0.1-1 ms: a timed sleep would add the
+    // kernel's timer slack, ~50 us, to every hand-off), then back off to short
+    // sleeps, so that a long batch does not keep a host core busy.
+    const auto spin_until = Clock::now() + std::chrono::microseconds(1000);
     while (wsr_batch_ready(h, s.b) == 0) {
       if (Clock::now() < spin_until) std::this_thread::yield();
       else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
-    const auto t_ready = Clock::now();
+    const int64_t t_ready = now_ns();
     int rc = wsr_batch_fetch_cols(h, s.b, hits, nh, s.kmax);
     for (size_t i = 0; i < s.reqs.size(); ++i) {
       Req* r = s.reqs[i];
@@ -147,9 +201,16 @@ struct wsr_server {
       r->signal();
     }
     s.reqs.clear();
-    const auto t_done = Clock::now();
-    gpu_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t_ready - s.t_launch).count());
-    handoff_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t_done - t_ready).count());
+    const int64_t t_done = now_ns();
+    gpu_ns += static_cast<uint64_t>(t_ready - s.t_launch);
+    handoff_ns += static_cast<uint64_t>(t_done - t_ready);
+  }
+
+  // a slot's batch is over: free it and wake a dispatcher that waits for one
+  void release(Slot& s) {
+    s.busy.store(false, std::memory_order_release);
+    n_busy.fetch_sub(1, std::memory_order_seq_cst);
+    wake((1 << kWantSlot) | (1 << kWantFull));
   }
 
   // Completer: retires launched batches in order and frees their slots.
@@ -164,14 +225,7 @@ struct wsr_server {
         inflight.pop_front();
       }
       complete(*s);
-      bool wake;
-      {
-        std::lock_guard<std::mutex> g(mu);
-        s->busy = false;
-        --n_busy;
-        wake = idle;
-      }
-      if (wake) cv_work.notify_one();
+      release(*s);
     }
   }
 
@@ -183,69 +237,75 @@ struct wsr_server {
   // its oldest request has waited `window`; with every slot in flight, it
   // waits for the completer.
   void run() {
-    uint64_t seq = 0;
+    uint64_t next = 0, seq = 0;
+    const uint64_t mask = kRing - 1;
+    std::vector<Req*> take;
     for (;;) {
-      std::vector<Req*> take;
-      Slot* slot = nullptr;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        for (;;) {
-          if (queue.empty() && stop) break;
-          if (!queue.empty() && n_busy < kSlots) {
-            if (n_busy >= depth && !stop && static_cast<int>(queue.size()) < max_batch) {
-              const auto due = queue.front()->t_enq + window;
-              if (Clock::now() < due) {   // (submit wakes us early when the batch fills)
-                idle = true;
-                cv_work.wait_until(lk, due);
-                idle = false;
-                continue;
-              }
-            }
-            break;
-          }
-          idle = true;
-          cv_work.wait(lk);
-          idle = false;
+      const uint32_t ww = wake_word.load(std::memory_order_seq_cst);
+      const uint64_t t = tail.load(std::memory_order_seq_cst);
+      const uint64_t queued = t - next;
+      const int busy = n_busy.load(std::memory_order_seq_cst);
+      if (queued == 0) {
+        if (stop.load()) break;   // everything submitted was launched
+        doze(kWantWork, ww, t, busy, -1);
+        continue;
+      }
+      if (busy >= kSlots) {
+        doze(kWantSlot, ww, t, busy, -1);
+        continue;
+      }
+      Entry& head = ring[next & mask];
+      if (head.seq.load(std::memory_order_acquire) != next + 1) {   // claimed, not yet written
+        std::this_thread::yield();
+        continue;
+      }
+      if (busy >= depth && !stop.load() && queued < static_cast<uint64_t>(max_batch)) {
+        const int64_t left = head.t_enq + window_ns - now_ns();
+        if (left > 0) {
+          doze(kWantFull, ww, t, busy, left);
+          continue;
         }
-        if (queue.empty()) break;   // stop, and everything was launched
-        const size_t n = std::min<size_t>(queue.size(), static_cast<size_t>(max_batch));
-        take.assign(queue.begin(), queue.begin() + static_cast<long>(n));
-        queue.erase(queue.begin(), queue.begin() + static_cast<long>(n));
-        for (auto& sl : slots)
-          if (!sl.busy) { slot = &sl; break; }
-        slot->busy = true;
-        ++n_busy;
       }
+      // the published prefix, at most max_batch
+      const int64_t t_launch = now_ns();
+      uint64_t wait_ns = 0;
+      take.clear();
+      qbuf.clear();
+      const uint64_t lim = std::min<uint64_t>(queued, static_cast<uint64_t>(max_batch));
+      for (uint64_t i = 0; i < lim; ++i) {
+        Entry& e = ring[(next + i) & mask];
+        if (e.seq.load(std::memory_order_acquire) != next + i + 1) break;
+        qbuf.push_back(e.q);
+        take.push_back(e.r);
+        wait_ns += static_cast<uint64_t>(t_launch - e.t_enq);
+      }
+      next += take.size();
+      consumed.store(next, std::memory_order_release);
+      queue_ns += wait_ns;
+      Slot* slot = nullptr;
+      for (auto& sl : slots)
+        if (!sl.busy.load(std::memory_order_acquire)) { slot = &sl; break; }
+      slot->busy.store(true, std::memory_order_relaxed);
+      n_busy.fetch_add(1, std::memory_order_seq_cst);
       Slot& s = *slot;
-      s.t_launch = Clock::now();
-      {
-        uint64_t w = 0;
-        for (Req* r : take)
-          w += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(s.t_launch - r->t_enq).count());
-        queue_ns += w;
-      }
-      qbuf.resize(take.size());
+      s.t_launch = t_launch;
       s.kmax = 1;
-      for (size_t i = 0; i < take.size(); ++i) {
-        qbuf[i] = take[i]->q;
-        s.kmax = std::max(s.kmax, qbuf[i].k);
-      }
+      for (const wsr_query& q : qbuf) s.kmax = std::max(s.kmax, q.k);
       int rc = wsr_batch_upload(h, s.b, qbuf.data(), static_cast<int32_t>(qbuf.size()));
       if (rc == WSR_OK) rc = wsr_batch_run(h, s.b);
       if (rc != WSR_OK) {
         // every request was checked at submit, so this is not one caller's bad
         // query: the batch is retried one request at a time, and only the
         // requests that fail on their own get an error
-        for (Req* r : take) {
-          r->fail_with(wsr_search_batch(h, &r->q, 1, std::max(1, r->q.k), r->out, r->n_out));
+        for (size_t i = 0; i < take.size(); ++i) {
+          Req* r = take[i];
+          r->fail_with(wsr_search_batch(h, &qbuf[i], 1, std::max(1, qbuf[i].k), r->out, r->n_out));
           r->signal();
         }
-        std::lock_guard<std::mutex> g(mu);
-        s.busy = false;
-        --n_busy;
+        release(s);
         continue;
       }
-      s.reqs = std::move(take);
+      s.reqs.swap(take);
       s.seq = ++seq;
       ++batches;
       queries += s.reqs.size();
@@ -262,23 +322,25 @@ struct wsr_server {
     cv_done.notify_one();
   }
 
-  int submit(Req* r) {
+  int submit(const wsr_query& q, Req* r) {
     // a bad request fails alone, here, and never joins a batch
     // (wsr_batch_upload rejects a whole batch for one bad query)
-    const int qrc = wsr_check_query(h, &r->q);
+    const int qrc = wsr_check_query(h, &q);
     if (qrc != WSR_OK) return qrc;
-    if (r->q.k > WSR_SERVER_MAX_K) return WSR_E_LIMIT;   // the slots' result columns
-    r->t_enq = Clock::now();
-    bool wake;
-    {
-      std::lock_guard<std::mutex> g(mu);
-      if (stop) return WSR_E_INVALID;
-      queue.push_back(r);
-      // the dispatcher sleeps with nothing to launch, or until a window ends:
-      // wake it for the first request, or when a batch is full
-      wake = idle && (queue.size() == 1 || static_cast<int>(queue.size()) == max_batch);
-    }
-    if (wake) cv_work.notify_one();
+    if (q.k > WSR_SERVER_MAX_K) return WSR_E_LIMIT;   // the slots' result columns
+    if (stop.load(std::memory_order_relaxed)) return WSR_E_INVALID;
+    const uint64_t i = tail.fetch_add(1, std::memory_order_seq_cst);
+    while (i - consumed.load(std::memory_order_acquire) >= kRing) std::this_thread::yield();   // (ring full)
+    Entry& e = ring[i & (kRing - 1)];
+    e.q = q;
+    e.r = r;
+    e.t_enq = now_ns();
+    e.seq.store(i + 1, std::memory_order_seq_cst);
+    // wake a dispatcher asleep for work, or for a full batch when this one fills it
+    const int s = sleeping.load(std::memory_order_seq_cst);
+    if (s == kWantWork || (s == kWantFull && i + 1 - consumed.load(std::memory_order_relaxed) >=
+                                                static_cast<uint64_t>(max_batch)))
+      wake((1 << kWantWork) | (1 << kWantFull));
     return WSR_OK;
   }
 
@@ -297,7 +359,8 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
   std::unique_ptr<wsr_server> s(new wsr_server());
   s->h = h;
   s->max_batch = max_batch;
-  s->window = std::chrono::microseconds(window_us);
+  s->window_ns = static_cast<int64_t>(window_us) * 1000;
+  s->ring.reset(new Entry[wsr_server::kRing]);
   if (const char* e = std::getenv("WSR_SERVER_DEPTH")) s->depth = std::max(1, std::min(wsr_server::kSlots, std::atoi(e)));
   for (auto& sl : s->slots) {
     int rc = wsr_batch_create(h, max_batch, WSR_SERVER_MAX_K, &sl.b);
@@ -323,11 +386,8 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
 
 void wsr_server_close(wsr_server* s) {
   if (!s) return;
-  {
-    std::lock_guard<std::mutex> g(s->mu);
-    s->stop = true;
-  }
-  s->cv_work.notify_all();
+  s->stop.store(true, std::memory_order_seq_cst);
+  s->wake((1 << kWantWork) | (1 << kWantFull) | (1 << kWantSlot));
   if (s->worker.joinable()) s->worker.join();         // launches what is queued, then stops the completer
   if (s->completer.joinable()) s->completer.join();   // retires what is in flight
   for (auto& sl : s->slots)
@@ -340,10 +400,9 @@ void wsr_server_close(wsr_server* s) {
 int wsr_server_search(wsr_server* s, const wsr_query* q, wsr_hit* hits, int32_t* n_hits) {
   if (!s || !q || !hits || !n_hits) return WSR_E_INVALID;
   Req r;
-  r.q = *q;
   r.out = hits;
   r.n_out = n_hits;
-  int rc = s->submit(&r);
+  int rc = s->submit(*q, &r);
   if (rc != WSR_OK) return rc;
   rc = s->wait(&r);
   if (rc != WSR_OK) wiser::set_last_error(r.err);   // (it failed on the dispatcher's or completer's thread)
@@ -355,7 +414,7 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
   if (!s || !q || nq < 1 || n_clients < 1 || depth < 1 || !st) return WSR_E_INVALID;
   std::atomic<int> first_rc{WSR_OK};
   std::vector<std::vector<float>> lat(static_cast<size_t>(n_clients));
-  std::atomic<uint64_t> done{0};
+  std::vector<uint64_t> done_per(static_cast<size_t>(n_clients), 0);
   const uint64_t b0 = s->batches.load(), q0 = s->queries.load();
   const uint64_t w0 = s->queue_ns.load(), g0 = s->gpu_ns.load(), h0 = s->handoff_ns.load();
   const auto t_start = Clock::now();
@@ -367,14 +426,14 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
     std::vector<int32_t> nout(static_cast<size_t>(depth));
     std::vector<Clock::time_point> t0(static_cast<size_t>(depth));
     uint64_t next_q = static_cast<uint64_t>(c) * 7919u;
+    uint64_t& done = done_per[static_cast<size_t>(c)];
     auto issue = [&](int i) {
       Req& r = rq[static_cast<size_t>(i)];
       r.reset();
-      r.q = q[next_q++ % static_cast<uint64_t>(nq)];
       r.out = out[static_cast<size_t>(i)].data();
       r.n_out = &nout[static_cast<size_t>(i)];
       t0[static_cast<size_t>(i)] = Clock::now();
-      const int rc = s->submit(&r);
+      const int rc = s->submit(q[next_q++ % static_cast<uint64_t>(nq)], &r);
       if (rc != WSR_OK) { r.rc = rc; r.done.store(kDone); }
     };
     for (int i = 0; i < depth; ++i) issue(i);
@@ -403,6 +462,8 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
   for (int c = 0; c < n_clients; ++c) ts.emplace_back(client, c);
   for (auto& t : ts) t.join();
   const double el = std::chrono::duration<double>(Clock::now() - t_start).count();
+  uint64_t n_done = 0;
+  for (uint64_t d : done_per) n_done += d;
   std::vector<float> all;
   for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
   std::sort(all.begin(), all.end());
@@ -411,9 +472,9 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
     size_t i = static_cast<size_t>(p * static_cast<double>(all.size() - 1) + 0.5);
     return static_cast<double>(all[std::min(i, all.size() - 1)]);
   };
-  st->queries = done.load();
+  st->queries = n_done;
   st->seconds = el;
-  st->qps = static_cast<double>(done.load()) / el;
+  st->qps = static_cast<double>(n_done) / el;
   st->p50_ms = pct(0.50);
   st->p99_ms = pct(0.99);
   st->batches = s->batches.load() - b0;
