@@ -39,8 +39,11 @@ def main():
     arr = (_capi.Query * len(lines))()
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=10))[0]
-    points = [(2, 4, 1024, 1000), (2, 8, 768, 1000), (2, 8, 1024, 1000), (2, 12, 512, 1000),
-              (1, 8, 768, 1000), (3, 8, 768, 1000), (2, 4, 64, 100), (2, 8, 128, 100)]
+    points = [(2, 8, 512, 1000), (2, 10, 512, 1000), (2, 12, 448, 1000), (2, 16, 384, 1000),
+              (2, 16, 320, 1000), (2, 12, 512, 1000), (3, 12, 512, 1000), (2, 8, 768, 1000),
+              (2, 12, 512, 300), (2, 4, 64, 100)]
+    if os.environ.get("SWEEP_POINTS"):   # "depth,clients,per,window;..."
+        points = [tuple(int(x) for x in p.split(",")) for p in os.environ["SWEEP_POINTS"].split(";")]
     for depth, clients, per, win in points:
         os.environ["WSR_SERVER_DEPTH"] = str(depth)
         srv = w.Server(eng, max_batch=4096, window_us=win)
