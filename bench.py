@@ -662,8 +662,8 @@ def snippet_leg(a, local, threads):
 
 
 def serving_leg(a, idx, qlog, local, threads):
-    """Single-query serving through the micro-batcher (wsr_server_*): 4 client
-    threads keep 1024 (or 64) queries each in flight (the reference client's
+    """Single-query serving through the micro-batcher (wsr_server_*): client
+    threads keep 512-768 (or 64) queries each in flight (the reference client's
     threads, grpc_client_impl.h:557-620) over the headline log; latency = submit ->
     result.  The clients share the box's 16-core CPU share with the dispatcher,
     so few client threads with deep windows load it best."""
@@ -676,14 +676,19 @@ def serving_leg(a, idx, qlog, local, threads):
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
     out = {}
-    for clients, depth, window in ((4, 1024, 1000), (4, 64, 100)):
+    # (10 clients x 512: the sweep's best point on the box's 16-core share,
+    # profiles/r03_serve_sweep.txt; more client threads than that oversubscribe
+    # the share beside the dispatcher, the completer and HIP's threads)
+    for clients, depth, window in ((10, 512, 1000), (8, 768, 1000), (4, 64, 100)):
         srv = w.Server(eng, max_batch=a.batch, window_us=window)
         st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
         srv.close()
         out[f"in_flight_{clients * depth}"] = {
             "value": round(st.qps, 1), "unit": "queries/s", "p50_ms": round(st.p50_ms, 3),
             "p99_ms": round(st.p99_ms, 3), "mean_batch": round(st.mean_batch, 1),
-            "window_us": window, "clients": clients, "depth": depth}
+            "window_us": window, "clients": clients, "depth": depth,
+            "queue_ms": round(st.queue_ms, 3), "gpu_ms": round(st.gpu_ms, 3),
+            "handoff_ms": round(st.handoff_ms, 3)}
     eng.close()
     return out
 
