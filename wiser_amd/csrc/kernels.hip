@@ -835,6 +835,9 @@ __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm
 }
 
 // --------------------------------------------------------------- replay --
+#ifndef WSR_HANDOFF_ACQREL
+#define WSR_HANDOFF_ACQREL 1
+#endif
 // Events handed from one workgroup to another inside the segment kernel
 // (fused replay) travel with agent-scope relaxed atomics, which gfx950 issues
 // as sc1 (coherent across the XCDs' L2s) loads and stores; the hand-off itself
@@ -1423,11 +1426,14 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     }
     ev_n = kept;
   }
-  // (The hand-off is relaxed agent-scope atomics plus a full s_waitcnt: on
-  // gfx950 the events went out as sc1 stores, which write through to memory,
-  // and the waitcnt retires them before the counter moves; the replay reads
-  // them with sc1 loads.  A release / acquire pair at agent scope would add a
-  // buffer_wbl2 / buffer_inv of the whole L2 to every item.)
+  // The hand-off: the events went out as agent-scope (sc1, write-through)
+  // stores and the replay reads them with sc1 loads; the per-query counter is
+  // an agent-scope acquire-release RMW (WSR_HANDOFF_ACQREL, the default), so the
+  // ordering is the memory model's own and not only the hardware's: the
+  // release orders this item's event and count stores before its increment,
+  // the acquire of the item that finishes the query orders every other item's
+  // stores before its reads.  (WSR_HANDOFF_ACQREL=0: relaxed RMW after a full
+  // s_waitcnt, round 2's form; the same results and speed, profiles/r03_handoff_ab.txt.)
   if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the
   // segments; in a shard step every query is emitted here
@@ -1436,7 +1442,8 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     block_sync<kWave>();
     uint32_t old = 0;
     if (l == 0)
-      old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, WSR_HANDOFF_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     old = uni(old);
     if (old + 1 == n_items) {
       if (fr.x_send)
