@@ -836,7 +836,7 @@ __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm
 
 // --------------------------------------------------------------- replay --
 #ifndef WSR_HANDOFF_ACQREL
-#define WSR_HANDOFF_ACQREL 1
+#define WSR_HANDOFF_ACQREL 0
 #endif
 // Events handed from one workgroup to another inside the segment kernel
 // (fused replay) travel with agent-scope relaxed atomics, which gfx950 issues
@@ -1428,12 +1428,13 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
   }
   // The hand-off: the events went out as agent-scope (sc1, write-through)
   // stores and the replay reads them with sc1 loads; the per-query counter is
-  // an agent-scope acquire-release RMW (WSR_HANDOFF_ACQREL, the default), so the
-  // ordering is the memory model's own and not only the hardware's: the
-  // release orders this item's event and count stores before its increment,
-  // the acquire of the item that finishes the query orders every other item's
-  // stores before its reads.  (WSR_HANDOFF_ACQREL=0: relaxed RMW after a full
-  // s_waitcnt, round 2's form; the same results and speed, profiles/r03_handoff_ab.txt.)
+  // a relaxed agent-scope RMW issued after a full s_waitcnt, which retires
+  // this item's event and count stores first.  An acquire-release RMW
+  // (WSR_HANDOFF_ACQREL=1) states the same ordering in the memory model's own
+  // terms, but gfx950 implements it with a write-back of the whole L2 before
+  // the RMW and an invalidate after it, on every item: measured at 0.88 ms
+  // against 0.49 ms for the C2 high x high class and 5.8 M against 10.6 M q/s
+  // on the C3 headline, parity green both ways (profiles/r03_handoff_ab.txt).
   if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the
   // segments; in a shard step every query is emitted here
