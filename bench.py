@@ -728,6 +728,30 @@ def kernel_accounting(eng, batches):
     return acc
 
 
+def staggered(dist, rank, world, fn, group=2):
+    """fn() on every rank, `group` ranks at a time: a full-image load holds the
+    host image (26.7 GB for the C3 stand-in) until its upload, so eight ranks
+    loading at once would need eight host images at the same time."""
+    if dist is None or world <= group:
+        return fn()
+    out = None
+    for g in range(0, world, group):
+        if g <= rank < g + group:
+            out = fn()
+        dist.barrier()
+    return out
+
+
+def open_full(idx, local, threads, rank, world, dist):
+    import wiser_amd as w
+
+    def load():
+        e = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+        e.Load()
+        return e
+    return staggered(dist, rank, world, load)
+
+
 def open_shard_engines(a, idx, rank, world, local, dist, threads, need_full):
     """This rank's doc-range shard image (with the engine's RCCL communicator)
     and, for the hybrid and replica forms, the full-index image."""
@@ -747,10 +771,7 @@ def open_shard_engines(a, idx, rank, world, local, dist, threads, need_full):
         S = HostExchangeShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
     else:
         S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
-    full = None
-    if need_full:
-        full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
-        full.Load()
+    full = open_full(idx, local, threads, rank, world, dist) if need_full else None
     log(f"rank {rank}: shard {S.doc_range}{' + full image' if full else ''} loaded in {time.time()-t:.1f}s")
     return S, full
 
@@ -1029,8 +1050,7 @@ def main():
     full = S = None
     t = time.time()
     if mode == "replica":
-        full = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
-        full.Load()
+        full = open_full(idx, local, threads, rank, world, dist)
         log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
     else:
         hb_default = max(64, 63 * world)
