@@ -2232,6 +2232,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       // stale word, which H never reads -- its doc is ~0u or outside the span)
       if (in0) Y.de0 = o_bm[(a0 - lo) / kDenseDocs];
       if (in1) Y.de1 = o_bm[(a1 - lo) / kDenseDocs];
+#elif defined(WSR_DIAG_PROBE_L2)   // timing diagnostic only (wrong hits): probes L2-resident
+      Y.de0 = o_bm[in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u];
+      Y.de1 = o_bm[in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u];
+#elif defined(WSR_DIAG_PROBE_NONE)   // timing diagnostic only (wrong results): no probes, no hits
+      // (k < 2^20: a zero mask the compiler cannot fold away)
+      Y.de0 = make_uint2(0u, in0 ? (Q.k >> 20) : 0u);
+      Y.de1 = make_uint2(0u, in1 ? (Q.k >> 20) : 0u);
 #else
       Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
       Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
