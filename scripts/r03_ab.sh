@@ -2,7 +2,7 @@
 # A/B on the C3 stand-in: per-class segment times (scripts/diag_types.py --wiki,
 # mixed and high x high) for the default build and every variant build under
 # wiser_amd/_lib/var_*, two rounds; then the headline bench (--no-cpu
-# --no-extra, 1000 steps) per build.  Usage: TAG
+# --no-extra, 3000 steps) per build.  Usage: TAG
 set -eu -o pipefail
 TAG=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -13,7 +13,7 @@ diag() {
   timeout -k 10 300 python3 scripts/diag_types.py --wiki | grep -E "^(mixed|high-high)|lean stages|sections"
 }
 bench() {
-  timeout -k 10 300 python3 bench.py --no-cpu --no-extra --steps 1000 --check 64 2>/dev/null | python3 -c \
+  timeout -k 10 300 python3 bench.py --no-cpu --no-extra --steps 3000 --check 64 2>/dev/null | python3 -c \
     "import json,sys;d=json.loads(sys.stdin.read());print('value', d['value'], 'ms_per_step', d['ms_per_step'])"
 }
 {

@@ -612,17 +612,23 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     }
     img.lists[id].tfmax = tfmax;   // (this worker's own list)
     if (in.dense) {
-      // rank bitmap: per 32 docs, the postings before them and the doc mask
+      // rank bitmap: per kDenseDocs docs, the postings before them and the doc mask
       DenseEnt* de = &img.dense[ld.bm];
       uint64_t i = 0;
       for (uint64_t e = 0; e < n_ent; ++e) {
         const uint64_t start = doc_lo + e * kDenseDocs;
         while (i < n_img && s.docs[i] < start) ++i;
-        de[e].rank = static_cast<uint32_t>(i);
-        uint32_t wbits = 0;
-        for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j)
-          wbits |= 1u << static_cast<uint32_t>(s.docs[j] - start);
-        de[e].w = wbits;
+        DenseEnt ent{};
+        ent.rank = static_cast<uint32_t>(i);
+        for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j) {
+          const uint32_t sh = static_cast<uint32_t>(s.docs[j] - start);
+#if WSR_DENSE_FMT
+          ent.w[sh >> 5] |= 1u << (sh & 31u);
+#else
+          ent.w |= 1u << sh;
+#endif
+        }
+        de[e] = ent;
       }
       uint8_t* t8 = &img.tf8[ld.tf8];
       for (uint64_t j = 0; j < n_img; ++j) t8[j] = static_cast<uint8_t>(s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape);
@@ -770,8 +776,8 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   if (rel >= img.dense_span) return -1;
   const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
   const uint32_t sh = rel % kDenseDocs;
-  if (!((e.w >> sh) & 1u)) return -1;
-  const uint32_t idx = e.rank + static_cast<uint32_t>(__builtin_popcount(e.w & ((1u << sh) - 1u)));
+  if (!dense_ent_bit(e, sh)) return -1;
+  const uint32_t idx = dense_ent_rank(e, sh);
   const uint8_t t = img.tf8[L.tf8 + idx];
   if (t != kTf8Escape) return t;
   const uint32_t j = idx / kPackSize;

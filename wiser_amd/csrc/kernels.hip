@@ -295,14 +295,57 @@ __device__ __forceinline__ bool use_dense(const IndexArgs& ix, bool has_bm, uint
   return has_bm && static_cast<float>(nblk_b) >= ix.dense_ratio * static_cast<float>(nblk_driver);
 }
 
+// A bitmap entry as loaded (one load per probe) and its bit test and rank
+// (engine_types.h, WSR_DENSE_FMT).
+#if WSR_DENSE_FMT
+using DenseVal = uint4;   // masks x, y, z (96 docs), rank w
+__device__ __forceinline__ bool dense_bit(const DenseVal v, uint32_t sh) {
+  const uint32_t wd = sh >> 5;
+  const uint32_t m = wd == 0 ? v.x : (wd == 1 ? v.y : v.z);
+  return (m >> (sh & 31u)) & 1u;
+}
+__device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
+  const uint32_t wd = sh >> 5, below = (1u << (sh & 31u)) - 1u;
+  const uint32_t m0 = wd == 0 ? below : ~0u, m1 = wd == 0 ? 0u : (wd == 1 ? below : ~0u);
+  const uint32_t m2 = wd == 2 ? below : 0u;
+  return v.w + __popc(v.x & m0) + __popc(v.y & m1) + __popc(v.z & m2);
+}
+#else
+using DenseVal = uint2;   // rank x, mask y (32 docs)
+__device__ __forceinline__ bool dense_bit(const DenseVal v, uint32_t sh) { return (v.y >> sh) & 1u; }
+__device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
+  return v.x + __popc(v.y & ((1u << sh) - 1u));
+}
+#endif
+__device__ __forceinline__ DenseVal dense_at(const DenseEnt* base, uint32_t e) {
+  return reinterpret_cast<const DenseVal*>(base)[e];
+}
+// mask word i of an entry (i < kDenseDocs / 32)
+__device__ __forceinline__ uint32_t dense_word(const DenseVal v, uint32_t i) {
+#if WSR_DENSE_FMT
+  return i == 0 ? v.x : (i == 1 ? v.y : v.z);
+#else
+  (void)i;
+  return v.y;
+#endif
+}
+// an entry whose masks are all m (and rank 0): 0 = no doc
+__device__ __forceinline__ DenseVal dense_fill(uint32_t m) {
+#if WSR_DENSE_FMT
+  return make_uint4(m, m, m, 0u);
+#else
+  return make_uint2(0u, m);
+#endif
+}
+
 // Bit of doc a in a prefetched bitmap entry; on a hit *idx = posting index.
-__device__ __forceinline__ bool dense_hit(const IndexArgs& ix, uint32_t a, const uint2 v,
+__device__ __forceinline__ bool dense_hit(const IndexArgs& ix, uint32_t a, const DenseVal v,
                                           uint32_t* idx) {
   const uint32_t rel = a - ix.doc_lo;
   if (rel >= ix.dense_span) return false;
   const uint32_t sh = rel % kDenseDocs;
-  if (!((v.y >> sh) & 1u)) return false;
-  *idx = v.x + __popc(v.y & ((1u << sh) - 1u));
+  if (!dense_bit(v, sh)) return false;
+  *idx = dense_rank(v, sh);
   return true;
 }
 
@@ -329,15 +372,15 @@ __device__ __forceinline__ uint32_t dense_tf_slow(const IndexArgs& ix, const Lis
 
 // Is doc a in B?  One 8-byte load (dense_load, issued early) and, on a hit,
 // the posting's rank gives its tf (dense_resolve).
-__device__ __forceinline__ uint2 dense_load(const IndexArgs& ix, const ListDev& B, uint32_t a,
-                                            bool act) {
+__device__ __forceinline__ DenseVal dense_load(const IndexArgs& ix, const ListDev& B, uint32_t a,
+                                               bool act) {
   const uint32_t rel = a - ix.doc_lo;
   const bool in = act && rel < ix.dense_span;
-  return reinterpret_cast<const uint2*>(ix.dense + B.bm)[in ? rel / kDenseDocs : 0u];
+  return dense_at(ix.dense + B.bm, in ? rel / kDenseDocs : 0u);
 }
 
 __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev& B, uint32_t a,
-                                              const uint2 v, uint32_t* tf, uint32_t* pidx = nullptr) {
+                                              const DenseVal v, uint32_t* tf, uint32_t* pidx = nullptr) {
   uint32_t idx;
   if (!dense_hit(ix, a, v, &idx)) return false;
   if (pidx) *pidx = idx;
@@ -1763,7 +1806,7 @@ struct LeanLdsT {
                                    // replay's segment scan
   Event evs[WSR_LEAN_EVS];   // events buffered in LDS, stored when a chunk could overflow them
                              // and at the end
-  uint32_t bx[kAnd ? 6 : 1][kAnd ? 64 : 1];   // bitmap-intersection step: per lane its word's
+  uint32_t bx[kAnd ? 1 + kDenseDocs / 32 : 1][kAnd ? 64 : 1];   // bitmap-intersection step: per lane its entry's
                         // survivors (exclusive prefix), intersected word, driver and O1 (rank, word)
   uint4 dblk[64];       // the driver's directory entries of the segment
   uint32_t dmeta[64];
@@ -1796,8 +1839,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint32_t min_last = in_vgpr(Q.min_last);
   const bool single = o1 == kNoSlot;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
-  const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
-                             : reinterpret_cast<const uint2*>(ix.dense + Q.o_bm);
+  const DenseEnt* o_bm = single ? reinterpret_cast<const DenseEnt*>(ix.blk_last) : ix.dense + Q.o_bm;
   const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
@@ -1933,7 +1975,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       } else {
         const ListDev B = ix.lists[qlist[s]];
         uint32_t t = 0, x = 0;
-        const uint2 v = dense_load(ix, B, doc, alive);
+        const DenseVal v = dense_load(ix, B, doc, alive);
         alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
         if (__ballot(alive) == 0) break;
         sc += bm25_term(B.idf, alive ? t : 0u, norm);
@@ -2019,7 +2061,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
-    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap words
+    DenseVal de0 = dense_fill(0u), de1 = dense_fill(0u);   // O1 bitmap entries
     // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
     // block, outside the image or pruned, a rank with bit 31 set is an O1 miss
     // -- so that they take no scalar lane-mask registers across the iteration)
@@ -2040,6 +2082,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   };
 #endif
   const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
+#if WSR_OOB_GATHERS && WSR_DENSE_FMT
+#error "WSR_OOB_GATHERS needs the 8-byte bitmap entries (WSR_DENSE_FMT=0)"
+#endif
 #if WSR_OOB_GATHERS
   // Buffer views of O1's bitmap and tf bytes: a lane with nothing to fetch
   // gives an offset past the view's end, so its load returns 0 without a
@@ -2124,10 +2169,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
       // (bitwise, not short-circuit: the compiler would branch on each term)
-      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & (((X.de0.y >> s0) & 1u) != 0u)));
-      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & (((X.de1.y >> s1) & 1u) != 0u)));
-      const uint32_t x0 = X.de0.x + __popc(X.de0.y & ((1u << s0) - 1u));
-      const uint32_t x1 = X.de1.x + __popc(X.de1.y & ((1u << s1) - 1u));
+      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & dense_bit(X.de0, s0)));
+      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & dense_bit(X.de1, s1)));
+      const uint32_t x0 = dense_rank(X.de0, s0);
+      const uint32_t x1 = dense_rank(X.de1, s1);
       uint32_t w;
 #ifdef WSR_DIAG_NO_TF8   // timing diagnostic only (wrong tfs): no O1 tf gathers
       Y.hf0 = 0x01010101u; Y.hf1 = 0x01010101u; (void)w;
@@ -2220,7 +2265,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #endif
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
-#if WSR_OOB_GATHERS
+#if WSR_OOB_GATHERS && !WSR_DENSE_FMT
       {
         const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in0 ? ((a0 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
         const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in1 ? ((a1 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
@@ -2230,18 +2275,18 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #elif WSR_MASKED_GATHERS
       // (only the postings that passed the bound probe: a pruned lane keeps a
       // stale word, which H never reads -- its doc is ~0u or outside the span)
-      if (in0) Y.de0 = o_bm[(a0 - lo) / kDenseDocs];
-      if (in1) Y.de1 = o_bm[(a1 - lo) / kDenseDocs];
+      if (in0) Y.de0 = dense_at(o_bm, (a0 - lo) / kDenseDocs);
+      if (in1) Y.de1 = dense_at(o_bm, (a1 - lo) / kDenseDocs);
 #elif defined(WSR_DIAG_PROBE_L2)   // timing diagnostic only (wrong hits): probes L2-resident
-      Y.de0 = o_bm[in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u];
-      Y.de1 = o_bm[in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u];
+      Y.de0 = dense_at(o_bm, in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u);
+      Y.de1 = dense_at(o_bm, in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u);
 #elif defined(WSR_DIAG_PROBE_NONE)   // timing diagnostic only (wrong results): no probes, no hits
       // (k < 2^20: a zero mask the compiler cannot fold away)
-      Y.de0 = make_uint2(0u, in0 ? (Q.k >> 20) : 0u);
-      Y.de1 = make_uint2(0u, in1 ? (Q.k >> 20) : 0u);
+      Y.de0 = dense_fill(in0 ? (Q.k >> 20) : 0u);
+      Y.de1 = dense_fill(in1 ? (Q.k >> 20) : 0u);
 #else
-      Y.de0 = o_bm[in0 ? (a0 - lo) / kDenseDocs : 0u];
-      Y.de1 = o_bm[in1 ? (a1 - lo) / kDenseDocs : 0u];
+      Y.de0 = dense_at(o_bm, in0 ? (a0 - lo) / kDenseDocs : 0u);
+      Y.de1 = dense_at(o_bm, in1 ? (a1 - lo) / kDenseDocs : 0u);
 #endif
       Y.dcc = c0 | (c1 << 8);
       Y.dt0 = t0; Y.dt1 = t1;
@@ -2298,42 +2343,59 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #endif
   };
   if (kAnd && and_path) {
-    // Bitmap intersection: the segment's doc span, 32 docs per word, one word
-    // per lane and step; the words of every list are ANDed, so a step costs a
-    // few loads per list whatever the driver's density.  Survivors are taken
-    // in rank order (= doc order) 64 at a time: lane l finds the word holding
-    // survivor c*64 + l by a search over the step's prefix counts and the bit
-    // by a popcount select, and appends it to the queue.
+    // Bitmap intersection: the segment's doc span, one bitmap entry
+    // (kDenseDocs docs) per lane and step; the entries of every list are
+    // ANDed, so a step costs a few loads per list whatever the driver's
+    // density.  Survivors are taken in rank order (= doc order) 64 at a time:
+    // lane l finds the entry holding survivor c*64 + l by a search over the
+    // step's prefix counts and the bit by a popcount select, and appends it to
+    // the queue.
+    constexpr uint32_t kDW = kDenseDocs / 32;   // mask words per entry
     const uint32_t last_doc = min(uni(S.dblk[b1 - 1 - b0].y), min_last);
     const uint32_t a_lo = first_doc > lo ? first_doc - lo : 0u;
     uint32_t a_hi = last_doc - lo;                      // inclusive, relative
     if (a_hi >= span) a_hi = span - 1;
-    const uint2* a_bm = reinterpret_cast<const uint2*>(ix.dense + Q.a_bm);
+    const DenseEnt* a_bm = ix.dense + Q.a_bm;
     const uint8_t* a_tf8 = ix.tf8 + Q.a_tf8;
     if (span && last_doc >= lo && a_lo <= a_hi) {
-      const uint32_t w0 = a_lo >> 5, w1 = a_hi >> 5;   // inclusive word range
+      const uint32_t w0 = a_lo / kDenseDocs, w1 = a_hi / kDenseDocs;   // inclusive entry range
       for (uint32_t base = w0; base <= w1; base += 64) {
         const uint32_t wi = base + l;
         const bool live = wi <= w1;
-        const uint2 va = a_bm[live ? wi : w0];
-        const uint2 vo = single ? make_uint2(0u, 0xFFFFFFFFu) : o_bm[live ? wi : w0];
-        uint32_t m = live ? (va.y & vo.y) : 0u;
-        if (wi == w0) m &= ~0u << (a_lo & 31u);
-        if (wi == w1 && (a_hi & 31u) != 31u) m &= (2u << (a_hi & 31u)) - 1u;
-        for (uint32_t s = 0; s < nt; ++s) {   // the further other lists
-          if (s == d || s == o1 || !__ballot(m)) continue;
-          const ListDev B = ix.lists[qlist[s]];
-          m &= reinterpret_cast<const uint2*>(ix.dense + B.bm)[live ? wi : w0].y;
+        const DenseVal va = dense_at(a_bm, live ? wi : w0);
+        const DenseVal vo = single ? dense_fill(~0u) : dense_at(o_bm, live ? wi : w0);
+        uint32_t m[kDW];
+#pragma unroll
+        for (uint32_t i = 0; i < kDW; ++i) {
+          uint32_t x = live ? (dense_word(va, i) & dense_word(vo, i)) : 0u;
+          const uint32_t r0 = wi * kDenseDocs + i * 32u;   // relative doc of the word's bit 0
+          if (r0 + 31u < a_lo || r0 > a_hi) x = 0u;
+          else {
+            if (r0 < a_lo) x &= ~0u << (a_lo - r0);
+            if (a_hi < r0 + 31u) x &= (2u << (a_hi - r0)) - 1u;
+          }
+          m[i] = x;
         }
-        const uint32_t c = __popc(m);
+        for (uint32_t s = 0; s < nt; ++s) {   // the further other lists
+          uint32_t any = 0;
+#pragma unroll
+          for (uint32_t i = 0; i < kDW; ++i) any |= m[i];
+          if (s == d || s == o1 || !__ballot(any)) continue;
+          const ListDev B = ix.lists[qlist[s]];
+          const DenseVal vb = dense_at(ix.dense + B.bm, live ? wi : w0);
+#pragma unroll
+          for (uint32_t i = 0; i < kDW; ++i) m[i] &= dense_word(vb, i);
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kDW; ++i) c += __popc(m[i]);
         const uint32_t inc = wave_incl_scan(c);
         const uint32_t total = uni(__builtin_amdgcn_readlane(inc, 63));
         if (total == 0) continue;
         __builtin_amdgcn_wave_barrier();
         S.bx[0][l] = inc - c;
-        S.bx[1][l] = m;
-        S.bx[2][l] = va.x; S.bx[3][l] = va.y;
-        S.bx[4][l] = vo.x; S.bx[5][l] = vo.y;
+#pragma unroll
+        for (uint32_t i = 0; i < kDW; ++i) S.bx[1 + i][l] = m[i];
         __builtin_amdgcn_wave_barrier();
         for (uint32_t c0 = 0; c0 < total; c0 += 64) {
           const uint32_t g = c0 + l;
@@ -2343,16 +2405,24 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #pragma unroll
           for (uint32_t st = 32; st; st >>= 1)
             if (S.bx[0][ow + st] <= g) ow += st;
-          uint32_t k = g - S.bx[0][ow], mw = S.bx[1][ow], bit = 0;
+          uint32_t k = g - S.bx[0][ow], wd = 0, mw = S.bx[1][ow];
+#pragma unroll
+          for (uint32_t i = 1; i < kDW; ++i) {   // the word holding the k-th set bit
+            const uint32_t pc = __popc(mw);
+            if (k >= pc) { k -= pc; wd = i; mw = S.bx[1 + i][ow]; }
+          }
+          uint32_t bit = 0;
 #pragma unroll
           for (uint32_t st = 16; st; st >>= 1) {   // k-th set bit of mw
             const uint32_t lowc = __popc(mw & ((1u << st) - 1u));
             if (k >= lowc) { k -= lowc; bit += st; mw >>= st; }
           }
-          const uint32_t below = (1u << bit) - 1u;
-          const uint32_t doc = lo + ((base + ow) << 5) + bit;
-          const uint32_t ra = S.bx[2][ow] + __popc(S.bx[3][ow] & below);
-          const uint32_t ro = S.bx[4][ow] + __popc(S.bx[5][ow] & below);
+          const uint32_t sh = wd * 32u + bit;
+          const uint32_t ent = has ? base + ow : w0;
+          const uint32_t doc = lo + (base + ow) * kDenseDocs + sh;
+          // (the entries again, from the cache: their ranks)
+          const uint32_t ra = dense_rank(dense_at(a_bm, ent), sh);
+          const uint32_t ro = single ? 0u : dense_rank(dense_at(o_bm, ent), sh);
           const uint32_t ta = load_byte(a_tf8 + (has ? ra : 0u));
           const uint32_t tb = single ? 0u : load_byte(o_tf8 + (has ? ro : 0u));
           const uint32_t cc = (has && doc < ix.n_c4) ? load_byte(ix.c4 + doc) : 0u;
@@ -2516,7 +2586,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     struct Stage {
       uint32_t a0, a1, c0, c1, ta0, ta1;
       bool al0, al1, ok0, ok1;
-      uint2 p0, p1;
+      DenseVal p0, p1;
     };
     // raw pack words of the driver block to decode next (issued a block ahead)
     uint32_t nx0 = 0, nx1 = 0;
@@ -2558,8 +2628,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       const uint32_t r0 = g.a0 - ix.doc_lo, r1 = g.a1 - ix.doc_lo;
       const bool d0 = fo_dense && g.al0 && r0 < ix.dense_span;
       const bool d1 = fo_dense && g.al1 && r1 < ix.dense_span;
-      g.p0 = reinterpret_cast<const uint2*>(f_dense)[d0 ? r0 / kDenseDocs : 0u];
-      g.p1 = reinterpret_cast<const uint2*>(f_dense)[d1 ? r1 / kDenseDocs : 0u];
+      g.p0 = dense_at(f_dense, d0 ? r0 / kDenseDocs : 0u);
+      g.p1 = dense_at(f_dense, d1 ? r1 / kDenseDocs : 0u);
     };
     auto flush_events = [&](uint32_t n) __attribute__((always_inline)) {
       __builtin_amdgcn_wave_barrier();
@@ -2627,8 +2697,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         }
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
           uint32_t t0 = 0, t1 = 0, x0 = 0, x1 = 0;
-          const uint2 v0 = dense_load(ix, B, a0, al0);
-          const uint2 v1 = dense_load(ix, B, a1, al1);
+          const DenseVal v0 = dense_load(ix, B, a0, al0);
+          const DenseVal v1 = dense_load(ix, B, a1, al1);
           const bool h0 = al0 && dense_resolve(ix, B, a0, v0, &t0, &x0);
           const bool h1 = al1 && dense_resolve(ix, B, a1, v1, &t1, &x1);
           const uint32_t blast = ix.blk_last[B.blk0 + B.nblk - 1];
@@ -3060,7 +3130,7 @@ __device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, 
       } else {
         const ListDev B = ix.lists[qlist[s]];
         uint32_t t = 0, x = 0;
-        const uint2 v = dense_load(ix, B, doc, alive);
+        const DenseVal v = dense_load(ix, B, doc, alive);
         alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
         if (__ballot(alive) == 0) break;
         sc += bm25_term(B.idf, alive ? t : 0u, norm);
