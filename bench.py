@@ -34,6 +34,7 @@ import json
 import math
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -47,6 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # workload only, with the file named in roofline.traffic_source.
 PMC_PROFILES = {"c3": "r03_pmc_segment_c3.json", "c2": "r03_pmc_segment_c2.json"}
 DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
+DEFERRED = []   # oracle work (parity checks, CPU baselines) run after every timed loop
 
 
 def cpu_share():
@@ -153,37 +155,52 @@ def c3_dir(a):
     return os.path.join(a.index_dir, f"c3_wiki_{a.c3_docs}_{a.c3_term_scale:g}")
 
 
+def in_child(code):
+    """Run `code` (Python, with `w` = wiser_amd) in a child process and return
+    the JSON it prints last.  Index builds run there: the writer's many
+    threads and gigabytes of short-lived host memory stay out of the process
+    whose HIP calls the timed loops measure (see snapshot)."""
+    prog = f"import sys, json, time\nsys.path.insert(0, {ROOT!r})\nimport wiser_amd as w\n{code}"
+    r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise SystemExit(f"child build failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def ensure_c3(a):
     """The C3 stand-in and its 100k two-term log (built once per box, ~35 s)."""
-    import wiser_amd as w
     d = c3_dir(a)
     qlog = os.path.join(d, "two_term_100000.log")
     info = None
     if not os.path.exists(os.path.join(d, "READY")):
         os.makedirs(d, exist_ok=True)
-        t = time.time()
-        st = w.build_wiki_standin(d, n_docs=a.c3_docs, term_scale=a.c3_term_scale, threads=HOST_THREADS)
-        w.gen_two_term_log(d, qlog, n_queries=100000, seed=7)
+        info = in_child(
+            f"t = time.time()\n"
+            f"st = w.build_wiki_standin({d!r}, n_docs={a.c3_docs}, term_scale={a.c3_term_scale!r}, "
+            f"threads={HOST_THREADS})\n"
+            f"w.gen_two_term_log({d!r}, {qlog!r}, n_queries=100000, seed=7)\n"
+            f"print(json.dumps({{'docs': st.n_docs, 'terms': st.n_terms, 'postings': st.n_postings, "
+            f"'vacuum_bytes': st.vacuum_bytes, 'avg_length': round(st.avg_length, 2), "
+            f"'build_s': round(time.time() - t, 1)}}))")
         open(os.path.join(d, "READY"), "w").write("ok")
-        info = {"docs": st.n_docs, "terms": st.n_terms, "postings": st.n_postings,
-                "vacuum_bytes": st.vacuum_bytes, "avg_length": round(st.avg_length, 2),
-                "build_s": round(time.time() - t, 1)}
         log(f"C3 stand-in built: {info}")
     return d, qlog, info
 
 
 def ensure_c2(a):
-    import wiser_amd as w
     idx = os.path.join(a.index_dir, f"c2_{a.docs}_{a.vocab}")
     qlog = os.path.join(idx, f"two_term_{a.queries}.log")
     if not os.path.exists(os.path.join(idx, "READY")):
         os.makedirs(idx, exist_ok=True)
-        t = time.time()
-        st = w.build_synthetic(idx, n_docs=a.docs, vocab=a.vocab, threads=HOST_THREADS)
-        w.gen_two_term_log(idx, qlog, n_queries=a.queries, seed=7)
+        st = in_child(
+            f"t = time.time()\n"
+            f"st = w.build_synthetic({idx!r}, n_docs={a.docs}, vocab={a.vocab}, threads={HOST_THREADS})\n"
+            f"w.gen_two_term_log({idx!r}, {qlog!r}, n_queries={a.queries}, seed=7)\n"
+            f"print(json.dumps({{'docs': st.n_docs, 'terms': st.n_terms, 'postings': st.n_postings, "
+            f"'gb': st.vacuum_bytes / 1e9, 's': time.time() - t}}))")
         open(os.path.join(idx, "READY"), "w").write("ok")
-        log(f"built index {st.n_docs} docs {st.n_terms} terms {st.n_postings} postings "
-            f"{st.vacuum_bytes/1e9:.2f} GB in {time.time()-t:.1f}s")
+        log(f"built index {st['docs']} docs {st['terms']} terms {st['postings']} postings "
+            f"{st['gb']:.2f} GB in {st['s']:.1f}s")
     return idx, qlog
 
 
@@ -247,15 +264,30 @@ def resolve(eng, chunk, k):
 
 
 def check_against_oracle(idx, chunk, hits, nh, k, n, phrase=False):
+    """Compare the first n queries' results with the oracle now."""
+    return verify_snapshot(snapshot(idx, chunk, hits, nh, k, n, phrase))
+
+
+def snapshot(idx, chunk, hits, nh, k, n, phrase=False):
+    """The first n queries' GPU results, copied, for a check against the
+    oracle later (verify_snapshot).  The oracle runs in this process and holds
+    the whole dictionary in a map: loaded before a timed loop it has slowed the
+    host's HIP calls of that loop by up to 8x (profiles/r03_steprate.txt), so
+    every bench check runs after all timed loops, on results of the last run."""
+    got = [[(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])]
+           for i in range(min(n, len(chunk)))]
+    return {"idx": idx, "chunk": [list(t) for t in chunk[:n]], "got": got, "k": k, "phrase": phrase}
+
+
+def verify_snapshot(snap):
     from oracle.oracle import OracleVacuum
-    orc = OracleVacuum(idx)
-    for i, terms in enumerate(chunk[:n]):
-        want, _ = orc.search(terms, k, phrase=phrase)
-        got = [(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])]
+    orc = OracleVacuum(snap["idx"])
+    for terms, got in zip(snap["chunk"], snap["got"]):
+        want, _ = orc.search(terms, snap["k"], phrase=snap["phrase"])
         if got != want:
             raise SystemExit(f"parity failure on {terms}: {got[:3]} vs {want[:3]}")
     orc.close()
-    return min(n, len(chunk))
+    return len(snap["got"])
 
 
 def cpu_rate(idx, lines, k, seconds, threads, phrases=None):
@@ -346,12 +378,6 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
         b.upload(arr)
         batches.append(b)
         chunks.append(chunk)
-    checked = 0
-    if check:
-        batches[0].run()
-        hits, nh = batches[0].fetch()
-        ph = bool(chunks[0][0][1])
-        checked = check_against_oracle(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=ph)
     for b in batches:
         b.run()
     w.sync(eng)
@@ -373,8 +399,11 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
     el = time.perf_counter() - t0
     seg = [b.stats() for b in batches]   # each batch's last run: inside the timed loop
     timed_seg = sum(st.segment_ms for st in seg) / len(seg)
-    for b in batches:   # device error flags of every batch's last run (fetch raises)
-        b.fetch()
+    for b in batches[::-1]:   # device error flags of every batch's last run (fetch raises)
+        hits, nh = b.fetch()
+    snaps = []
+    if check:   # batch 0's last timed run, checked after every timed loop (snapshot)
+        snaps.append(snapshot(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=bool(chunks[0][0][1])))
     nq = len(items) * passes
     for b in batches:
         b.close()
@@ -386,14 +415,18 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
            "survivors_per_batch": int(acc["surv"] / nbk),
            "driver_blocks_per_batch": int(acc["dblk"] / nbk),
            "roofline": roofline_of(acc, nbk, timed_seg, "timed region"),
-           "parity_checked_queries": checked}
-    if cpu_seconds:
-        lines = [t for t, _ in items]
-        phr = [p for _, p in items]
-        d, c = cpu_rate(idx, lines, k, cpu_seconds, HOST_THREADS, phrases=phr)
-        out["cpu_baseline"] = {"value": round(d / c, 1), "cores": HOST_THREADS, "kind": "port",
-                               "sample": f"{d} queries of the leg's log (cycled), {HOST_THREADS} "
-                                         f"persistent workers, {c:.1f}s"}
+           "parity_checked_queries": 0}
+
+    def deferred():   # oracle work, after every timed loop of the run (see snapshot)
+        out["parity_checked_queries"] = sum(verify_snapshot(sn) for sn in snaps)
+        if cpu_seconds:
+            lines = [t for t, _ in items]
+            phr = [p for _, p in items]
+            d, c = cpu_rate(idx, lines, k, cpu_seconds, HOST_THREADS, phrases=phr)
+            out["cpu_baseline"] = {"value": round(d / c, 1), "cores": HOST_THREADS, "kind": "port",
+                                   "sample": f"{d} queries of the leg's log (cycled), {HOST_THREADS} "
+                                             f"persistent workers, {c:.1f}s"}
+    DEFERRED.append(deferred)
     return out
 
 
@@ -515,7 +548,7 @@ def extra_legs(a, idx, qlog, local, threads):
     if want("c4_mixed_1to5"):
         mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
         if not os.path.exists(mixed):
-            w.gen_mixed_log(idx, mixed, n_queries=20000, seed=7)
+            in_child(f"w.gen_mixed_log({idx!r}, {mixed!r}, n_queries=20000, seed=7)\nprint('{{}}')")
         eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
         eng.Load()
         items = [(l.split(), False) for l in open(mixed).read().splitlines()]
@@ -531,7 +564,7 @@ def extra_legs(a, idx, qlog, local, threads):
         ptag = os.path.basename(pidx.rstrip("/"))
         phr = os.path.join(a.index_dir, f"phrase_{ptag}_10000.log")
         if not os.path.exists(phr):
-            w.gen_phrase_log(pidx, phr, n_queries=10000, seed=7)
+            in_child(f"w.gen_phrase_log({pidx!r}, {phr!r}, n_queries=10000, seed=7)\nprint('{{}}')")
         t = time.time()
         eng = w.VacuumEngine(pidx, device=local, threads=threads, positions=True)
         eng.Load()
@@ -615,18 +648,12 @@ def snippet_leg(a, local, threads):
     # Python mirror, for parity: SearchBatch with return_snippets
     res = eng.SearchBatch([w.SearchQuery([t], n_results=a.k, return_snippets=True)
                            for t in terms[: a.check]])
-    orc = OracleVacuum(d)
-    bad = 0
-    for t, r in zip(terms[: a.check], res):
-        want = orc.search_snippets([t], a.k)
-        bad += [(e.doc_id, e.doc_score, e.snippet) for e in r.entries] != want
-    if bad:
-        raise SystemExit(f"c1 snippet leg: {bad} queries differ from the oracle")
+    got = [[(e.doc_id, e.doc_score, e.snippet) for e in r.entries] for r in res]
     out = {"value": round(len(terms) / el, 1), "unit": "queries/s", "queries": len(terms),
            "snippets": n_snip, "snippets_per_s": round(n_snip / t_snip, 1), "snippet_threads": HOST_THREADS,
            "topk_ms_per_batch": round(1e3 * t_topk / len(batches), 3),
            "snippet_ms_per_batch": round(1e3 * t_snip / len(batches), 3),
-           "parity_checked_queries": min(a.check, len(terms)),
+           "parity_checked_queries": 0,
            "workload": ("C1: the reference's 10k-doc TOKEN_ONLY linedoc, single-term top-10 over every "
                         f"distinct token ({len(distinct)}) + 10000 sampled (seed 1), return_snippets, "
                         "3 passages; per batch of 4096: GPU top-k (wsr_search_batch, host arrays in and "
@@ -636,28 +663,38 @@ def snippet_leg(a, local, threads):
     t_topk_only, _, _ = run(False)
     out["topk_only"] = {"value": round(len(terms) / t_topk_only, 1), "unit": "queries/s",
                         "note": "wsr_search_batch per 4096 (host arrays in and out), no snippets"}
-    if not a.no_cpu:
-        t0, n, i = time.time(), 0, 0
-        while time.time() - t0 < 2.0:
-            orc.search_snippets([terms[i % len(terms)]], a.k)
-            n += 1
-            i += 1
-        out["cpu_baseline"] = {"value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
-                               "sample": f"{n} queries of the leg's list, oracle Search + GenerateSnippet, 2s"}
-        from oracle.oracle import OracleQqMem
-        qq = OracleQqMem(src, "TOKEN_ONLY")
-        t0, n, i = time.time(), 0, 0
-        while time.time() - t0 < 2.0:
-            qq.search([terms[i % len(terms)]], a.k)
-            n += 1
-            i += 1
-        out["topk_only"]["cpu_baseline"] = {
-            "value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
-            "sample": f"{n} single-term top-{a.k} queries of the leg's list through the oracle's "
-                      "QqMemEngineDelta (varint PostingListDelta, skip span 100), 2s"}
-        qq.close()
-    orc.close()
     eng.close()
+
+    def deferred():   # oracle work, after every timed loop of the run (see snapshot)
+        orc = OracleVacuum(d)
+        bad = 0
+        for t, g in zip(terms[: a.check], got):
+            bad += g != orc.search_snippets([t], a.k)
+        if bad:
+            raise SystemExit(f"c1 snippet leg: {bad} queries differ from the oracle")
+        out["parity_checked_queries"] = len(got)
+        if not a.no_cpu:
+            t0, n, i = time.time(), 0, 0
+            while time.time() - t0 < 2.0:
+                orc.search_snippets([terms[i % len(terms)]], a.k)
+                n += 1
+                i += 1
+            out["cpu_baseline"] = {"value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
+                                   "sample": f"{n} queries of the leg's list, oracle Search + GenerateSnippet, 2s"}
+            from oracle.oracle import OracleQqMem
+            qq = OracleQqMem(src, "TOKEN_ONLY")
+            t0, n, i = time.time(), 0, 0
+            while time.time() - t0 < 2.0:
+                qq.search([terms[i % len(terms)]], a.k)
+                n += 1
+                i += 1
+            out["topk_only"]["cpu_baseline"] = {
+                "value": round(n / (time.time() - t0), 1), "cores": 1, "kind": "port",
+                "sample": f"{n} single-term top-{a.k} queries of the leg's list through the oracle's "
+                          "QqMemEngineDelta (varint PostingListDelta, skip span 100), 2s"}
+            qq.close()
+        orc.close()
+    DEFERRED.append(deferred)
     return out
 
 
@@ -877,15 +914,6 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
         if full:
             w.sync(full)
 
-    checked = 0
-    if a.check:   # every rank takes part in the collectives; rank 0 checks
-        (hres, cres) = step(0, fetch=True)
-        if rank == 0:
-            hb, hq, hchunk, cb, cheap = steps[0]
-            if hres:
-                checked += check_against_oracle(S.engine.engine_dir_path, hchunk[:hq], hres[0], hres[1], a.k, a.check)
-            if cres:
-                checked += check_against_oracle(S.engine.engine_dir_path, cheap, cres[0], cres[1], a.k, a.check)
     for s_ in range(a.warmup):
         step(s_)
     sync_all()
@@ -903,11 +931,15 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     sync_all()
     el = time.perf_counter() - t0
-    for hb, hq, _, cb, _ in steps:   # error flags (a slot overflow among them) of every last step
-        if hb:
-            S.fetch_owned(hb, hq)
-        if cb:
-            cb.fetch()
+    snaps = []
+    for i, (hb, hq, hchunk, cb, cheap) in enumerate(steps):   # error flags (a slot overflow among
+        hres = S.fetch_owned(hb, hq) if hb else None         # them) of every last step
+        cres = cb.fetch() if cb else None
+        if i == 0 and a.check and rank == 0:   # step 0's last timed run, checked after the timed loops
+            if hres:
+                snaps.append(snapshot(S.engine.engine_dir_path, hchunk[:hq], hres[0], hres[1], a.k, a.check))
+            if cres:
+                snaps.append(snapshot(S.engine.engine_dir_path, cheap, cres[0], cres[1], a.k, a.check))
     # every rank completes its own 4096 queries per step (heavy owned + cheap)
     queries = sum(len(steps[s_ % nb][4]) + sum(1 for q in steps[s_ % nb][2][rank * steps[s_ % nb][1]:
                                                                           (rank + 1) * steps[s_ % nb][1]] if q)
@@ -919,7 +951,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
             for x in (hb, cb):
                 if x:
                     x.close()
-    return {"queries": queries, "el": el, "p50": statistics.median(lat), "checked": checked,
+    return {"queries": queries, "el": el, "p50": statistics.median(lat), "snaps": snaps,
             "slot": slot, "heavy_share": share, "heavy_blocks": heavy_blocks, "every": every,
             "host_ms": host_ms,
             "batches": [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]],
@@ -940,11 +972,6 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
         batches.append(b)
         chunks.append(chunk)
     nb = len(batches)
-    checked = 0
-    if a.check and rank == 0:
-        batches[0].run()
-        hits, nh = batches[0].fetch()
-        checked = check_against_oracle(idx, chunks[0], hits, nh, a.k, a.check)
     for s in range(a.warmup):
         batches[s % nb].run()
     w.sync(eng)
@@ -969,14 +996,17 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
     timed_launch_stats(batches, a.steps)
     # every batch's last run: the device error flags (capacity, limits) must be
     # clear, or the pass does not count (fetch raises on any flag)
-    for b in batches:
-        b.fetch()
+    for b in batches[::-1]:
+        hits, nh = b.fetch()
+    snaps = []
+    if a.check and rank == 0:   # batch 0's last timed run, checked after every timed loop
+        snaps.append(snapshot(idx, chunks[0], hits, nh, a.k, a.check))
     queries = sum(batches[s % nb].nq for s in range(a.steps))
 
     def close():
         for b in batches:
             b.close()
-    return {"queries": queries, "el": el, "p50": statistics.median(lat), "checked": checked,
+    return {"queries": queries, "el": el, "p50": statistics.median(lat), "snaps": snaps,
             "host_ms": host_ms, "batches": batches, "engine": eng, "close": close}
 
 
@@ -1083,7 +1113,7 @@ def main():
     seg_src = "timed region" if "timed_seg_ms" in DIAG else "one batch at a time"
     lean_avg_ms = DIAG.get("timed_lean_ms", acc["lean"] / nbk)
     mres = reduced(main_run)
-    checked = main_run["checked"]
+    snaps = main_run["snaps"]
     host_ms = main_run["host_ms"]
     main_run["close"]()
     if world > 1 and a.mode == "auto":
@@ -1107,12 +1137,17 @@ def main():
     if full is not None:
         full.close()
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds, "the headline workload's log")
     extra = None
     if rank == 0 and world == 1 and not a.no_extra:
         extra = extra_legs(a, idx, qlog, local, threads)
+    # oracle work only now, after every timed loop (see snapshot): parity of the
+    # headline's and every leg's last timed run, then the CPU baselines
+    checked = sum(verify_snapshot(sn) for sn in snaps)
+    for fn in DEFERRED:
+        fn()
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds, "the headline workload's log")
 
     if rank == 0:
         roof = roofline_of(acc, nbk, seg_avg_ms, seg_src)

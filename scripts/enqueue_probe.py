@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--window", type=int, default=100)
     ap.add_argument("--sync-windows", action="store_true")
+    ap.add_argument("--oracle-check", type=int, default=0, help="check this many queries of batch 0 "
+                    "against the oracle first, as bench.py does")
+    ap.add_argument("--warmup", type=int, default=0)
     args = ap.parse_args()
     import torch  # noqa: F401  (the bench's import order)
     import bench
@@ -55,6 +58,13 @@ def main():
         b = w.ResidentBatch(eng, a.batch, a.k)
         b.upload(bench.resolve(eng, lines[s:s + a.batch], a.k))
         batches.append(b)
+    if args.oracle_check:
+        batches[0].run()
+        hits, nh = batches[0].fetch()
+        bench.check_against_oracle(idx, lines[:a.batch], hits, nh, a.k, args.oracle_check)
+    for s in range(args.warmup):
+        batches[s % len(batches)].run()
+    w.sync(eng)
     for b in batches:
         b.run()
         b.fetch()
