@@ -100,6 +100,7 @@ struct wsr_handle {
   uint8_t* d_c4 = nullptr;
   double* d_cache = nullptr;
   DenseEnt* d_dense = nullptr;
+  uint32_t* d_dense_rk = nullptr;   // WSR_DENSE_FMT 2: the bitmap entries' ranks
   uint8_t* d_tf8 = nullptr;
   uint8_t* d_wmax = nullptr;
   uint8_t* d_plen = nullptr;
@@ -267,12 +268,14 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
       std::vector<uint32_t>().swap(img.pos_start);
     }
     h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
+    h->info.dense_bytes += dev_upload(&h->d_dense_rk, img.dense_rank);
     h->info.dense_bytes += dev_upload(&h->d_wmax, img.wmax);   // (the window maxima with the bitmaps)
     h->info.tf8_bytes = dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
     h->info.dense_lists = img.dense_lists;
     h->info.n_lists = static_cast<uint32_t>(img.lists.size());
     h->args.dense = h->d_dense;
+    h->args.dense_rk = h->d_dense_rk;
     h->args.tf8 = h->d_tf8;
     h->args.wmax = h->d_wmax;
     h->args.dense_span = img.dense_span;
@@ -345,7 +348,8 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_blocks), static_cast<void*>(h->d_last),
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
-                  static_cast<void*>(h->d_dense), static_cast<void*>(h->d_tf8),
+                  static_cast<void*>(h->d_dense), static_cast<void*>(h->d_dense_rk),
+                  static_cast<void*>(h->d_tf8),
                   static_cast<void*>(h->d_wmax),
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),

@@ -41,49 +41,43 @@ constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 // image's blocks) before the entry's first doc; posting index = rank +
 // popcount of the lower bits; block = index / 128.
 //
-// WSR_DENSE_FMT 1 (the default): 96 docs per 16-byte entry, three 32-bit masks
-// and the rank (1.33 bits per doc: one 128-byte line covers 768 docs).  At the
-// en-Wikipedia shape a high-df driver's postings are ~180 docs apart, so nearly
-// every probe of the 8-byte form (0: 32 docs, 2 bits per doc, 512 docs per line)
-// fetched a line of its own from HBM, and those line fetches bound the lean
-// kernel (profiles/r03_probe_sweep.jsonl: ~12 CU-cycles per HBM line).
+// WSR_DENSE_FMT 2 (the default): the masks and the ranks in two arrays (4
+// bytes per 32 docs each, DenseEnt = the mask word, HostImage::dense_rank the
+// ranks).  The lean kernel's probe of the most selective other list reads the
+// mask word alone (a 128-byte line covers 1,024 docs) and only a hit reads its
+// rank; at the en-Wikipedia shape a high-df driver's postings are ~180 docs
+// apart, so with the ranks beside the masks (WSR_DENSE_FMT 0: 8 bytes per 32
+// docs, 512 docs per line) nearly every probe fetched a line of its own from
+// HBM, and those line fetches bound the lean kernel (profiles/r03_probe_sweep.jsonl:
+// ~12 CU-cycles per HBM line; r03_probe_forms.txt).  Other users (further
+// lists, the general kernel) load both words at once: one probe = two
+// independent loads.
 #ifndef WSR_DENSE_FMT
-#define WSR_DENSE_FMT 1
+#define WSR_DENSE_FMT 2
 #endif
-#if WSR_DENSE_FMT
-constexpr uint32_t kDenseDocs = 96;   // doc ids per DenseEnt
-struct DenseEnt {
-  uint32_t w[3];     // bit (d - doc_lo) % 96 of doc d: word (.. / 32), bit (.. % 32)
-  uint32_t rank;
-};
-static_assert(sizeof(DenseEnt) == 16, "DenseEnt layout");
-#else
 constexpr uint32_t kDenseDocs = 32;   // doc ids per DenseEnt
+#if WSR_DENSE_FMT == 2
+struct DenseEnt {
+  uint32_t w;        // bit (d - doc_lo) % 32 of doc d; its rank: HostImage::dense_rank, same index
+};
+static_assert(sizeof(DenseEnt) == 4, "DenseEnt layout");
+#elif WSR_DENSE_FMT == 0
 struct DenseEnt {
   uint32_t rank;
   uint32_t w;        // bit (d - doc_lo) % 32 of doc d
 };
 static_assert(sizeof(DenseEnt) == 8, "DenseEnt layout");
+#else
+#error "WSR_DENSE_FMT is 0 or 2"
 #endif
+constexpr uint64_t kDenseEntBytes = WSR_DENSE_FMT == 2 ? 8 : sizeof(DenseEnt);   // mask + rank
 constexpr uint32_t kWinEnts = 64;     // DenseEnts per tf-maximum window; every list's bitmap
                                       // starts at a multiple of it
 
 // Host form of an entry's bit test and rank (the kernels have their own).
-inline bool dense_ent_bit(const DenseEnt& e, uint32_t sh) {
-#if WSR_DENSE_FMT
-  return (e.w[sh >> 5] >> (sh & 31u)) & 1u;
-#else
-  return (e.w >> sh) & 1u;
-#endif
-}
-inline uint32_t dense_ent_rank(const DenseEnt& e, uint32_t sh) {   // postings before bit sh
-#if WSR_DENSE_FMT
-  uint32_t r = e.rank;
-  for (uint32_t i = 0; i < (sh >> 5); ++i) r += static_cast<uint32_t>(__builtin_popcount(e.w[i]));
-  return r + static_cast<uint32_t>(__builtin_popcount(e.w[sh >> 5] & ((1u << (sh & 31u)) - 1u)));
-#else
-  return e.rank + static_cast<uint32_t>(__builtin_popcount(e.w & ((1u << sh) - 1u)));
-#endif
+inline bool dense_ent_bit(const DenseEnt& e, uint32_t sh) { return (e.w >> sh) & 1u; }
+inline uint32_t dense_ent_rank(const DenseEnt& e, uint32_t rank, uint32_t sh) {   // postings before bit sh
+  return rank + static_cast<uint32_t>(__builtin_popcount(e.w & ((1u << sh) - 1u)));
 }
 
 // One 128-posting block (= one skip-list row, flash_containers.h:312-350).

@@ -466,7 +466,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     });
     uint64_t used = 0;
     for (const auto& c : cand) {
-      const uint64_t bytes = n_ent * sizeof(DenseEnt) + c.first;
+      const uint64_t bytes = n_ent * kDenseEntBytes + c.first;
       if (used + bytes > dense_budget) info[c.second].dense = 0;
       else used += bytes;
     }
@@ -519,6 +519,9 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.plen.resize(nb * kPackSize);
   img.tails.resize(ntail);
   img.dense.resize(ne);
+#if WSR_DENSE_FMT == 2
+  img.dense_rank.resize(ne);
+#endif
   img.tf8.resize(ntf8);
   img.wmax.resize(ne / kWinEnts);
 
@@ -619,15 +622,13 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         const uint64_t start = doc_lo + e * kDenseDocs;
         while (i < n_img && s.docs[i] < start) ++i;
         DenseEnt ent{};
-        ent.rank = static_cast<uint32_t>(i);
-        for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j) {
-          const uint32_t sh = static_cast<uint32_t>(s.docs[j] - start);
-#if WSR_DENSE_FMT
-          ent.w[sh >> 5] |= 1u << (sh & 31u);
+#if WSR_DENSE_FMT == 2
+        img.dense_rank[ld.bm + e] = static_cast<uint32_t>(i);
 #else
-          ent.w |= 1u << sh;
+        ent.rank = static_cast<uint32_t>(i);
 #endif
-        }
+        for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j)
+          ent.w |= 1u << static_cast<uint32_t>(s.docs[j] - start);
         de[e] = ent;
       }
       uint8_t* t8 = &img.tf8[ld.tf8];
@@ -777,7 +778,11 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
   const uint32_t sh = rel % kDenseDocs;
   if (!dense_ent_bit(e, sh)) return -1;
-  const uint32_t idx = dense_ent_rank(e, sh);
+#if WSR_DENSE_FMT == 2
+  const uint32_t idx = dense_ent_rank(e, img.dense_rank[L.bm + rel / kDenseDocs], sh);
+#else
+  const uint32_t idx = dense_ent_rank(e, e.rank, sh);
+#endif
   const uint8_t t = img.tf8[L.tf8 + idx];
   if (t != kTf8Escape) return t;
   const uint32_t j = idx / kPackSize;

@@ -125,6 +125,7 @@ struct HostImage {
   uint32_t doc_lo = 0, doc_hi = 0;
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
   big_vector<DenseEnt> dense;   // rank bitmaps of the dense lists
+  big_vector<uint32_t> dense_rank;   // WSR_DENSE_FMT 2: the rank of each DenseEnt, same index
   big_vector<uint8_t> tf8;      // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
   big_vector<uint8_t> wmax;     // per dense list and 2,048-doc window (64 bitmap entries): its
                                 // largest tf, 255 = 255 or more (entry ListDev::bm / 64 + window)

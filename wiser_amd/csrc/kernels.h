@@ -23,6 +23,7 @@ struct IndexArgs {
   uint32_t doc_lo, doc_hi;  // doc-id range of this image (shard)
   double avg;               // average doc length stored in my.doc_length
   const DenseEnt* dense;    // rank bitmaps of the dense lists (ListDev::bm)
+  const uint32_t* dense_rk; // WSR_DENSE_FMT 2: their ranks (same index), else null
   const uint8_t* tf8;       // their 1-byte tfs (ListDev::tf8)
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)

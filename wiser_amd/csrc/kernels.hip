@@ -295,48 +295,24 @@ __device__ __forceinline__ bool use_dense(const IndexArgs& ix, bool has_bm, uint
   return has_bm && static_cast<float>(nblk_b) >= ix.dense_ratio * static_cast<float>(nblk_driver);
 }
 
-// A bitmap entry as loaded (one load per probe) and its bit test and rank
-// (engine_types.h, WSR_DENSE_FMT).
-#if WSR_DENSE_FMT
-using DenseVal = uint4;   // masks x, y, z (96 docs), rank w
-__device__ __forceinline__ bool dense_bit(const DenseVal v, uint32_t sh) {
-  const uint32_t wd = sh >> 5;
-  const uint32_t m = wd == 0 ? v.x : (wd == 1 ? v.y : v.z);
-  return (m >> (sh & 31u)) & 1u;
-}
-__device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
-  const uint32_t wd = sh >> 5, below = (1u << (sh & 31u)) - 1u;
-  const uint32_t m0 = wd == 0 ? below : ~0u, m1 = wd == 0 ? 0u : (wd == 1 ? below : ~0u);
-  const uint32_t m2 = wd == 2 ? below : 0u;
-  return v.w + __popc(v.x & m0) + __popc(v.y & m1) + __popc(v.z & m2);
-}
-#else
-using DenseVal = uint2;   // rank x, mask y (32 docs)
+// A bitmap entry as loaded for a probe: x = rank, y = mask word (WSR_DENSE_FMT
+// 2: two independent loads, one from each array; 0: one 8-byte load).
+using DenseVal = uint2;
 __device__ __forceinline__ bool dense_bit(const DenseVal v, uint32_t sh) { return (v.y >> sh) & 1u; }
 __device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
   return v.x + __popc(v.y & ((1u << sh) - 1u));
 }
-#endif
-__device__ __forceinline__ DenseVal dense_at(const DenseEnt* base, uint32_t e) {
-  return reinterpret_cast<const DenseVal*>(base)[e];
-}
-// mask word i of an entry (i < kDenseDocs / 32)
-__device__ __forceinline__ uint32_t dense_word(const DenseVal v, uint32_t i) {
-#if WSR_DENSE_FMT
-  return i == 0 ? v.x : (i == 1 ? v.y : v.z);
+// entry e of the bitmap that starts at entry bm (ListDev::bm)
+__device__ __forceinline__ DenseVal dense_at(const IndexArgs& ix, uint64_t bm, uint32_t e) {
+#if WSR_DENSE_FMT == 2
+  return make_uint2(ix.dense_rk[bm + e], ix.dense[bm + e].w);
 #else
-  (void)i;
-  return v.y;
+  return reinterpret_cast<const uint2*>(ix.dense + bm)[e];
 #endif
 }
-// an entry whose masks are all m (and rank 0): 0 = no doc
-__device__ __forceinline__ DenseVal dense_fill(uint32_t m) {
-#if WSR_DENSE_FMT
-  return make_uint4(m, m, m, 0u);
-#else
-  return make_uint2(0u, m);
-#endif
-}
+__device__ __forceinline__ uint32_t dense_word(const DenseVal v, uint32_t) { return v.y; }
+// an entry whose mask is m (and rank 0): 0 = no doc
+__device__ __forceinline__ DenseVal dense_fill(uint32_t m) { return make_uint2(0u, m); }
 
 // Bit of doc a in a prefetched bitmap entry; on a hit *idx = posting index.
 __device__ __forceinline__ bool dense_hit(const IndexArgs& ix, uint32_t a, const DenseVal v,
@@ -376,7 +352,7 @@ __device__ __forceinline__ DenseVal dense_load(const IndexArgs& ix, const ListDe
                                                bool act) {
   const uint32_t rel = a - ix.doc_lo;
   const bool in = act && rel < ix.dense_span;
-  return dense_at(ix.dense + B.bm, in ? rel / kDenseDocs : 0u);
+  return dense_at(ix, B.bm, in ? rel / kDenseDocs : 0u);
 }
 
 __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev& B, uint32_t a,
@@ -1839,7 +1815,28 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const uint32_t min_last = in_vgpr(Q.min_last);
   const bool single = o1 == kNoSlot;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
-  const DenseEnt* o_bm = single ? reinterpret_cast<const DenseEnt*>(ix.blk_last) : ix.dense + Q.o_bm;
+  // O1's bitmap (single term: reads go to a valid dummy word)
+#if WSR_DENSE_FMT == 2
+  // the probe reads the mask word alone; a hit reads its rank (H stage)
+  const uint32_t* o_mk = single ? ix.blk_last : &ix.dense[Q.o_bm].w;
+  const uint32_t* o_rk = single ? ix.blk_last : ix.dense_rk + Q.o_bm;
+  auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_mk[e]; };
+  auto probe_fill = [&](uint32_t m) __attribute__((always_inline)) { return m; };
+  (void)probe_fill;   // (the WSR_DIAG_PROBE_NONE diagnostic)
+  auto probe_bit = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) { return ((v >> sh) & 1u) != 0u; };
+  // posting rank of a hit, without the rank word (added at compaction)
+  auto probe_rank = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) {
+    return static_cast<uint32_t>(__popc(v & ((1u << sh) - 1u)));
+  };
+#else
+  const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
+                             : reinterpret_cast<const uint2*>(ix.dense + Q.o_bm);
+  auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_bm[e]; };
+  auto probe_fill = [&](uint32_t m) __attribute__((always_inline)) { return dense_fill(m); };
+  (void)probe_fill;
+  auto probe_bit = [&](uint2 v, uint32_t sh) __attribute__((always_inline)) { return dense_bit(v, sh); };
+  auto probe_rank = [&](uint2 v, uint32_t sh) __attribute__((always_inline)) { return dense_rank(v, sh); };
+#endif
   const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
@@ -1950,10 +1947,22 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     const uint32_t pd = kPh ? qpd[e] : 0u, po = kPh ? qpo[e] : 0u;
     __builtin_amdgcn_wave_barrier();
     qhead += n;
+#if WSR_DENSE_FMT == 2
+    if (!single) {   // O1's tf bytes of the chunk, by rank (bit 31 set: a rank)
+      const bool rk = alive && (to & 0x80000000u);
+      uint32_t t = load_byte(o_tf8 + (rk ? (to & 0x7FFFFFFFu) : 0u));
+      if (__ballot(rk && t == kTf8Escape)) {
+        const ListDev O = ix.lists[Q.o_list];
+        if (rk && t == kTf8Escape) t = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
+      }
+      if (rk) to = t;
+    }
+#else
     if (__ballot(alive && (to & 0x80000000u))) {
       const ListDev O = ix.lists[Q.o_list];
       if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
     }
+#endif
     if (and_path && __ballot(alive && (td & 0x80000000u))) {   // (bitmap path: driver tf >= 255)
       const ListDev A = ix.lists[qlist[d]];
       if (alive && (td & 0x80000000u)) td = dense_tf_slow(ix, A, td & 0x7FFFFFFFu);
@@ -2061,13 +2070,17 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
-    DenseVal de0 = dense_fill(0u), de1 = dense_fill(0u);   // O1 bitmap entries
+#if WSR_DENSE_FMT == 2
+    uint32_t de0 = 0, de1 = 0;                     // O1 bitmap mask words
+#else
+    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap entries
+#endif
     // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
     // block, outside the image or pruned, a rank with bit 31 set is an O1 miss
     // -- so that they take no scalar lane-mask registers across the iteration)
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
-    uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (in flight)
+    uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (fmt 2: rank words; in flight)
     uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit)
 
   };
@@ -2082,8 +2095,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   };
 #endif
   const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
-#if WSR_OOB_GATHERS && WSR_DENSE_FMT
-#error "WSR_OOB_GATHERS needs the 8-byte bitmap entries (WSR_DENSE_FMT=0)"
+#if WSR_DENSE_FMT == 2
+  (void)tf8_mis;
+#endif
+#if (WSR_OOB_GATHERS || WSR_MASKED_GATHERS || WSR_WIN_BOUND) && WSR_DENSE_FMT == 2
+#error "WSR_OOB_GATHERS / WSR_MASKED_GATHERS / WSR_WIN_BOUND need the 8-byte bitmap entries (WSR_DENSE_FMT=0)"
 #endif
 #if WSR_OOB_GATHERS
   // Buffer views of O1's bitmap and tf bytes: a lane with nothing to fetch
@@ -2135,11 +2151,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   auto stage_C = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // C(j-2): compaction of block j-2 (its H fields are in X)
     if (j >= b0 + 2) {
+#if WSR_DENSE_FMT == 2
+      // O1 posting ranks (hits): rank word + bits below; the tf byte is read by
+      // rank when the chunk is scored (flag bit 31)
+      const uint32_t rk0 = X.hf0 + X.hx0, rk1 = X.hf1 + X.hx1;
+      const uint32_t to0 = 0x80000000u | rk0, to1 = 0x80000000u | rk1;
+#else
       const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
       const uint32_t f0 = single ? 0u : (X.hf0 >> xs0) & 0xFFu;
       const uint32_t f1 = single ? 0u : (X.hf1 >> xs1) & 0xFFu;
       const uint32_t to0 = f0 == kTf8Escape ? (0x80000000u | X.hx0) : f0;
       const uint32_t to1 = f1 == kTf8Escape ? (0x80000000u | X.hx1) : f1;
+      const uint32_t rk0 = X.hx0, rk1 = X.hx1;
+#endif
       const bool hh0 = !(X.hx0 >> 31), hh1 = !(X.hx1 >> 31);
       const uint64_t m0 = __ballot(hh0), m1 = __ballot(hh1);
       const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
@@ -2152,8 +2176,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       qdoc[e1] = X.ha1; qc4[e1] = X.hc1; qtd[e1] = X.ht1; qto[e1] = to1;
       if (kPh) {   // block j-2's postings 2l, 2l+1 and their O1 ranks
         const uint32_t pd0 = (Q.a_blk0 + j - 2) * 128u + 2 * l;
-        qpd[e0] = pd0; qpo[e0] = X.hx0;
-        qpd[e1] = pd0 + 1; qpo[e1] = X.hx1;
+        qpd[e0] = pd0; qpo[e0] = rk0;
+        qpd[e1] = pd0 + 1; qpo[e1] = rk1;
       }
       qtail += __popcll(m0) + __popcll(m1);
       // (at most two full chunks: fewer than 64 + 128 entries are queued;
@@ -2169,12 +2193,17 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
       // (bitwise, not short-circuit: the compiler would branch on each term)
-      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & dense_bit(X.de0, s0)));
-      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & dense_bit(X.de1, s1)));
-      const uint32_t x0 = dense_rank(X.de0, s0);
-      const uint32_t x1 = dense_rank(X.de1, s1);
+      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & probe_bit(X.de0, s0)));
+      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & probe_bit(X.de1, s1)));
+      const uint32_t x0 = probe_rank(X.de0, s0);
+      const uint32_t x1 = probe_rank(X.de1, s1);
       uint32_t w;
-#ifdef WSR_DIAG_NO_TF8   // timing diagnostic only (wrong tfs): no O1 tf gathers
+#if WSR_DENSE_FMT == 2
+      // the hits' rank words (O1's tf bytes are read by rank when the chunk is scored)
+      (void)w;
+      Y.hf0 = o_rk[(h0 && !single) ? q0 / kDenseDocs : 0u];
+      Y.hf1 = o_rk[(h1 && !single) ? q1 / kDenseDocs : 0u];
+#elif defined(WSR_DIAG_NO_TF8)   // timing diagnostic only (wrong tfs): no O1 tf gathers
       Y.hf0 = 0x01010101u; Y.hf1 = 0x01010101u; (void)w;
 #else
 #if WSR_OOB_GATHERS
@@ -2265,7 +2294,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #endif
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
-#if WSR_OOB_GATHERS && !WSR_DENSE_FMT
+#if WSR_OOB_GATHERS
       {
         const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in0 ? ((a0 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
         const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in1 ? ((a1 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
@@ -2275,18 +2304,18 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #elif WSR_MASKED_GATHERS
       // (only the postings that passed the bound probe: a pruned lane keeps a
       // stale word, which H never reads -- its doc is ~0u or outside the span)
-      if (in0) Y.de0 = dense_at(o_bm, (a0 - lo) / kDenseDocs);
-      if (in1) Y.de1 = dense_at(o_bm, (a1 - lo) / kDenseDocs);
+      if (in0) Y.de0 = o_probe((a0 - lo) / kDenseDocs);
+      if (in1) Y.de1 = o_probe((a1 - lo) / kDenseDocs);
 #elif defined(WSR_DIAG_PROBE_L2)   // timing diagnostic only (wrong hits): probes L2-resident
-      Y.de0 = dense_at(o_bm, in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u);
-      Y.de1 = dense_at(o_bm, in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u);
+      Y.de0 = o_probe(in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u);
+      Y.de1 = o_probe(in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u);
 #elif defined(WSR_DIAG_PROBE_NONE)   // timing diagnostic only (wrong results): no probes, no hits
       // (k < 2^20: a zero mask the compiler cannot fold away)
-      Y.de0 = dense_fill(in0 ? (Q.k >> 20) : 0u);
-      Y.de1 = dense_fill(in1 ? (Q.k >> 20) : 0u);
+      Y.de0 = probe_fill(in0 ? (Q.k >> 20) : 0u);
+      Y.de1 = probe_fill(in1 ? (Q.k >> 20) : 0u);
 #else
-      Y.de0 = dense_at(o_bm, in0 ? (a0 - lo) / kDenseDocs : 0u);
-      Y.de1 = dense_at(o_bm, in1 ? (a1 - lo) / kDenseDocs : 0u);
+      Y.de0 = o_probe(in0 ? (a0 - lo) / kDenseDocs : 0u);
+      Y.de1 = o_probe(in1 ? (a1 - lo) / kDenseDocs : 0u);
 #endif
       Y.dcc = c0 | (c1 << 8);
       Y.dt0 = t0; Y.dt1 = t1;
@@ -2355,15 +2384,15 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     const uint32_t a_lo = first_doc > lo ? first_doc - lo : 0u;
     uint32_t a_hi = last_doc - lo;                      // inclusive, relative
     if (a_hi >= span) a_hi = span - 1;
-    const DenseEnt* a_bm = ix.dense + Q.a_bm;
+    const uint64_t a_bm = Q.a_bm;
     const uint8_t* a_tf8 = ix.tf8 + Q.a_tf8;
     if (span && last_doc >= lo && a_lo <= a_hi) {
       const uint32_t w0 = a_lo / kDenseDocs, w1 = a_hi / kDenseDocs;   // inclusive entry range
       for (uint32_t base = w0; base <= w1; base += 64) {
         const uint32_t wi = base + l;
         const bool live = wi <= w1;
-        const DenseVal va = dense_at(a_bm, live ? wi : w0);
-        const DenseVal vo = single ? dense_fill(~0u) : dense_at(o_bm, live ? wi : w0);
+        const DenseVal va = dense_at(ix, a_bm, live ? wi : w0);
+        const DenseVal vo = single ? dense_fill(~0u) : dense_at(ix, Q.o_bm, live ? wi : w0);
         uint32_t m[kDW];
 #pragma unroll
         for (uint32_t i = 0; i < kDW; ++i) {
@@ -2382,7 +2411,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
           for (uint32_t i = 0; i < kDW; ++i) any |= m[i];
           if (s == d || s == o1 || !__ballot(any)) continue;
           const ListDev B = ix.lists[qlist[s]];
-          const DenseVal vb = dense_at(ix.dense + B.bm, live ? wi : w0);
+          const DenseVal vb = dense_at(ix, B.bm, live ? wi : w0);
 #pragma unroll
           for (uint32_t i = 0; i < kDW; ++i) m[i] &= dense_word(vb, i);
         }
@@ -2421,16 +2450,20 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
           const uint32_t ent = has ? base + ow : w0;
           const uint32_t doc = lo + (base + ow) * kDenseDocs + sh;
           // (the entries again, from the cache: their ranks)
-          const uint32_t ra = dense_rank(dense_at(a_bm, ent), sh);
-          const uint32_t ro = single ? 0u : dense_rank(dense_at(o_bm, ent), sh);
+          const uint32_t ra = dense_rank(dense_at(ix, a_bm, ent), sh);
+          const uint32_t ro = single ? 0u : dense_rank(dense_at(ix, Q.o_bm, ent), sh);
           const uint32_t ta = load_byte(a_tf8 + (has ? ra : 0u));
+#if WSR_DENSE_FMT == 2
+          const uint32_t tb = 0u;   // (O1's tf: read by rank when the chunk is scored)
+#else
           const uint32_t tb = single ? 0u : load_byte(o_tf8 + (has ? ro : 0u));
+#endif
           const uint32_t cc = (has && doc < ix.n_c4) ? load_byte(ix.c4 + doc) : 0u;
           const uint32_t e = (qtail + l) & 255u;
           if (has) {
             qdoc[e] = doc; qc4[e] = cc;
             qtd[e] = ta == kTf8Escape ? (0x80000000u | ra) : ta;
-            qto[e] = tb == kTf8Escape ? (0x80000000u | ro) : tb;
+            qto[e] = (WSR_DENSE_FMT == 2 || tb == kTf8Escape) ? (0x80000000u | ro) : tb;
             if (kPh) { qpd[e] = Q.a_blk0 * 128u + ra; qpo[e] = ro; }
           }
           qtail += min(64u, total - c0);
@@ -2549,7 +2582,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       F = ix.lists[qlist[fo]];
       fo_dense = use_dense(ix, F.bm != kNoDense, F.nblk, A.nblk);
     }
-    const DenseEnt* f_dense = fo_dense ? ix.dense + F.bm : ix.dense;
+    const uint64_t f_bm = fo_dense ? F.bm : 0ull;
     const uint8_t* f_tf8 = ix.tf8 + (fo_dense ? F.tf8 : 0ull);
     const uint32_t f_last = fo_dense ? uni(ix.blk_last[F.blk0 + F.nblk - 1]) : 0u;
 
@@ -2628,8 +2661,8 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       const uint32_t r0 = g.a0 - ix.doc_lo, r1 = g.a1 - ix.doc_lo;
       const bool d0 = fo_dense && g.al0 && r0 < ix.dense_span;
       const bool d1 = fo_dense && g.al1 && r1 < ix.dense_span;
-      g.p0 = dense_at(f_dense, d0 ? r0 / kDenseDocs : 0u);
-      g.p1 = dense_at(f_dense, d1 ? r1 / kDenseDocs : 0u);
+      g.p0 = dense_at(ix, f_bm, d0 ? r0 / kDenseDocs : 0u);
+      g.p1 = dense_at(ix, f_bm, d1 ? r1 / kDenseDocs : 0u);
     };
     auto flush_events = [&](uint32_t n) __attribute__((always_inline)) {
       __builtin_amdgcn_wave_barrier();
