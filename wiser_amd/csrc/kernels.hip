@@ -1772,9 +1772,11 @@ __device__ __forceinline__ void pick_words(uint32_t r0, uint32_t r1, uint32_t bi
 // (kAnd: the instance that may take the bitmap-intersection path; the others
 // leave out its step buffer, so that more workgroups fit a CU's LDS)
 // (WSR_LEAN_EVS: capacity of the LDS event buffer, 128 or 64; at 64 it is
-// flushed after every chunk that added events)
+// flushed after every chunk that added events.  64 since round 3: C2 leg
+// 31.5 -> 33.2 M q/s, C4 11.8 -> 12.5 M, C3 headline unchanged; 4 KB less
+// LDS per workgroup, profiles/r03_knob_ab.txt)
 #ifndef WSR_LEAN_EVS
-#define WSR_LEAN_EVS 128
+#define WSR_LEAN_EVS 64
 #endif
 template <bool kPh, bool kAnd>
 struct LeanLdsT {
@@ -1991,9 +1993,25 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         rec(s, B.blk0 * 128u + x, t);
       }
     }
-    // HandleTheFoundDoc: a phrase query ranks only docs that hold the phrase
+    // HandleTheFoundDoc: a phrase query ranks only docs that hold the phrase.
+    // Only a doc that can still enter the running top-k needs its position
+    // check: the chunk's candidates at the k-th best before it (and the floor)
+    // are a superset of the chunk's events whatever the phrase matches among
+    // them, and a doc that is no candidate is no event either way.
     if (kPh && phrase && __ballot(alive)) {
-      if (alive) alive = phrase_match(ix, qlist, nt, ph, l);
+      bool need = alive;
+      if (!wide) {
+        const uint64_t fb0 = floor_bits;
+        const double flo0 = __longlong_as_double(static_cast<long long>(
+            (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb0 >> 32))) << 32) |
+            uni(static_cast<uint32_t>(fb0))));
+        const double kth0 = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+        need = alive && sc > flo0 && (pt_n < k || sc > kth0);
+      }
+      if (__ballot(need)) {
+        if (need) need = phrase_match(ix, qlist, nt, ph, l);
+      }
+      alive = need;
     }
     const uint64_t am = __ballot(alive);
     if (am == 0) return;
@@ -2858,6 +2876,15 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       }
       if (__ballot(al0 || al1) == 0) return;
       if (phrase) {   // HandleTheFoundDoc: rank only docs that hold the phrase
+        // (only the block's top-k candidates are checked, as in lean_segment)
+        if (!wide) {
+          const double flo0 = __longlong_as_double(static_cast<long long>(
+              (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
+              uni(static_cast<uint32_t>(floor_bits))));
+          const double kth0 = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+          al0 = al0 && s0 > flo0 && (pt_n < k || s0 > kth0);
+          al1 = al1 && s1 > flo0 && (pt_n < k || s1 > kth0);
+        }
         if (al0) al0 = phrase_match(ix, qlist, nt, ph, 2 * l);
         if (al1) al1 = phrase_match(ix, qlist, nt, ph, 2 * l + 1);
         if (__ballot(al0 || al1) == 0) return;
