@@ -149,6 +149,7 @@ struct wsr_batch {
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
+  bool two_only = false;         // every query: two terms (or empty), k <= kMaxK, no phrase
   int seg_grid = 0;
   int lean_wgs = 0;
   int merge_wgs = 0;              // 0: the batch has no merge item
@@ -641,7 +642,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, gen_need = 0, merge_need = 0;
   const float dense_ratio = h->args.dense_ratio;
-  bool has_phrase = false, has_wide = false;
+  bool has_phrase = false, has_wide = false, two_only = true;
   std::vector<int32_t> ids;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
@@ -652,6 +653,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
     has_phrase = has_phrase || phrase;
     has_wide = has_wide || s.k > kMaxK;
+    two_only = two_only && !phrase && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
@@ -738,6 +740,12 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->nq = nq;
   b->has_phrase = has_phrase;
   b->has_wide = has_wide;
+#ifdef WSR_NO_TWO   // A/B: every batch on the general lean instance
+  b->two_only = false;
+  (void)two_only;
+#else
+  b->two_only = two_only;
+#endif
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
@@ -818,7 +826,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
                        b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc,
                        b->has_phrase ? b->d_ph + static_cast<size_t>(kPhraseScratch) * std::max(h->gen_cap, 1)
-                                     : nullptr, st));
+                                     : nullptr, b->two_only, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     if (b->merge_wgs) HIP_OK(hipStreamWaitEvent(st, b->join3, 0));

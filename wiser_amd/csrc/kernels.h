@@ -162,11 +162,12 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
                            uint64_t* pub, uint32_t* ph, hipStream_t st);
 
 // lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride];
-// ph: phrase scratch (lean_wgs * kLeanWaves * kPhraseScratch u32), null without phrase queries
+// ph: phrase scratch (lean_wgs * kLeanWaves * kPhraseScratch u32), null without phrase queries;
+// two: every query of the batch has two terms (or none), k <= kMaxK, no phrase
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st);
+                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st);
 int lean_kernel_occupancy();
 // merge items (QueryPlan kPlanMerge): merge_wgs workgroups of kMergeWaves waves;
 // stats of wave w at stats[w * kStatStride]

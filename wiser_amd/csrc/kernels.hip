@@ -1796,7 +1796,11 @@ struct LeanLdsT {
 // o1 == kNoSlot: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
-template <bool kPh, bool kAnd>
+// kTwo: every item of the launch is a two-term, k <= kMaxK, non-phrase query
+// (the headline's and C2's batches): two terms scored inline, no wide or
+// single-term paths, so the instance keeps fewer registers (86 VGPRs, no
+// scratch, half the SGPR spill reloads of the general instance).
+template <bool kPh, bool kAnd, bool kTwo = false>
 __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, kAnd>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t* ph,
@@ -1810,12 +1814,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                                              uint32_t* prof) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
-  const uint32_t d = Q.slots & 0xFFFFu, o1 = Q.slots >> 16;
-  const uint32_t nt = Q.nt & 0xFFFFu, k = Q.k;
+  const uint32_t d = kTwo ? (Q.slots & 1u) : (Q.slots & 0xFFFFu);
+  const uint32_t o1 = kTwo ? (d ^ 1u) : (Q.slots >> 16);
+  const uint32_t nt = kTwo ? 2u : (Q.nt & 0xFFFFu), k = Q.k;
   // k > kMaxK: every survivor is an event; the replay's heap in LDS decides
-  const bool wide = k > static_cast<uint32_t>(kMaxK);
+  const bool wide = !kTwo && k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
-  const bool single = o1 == kNoSlot;
+  const bool single = !kTwo && o1 == kNoSlot;
   // (single term: reads go to a valid dummy word; the image may have no bitmaps)
   // O1's bitmap (single term: reads go to a valid dummy word)
 #if WSR_DENSE_FMT == 2
@@ -1975,7 +1980,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     };
     const double norm = norm_tab[c4 & 255u];
     double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
-    for (uint32_t s = 0; s < nt; ++s) {
+    if constexpr (kTwo) {   // the two terms in query order: the driver's slot first or second
+      const double sd = bm25_term(idf_d, alive ? td : 0u, norm), so = bm25_term(idf_o, alive ? to : 0u, norm);
+      if (d == 0) { sc += sd; sc += so; } else { sc += so; sc += sd; }
+    }
+    for (uint32_t s = 0; s < (kTwo ? 0u : nt); ++s) {
       if (s == d) {
         sc += bm25_term(idf_d, alive ? td : 0u, norm);
         rec(s, pd, td);
@@ -2982,7 +2991,7 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 #ifndef WSR_LEAN_WGS_PHRASE
 #define WSR_LEAN_WGS_PHRASE 3
 #endif
-template <bool kPh, bool kAnd>
+template <bool kPh, bool kAnd, bool kTwo = false>
 __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd ? 4 : WSR_LEAN_WGS)) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
@@ -3060,7 +3069,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd 
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
     if (!done && b0 < b1)
-      lean_segment<kPh, kAnd>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
+      lean_segment<kPh, kAnd, kTwo>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
                    kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
                    ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
                    my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
@@ -3801,7 +3810,7 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, hipStream_t st) {
+                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st) {
   // (a persistent grid sized for the conjunctive instance: waves of a larger
   // instance that find no room start later and find the queue drained)
   // (phrase batches: the bitmap-intersection path only when it is on, so the
@@ -3814,6 +3823,9 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   else if (ix.and_wpb > 0.0f)
     hipLaunchKernelGGL((lean_kernel<false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
+                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+  else if (two)
+    hipLaunchKernelGGL((lean_kernel<false, false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
                        plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   else
     hipLaunchKernelGGL((lean_kernel<false, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
