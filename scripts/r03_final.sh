@@ -4,7 +4,7 @@
 # two-rank launcher rehearsal on one GPU (gloo exchange).  Usage: TAG [steps...]
 set -eu -o pipefail
 TAG=$1; shift
-STEPS=${*:-tests bench driver shard1 n2}
+STEPS=${*:-tests bench driver classes shard1 n2}
 R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
@@ -33,5 +33,9 @@ if has n2; then
       --master-port 29533 bench.py --gpus 2 --exchange gloo --no-cpu --steps 200 --warmup 10 \
       > "$O/bench_n2_gloo.json" 2> "$O/bench_n2_gloo.err" || { tail -40 "$O/bench_n2_gloo.err"; exit 1; }
   head -c 600 "$O/bench_n2_gloo.json"; echo
+fi
+if has classes; then
+  timeout -k 10 300 python3 scripts/diag_types.py --wiki > "$O/classes_c3.txt" 2>&1
+  grep -E "^(mixed|high-high)" "$O/classes_c3.txt"
 fi
 echo done
