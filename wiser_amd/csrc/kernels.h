@@ -87,12 +87,13 @@ constexpr int kMaxOwners = 1024;   // doc-range shards (ranks) of one exchange
 #endif
 constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
-// phrase queries: every survivor also runs the position check, so an item of
-// kSegCost blocks is longer; smaller items keep the queue's tail balanced
-// (5: the 5-block phrase items of the round-1 tuning, now that a bitmap probe
-// round no longer adds to an item's cost, WSR_DENSE_COST)
+// phrase queries: items of kSegCost blocks as well since round 3.  Items of 5
+// blocks were kept while every conjunctive survivor ran the position check;
+// now only the running top-k's candidates do (lean_segment), and longer items
+// prune more: C5 leg 3.50 -> 4.95 M q/s at 63 blocks (16: 4.27, 32: 4.56 M),
+// profiles/r03_phrase_item_ab.txt
 #ifndef WSR_SEG_COST_PHRASE
-#define WSR_SEG_COST_PHRASE 5
+#define WSR_SEG_COST_PHRASE 63
 #endif
 constexpr int kSegCostPhrase = WSR_SEG_COST_PHRASE;
 static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSegCost");
