@@ -231,9 +231,10 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // (1024: every list that is at least 1/1024 of the doc range -- on the
     // en-Wikipedia-shaped C3 corpus this halves the mixed batch against 128,
     // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
-    // caps the bitmaps' HBM, longest lists first)
+    // caps the bitmaps' HBM, longest lists first: 48 GB, as the 8-byte rank
+    // records (WSR_RANK_TF) put the C3 stand-in's at 33 GB)
     const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048));
-    const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 32) * 1e9);
+    const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 48) * 1e9);
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
     // replay inside the segment kernel (WSR_FUSE_REPLAY=0: separate launch)
     h->fuse_replay = env_number("WSR_FUSE_REPLAY", 1) != 0;

@@ -70,7 +70,14 @@ static_assert(sizeof(DenseEnt) == 8, "DenseEnt layout");
 #else
 #error "WSR_DENSE_FMT is 0 or 2"
 #endif
-constexpr uint64_t kDenseEntBytes = WSR_DENSE_FMT == 2 ? 8 : sizeof(DenseEnt);   // mask + rank
+// WSR_RANK_TF (format 2): a rank record is 8 bytes, the rank and the 1-byte
+// tfs of the word's first four postings (255: more, or tf >= 255: read tf8),
+// so that a hit's rank and tf come in one line; 0: the rank alone (4 bytes)
+#ifndef WSR_RANK_TF
+#define WSR_RANK_TF 1
+#endif
+constexpr uint32_t kRankWords = (WSR_DENSE_FMT == 2 && WSR_RANK_TF) ? 2 : 1;   // u32 per rank record
+constexpr uint64_t kDenseEntBytes = WSR_DENSE_FMT == 2 ? 4 + 4 * kRankWords : sizeof(DenseEnt);   // mask + rank
 constexpr uint32_t kWinEnts = 64;     // DenseEnts per tf-maximum window; every list's bitmap
                                       // starts at a multiple of it
 

@@ -520,7 +520,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.tails.resize(ntail);
   img.dense.resize(ne);
 #if WSR_DENSE_FMT == 2
-  img.dense_rank.resize(ne);
+  img.dense_rank.resize(kRankWords * ne);
 #endif
   img.tf8.resize(ntf8);
   img.wmax.resize(ne / kWinEnts);
@@ -623,7 +623,15 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         while (i < n_img && s.docs[i] < start) ++i;
         DenseEnt ent{};
 #if WSR_DENSE_FMT == 2
-        img.dense_rank[ld.bm + e] = static_cast<uint32_t>(i);
+        img.dense_rank[kRankWords * (ld.bm + e)] = static_cast<uint32_t>(i);
+        if (kRankWords == 2) {   // the tfs of the word's first four postings (255: none / escape)
+          uint32_t t4 = 0xFFFFFFFFu;
+          for (uint64_t j = i, n = 0; n < 4 && j < n_img && s.docs[j] < start + kDenseDocs; ++j, ++n) {
+            const uint32_t t = s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape;
+            t4 = (t4 & ~(0xFFu << (8 * n))) | (t << (8 * n));
+          }
+          img.dense_rank[kRankWords * (ld.bm + e) + 1] = t4;
+        }
 #else
         ent.rank = static_cast<uint32_t>(i);
 #endif
@@ -779,7 +787,7 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   const uint32_t sh = rel % kDenseDocs;
   if (!dense_ent_bit(e, sh)) return -1;
 #if WSR_DENSE_FMT == 2
-  const uint32_t idx = dense_ent_rank(e, img.dense_rank[L.bm + rel / kDenseDocs], sh);
+  const uint32_t idx = dense_ent_rank(e, img.dense_rank[kRankWords * (L.bm + rel / kDenseDocs)], sh);
 #else
   const uint32_t idx = dense_ent_rank(e, e.rank, sh);
 #endif

@@ -305,7 +305,7 @@ __device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
 // entry e of the bitmap that starts at entry bm (ListDev::bm)
 __device__ __forceinline__ DenseVal dense_at(const IndexArgs& ix, uint64_t bm, uint32_t e) {
 #if WSR_DENSE_FMT == 2
-  return make_uint2(ix.dense_rk[bm + e], ix.dense[bm + e].w);
+  return make_uint2(ix.dense_rk[kRankWords * (bm + e)], ix.dense[bm + e].w);
 #else
   return reinterpret_cast<const uint2*>(ix.dense + bm)[e];
 #endif
@@ -1826,7 +1826,12 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #if WSR_DENSE_FMT == 2
   // the probe reads the mask word alone; a hit reads its rank (H stage)
   const uint32_t* o_mk = single ? ix.blk_last : &ix.dense[Q.o_bm].w;
+#if WSR_RANK_TF
+  const uint2* o_rk = single ? reinterpret_cast<const uint2*>(ix.blk_last)
+                             : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
+#else
   const uint32_t* o_rk = single ? ix.blk_last : ix.dense_rk + Q.o_bm;
+#endif
   auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_mk[e]; };
   auto probe_fill = [&](uint32_t m) __attribute__((always_inline)) { return m; };
   (void)probe_fill;   // (the WSR_DIAG_PROBE_NONE diagnostic)
@@ -1955,7 +1960,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     __builtin_amdgcn_wave_barrier();
     qhead += n;
 #if WSR_DENSE_FMT == 2
-    if (!single) {   // O1's tf bytes of the chunk, by rank (bit 31 set: a rank)
+    if (!single && __ballot(alive && (to & 0x80000000u))) {   // O1's tf bytes by rank (bit 31: a rank)
       const bool rk = alive && (to & 0x80000000u);
       uint32_t t = load_byte(o_tf8 + (rk ? (to & 0x7FFFFFFFu) : 0u));
       if (__ballot(rk && t == kTf8Escape)) {
@@ -2107,7 +2112,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     // -- so that they take no scalar lane-mask registers across the iteration)
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
+#if WSR_DENSE_FMT == 2 && WSR_RANK_TF
+    uint2 hf0 = make_uint2(0, 0), hf1 = make_uint2(0, 0);   // O1 rank records (rank, 4 tfs; in flight)
+#else
     uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (fmt 2: rank words; in flight)
+#endif
     uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit)
 
   };
@@ -2181,8 +2190,17 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 #if WSR_DENSE_FMT == 2
       // O1 posting ranks (hits): rank word + bits below; the tf byte is read by
       // rank when the chunk is scored (flag bit 31)
+#if WSR_RANK_TF
+      // (the record's tf bytes cover the word's first four postings)
+      const uint32_t rk0 = X.hf0.x + X.hx0, rk1 = X.hf1.x + X.hx1;
+      const uint32_t f0 = X.hx0 < 4u ? (X.hf0.y >> ((X.hx0 & 3u) << 3)) & 0xFFu : kTf8Escape;
+      const uint32_t f1 = X.hx1 < 4u ? (X.hf1.y >> ((X.hx1 & 3u) << 3)) & 0xFFu : kTf8Escape;
+      const uint32_t to0 = f0 != kTf8Escape ? f0 : (0x80000000u | rk0);
+      const uint32_t to1 = f1 != kTf8Escape ? f1 : (0x80000000u | rk1);
+#else
       const uint32_t rk0 = X.hf0 + X.hx0, rk1 = X.hf1 + X.hx1;
       const uint32_t to0 = 0x80000000u | rk0, to1 = 0x80000000u | rk1;
+#endif
 #else
       const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
       const uint32_t f0 = single ? 0u : (X.hf0 >> xs0) & 0xFFu;
