@@ -47,19 +47,7 @@ $(ORACLE): oracle/oracle.cc oracle/oracle.h
 	@mkdir -p oracle/_build
 	$(CXX) $(ORAFLAGS) -o $@ oracle/oracle.cc -lpthread -l:liblz4.so.1
 
-# diagnostics only: segment-kernel section timers (scripts/diag_types.py --prof)
-PROFLIB := wiser_amd/_lib/prof/libwiser_hip.so
-prof: $(PROFLIB)
-$(PROFLIB): $(SRCS) $(HDRS)
-	@mkdir -p wiser_amd/_lib/prof
-	$(HIPCC) $(HIPFLAGS) -DWSR_PROFILE -shared -o $@ $(SRCS) -lpthread -l:liblz4.so.1 -lrccl
-
-# tuning variants (diagnostics only): make variant V=name F="-DFLAG=..."
-variant: $(SRCS) $(HDRS)
-	@mkdir -p wiser_amd/_lib/var_$(V)
-	$(HIPCC) $(HIPFLAGS) $(F) -shared -o wiser_amd/_lib/var_$(V)/libwiser_hip.so $(SRCS) -lpthread -l:liblz4.so.1 -lrccl
-
 clean:
 	rm -rf wiser_amd/_lib oracle/_build
 
-.PHONY: all clean prof variant
+.PHONY: all clean

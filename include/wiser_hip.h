@@ -190,11 +190,13 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t hit_
  * query_pool.h:319-378): one query per line, terms separated by spaces, a
  * line in double quotes is a phrase query.  Every term is resolved through the
  * term index (VacuumInvertedIndex::FindIteratorsSolid, vacuum_engine.h:89-99);
- * q[0..*nq) receives the queries (k results each).  The more_ids of a query
- * with more than WSR_MAX_TERMS terms point into storage owned by the calling
- * thread, valid until that thread's next wsr_resolve_text call. */
+ * q[0..*nq) receives the queries (k results each).  The list ids of terms past
+ * the first WSR_MAX_TERMS of a query go to the caller's more_store (more_cap
+ * int32 entries; may be NULL when no query is that long) and the query's
+ * more_ids points there, so the ids live as long as the caller's storage;
+ * WSR_E_LIMIT when more_store is too small. */
 int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t max_q,
-                     wsr_query* q, int32_t* nq);
+                     wsr_query* q, int32_t* nq, int32_t* more_store, int64_t more_cap);
 /* The whole Search chain from strings: wsr_resolve_text, then wsr_search_batch
  * (upload, run, results to the host). */
 int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t hit_stride,
@@ -205,10 +207,8 @@ int wsr_batch_create(wsr_handle* h, int32_t max_queries, int32_t hit_stride, wsr
 void wsr_batch_destroy(wsr_handle* h, wsr_batch* b);
 /* copy queries to HBM (synchronous) and size the event workspace */
 int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq);
-/* enqueue plan + segment + replay kernels on the engine stream (asynchronous) */
+/* enqueue plan + segment + replay kernels on the batch's streams (asynchronous) */
 int wsr_batch_run(wsr_handle* h, wsr_batch* b);
-/* plan + segment only (a doc-range shard: events go to wsr_shard_reduce) */
-int wsr_batch_run_events(wsr_handle* h, wsr_batch* b);
 /* wait for the engine stream */
 int wsr_sync(wsr_handle* h);
 /* copy results to the host: the copies are queued behind the batch's kernels,
@@ -224,8 +224,6 @@ int wsr_pinned_alloc(uint64_t bytes, void** out);
 void wsr_pinned_free(void* p);
 /* 1 when the batch's last run has finished on the device, 0 while it runs */
 int wsr_batch_ready(wsr_handle* h, wsr_batch* b);
-/* device pointers of the batch's results (for collectives on the caller's side) */
-int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits);
 
 /* ---- serving: micro-batcher over one handle --------------------------
  * The reference serves single queries from N gRPC worker threads sharing one
@@ -265,61 +263,26 @@ int wsr_server_bench(wsr_server* s, const wsr_query* q, int32_t nq, int32_t n_cl
 /* ---- doc-range shards (multi-GPU) ------------------------------------
  * A shard engine (wsr_open_opts.doc_lo/doc_hi) runs every query of a batch over
  * its doc range.  Queries are owned by contiguous slices of q_per_owner queries
- * (owner o = query / q_per_owner).  Exchange (caller's collectives, e.g. RCCL
- * all_to_all): counts and events per owner; the owner then replays the events
- * of all shards in shard (= doc-id range) order.  Results are bit-identical to
- * an unsharded run ("Why replaying events is exact").          */
-/* After wsr_batch_run: reduce each query's events to the insertions of a heap
- * run from empty over the shard; d_counts (device, nq int32) receives the per
- * query event counts, owner_totals (host, n_owners) the events per owner. */
-int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
-                     int32_t* d_counts, int64_t* owner_totals);
-/* Pack the reduced events owner-major into d_send (device, 16-byte events). */
-int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send);
-/* Owner side: d_rcounts (device, n_shards x nq_owned int32, shard-major),
- * d_recv (device events: shard 0's block for my queries, then shard 1's, ...;
- * shard g's block starts at event rbase[g], host array) -> results of the
- * batch's queries [q0, q0 + nq_owned). */
-int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                     const int32_t* d_rcounts, const void* d_recv, const uint64_t* rbase);
+ * (owner o = query / q_per_owner).  Per step, every shard's segment kernels
+ * reduce each query's events to those of a heap run from empty over the shard
+ * and append them to the owner's region of an exchange buffer; one all-to-all
+ * moves the regions; the owner replays the events of all shards in shard (=
+ * doc-id range) order.  Results are bit-identical to an unsharded run (see
+ * DESIGN.md, "Why replaying events is exact").  A region = the {count, offset}
+ * pairs of the owner's q_per_owner queries, padded to whole 16-byte events,
+ * then a slot of `slot` events; a query whose events overflow the slot is
+ * flagged (count -1 and an error flag that wsr_batch_fetch* reports). */
+/* results of the batch's queries [q0, q0 + nq) (an owner's slice) */
 int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,
                           int32_t* n_hits);
 /* the engine's HIP stream (a hipStream_t) for ordering the caller's work */
 int wsr_stream(wsr_handle* h, void** stream);
-/* the batch's own stream (a hipStream_t): its runs, packs and replays are
- * ordered on it, so a caller's collectives enqueued there need no host wait */
+/* the batch's own stream (a hipStream_t): its runs and its shard step's
+ * emission are ordered on it */
 int wsr_batch_stream(wsr_handle* h, wsr_batch* b, void** stream);
-
-/* ---- fixed-slot exchange: no host round trip inside a step -----------
- * Every (shard, owner) pair gets a slot of `slot` events, so the exchange
- * sizes are known without reading counts back: a step is run_events ->
- * pack_fixed -> all-to-all of counts (q_per_owner int32 per pair) and slots
- * (slot * 16 B per pair) -> owner_replay_fixed, all on the batch's stream.  A
- * query whose events would overflow its slot is flagged (count -1 and an error
- * flag that wsr_batch_fetch* reports); the caller re-runs with a larger slot.
- * wsr_shard_fill reads back the events per owner of the last pack (it waits
- * for the batch), to size the slot. */
-int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
-                         int64_t slot, int32_t* d_counts, void* d_send);
+/* events appended per owner by the last shard step's emission (waits for the
+ * batch), to size the slot */
 int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals);
-/* d_rcounts: n_shards x nq_owned (shard-major); d_recv: n_shards slots */
-int wsr_owner_replay_fixed(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                           int64_t slot, const int32_t* d_rcounts, const void* d_recv);
-
-/* ---- fused fixed-slot exchange --------------------------------------
- * wsr_shard_emit runs the batch (plan + segment kernels) and, as each query's
- * last work item finishes, reduces its events and appends them to its owner's
- * slot of d_send (n_owners slots of `slot` 16-byte events) at an offset taken
- * from the owner's fill counter; d_meta (device, 2 x nq int32) receives
- * {count, offset} per query (count -1: the slot was full, error flag set).
- * Nothing runs between the segment kernels and the exchange.  The owner side:
- * d_rmeta = n_shards x nq_owned {count, offset} pairs (shard-major), d_recv =
- * n_shards slots; results of [q0, q0 + nq_owned) as wsr_owner_replay_fixed.
- * wsr_shard_fill after wsr_shard_emit / wsr_shard_step reads the fill counters. */
-int wsr_shard_emit(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners, int64_t slot,
-                   int32_t* d_meta, void* d_send);
-int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                          int64_t slot, const int32_t* d_rmeta, const void* d_recv);
 
 /* ---- native RCCL exchange (one process per GPU; a C++ host needs no Python):
  * rank 0 makes the id, every rank opens the communicator with it (the id
@@ -358,14 +321,9 @@ int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t wor
 int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_t which,
                            uint32_t* out, int32_t* count);
 
-/* Diagnostics build only (-DWSR_REPLAY_PROF): after wsr_batch_run_events,
- * replay the batch (replay_kernel) and return 6 u32 per query: filter cycles,
- * finish cycles, events, filter candidates, heap insertions, work items. */
-int wsr_debug_replay_profile(wsr_handle* h, wsr_batch* b, uint32_t* rows);
-
 /* Raw per-workgroup counters of the last segment launch (diagnostics):
- * n_wg rows of `stride` u32 {survivors, driver blocks, other blocks, ...;
- * section cycle counts in a -DWSR_PROFILE build}.  out may be NULL to query. */
+ * n_wg rows of `stride` u32 {survivors, driver blocks, other blocks, 0}.
+ * out may be NULL to query. */
 int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_words,
                        int32_t* n_wg, int32_t* stride);
 

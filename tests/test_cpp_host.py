@@ -26,6 +26,7 @@ def test_cpp_host_matches_oracle(indexes, tmp_path):
     log.write_text("\n".join(" ".join(q) for q in qs) + "\n")
     out = subprocess.run([CLI, d, str(log), "10"], capture_output=True, text=True, check=True)
     lines = out.stdout.split("\n")
+    assert lines[-1] == "" and len(lines) == len(qs) + 1, len(lines)   # one line per query, no truncation
     o = OracleVacuum(d)
     for q, line in zip(qs, lines):
         want, _ = o.search(q, 10)
@@ -46,6 +47,7 @@ def test_cpp_host_snippets_match_oracle(indexes, tmp_path):
     log.write_text("\n".join(" ".join(q) for q in qs) + "\n")
     out = subprocess.run([CLI, d, str(log), "10", "snippets"], capture_output=True, text=True, check=True)
     lines = out.stdout.split("\n")
+    assert lines[-1] == "" and len(lines) == 2 * len(qs) + 1, len(lines)   # two lines per query
     o = OracleVacuum(d)
     n = 0
     for i, q in enumerate(qs):

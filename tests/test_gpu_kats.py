@@ -61,11 +61,23 @@ def test_tests_16_log_through_resolve_text(built, indexes):
     text = open(os.path.join(DATA, "query_log_with_phrases"), "rb").read()
     q = (_capi.Query * 16)()
     nq = C.c_int32()
-    _capi.check(_capi.lib.wsr_resolve_text(eng._h, text, len(text), 10, 16, q, C.byref(nq)))
+    _capi.check(_capi.lib.wsr_resolve_text(eng._h, text, len(text), 10, 16, q, C.byref(nq), None, 0))
     assert nq.value == 10
     assert q[0].n_terms == 2 and q[0].flags == _capi.QUERY_PHRASE
     assert q[1].n_terms == 3 and q[1].flags == 0
     assert [eng.lookup(t)[0] for t in ("nightt", "rain", "nashvil")] == list(q[1].list_ids[:3])
+    # a query past WSR_MAX_TERMS terms: its ids past 16 land in the caller's
+    # more_store (too small: WSR_E_LIMIT, nothing written there)
+    toks = [f"nosuch{i}" for i in range(20)]
+    long_text = (" ".join(["nightt"] * 17 + ["rain"] * 3) + "\n" + " ".join(toks)).encode()
+    store = (C.c_int32 * 8)(*([-9] * 8))
+    rc = _capi.lib.wsr_resolve_text(eng._h, long_text, len(long_text), 10, 4, q, C.byref(nq), store, 7)
+    assert rc == _capi.E_LIMIT and list(store) == [-9] * 8
+    _capi.check(_capi.lib.wsr_resolve_text(eng._h, long_text, len(long_text), 10, 4, q, C.byref(nq), store, 8))
+    assert nq.value == 2 and q[0].n_terms == 20 and q[1].n_terms == 20
+    night, rain = eng.lookup("nightt")[0], eng.lookup("rain")[0]
+    assert [q[0].more_ids[i] for i in range(4)] == [night, rain, rain, rain]
+    assert [q[1].more_ids[i] for i in range(4)] == [-1] * 4
     eng.close()
 
 

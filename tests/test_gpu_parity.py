@@ -24,15 +24,8 @@ DENSE_MODES = {
     "blocks": {"WSR_DENSE_DIV": "0"},
     "dense": {},
     "dense_all": {"WSR_DENSE_DIV": "1000000000", "WSR_DENSE_RATIO": "0"},
-    # every lean item whose driver has a bitmap intersects bitmaps word by word
-    "and_all": {"WSR_DENSE_DIV": "1000000000", "WSR_DENSE_RATIO": "0", "WSR_AND_WPB": "1000000000"},
-    # every conjunctive query of two or more terms whose lists past O1 have
-    # bitmaps runs in merge_kernel (driver and O1 decoded and merged)
-    "merge": {"WSR_MERGE_RATIO": "1000000000", "WSR_MERGE_MIN": "1"},
-    # ... with no bitmaps at all: every two-term query merges
-    "merge_blocks": {"WSR_DENSE_DIV": "0", "WSR_MERGE_RATIO": "1000000000", "WSR_MERGE_MIN": "1"},
 }
-ENGINE_ENV = ("WSR_DENSE_DIV", "WSR_DENSE_RATIO", "WSR_AND_WPB", "WSR_MERGE_RATIO", "WSR_MERGE_MIN")
+ENGINE_ENV = ("WSR_DENSE_DIV", "WSR_DENSE_RATIO")
 
 
 def _engine(d, mode="dense"):

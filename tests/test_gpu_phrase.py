@@ -115,12 +115,12 @@ def test_phrase_doc_range_shards(positions_index):
     """Shard images keep the whole position box of a list; phrase results of a
     W-way doc-range split replayed in order equal the unsharded oracle."""
     from oracle.oracle import OracleVacuum
-    from test_shard_gpu import _run_sharded
+    from test_shard_gpu import _run_step_regions
     d, seqs = positions_index
     orc = OracleVacuum(d)
     qs = phrase_cases(seqs, 240, seed=29)
-    for world in (2, 3):
-        qs2, got = _run_sharded(d, qs, 10, world, phrase=True)
+    for world in (2, 3, 8):
+        qs2, got = _run_step_regions(d, qs, 10, world, slot=None, phrase=True)
         for q, g in zip(qs2, got):
             assert g == orc.search(q, 10, phrase=True)[0], (world, q)
     orc.close()

@@ -205,26 +205,59 @@ def test_c5_full_size_phrases(c3_full):
     assert sum(1 for x in want if x) > len(qs) // 2
 
 
-def test_c3_full_size_merge_class(c3_full):
-    """The merge class (merge_kernel: driver and O1 decoded and merged) on the
-    full-size stand-in's log: 2,048 queries, bit for bit, with every eligible
-    query merged (WSR_MERGE_RATIO huge) and at the bench's setting (8)."""
+# ---- configs[3] / configs[4] in their stated form: doc-range sharded 8x ----
+#  The full-size stand-in split into W = 8 doc-range shard
+# engines on the one GPU (each holds its eighth of the blocks, with positions),
+# driven through wsr_shard_step's device halves with the regions moved exactly
+# as its ncclAllToAll moves them (tests/test_shard_gpu.py::_run_step_regions).
+@pytest.fixture(scope="module")
+def c3_shards8(c3_full):
+    from test_shard_gpu import open_shards
+    engs = open_shards(c3_full[0], 8, positions=True)
+    yield engs
+    for e in engs:
+        e.close()
+
+
+def _oracle_lines(d, qs, k, phrases=None):
+    from oracle.oracle import OracleVacuum
+    orc = OracleVacuum(d)
+    try:
+        return orc.search_lines(qs, k, threads=min(16, os.cpu_count()), phrases=phrases)
+    finally:
+        orc.close()
+
+
+def test_c4_full_size_docshard8(c3_full, c3_shards8):
+    """configs[3]: 2,048 mixed 1-5-term AND queries (AOL shares) over the
+    5.5 M-doc stand-in, doc-range sharded 8x, top-10, bit for bit."""
     import wiser_amd as w
-    d, log, _ = c3_full
-    for ratio in ("1000000000", "8"):
-        saved = {k: os.environ.get(k) for k in ("WSR_MERGE_RATIO", "WSR_MERGE_MIN")}
-        os.environ["WSR_MERGE_RATIO"] = ratio
-        os.environ["WSR_MERGE_MIN"] = "1"
-        try:
-            eng = w.VacuumEngine(d, positions=False)
-            eng.Load()
-        finally:
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
-        try:
-            _check_log(d, log, 2048, stride=47, eng=eng)
-        finally:
-            eng.close()
+    from test_shard_gpu import _run_step_regions
+    d, _, _ = c3_full
+    mixed = os.path.join(d, "mixed_20000.log")
+    if not os.path.exists(mixed):
+        w.gen_mixed_log(d, mixed, n_queries=20_000, seed=7)
+    qs = [l.split() for l in open(mixed).read().splitlines()][::9][:2048]
+    qs2, got = _run_step_regions(d, qs, 10, 8, slot=None, engines=c3_shards8)
+    want = _oracle_lines(d, qs2, 10)
+    bad = [(q, g[:3], x[:3]) for q, g, x in zip(qs2, got, want) if g != x]
+    assert not bad, bad[:3]
+    assert sum(1 for x in want if x) > 500
+
+
+def test_c5_full_size_docshard8(c3_full, c3_shards8):
+    """configs[4]: 1,024 two-term phrase queries from the stand-in's phrase pool,
+    doc-range sharded 8x (each shard keeps its lists' whole position boxes),
+    top-10, bit for bit against the oracle's PhraseQueryProcessor2."""
+    import wiser_amd as w
+    from test_shard_gpu import _run_step_regions
+    d, _, _ = c3_full
+    log = os.path.join(d, "phrase_10000.log")
+    if not os.path.exists(log):
+        w.gen_phrase_log(d, log, n_queries=10_000, seed=7)
+    qs = [t for t, _ in w.read_query_log(log)][1::8][:1024]
+    qs2, got = _run_step_regions(d, qs, 10, 8, slot=None, phrase=True, engines=c3_shards8)
+    want = _oracle_lines(d, qs2, 10, phrases=[True] * len(qs2))
+    bad = [(q, g[:3], x[:3]) for q, g, x in zip(qs2, got, want) if g != x]
+    assert not bad, bad[:3]
+    assert sum(1 for x in want if x) > len(qs2) // 2

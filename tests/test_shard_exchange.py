@@ -1,8 +1,11 @@
 """Doc-range sharding on CPU with gloo (world_size 2): every rank computes the
 heap-insertion events of its doc range (pure-Python model of the reference
-ranking), the product's exchange() moves them owner-major with all_to_all, and
-each owner replays them; the result must equal the single-engine oracle bit for
-bit.  Also checks that shard events are a superset of the global insertions."""
+ranking), packs them into the product's exchange regions (wiser_amd.shard
+REGION LAYOUT: per owner the {count, offset} pairs padded to whole events,
+then the slot), moves them with the product's exchange_regions (the
+all-to-all wsr_shard_step runs with RCCL), and each owner replays the regions
+in shard order; the result must equal the single-engine oracle bit for bit.
+Also checks that shard events are a superset of the global insertions."""
 import os
 import socket
 
@@ -37,14 +40,14 @@ def _scored_survivors(post, lens, avg, n, terms):
     return out
 
 
-def _worker(rank, world, port, index_dir, queries, k, result_q, fixed=False):
+def _worker(rank, world, port, index_dir, queries, k, result_q):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import heapmodel as hm
     import struct
     from oracle.oracle import OracleVacuum
-    from wiser_amd.shard import exchange, exchange_fixed, shard_range, index_doc_count
+    from wiser_amd.shard import exchange_regions, region_events, shard_range, index_doc_count
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -69,39 +72,46 @@ def _worker(rank, world, port, index_dir, queries, k, result_q, fixed=False):
         superset_ok &= set(g for g in gins if lo <= g[1] < hi) <= set(ins)
         counts.append(len(ins))
         events.extend(ins)
-    totals = [sum(counts[o_ * qpr:(o_ + 1) * qpr]) for o_ in range(world)]
-    send = torch.zeros((max(len(events), 1), 2), dtype=torch.int64)
-    for i, (s, d) in enumerate(events):
-        send[i, 0] = struct.unpack("<q", struct.pack("<d", s))[0]
-        send[i, 1] = d
-    if fixed:
-        # the product's fixed slots: owner o's events at [o * slot, ...), query order
-        slot = max(totals) + 3
-        fsend = torch.zeros((world * slot, 2), dtype=torch.int64)
-        at = 0
-        for o_ in range(world):
-            fsend[o_ * slot:o_ * slot + totals[o_]] = send[at:at + totals[o_]]
-            at += totals[o_]
-        rcounts, recv = exchange_fixed(torch.tensor(counts, dtype=torch.int32), fsend, world, qpr, slot)
-        rbase = [g * slot for g in range(world)]
-    else:
-        rcounts, recv, rbase = exchange(torch.tensor(counts, dtype=torch.int32), send, totals, world, qpr)
+    # the product's regions: owner o's queries o*qpr .. o*qpr+qpr-1
+    slot = max(1, max(sum(counts[o_ * qpr:(o_ + 1) * qpr]) for o_ in range(world)) + 3)
+    rw = 2 * region_events(qpr, slot)            # int64 words per region
+    meta_words = 2 * ((qpr + 1) // 2)
+    send = torch.full((world * rw,), -7, dtype=torch.int64)
+    ev = 0
+    for o_ in range(world):
+        base = o_ * rw
+        meta = torch.zeros(2 * meta_words, dtype=torch.int32)
+        off = 0
+        for i in range(qpr):
+            c = counts[o_ * qpr + i]
+            meta[2 * i], meta[2 * i + 1] = c, off
+            for j in range(c):
+                s_, d_ = events[ev + j]
+                send[base + meta_words + 2 * (off + j)] = struct.unpack("<q", struct.pack("<d", s_))[0]
+                send[base + meta_words + 2 * (off + j) + 1] = d_
+            ev += c
+            off += c
+        send[base:base + meta_words] = meta.view(torch.int64)
+    recv = exchange_regions(send, world)
     res = []
     for qi in range(qpr):
         stream = []
         for g in range(world):
-            off = rbase[g] + int(rcounts[g, :qi].sum())
-            for j in range(int(rcounts[g, qi])):
-                s = struct.unpack("<d", struct.pack("<q", int(recv[off + j, 0])))[0]
-                stream.append((s, int(recv[off + j, 1])))
+            base = g * rw
+            meta = recv[base:base + meta_words].view(torch.int32)
+            c, off = int(meta[2 * qi]), int(meta[2 * qi + 1])
+            for j in range(c):
+                w0 = int(recv[base + meta_words + 2 * (off + j)])
+                stream.append((struct.unpack("<d", struct.pack("<q", w0))[0],
+                               int(recv[base + meta_words + 2 * (off + j) + 1])))
         top, _ = hm.rank_stream(stream, k)
         res.append([(d, s) for s, d in top])
     result_q.put((rank, res, superset_ok))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k,fixed", [(3, False), (10, False), (10, True)])
-def test_gloo_two_rank_exchange_is_exact(indexes, k, fixed):
+@pytest.mark.parametrize("k", [3, 10])
+def test_gloo_two_rank_exchange_is_exact(indexes, k):
     import random
     from oracle.oracle import OracleVacuum
     d = indexes["wiki5"][0]
@@ -114,7 +124,7 @@ def test_gloo_two_rank_exchange_is_exact(indexes, k, fixed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, d, queries, k, q, fixed)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, d, queries, k, q)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}

@@ -1,7 +1,10 @@
 """Doc-range shards on one GPU: W shard engines in one process run the device
-shard-reduce / pack / owner-replay kernels; the all_to_all is done by tensor
-slicing (the collective itself is covered by test_shard_exchange.py with gloo).
-Results must equal the unsharded engine and the oracle bit for bit."""
+halves of wsr_shard_step (wsr_shard_step_emit: plan + segments with each
+query's reduced events emitted into its owner's region; wsr_shard_step_replay:
+the owner replay), with the regions moved by copies exactly as the step's
+ncclAllToAll moves them (the collective itself is covered by
+test_shard_exchange.py with gloo, and with one RCCL rank below).  Results must
+equal the oracle bit for bit."""
 import ctypes as C
 import os
 import random
@@ -13,56 +16,87 @@ from conftest import DATA
 pytestmark = pytest.mark.gpu
 
 
-def _run_sharded(index_dir, queries, k, world, phrase=False):
-    import torch
+def open_shards(index_dir, world, positions=False):
+    """The W shard engines of a doc-range split of index_dir."""
+    import wiser_amd as w
+    from wiser_amd.shard import index_doc_count, shard_range
+    n = index_doc_count(index_dir)
+    engs = []
+    try:
+        for r in range(world):
+            e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=positions)
+            e.Load()
+            engs.append(e)
+    except Exception:
+        for e in engs:
+            e.close()
+        raise
+    return engs
+
+
+def _run_step_regions(index_dir, queries, k, world, slot, phrase=False, engines=None):
+    """wsr_shard_step's own buffers at W > 1 (ADVICE r2): every shard runs
+    wsr_shard_step_emit (fused emission into the engine's region buffer, owner
+    o's {count, offset} block inside region o, region stride = meta + slot), the
+    regions are moved exactly as ncclAllToAll moves them (region o of rank g ->
+    region g of rank o), and wsr_shard_step_replay replays each owner.  slot
+    None: sized from a first emission's fill (wsr_shard_fill), as bench.py does."""
+    import numpy as np
     import wiser_amd as w
     from wiser_amd import _capi
     from wiser_amd._capi import check, lib
-    from wiser_amd.shard import index_doc_count, shard_range
+    from wiser_amd.shard import slot_for_fill
     qpr = len(queries) // world
     queries = queries[:qpr * world]
-    n = index_doc_count(index_dir)
-    engs, batches, counts, sends, totals = [], [], [], [], []
-    for r in range(world):
-        e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world))
-        e.Load()
-        arr = (_capi.Query * len(queries))()
-        for i, q in enumerate(queries):
-            arr[i] = e.resolve(w.SearchQuery(q, n_results=k, is_phrase=phrase))[0]
-        b = w.ResidentBatch(e, len(queries), k)
-        b.upload(arr)
-        check(lib.wsr_batch_run_events(e._h, b._b))
-        cnt = torch.empty(len(queries), dtype=torch.int32, device="cuda")
-        tot = (C.c_int64 * world)()
-        check(lib.wsr_shard_reduce(e._h, b._b, qpr, world, C.c_void_p(cnt.data_ptr()), tot))
-        send = torch.empty((max(sum(tot), 1), 2), dtype=torch.int64, device="cuda")
-        check(lib.wsr_shard_pack(e._h, b._b, C.c_void_p(send.data_ptr())))
-        engs.append(e); batches.append(b); counts.append(cnt); sends.append(send)
-        totals.append(list(tot))
-    out = []
-    for o in range(world):   # owner o receives slice o of every shard's send buffer
-        rcounts = torch.stack([counts[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
-        parts, rbase, acc = [], [], 0
-        for g in range(world):
-            start = sum(totals[g][:o])
-            parts.append(sends[g][start:start + totals[g][o]])
-            rbase.append(acc)
-            acc += totals[g][o]
-        recv = torch.cat(parts + [torch.zeros((1, 2), dtype=torch.int64, device="cuda")]).contiguous()
-        e, b = engs[o], batches[o]
-        torch.cuda.synchronize()   # (torch built rcounts / recv on its own stream)
-        check(lib.wsr_owner_replay(e._h, b._b, o * qpr, qpr, world, C.c_void_p(rcounts.data_ptr()),
-                                   C.c_void_p(recv.data_ptr()), (C.c_uint64 * world)(*rbase)))
-        hits = (_capi.Hit * (qpr * k))()
-        nh = (C.c_int32 * qpr)()
-        check(lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh))
-        for i in range(qpr):
-            out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
-    for b in batches:
-        b.close()
-    for e in engs:
-        e.close()
-    return queries, out
+    engs = engines or open_shards(index_dir, world, positions=phrase)
+    batches = []
+    try:
+        for e in engs:
+            arr = (_capi.Query * len(queries))()
+            for i, q in enumerate(queries):
+                arr[i] = e.resolve(w.SearchQuery(q, n_results=k, is_phrase=phrase))[0]
+            b = w.ResidentBatch(e, len(queries), k)
+            batches.append(b)
+            b.upload(arr)
+
+        def emit(slot):
+            rb = C.c_uint64()
+            check(lib.wsr_shard_step_regions(qpr, slot, C.byref(rb)))
+            words = rb.value // 8
+            sends = []
+            for e, b in zip(engs, batches):
+                send = np.full(world * words, -7, dtype=np.int64)
+                check(lib.wsr_shard_step_emit(e._h, b._b, world, qpr, slot, C.c_void_p(send.ctypes.data)))
+                sends.append(send.reshape(world, words))
+            return sends
+        if slot is None:
+            sends = emit(64 * qpr)
+            fill = 0
+            for e, b in zip(engs, batches):
+                tot = (C.c_int64 * world)()
+                check(lib.wsr_shard_fill(e._h, b._b, world, tot))
+                fill = max(fill, max(tot))
+            slot = slot_for_fill(fill, qpr)
+        sends = emit(slot)
+        out = []
+        for o in range(world):
+            recv = np.ascontiguousarray(np.stack([sends[g][o] for g in range(world)]))
+            e, b = engs[o], batches[o]
+            check(lib.wsr_shard_step_replay(e._h, b._b, o, world, qpr, slot, C.c_void_p(recv.ctypes.data)))
+            hits = (_capi.Hit * (qpr * k))()
+            nh = (C.c_int32 * qpr)()
+            rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
+            if rc:
+                raise _capi.WiserError(rc, lib.wsr_last_error().decode())
+            for i in range(qpr):
+                out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
+        return queries, out
+    finally:
+        for b in batches:
+            b.close()
+        if engines is None:
+            for e in engs:
+                e.close()
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
@@ -76,7 +110,7 @@ def test_sharded_equals_oracle_wiki5(indexes, world):
     qs = ([rng.sample(freq, 2) for _ in range(120)] + [[t] for t in rng.sample(toks, 60)] +
           [rng.sample(toks, 2) for _ in range(60)] + [rng.sample(freq, 3) for _ in range(40)])
     for k in (1, 10):
-        qs2, got = _run_sharded(d, qs, k, world)
+        qs2, got = _run_step_regions(d, qs, k, world, slot=None)
         for q, g in zip(qs2, got):
             assert g == o.search(q, k)[0], (world, k, q)
 
@@ -90,193 +124,13 @@ def test_sharded_equals_oracle_synthetic(synth_small, world):
     w.gen_two_term_log(d, log, n_queries=800, seed=11)
     qs = [l.split() for l in open(log).read().splitlines()]
     o = OracleVacuum(d)
-    qs2, got = _run_sharded(d, qs, 10, world)
+    qs2, got = _run_step_regions(d, qs, 10, world, slot=None)
     for q, g in zip(qs2, got):
         assert g == o.search(q, 10)[0], q
 
 
-def _run_sharded_fixed(index_dir, queries, k, world, slot):
-    """The fixed-slot exchange (wsr_shard_pack_fixed / wsr_owner_replay_fixed):
-    slot o of shard g's send buffer goes to owner o as its slot g."""
-    import torch
-    import wiser_amd as w
-    from wiser_amd import _capi
-    from wiser_amd._capi import check, lib
-    from wiser_amd.shard import index_doc_count, shard_range
-    qpr = len(queries) // world
-    queries = queries[:qpr * world]
-    n = index_doc_count(index_dir)
-    engs, batches, counts, sends = [], [], [], []
-    for r in range(world):
-        e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
-        e.Load()
-        arr = (_capi.Query * len(queries))()
-        for i, q in enumerate(queries):
-            arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
-        b = w.ResidentBatch(e, len(queries), k)
-        b.upload(arr)
-        check(lib.wsr_batch_run_events(e._h, b._b))
-        cnt = torch.empty(len(queries), dtype=torch.int32, device="cuda")
-        send = torch.empty((world * slot, 2), dtype=torch.int64, device="cuda")
-        check(lib.wsr_shard_pack_fixed(e._h, b._b, qpr, world, slot, C.c_void_p(cnt.data_ptr()),
-                                       C.c_void_p(send.data_ptr())))
-        check(lib.wsr_sync(e._h))
-        engs.append(e); batches.append(b); counts.append(cnt); sends.append(send)
-    out = []
-    for o in range(world):
-        rcounts = torch.stack([counts[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
-        recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
-        e, b = engs[o], batches[o]
-        torch.cuda.synchronize()   # (torch built rcounts / recv on its own stream)
-        check(lib.wsr_owner_replay_fixed(e._h, b._b, o * qpr, qpr, world, slot,
-                                         C.c_void_p(rcounts.data_ptr()), C.c_void_p(recv.data_ptr())))
-        hits = (_capi.Hit * (qpr * k))()
-        nh = (C.c_int32 * qpr)()
-        rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
-        if rc:
-            for x in batches:
-                x.close()
-            for x in engs:
-                x.close()
-            raise _capi.WiserError(rc, lib.wsr_last_error().decode())
-        for i in range(qpr):
-            out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
-    for b in batches:
-        b.close()
-    for e in engs:
-        e.close()
-    return queries, out
-
-
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_fixed_slot_exchange_equals_oracle(synth_small, world):
-    from oracle.oracle import OracleVacuum
-    import wiser_amd as w
-    d, _ = synth_small
-    log = os.path.join(d, "qshard_fixed.log")
-    w.gen_two_term_log(d, log, n_queries=960, seed=12)
-    qs = [l.split() for l in open(log).read().splitlines()]
-    o = OracleVacuum(d)
-    qpr = len(qs) // world
-    qs2, got = _run_sharded_fixed(d, qs, 10, world, slot=64 * qpr)
-    for q, g in zip(qs2, got):
-        assert g == o.search(q, 10)[0], (world, q)
-
-
-def test_fixed_slot_overflow_is_loud(synth_small):
-    """A slot too small for a shard's events fails the owner's fetch (exchange
-    flag) instead of returning a result built from dropped events."""
-    import wiser_amd as w
-    from wiser_amd import _capi
-    d, _ = synth_small
-    head = [f"t{i:07d}" for i in range(8)]
-    qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
-    with pytest.raises(_capi.WiserError, match="exchange slot"):
-        _run_sharded_fixed(d, qs, 10, 2, slot=4)
-
-
-def _run_sharded_emit(index_dir, queries, k, world, slot):
-    """The fused exchange of wsr_shard_step with the RCCL transfer done by
-    copies on one device: wsr_shard_emit per shard (segment kernels append
-    reduced events to the owners' slots), then wsr_owner_replay_meta per owner."""
-    import torch
-    import wiser_amd as w
-    from wiser_amd import _capi
-    from wiser_amd._capi import check, lib
-    from wiser_amd.shard import index_doc_count, shard_range
-    qpr = len(queries) // world
-    queries = queries[:qpr * world]
-    n = index_doc_count(index_dir)
-    engs, batches, metas, sends = [], [], [], []
-    try:
-        for r in range(world):
-            e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
-            e.Load()
-            engs.append(e)
-            arr = (_capi.Query * len(queries))()
-            for i, q in enumerate(queries):
-                arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
-            b = w.ResidentBatch(e, len(queries), k)
-            batches.append(b)
-            b.upload(arr)
-            meta = torch.full((len(queries), 2), -7, dtype=torch.int32, device="cuda")
-            send = torch.zeros((world * slot, 2), dtype=torch.int64, device="cuda")
-            torch.cuda.synchronize()   # (the fills run on torch's stream, the emit on the batch's)
-            check(lib.wsr_shard_emit(e._h, b._b, qpr, world, slot, C.c_void_p(meta.data_ptr()),
-                                     C.c_void_p(send.data_ptr())))
-            check(lib.wsr_sync(e._h))
-            fill = (C.c_int64 * world)()
-            check(lib.wsr_shard_fill(e._h, b._b, world, fill))
-            assert all(0 <= f for f in fill)
-            metas.append(meta)
-            sends.append(send)
-        out = []
-        for o in range(world):
-            rmeta = torch.stack([metas[g][o * qpr:(o + 1) * qpr] for g in range(world)]).contiguous()
-            recv = torch.cat([sends[g][o * slot:(o + 1) * slot] for g in range(world)]).contiguous()
-            e, b = engs[o], batches[o]
-            torch.cuda.synchronize()   # (torch built rmeta / recv on its own stream)
-            check(lib.wsr_owner_replay_meta(e._h, b._b, o * qpr, qpr, world, slot,
-                                            C.c_void_p(rmeta.data_ptr()), C.c_void_p(recv.data_ptr())))
-            hits = (_capi.Hit * (qpr * k))()
-            nh = (C.c_int32 * qpr)()
-            rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
-            if rc:
-                raise _capi.WiserError(rc, lib.wsr_last_error().decode())
-            for i in range(qpr):
-                out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
-        return queries, out
-    finally:
-        for b in batches:
-            b.close()
-        for e in engs:
-            e.close()
-
-
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_fused_emit_exchange_equals_oracle(synth_small, world):
-    from oracle.oracle import OracleVacuum
-    import wiser_amd as w
-    d, _ = synth_small
-    log = os.path.join(d, "qshard_emit.log")
-    w.gen_two_term_log(d, log, n_queries=960, seed=15)
-    qs = [l.split() for l in open(log).read().splitlines()]
-    o = OracleVacuum(d)
-    qpr = len(qs) // world
-    qs2, got = _run_sharded_emit(d, qs, 10, world, slot=64 * qpr)
-    for q, g in zip(qs2, got):
-        assert g == o.search(q, 10)[0], (world, q)
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_fused_emit_wide_k(synth_small, world):
-    """k > 64: the fused emission keeps every survivor of a wide query; the
-    owner replays them with the heap in LDS (owner_replay_meta_kernel<true>)."""
-    from oracle.oracle import OracleVacuum
-    import wiser_amd as w
-    d, _ = synth_small
-    log = os.path.join(d, "qshard_emit_wide.log")
-    w.gen_two_term_log(d, log, n_queries=240, seed=16)
-    qs = [l.split() for l in open(log).read().splitlines()]
-    o = OracleVacuum(d)
-    qpr = len(qs) // world
-    qs2, got = _run_sharded_emit(d, qs, 200, world, slot=4096 * qpr)
-    for q, g in zip(qs2, got):
-        assert g == o.search(q, 200)[0], (world, q)
-
-
-def test_fused_emit_overflow_is_loud(synth_small):
-    import wiser_amd as w  # noqa: F401
-    from wiser_amd import _capi
-    d, _ = synth_small
-    head = [f"t{i:07d}" for i in range(8)]
-    qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
-    with pytest.raises(_capi.WiserError, match="exchange slot"):
-        _run_sharded_emit(d, qs, 10, 2, slot=4)
-
-
 def test_native_rccl_step_one_rank(synth_small):
-    """wsr_shard_step (fused emission, RCCL communicator, grouped send/recv,
+    """wsr_shard_step (fused emission, RCCL communicator, one ncclAllToAll,
     owner replay on the communicator's stream) with a communicator of one rank,
     several steps in flight on two batches: equal to the oracle."""
     import wiser_amd as w
@@ -315,75 +169,6 @@ def test_native_rccl_step_one_rank(synth_small):
     for b in bs:
         b.close()
     S.close()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_fixed_slot_wide_k(synth_small, world):
-    """k > 64 through doc-range shards: the shard reduce keeps every survivor of
-    a wide query and the owner replays them with the heap in LDS."""
-    from oracle.oracle import OracleVacuum
-    import wiser_amd as w
-    d, _ = synth_small
-    log = os.path.join(d, "qshard_wide.log")
-    w.gen_two_term_log(d, log, n_queries=240, seed=14)
-    qs = [l.split() for l in open(log).read().splitlines()]
-    o = OracleVacuum(d)
-    qpr = len(qs) // world
-    qs2, got = _run_sharded_fixed(d, qs, 200, world, slot=4096 * qpr)
-    for q, g in zip(qs2, got):
-        assert g == o.search(q, 200)[0], (world, q)
-
-
-def _run_step_regions(index_dir, queries, k, world, slot):
-    """wsr_shard_step's own buffers at W > 1 (ADVICE r2): every shard runs
-    wsr_shard_step_emit (fused emission into the engine's region buffer, owner
-    o's {count, offset} block inside region o, region stride = meta + slot), the
-    regions are moved exactly as ncclAllToAll moves them (region o of rank g ->
-    region g of rank o), and wsr_shard_step_replay replays each owner."""
-    import numpy as np
-    import wiser_amd as w
-    from wiser_amd import _capi
-    from wiser_amd._capi import check, lib
-    from wiser_amd.shard import index_doc_count, shard_range
-    qpr = len(queries) // world
-    queries = queries[:qpr * world]
-    n = index_doc_count(index_dir)
-    rb = C.c_uint64()
-    check(lib.wsr_shard_step_regions(qpr, slot, C.byref(rb)))
-    words = rb.value // 8
-    engs, batches, sends = [], [], []
-    try:
-        for r in range(world):
-            e = w.VacuumEngine(index_dir, doc_range=shard_range(n, r, world), positions=False)
-            e.Load()
-            engs.append(e)
-            arr = (_capi.Query * len(queries))()
-            for i, q in enumerate(queries):
-                arr[i] = e.resolve(w.SearchQuery(q, n_results=k))[0]
-            b = w.ResidentBatch(e, len(queries), k)
-            batches.append(b)
-            b.upload(arr)
-            send = np.full(world * words, -7, dtype=np.int64)
-            check(lib.wsr_shard_step_emit(e._h, b._b, world, qpr, slot, C.c_void_p(send.ctypes.data)))
-            sends.append(send.reshape(world, words))
-        out = []
-        for o in range(world):
-            recv = np.ascontiguousarray(np.stack([sends[g][o] for g in range(world)]))
-            e, b = engs[o], batches[o]
-            check(lib.wsr_shard_step_replay(e._h, b._b, o, world, qpr, slot, C.c_void_p(recv.ctypes.data)))
-            hits = (_capi.Hit * (qpr * k))()
-            nh = (C.c_int32 * qpr)()
-            rc = lib.wsr_batch_fetch_range(e._h, b._b, o * qpr, qpr, hits, nh)
-            if rc:
-                raise _capi.WiserError(rc, lib.wsr_last_error().decode())
-            for i in range(qpr):
-                out.append([(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])])
-        return queries, out
-    finally:
-        for b in batches:
-            b.close()
-        for e in engs:
-            e.close()
 
 
 @pytest.mark.parametrize("world,k", [(2, 10), (3, 10), (8, 10), (3, 200)])

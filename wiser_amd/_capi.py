@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# WISER_HIP_LIB: diagnostics only (the section-timer build, `make prof`)
+# WISER_HIP_LIB: an A/B build of the same sources (scripts only)
 LIB_PATH = os.environ.get("WISER_HIP_LIB") or os.path.join(HERE, "_lib", "libwiser_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "wiser_hip.h")
 
@@ -100,39 +100,28 @@ _sigs = {
                                    C.POINTER(C.c_int32)]),
     "wsr_check_query": (C.c_int, [_P, C.POINTER(Query)]),
     "wsr_resolve_text": (C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int32, C.c_int32, C.POINTER(Query),
-                                   C.POINTER(C.c_int32)]),
+                                   C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int64]),
     "wsr_search_text": (C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                   C.POINTER(Hit), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_batch_create": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_batch_destroy": (None, [_P, _P]),
     "wsr_batch_upload": (C.c_int, [_P, _P, C.POINTER(Query), C.c_int32]),
     "wsr_batch_run": (C.c_int, [_P, _P]),
-    "wsr_batch_run_events": (C.c_int, [_P, _P]),
     "wsr_sync": (C.c_int, [_P]),
     "wsr_batch_fetch": (C.c_int, [_P, _P, C.POINTER(Hit), C.POINTER(C.c_int32)]),
     "wsr_batch_stats_get": (C.c_int, [_P, _P, C.POINTER(BatchStats)]),
-    "wsr_batch_device_results": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_P)]),
-    "wsr_shard_reduce": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_int64)]),
-    "wsr_shard_pack": (C.c_int, [_P, _P, _P]),
-    "wsr_owner_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, _P, _P,
-                                   C.POINTER(C.c_uint64)]),
     "wsr_batch_fetch_range": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.POINTER(Hit),
                                         C.POINTER(C.c_int32)]),
     "wsr_stream": (C.c_int, [_P, C.POINTER(_P)]),
     "wsr_batch_stream": (C.c_int, [_P, _P, C.POINTER(_P)]),
-    "wsr_shard_pack_fixed": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_shard_fill": (C.c_int, [_P, _P, C.c_int32, C.POINTER(C.c_int64)]),
-    "wsr_owner_replay_fixed": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_close": (None, [_P]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
-    "wsr_shard_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_shard_step_regions": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint64)]),
     "wsr_shard_step_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_shard_step_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),
-    "wsr_debug_replay_profile": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
-    "wsr_owner_replay_meta": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,

@@ -100,9 +100,8 @@ struct wsr_handle {
   uint8_t* d_c4 = nullptr;
   double* d_cache = nullptr;
   DenseEnt* d_dense = nullptr;
-  uint32_t* d_dense_rk = nullptr;   // WSR_DENSE_FMT 2: the bitmap entries' ranks
+  uint32_t* d_dense_rk = nullptr;   // the bitmap entries' rank records
   uint8_t* d_tf8 = nullptr;
-  uint8_t* d_wmax = nullptr;
   uint8_t* d_plen = nullptr;
   uint32_t* d_tails = nullptr;
   uint8_t* d_pos_blob = nullptr;    // positions (opened with wsr_open_opts::positions)
@@ -115,15 +114,12 @@ struct wsr_handle {
   bool positions = false;
   uint32_t dense_lists = 0;
   wsr_image_info info{};            // HBM bytes of the image's buffers
-  bool fuse_replay = true;
-  bool seg_floor = true;
   std::vector<ListDev> lists;       // host copy of the directory heads
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
   std::vector<BlockDev> blocks;     // host copy (debug decode)
   std::vector<uint32_t> meta;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
-  int merge_wgs = 0;   // merge kernel: workgroups of kMergeWaves waves
   int gen_cap = 0;     // general workgroups launched at most
 };
 
@@ -152,32 +148,25 @@ struct wsr_batch {
   bool two_only = false;         // every query: two terms (or empty), k <= kMaxK, no phrase
   int seg_grid = 0;
   int lean_wgs = 0;
-  int merge_wgs = 0;              // 0: the batch has no merge item
-  // doc-range shard exchange
-  uint64_t* d_soff = nullptr;     // per query send offset (events)
-  int64_t* d_otot = nullptr;      // per owner totals
-  int32_t* d_scount = nullptr;    // per query reduced event count (last wsr_shard_reduce)
-  uint64_t* d_roff = nullptr;     // owner side per (shard, query) offsets
-  uint64_t* d_rbase = nullptr;
-  size_t roff_cap = 0;
-  // native exchange (wsr_shard_step): per owner a region of {count, offset}
-  // pairs + an event slot, owner-major to send, shard-major received;
+  // doc-range shard exchange (wsr_shard_step): per owner a region of {count,
+  // offset} pairs + an event slot, owner-major to send, shard-major received;
   // allocated on first use
   Event* d_xsend = nullptr;
   Event* d_xrecv = nullptr;
   uint64_t x_slots = 0;     // region events * pairs the two exchange buffers were sized for
   int x_pairs = 0;
-  hipEvent_t xev[2] = {nullptr, nullptr};   // pack done -> comm stream; exchange done -> replay
+  hipEvent_t xev[2] = {nullptr, nullptr};   // emission done -> comm stream; exchange done -> replay
   bool x_pending = false;   // a shard step's exchange + owner replay (xev[1]) not yet joined
-  bool x_fused = false;     // the last exchange was a wsr_shard_step (fill counters after d_ctr)
+  bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
+  int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
+  int64_t x_slot = 0;           //     and slot (the replay half must match them)
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
   // device (one's plan and first items under the other's last items); the
-  // general kernel goes to st2 and the merge kernel to st3, forked from and
-  // joined back into st.
-  hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, join3 = nullptr;
+  // general kernel goes to st2, forked from and joined back into st.
+  hipStream_t st = nullptr, st2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   bool ran = false;
 };
 
@@ -232,19 +221,18 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // en-Wikipedia-shaped C3 corpus this halves the mixed batch against 128,
     // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
     // caps the bitmaps' HBM, longest lists first: 48 GB, as the 8-byte rank
-    // records (WSR_RANK_TF) put the C3 stand-in's at 33 GB)
+    // records put the C3 stand-in's at 33 GB)
     const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048));
     const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 48) * 1e9);
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
-    // replay inside the segment kernel (WSR_FUSE_REPLAY=0: separate launch)
-    h->fuse_replay = env_number("WSR_FUSE_REPLAY", 1) != 0;
-    // segments start from the score floor of the query's earlier segments
-    // (WSR_SEG_FLOOR=0: every segment from an empty top-k)
-    h->seg_floor = env_number("WSR_SEG_FLOOR", 1) != 0;
     h->positions = opts && opts->positions;
     const uint32_t bloom_factor = opts && opts->bloom_factor > 0 ? static_cast<uint32_t>(opts->bloom_factor) : 0u;
+    // (the bitmaps are sized to what the device has free: an image larger than
+    // the free HBM drops the bitmaps of its shortest dense lists first)
+    size_t hbm_free = 0, hbm_total = 0;
+    HIP_OK(hipMemGetInfo(&hbm_free, &hbm_total));
     HostImage img = build_image(h->idx, lo, hi, std::min(threads, 32), dense_div, h->positions, dense_budget,
-                                bloom_factor > 0);
+                                bloom_factor > 0, hbm_free);
     if (img.has_blooms) {   // (counted with the position boxes)
       h->info.pos_bytes += dev_upload(&h->d_blm, img.blm);
       h->info.pos_bytes += dev_upload(&h->d_blm_hash, img.blm_hash);
@@ -271,7 +259,6 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     }
     h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
     h->info.dense_bytes += dev_upload(&h->d_dense_rk, img.dense_rank);
-    h->info.dense_bytes += dev_upload(&h->d_wmax, img.wmax);   // (the window maxima with the bitmaps)
     h->info.tf8_bytes = dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
     h->info.dense_lists = img.dense_lists;
@@ -279,14 +266,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.dense = h->d_dense;
     h->args.dense_rk = h->d_dense_rk;
     h->args.tf8 = h->d_tf8;
-    h->args.wmax = h->d_wmax;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
-    h->args.and_wpb = static_cast<float>(env_number("WSR_AND_WPB", 0.0));
-    // merge class (merge_kernel): O1 at most WSR_MERGE_RATIO times the driver's
-    // blocks (0: off), a driver of at least WSR_MERGE_MIN blocks
-    h->args.merge_ratio = static_cast<float>(env_number("WSR_MERGE_RATIO", 0.0));
-    h->args.merge_min = static_cast<uint32_t>(env_number("WSR_MERGE_MIN", 2));
     h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
     h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
@@ -329,9 +310,6 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     int locc = lean_kernel_occupancy();
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
-    int mocc = merge_kernel_occupancy();
-    if (mocc < 1) mocc = 1;
-    h->merge_wgs = prop.multiProcessorCount * std::min(mocc, 16);
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -352,7 +330,6 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_dense_rk),
                   static_cast<void*>(h->d_tf8),
-                  static_cast<void*>(h->d_wmax),
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
@@ -572,15 +549,12 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
-                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1) +
-                                       kMergeWaves * std::max(h->merge_wgs, 1))));
+                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&b->st3, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&b->fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&b->join, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&b->join3, hipEventDisableTiming));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
     return fail(WSR_E_HIP, e.what());
@@ -593,7 +567,6 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (!b) return;
   if (b->st) (void)hipStreamSynchronize(b->st);
   if (b->st2) (void)hipStreamSynchronize(b->st2);
-  if (b->st3) (void)hipStreamSynchronize(b->st3);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_desc), static_cast<void*>(b->d_part),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
@@ -601,8 +574,6 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
                   static_cast<void*>(b->d_nhits), static_cast<void*>(b->d_stats),
                   static_cast<void*>(b->d_qdone), static_cast<void*>(b->d_itemq),
                   static_cast<void*>(b->d_pub), static_cast<void*>(b->d_ph),
-                  static_cast<void*>(b->d_soff), static_cast<void*>(b->d_otot),
-                  static_cast<void*>(b->d_roff), static_cast<void*>(b->d_rbase),
                   static_cast<void*>(b->d_xsend), static_cast<void*>(b->d_xrecv)})
     if (p) (void)hipFree(p);
   if (b->h_ctr) (void)hipHostFree(b->h_ctr);
@@ -610,10 +581,8 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
   if (b->fork) (void)hipEventDestroy(b->fork);
   if (b->join) (void)hipEventDestroy(b->join);
-  if (b->join3) (void)hipEventDestroy(b->join3);
   if (b->st) (void)hipStreamDestroy(b->st);
   if (b->st2) (void)hipStreamDestroy(b->st2);
-  if (b->st3) (void)hipStreamDestroy(b->st3);
   delete b;
 }
 
@@ -641,7 +610,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   uint64_t ev_need = 0, items_need = 0, algo = 0;
   // the device's class rule (plan_query_kernel), restated to size the two
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
-  uint64_t lean_need = 0, gen_need = 0, merge_need = 0;
+  uint64_t lean_need = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
   bool has_phrase = false, has_wide = false, two_only = true;
   std::vector<int32_t> ids;
@@ -683,19 +652,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
         const ListDev& L = h->lists[ids[t]];
         return L.bm != kNoDense && static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin);
       };
-      int o1 = -1;
+      bool lean = true;
       for (int t = 0; t < d.n_terms; ++t)
-        if (t != drv && (o1 < 0 || h->lists[ids[t]].nblk < h->lists[ids[o1]].nblk)) o1 = t;
-      bool lean = true, merge = o1 >= 0 && !phrase && nbmin >= h->args.merge_min &&
-                                static_cast<float>(h->lists[ids[o1]].nblk) <=
-                                    h->args.merge_ratio * static_cast<float>(nbmin);
-      for (int t = 0; t < d.n_terms; ++t) {
-        if (t == drv || dense(t)) continue;
-        lean = false;
-        if (t != o1) merge = false;
-      }
-      // (the device's rule, plan_query_kernel: merge before lean and general)
-      (merge ? merge_need : lean ? lean_need : gen_need) += nbmin;
+        if (t != drv && !dense(t)) lean = false;
+      (lean ? lean_need : gen_need) += nbmin;
       for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[ids[t]];
       algo += 12ull * d.k;
     }
@@ -741,22 +701,12 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->nq = nq;
   b->has_phrase = has_phrase;
   b->has_wide = has_wide;
-#ifdef WSR_NO_TWO   // A/B: every batch on the general lean instance
-  b->two_only = false;
-  (void)two_only;
-#else
   b->two_only = two_only;
-#endif
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
       1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
-  // (merge items exist only when the merge class is on; the grid drains them all)
-  b->merge_wgs = h->args.merge_ratio > 0.0f
-                     ? static_cast<int>(std::max<uint64_t>(
-                           1, std::min<uint64_t>(h->merge_wgs, (merge_need + kMergeWaves - 1) / kMergeWaves)))
-                     : 0;
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -774,12 +724,16 @@ struct ShardEmit {
   uint64_t meta_stride;
 };
 
-static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* se = nullptr);
+static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se = nullptr);
 
-int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, true); }
-int wsr_batch_run_events(wsr_handle* h, wsr_batch* b) { return batch_run(h, b, false); }
+int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
 
-static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* se) {
+// One run of the batch: plan, then the lean and general segment kernels on
+// two streams; the worker that finishes a query's last item replays it
+// (se == nullptr) or emits its reduced events into the owner's exchange
+// region (a shard step).  Wide queries (k > kMaxK) of a plain run are
+// replayed by one more launch after the segments.
+static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   try {
     HIP_OK(hipSetDevice(h->device));
@@ -789,8 +743,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
     if (b->x_pending) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));
     b->x_pending = false;
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * (kNumCounters + (se ? se->owners : 0)), st));
-    const bool fused = (replay && h->fuse_replay) || se;
-    FusedReplay fr{fused ? b->d_qdone : nullptr, b->d_hits, b->stride, b->d_nhits};
+    FusedReplay fr{b->d_qdone, b->d_hits, b->stride, b->d_nhits};
     if (se) {
       fr.x_send = se->send;
       fr.x_meta = se->meta;
@@ -804,38 +757,26 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
     HIP_OK(hipEventRecord(b->ev[0], st));
     HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       kLeanWaves * b->lean_wgs, kMergeWaves * b->merge_wgs, b->seg_grid, fr, b->d_itemq,
-                       h->seg_floor ? b->d_pub : nullptr, b->d_desc, b->d_part, st));
+                       kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq, b->d_pub, b->d_desc,
+                       b->d_part, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
     // own queue, then the streams join
     HIP_OK(hipEventRecord(b->fork, st));
     HIP_OK(hipStreamWaitEvent(b->st2, b->fork, 0));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                           b->d_stats, b->seg_grid, fr, b->d_itemq,
-                           h->seg_floor ? b->d_pub : nullptr,
+                           b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
                            b->has_phrase ? b->d_ph : nullptr, b->st2));
     HIP_OK(hipEventRecord(b->join, b->st2));
-    if (b->merge_wgs) {   // merge items on the third stream
-      HIP_OK(hipStreamWaitEvent(b->st3, b->fork, 0));
-      HIP_OK(launch_merge(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                          b->d_stats + static_cast<size_t>(kStatStride) * (b->seg_grid + kLeanWaves * b->lean_wgs),
-                          b->merge_wgs, fr, b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc, b->st3));
-      HIP_OK(hipEventRecord(b->join3, b->st3));
-    }
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
-                       b->d_itemq, h->seg_floor ? b->d_pub : nullptr, b->d_desc,
+                       b->d_itemq, b->d_pub, b->d_desc,
                        b->has_phrase ? b->d_ph + static_cast<size_t>(kPhraseScratch) * std::max(h->gen_cap, 1)
                                      : nullptr, b->two_only, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
-    if (b->merge_wgs) HIP_OK(hipStreamWaitEvent(st, b->join3, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
-    if (replay && !fused)
-      HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
-                           b->d_nhits, st));
-    if (replay && b->has_wide)
+    if (!se && b->has_wide)
       HIP_OK(launch_wide_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
                                 b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
@@ -843,6 +784,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, bool replay, const ShardEmit* 
     return fail(WSR_E_HIP, e.what());
   }
   b->ran = true;
+  b->x_fused = se != nullptr;
   return WSR_OK;
 }
 
@@ -951,7 +893,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs + kMergeWaves * b->merge_wgs;
+    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
     std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * rows);
     HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     uint64_t sv = 0, db = 0, ob = 0;
@@ -990,13 +932,6 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
   return WSR_OK;
 }
 
-int wsr_batch_device_results(wsr_handle* h, wsr_batch* b, void** hits, void** n_hits) {
-  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
-  if (hits) *hits = b->d_hits;
-  if (n_hits) *n_hits = b->d_nhits;
-  return WSR_OK;
-}
-
 int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stride, wsr_hit* hits,
                      int32_t* n_hits) {
   if (!h || nq < 0 || (nq && (!q || !hits || !n_hits))) return fail(WSR_E_INVALID, "bad arguments");
@@ -1031,8 +966,9 @@ int wsr_search_batch(wsr_handle* h, const wsr_query* q, int32_t nq, int32_t stri
 }
 
 int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t max_q,
-                     wsr_query* q, int32_t* nq_out) {
-  if (!h || (!text && len > 0) || len < 0 || max_q < 0 || (max_q && !q) || !nq_out || k < 0)
+                     wsr_query* q, int32_t* nq_out, int32_t* more_store, int64_t more_cap) {
+  if (!h || (!text && len > 0) || len < 0 || max_q < 0 || (max_q && !q) || !nq_out || k < 0 ||
+      more_cap < 0 || (more_cap > 0 && !more_store))
     return fail(WSR_E_INVALID, "bad resolve_text arguments");
   // QueryProducerByLog (query_pool.h:319-378): one query per line, terms
   // separated by spaces, a line in double quotes is a phrase query; each term
@@ -1044,9 +980,8 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
   std::vector<const char*> tp;
   std::vector<uint32_t> tn;
   // (query, slot) of every parsed term; ids land in list_ids, or past 16 in
-  // this thread's overflow table (more_ids), once every term is looked up
+  // the caller's more_store (more_ids), once every term is looked up
   std::vector<std::pair<int32_t, int32_t>> dst;
-  thread_local std::vector<int32_t> overflow;
   std::vector<size_t> more_at(static_cast<size_t>(max_q), 0);
   size_t n_more = 0;
   tp.reserve(static_cast<size_t>(max_q) * 2);
@@ -1083,16 +1018,18 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
     for (int t = w.n_terms; t < WSR_MAX_TERMS; ++t) w.list_ids[t] = -1;
     ++n;
   }
+  if (static_cast<int64_t>(n_more) > more_cap)
+    return fail(WSR_E_LIMIT, "the text's queries need " + std::to_string(n_more) +
+                                 " more_ids entries, more_store holds " + std::to_string(more_cap));
   std::vector<int32_t> ids(tp.size());
   h->idx.find_many(tp.data(), tn.data(), tp.size(), ids.data());
-  overflow.assign(n_more, -1);
   for (size_t i = 0; i < ids.size(); ++i) {
     const int32_t qi = dst[i].first, slot = dst[i].second;
     if (slot < WSR_MAX_TERMS) q[qi].list_ids[slot] = ids[i];
-    else overflow[more_at[qi] + (slot - WSR_MAX_TERMS)] = ids[i];
+    else more_store[more_at[qi] + (slot - WSR_MAX_TERMS)] = ids[i];
   }
   for (int32_t i = 0; i < n; ++i)
-    if (q[i].n_terms > WSR_MAX_TERMS) q[i].more_ids = overflow.data() + more_at[i];
+    if (q[i].n_terms > WSR_MAX_TERMS) q[i].more_ids = more_store + more_at[i];
   *nq_out = n;
   return WSR_OK;
 }
@@ -1101,142 +1038,28 @@ int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int
                     int32_t max_q, wsr_hit* hits, int32_t* n_hits, int32_t* nq_out) {
   if (!h || !nq_out || max_q < 0) return fail(WSR_E_INVALID, "bad search_text arguments");
   std::vector<wsr_query> q(static_cast<size_t>(max_q));
-  int rc = wsr_resolve_text(h, text, len, k, max_q, q.data(), nq_out);
+  // (at most one more_ids entry per two text bytes: every term has a byte and
+  // a separator; the ids are consumed within this call, so a per-thread
+  // buffer is safe here)
+  thread_local std::vector<int32_t> more;
+  if (more.size() < static_cast<size_t>(len / 2 + 1)) more.resize(static_cast<size_t>(len / 2 + 1));
+  int rc = wsr_resolve_text(h, text, len, k, max_q, q.data(), nq_out, more.data(),
+                            static_cast<int64_t>(more.size()));
   if (rc) return rc;
   return wsr_search_batch(h, q.data(), *nq_out, hit_stride, hits, n_hits);
 }
 
-int wsr_shard_reduce(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
-                     int32_t* d_counts, int64_t* owner_totals) {
-  if (!h || !b || !b->ran || !d_counts || !owner_totals || q_per_owner <= 0 || n_owners <= 0 ||
-      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
-    return fail(WSR_E_INVALID, "bad shard_reduce arguments");
-  std::lock_guard<std::mutex> g(h->mu);
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = b->st;
-    if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
-    if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
-    if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
-    HIP_OK(hipMemsetAsync(b->d_otot, 0, sizeof(int64_t) * n_owners, st));
-    b->x_fused = false;
-    HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
-    HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
-    HIP_OK(hipMemcpyAsync(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    b->d_scount = d_counts;
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
-int wsr_shard_pack(wsr_handle* h, wsr_batch* b, void* d_send) {
-  if (!h || !b || !b->d_scount || !d_send) return fail(WSR_E_INVALID, "call wsr_shard_reduce first");
-  std::lock_guard<std::mutex> g(h->mu);
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    HIP_OK(launch_pack_events(b->d_plan, b->nq, b->d_events, b->d_scount, b->d_soff,
-                              static_cast<Event*>(d_send), b->st));
-    HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
-int wsr_owner_replay(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                     const int32_t* d_rcounts, const void* d_recv, const uint64_t* rbase) {
-  if (!h || !b || n_shards <= 0 || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq ||
-      (nq_owned && (!d_rcounts || !rbase)))
-    return fail(WSR_E_INVALID, "bad owner_replay arguments");
-  std::lock_guard<std::mutex> g(h->mu);
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = b->st;
-    const size_t n = static_cast<size_t>(n_shards) * nq_owned;
-    if (n > b->roff_cap) {
-      if (b->d_roff) HIP_OK(hipFree(b->d_roff));
-      b->roff_cap = n + 1024;
-      HIP_OK(hipMalloc(&b->d_roff, sizeof(uint64_t) * b->roff_cap));
-    }
-    if (!b->d_rbase) HIP_OK(hipMalloc(&b->d_rbase, sizeof(uint64_t) * 1024));
-    if (n_shards > 1024) return fail(WSR_E_LIMIT, "more than 1024 shards");
-    HIP_OK(hipMemcpyAsync(b->d_rbase, rbase, sizeof(uint64_t) * n_shards, hipMemcpyHostToDevice, st));
-    // per shard: exclusive scan of its counts over my queries
-    for (int32_t s2 = 0; s2 < n_shards; ++s2)
-      HIP_OK(launch_scan_counts(d_rcounts + static_cast<size_t>(s2) * nq_owned, nq_owned, 0,
-                                b->d_roff + static_cast<size_t>(s2) * nq_owned, nullptr, st));
-    HIP_OK(launch_owner_replay(b->d_q, q0, nq_owned, n_shards, d_rcounts, b->d_roff, b->d_rbase,
-                               static_cast<const Event*>(d_recv), b->d_hits, b->stride, b->d_nhits, st));
-    HIP_OK(hipStreamSynchronize(st));
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
-int wsr_shard_pack_fixed(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners,
-                         int64_t slot, int32_t* d_counts, void* d_send) {
-  if (!h || !b || !b->ran || !d_counts || !d_send || q_per_owner <= 0 || n_owners <= 0 || slot <= 0 ||
-      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
-    return fail(WSR_E_INVALID, "bad shard_pack_fixed arguments");
-  if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    hipStream_t st = b->st;
-    if (!b->d_soff) HIP_OK(hipMalloc(&b->d_soff, sizeof(uint64_t) * b->max_q));
-    if (!b->d_otot) HIP_OK(hipMalloc(&b->d_otot, sizeof(int64_t) * 1024));
-    b->x_fused = false;
-    HIP_OK(launch_shard_reduce(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, d_counts, st));
-    HIP_OK(launch_scan_counts(d_counts, b->nq, q_per_owner, b->d_soff, b->d_otot, st));
-    HIP_OK(launch_pack_fixed(b->d_plan, b->nq, b->d_events, d_counts, b->d_soff, q_per_owner,
-                             static_cast<uint64_t>(slot), static_cast<Event*>(d_send), b->d_ctr, st));
-    b->d_scount = d_counts;
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
 int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals) {
-  if (!h || !b || !(b->d_otot || b->x_fused) || !owner_totals || n_owners <= 0 || n_owners > kMaxOwners)
-    return fail(WSR_E_INVALID, "call wsr_shard_pack_fixed or wsr_shard_step first");
+  if (!h || !b || !b->x_fused || !owner_totals || n_owners <= 0 || n_owners > b->x_world)
+    return fail(WSR_E_INVALID, "call wsr_shard_step (or wsr_shard_step_emit) first");
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
     if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
-    if (b->x_fused) {   // the segment kernels' per-owner fill counters
-      std::vector<uint32_t> fill(n_owners);
-      HIP_OK(hipMemcpy(fill.data(), b->d_ctr + kNumCounters, sizeof(uint32_t) * n_owners, hipMemcpyDeviceToHost));
-      for (int i = 0; i < n_owners; ++i) owner_totals[i] = fill[i];
-    } else {
-      HIP_OK(hipMemcpy(owner_totals, b->d_otot, sizeof(int64_t) * n_owners, hipMemcpyDeviceToHost));
-    }
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
-int wsr_owner_replay_fixed(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                           int64_t slot, const int32_t* d_rcounts, const void* d_recv) {
-  if (!h || !b || n_shards <= 0 || nq_owned < 0 || q0 < 0 || q0 + nq_owned > b->nq || slot <= 0 ||
-      (nq_owned && (!d_rcounts || !d_recv)))
-    return fail(WSR_E_INVALID, "bad owner_replay_fixed arguments");
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    const size_t n = static_cast<size_t>(n_shards) * nq_owned;
-    if (n > b->roff_cap) {
-      if (b->d_roff) HIP_OK(hipFree(b->d_roff));
-      b->d_roff = nullptr;
-      b->roff_cap = n + 1024;
-      HIP_OK(hipMalloc(&b->d_roff, sizeof(uint64_t) * b->roff_cap));
-    }
-    HIP_OK(launch_owner_replay_fixed(b->d_q, q0, nq_owned, n_shards, d_rcounts, b->d_roff,
-                                     static_cast<uint64_t>(slot), static_cast<const Event*>(d_recv),
-                                     b->d_hits, b->stride, b->d_nhits, b->d_ctr, b->st));
+    // the segment kernels' per-owner fill counters
+    std::vector<uint32_t> fill(n_owners);
+    HIP_OK(hipMemcpy(fill.data(), b->d_ctr + kNumCounters, sizeof(uint32_t) * n_owners, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n_owners; ++i) owner_totals[i] = fill[i];
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
@@ -1322,20 +1145,6 @@ void wsr_comm_close(wsr_comm* c) {
   delete c;
 }
 
-int wsr_shard_emit(wsr_handle* h, wsr_batch* b, int32_t q_per_owner, int32_t n_owners, int64_t slot,
-                   int32_t* d_meta, void* d_send) {
-  if (!h || !b || !d_meta || !d_send || q_per_owner <= 0 || n_owners <= 0 || slot <= 0 ||
-      static_cast<int64_t>(q_per_owner) * n_owners < b->nq)
-    return fail(WSR_E_INVALID, "bad shard_emit arguments");
-  if (n_owners > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners owners");
-  if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
-  const ShardEmit se{n_owners, q_per_owner, static_cast<uint64_t>(slot), static_cast<Event*>(d_send),
-                     static_cast<uint64_t>(slot), d_meta, 2ull * static_cast<uint64_t>(q_per_owner)};
-  const int rc = batch_run(h, b, false, &se);
-  if (rc == WSR_OK) b->x_fused = true;
-  return rc;
-}
-
 static int owner_replay_meta_on(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
                                 const int32_t* d_rmeta, uint64_t meta_stride, uint64_t stride,
                                 const void* d_recv, hipStream_t st) {
@@ -1351,13 +1160,6 @@ static int owner_replay_meta_on(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t
     return fail(WSR_E_HIP, e.what());
   }
   return WSR_OK;
-}
-
-int wsr_owner_replay_meta(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq_owned, int32_t n_shards,
-                          int64_t slot, const int32_t* d_rmeta, const void* d_recv) {
-  if (!b || slot <= 0) return fail(WSR_E_INVALID, "bad owner_replay_meta arguments");
-  return owner_replay_meta_on(h, b, q0, nq_owned, n_shards, d_rmeta, 2ull * static_cast<uint64_t>(nq_owned),
-                              static_cast<uint64_t>(slot), d_recv, b->st);
 }
 
 // One step of a doc-range sharded batch, all of it enqueued, nothing waited on:
@@ -1409,8 +1211,12 @@ static int step_emit(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, in
   const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));   // int32 per region
   const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), b->d_xsend + meta_events, region,
                      reinterpret_cast<int32_t*>(b->d_xsend), meta_stride};
-  const int rc = batch_run(h, b, false, &se);
-  if (rc == WSR_OK) b->x_fused = true;
+  const int rc = batch_run(h, b, &se);
+  if (rc == WSR_OK) {
+    b->x_world = W;
+    b->x_qpr = q_per_owner;
+    b->x_slot = slot;
+  }
   return rc;
 }
 
@@ -1482,8 +1288,11 @@ int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_pe
 
 int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
                           int64_t slot, const void* host_recv) {
-  if (!h || !b || !host_recv || world < 1 || rank < 0 || rank >= world || !b->x_fused ||
-      b->x_pairs != world || region_events_of(q_per_owner, slot) * world > b->x_slots)
+  // (the regions are read at the strides the emission wrote them with: the
+  // arguments must be the ones of the preceding wsr_shard_step_emit)
+  if (!h || !b || !host_recv || world < 1 || rank < 0 || rank >= world || q_per_owner <= 0 || slot <= 0 ||
+      !b->x_fused || b->x_world != world || b->x_qpr != q_per_owner || b->x_slot != slot ||
+      static_cast<int64_t>(q_per_owner) * world != b->nq)
     return fail(WSR_E_INVALID, "call wsr_shard_step_emit with the same world, q_per_owner and slot first");
   try {
     HIP_OK(hipSetDevice(h->device));
@@ -1554,8 +1363,8 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                        int32_t* n_wg, int32_t* stride) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
-  // general workgroups, then lean waves, then merge waves
-  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs + kMergeWaves * b->merge_wgs;
+  // general workgroups, then lean waves
+  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
   if (n_wg) *n_wg = rows;
   if (stride) *stride = kStatStride;
   if (!out) return WSR_OK;
@@ -1567,33 +1376,6 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
     HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
-  }
-  return WSR_OK;
-}
-
-int wsr_debug_replay_profile(wsr_handle* h, wsr_batch* b, uint32_t* rows) {
-  if (!h || !b || !rows || !b->ran) return fail(WSR_E_INVALID, "run the batch (events) first");
-  std::lock_guard<std::mutex> g(h->mu);
-  uint32_t* d = nullptr;
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(b->st));
-    HIP_OK(hipMalloc(&d, sizeof(uint32_t) * 6 * std::max(b->nq, 1)));
-    HIP_OK(hipMemset(d, 0, sizeof(uint32_t) * 6 * std::max(b->nq, 1)));
-    const hipError_t e = set_replay_prof(d);
-    if (e != hipSuccess) {
-      (void)hipFree(d);
-      return fail(WSR_E_INVALID, "replay profile needs a -DWSR_REPLAY_PROF build");
-    }
-    HIP_OK(launch_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride, b->d_nhits,
-                         b->st));
-    HIP_OK(hipStreamSynchronize(b->st));
-    HIP_OK(set_replay_prof(nullptr));
-    HIP_OK(hipMemcpy(rows, d, sizeof(uint32_t) * 6 * b->nq, hipMemcpyDeviceToHost));
-    HIP_OK(hipFree(d));
-  } catch (const std::exception& ex) {
-    if (d) (void)hipFree(d);
-    return fail(WSR_E_HIP, ex.what());
   }
   return WSR_OK;
 }

@@ -37,49 +37,29 @@ constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 
 // Dense lists (df >= span / dense_div) also carry a rank bitmap of their doc
 // ids over the image's doc range, so that a probe costs one load + a popcount
-// instead of decoding the list's blocks.  rank = postings of the list (in the
-// image's blocks) before the entry's first doc; posting index = rank +
-// popcount of the lower bits; block = index / 128.
-//
-// WSR_DENSE_FMT 2 (the default): the masks and the ranks in two arrays (4
-// bytes per 32 docs each, DenseEnt = the mask word, HostImage::dense_rank the
-// ranks).  The lean kernel's probe of the most selective other list reads the
-// mask word alone (a 128-byte line covers 1,024 docs) and only a hit reads its
-// rank; at the en-Wikipedia shape a high-df driver's postings are ~180 docs
-// apart, so with the ranks beside the masks (WSR_DENSE_FMT 0: 8 bytes per 32
-// docs, 512 docs per line) nearly every probe fetched a line of its own from
-// HBM, and those line fetches bound the lean kernel (profiles/r03_probe_sweep.jsonl:
+// instead of decoding the list's blocks.  The masks and the rank records are
+// two arrays at the same index: DenseEnt = the 32-doc mask word (bit
+// (d - doc_lo) % 32 of doc d), HostImage::dense_rank = per entry an 8-byte
+// rank record {postings of the list (in the image's blocks) before the
+// entry's first doc, the 1-byte tfs of the word's first four postings (255:
+// more, or tf >= 255: read tf8)}; posting index = rank + popcount of the lower
+// bits, block = index / 128.  The lean kernel's probe of the most selective
+// other list reads the mask word alone (a 128-byte line covers 1,024 docs) and
+// only a hit reads its rank record, whose tf bytes give the hit's tf in the
+// same line.  At the en-Wikipedia shape a high-df driver's postings are ~180
+// docs apart, so with the ranks beside the masks (8 bytes per 32 docs, 512
+// docs per line) nearly every probe fetched a line of its own from HBM, and
+// those line fetches bound the lean kernel (profiles/r03_probe_sweep.jsonl:
 // ~12 CU-cycles per HBM line; r03_probe_forms.txt).  Other users (further
 // lists, the general kernel) load both words at once: one probe = two
 // independent loads.
-#ifndef WSR_DENSE_FMT
-#define WSR_DENSE_FMT 2
-#endif
 constexpr uint32_t kDenseDocs = 32;   // doc ids per DenseEnt
-#if WSR_DENSE_FMT == 2
 struct DenseEnt {
-  uint32_t w;        // bit (d - doc_lo) % 32 of doc d; its rank: HostImage::dense_rank, same index
+  uint32_t w;        // bit (d - doc_lo) % 32 of doc d; its rank record: HostImage::dense_rank, same index
 };
 static_assert(sizeof(DenseEnt) == 4, "DenseEnt layout");
-#elif WSR_DENSE_FMT == 0
-struct DenseEnt {
-  uint32_t rank;
-  uint32_t w;        // bit (d - doc_lo) % 32 of doc d
-};
-static_assert(sizeof(DenseEnt) == 8, "DenseEnt layout");
-#else
-#error "WSR_DENSE_FMT is 0 or 2"
-#endif
-// WSR_RANK_TF (format 2): a rank record is 8 bytes, the rank and the 1-byte
-// tfs of the word's first four postings (255: more, or tf >= 255: read tf8),
-// so that a hit's rank and tf come in one line; 0: the rank alone (4 bytes)
-#ifndef WSR_RANK_TF
-#define WSR_RANK_TF 1
-#endif
-constexpr uint32_t kRankWords = (WSR_DENSE_FMT == 2 && WSR_RANK_TF) ? 2 : 1;   // u32 per rank record
-constexpr uint64_t kDenseEntBytes = WSR_DENSE_FMT == 2 ? 4 + 4 * kRankWords : sizeof(DenseEnt);   // mask + rank
-constexpr uint32_t kWinEnts = 64;     // DenseEnts per tf-maximum window; every list's bitmap
-                                      // starts at a multiple of it
+constexpr uint32_t kRankWords = 2;                          // u32 per rank record
+constexpr uint64_t kDenseEntBytes = 4 + 4 * kRankWords;     // mask + rank record
 
 // Host form of an entry's bit test and rank (the kernels have their own).
 inline bool dense_ent_bit(const DenseEnt& e, uint32_t sh) { return (e.w >> sh) & 1u; }
@@ -142,8 +122,7 @@ struct QueryDesc {
   uint64_t o_bm;        // O1 (the other list with the fewest blocks): first bitmap entry
   uint64_t o_tf8;       //   offset of its 1-byte tfs
   uint64_t ev_base;     // = QueryPlan::ev_base
-  uint64_t a_bm;        // driver's bitmap / 1-byte tfs (kNoDense: none), for the
-  uint64_t a_tf8;       //   bitmap-intersection path of dense drivers
+  uint64_t rsv0, rsv1;
   double a_idf, o_idf;
   uint32_t a_blk0, a_nblk, a_tail_cnt;
   uint32_t min_last;    // smallest last doc id over the other lists
@@ -156,12 +135,10 @@ struct QueryDesc {
   // term (b_id = 2.2 * idf), b_iom / (b_m + norm) bounds all the other terms
   // (b_m = their largest tfmax, b_iom = sum of 2.2 * idf over them, times b_m)
   float b_id, b_iom, b_m;
-  uint32_t nt;          // n_terms | kDescWinBound (bit 31: a two-term query whose other-term
-                        // bound may use O1's per-window tf maxima)
+  uint32_t nt;          // n_terms
 };
 static_assert(sizeof(QueryDesc) == 128, "QueryDesc layout");
 constexpr uint32_t kNoSlot = 0xFFFFu;
-constexpr uint32_t kDescWinBound = 0x80000000u;
 
 // A heap-insertion event: a survivor that a top-k heap run from empty over its
 // segment inserts (query_processing.h:595-602).

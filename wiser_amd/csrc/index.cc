@@ -354,16 +354,15 @@ void for_each_list(int32_t L, int threads, F&& fn) {
 // the arrays in place.  (Millions of one-block lists -- the en-Wikipedia shape
 // -- made per-list vectors and their serial concatenation the load's cost.)
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
-                      uint32_t dense_div, bool positions, uint64_t dense_budget, bool blooms) {
+                      uint32_t dense_div, bool positions, uint64_t dense_budget, bool blooms,
+                      uint64_t hbm_free) {
   const int32_t L = idx.n_lists();
   const uint8_t* file = idx.file();
   const uint8_t* fend = file + idx.file_bytes();
   // doc ids a bitmap covers: the image's range clipped to the doc-length records
   const uint64_t span_end = std::min<uint64_t>(doc_hi, static_cast<uint64_t>(std::max(idx.n_docs(), 0)));
   const uint32_t span = span_end > doc_lo ? static_cast<uint32_t>(span_end - doc_lo) : 0u;
-  // (whole tf-maximum windows, so that every list's bitmap starts at a multiple of kWinEnts)
-  const uint64_t n_ent = ((static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs + kWinEnts - 1) /
-                         kWinEnts * kWinEnts;
+  const uint64_t n_ent = (static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs;   // entries per bitmap
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
   struct Info {            // pass 1: the list's share of the image
     uint32_t r0 = 0, r1 = 0;   // image rows [r0, r1); r0 >= r1: no docs in the image
@@ -454,6 +453,21 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   });
 
   lap("pass 1 (sizes)");
+  if (hbm_free) {
+    // the rest of the image: blob, directory and plen (152 B per block),
+    // decoded tails, blooms (positions are not sized yet: the 10 % margin)
+    uint64_t other = static_cast<uint64_t>(std::max(idx.n_docs(), 0));
+    for (int32_t id = 0; id < L; ++id) {
+      const Info& in = info[id];
+      if (in.r1 <= in.r0) continue;
+      const uint64_t nbl = in.r1 - in.r0;
+      other += in.bytes + nbl * (sizeof(BlockDev) + 8 + kPackSize) + (in.vtail ? 8ull * in.tail_cnt : 0);
+      if (blooms && positions) other += nbl * kPackSize * 32;
+    }
+    const uint64_t cap = hbm_free / 10 * 9;
+    const uint64_t room = cap > other ? cap - other : 0;
+    if (!dense_budget || dense_budget > room) dense_budget = room ? room : 1;
+  }
   // bitmap budget: when the dense lists' bitmaps + 1-byte tfs would exceed it,
   // the longest lists keep theirs (they are the ones probed most)
   if (dense_budget) {
@@ -519,11 +533,8 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.plen.resize(nb * kPackSize);
   img.tails.resize(ntail);
   img.dense.resize(ne);
-#if WSR_DENSE_FMT == 2
   img.dense_rank.resize(kRankWords * ne);
-#endif
   img.tf8.resize(ntf8);
-  img.wmax.resize(ne / kWinEnts);
 
   lap("pass 2 (offsets, allocation)");
   // ---- pass 3: fill in place
@@ -615,41 +626,28 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     }
     img.lists[id].tfmax = tfmax;   // (this worker's own list)
     if (in.dense) {
-      // rank bitmap: per kDenseDocs docs, the postings before them and the doc mask
+      // rank bitmap: per kDenseDocs docs the doc mask and the rank record (the
+      // postings before them, the tfs of the word's first four postings; 255:
+      // none, or escaped)
       DenseEnt* de = &img.dense[ld.bm];
       uint64_t i = 0;
       for (uint64_t e = 0; e < n_ent; ++e) {
         const uint64_t start = doc_lo + e * kDenseDocs;
         while (i < n_img && s.docs[i] < start) ++i;
         DenseEnt ent{};
-#if WSR_DENSE_FMT == 2
         img.dense_rank[kRankWords * (ld.bm + e)] = static_cast<uint32_t>(i);
-        if (kRankWords == 2) {   // the tfs of the word's first four postings (255: none / escape)
-          uint32_t t4 = 0xFFFFFFFFu;
-          for (uint64_t j = i, n = 0; n < 4 && j < n_img && s.docs[j] < start + kDenseDocs; ++j, ++n) {
-            const uint32_t t = s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape;
-            t4 = (t4 & ~(0xFFu << (8 * n))) | (t << (8 * n));
-          }
-          img.dense_rank[kRankWords * (ld.bm + e) + 1] = t4;
+        uint32_t t4 = 0xFFFFFFFFu;
+        for (uint64_t j = i, n = 0; n < 4 && j < n_img && s.docs[j] < start + kDenseDocs; ++j, ++n) {
+          const uint32_t t = s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape;
+          t4 = (t4 & ~(0xFFu << (8 * n))) | (t << (8 * n));
         }
-#else
-        ent.rank = static_cast<uint32_t>(i);
-#endif
+        img.dense_rank[kRankWords * (ld.bm + e) + 1] = t4;
         for (uint64_t j = i; j < n_img && s.docs[j] < start + kDenseDocs; ++j)
           ent.w |= 1u << static_cast<uint32_t>(s.docs[j] - start);
         de[e] = ent;
       }
       uint8_t* t8 = &img.tf8[ld.tf8];
       for (uint64_t j = 0; j < n_img; ++j) t8[j] = static_cast<uint8_t>(s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape);
-      // largest tf per 2,048-doc window (the lean kernel's pre-probe bound)
-      uint8_t* wm = &img.wmax[ld.bm / kWinEnts];
-      std::memset(wm, 0, n_ent / kWinEnts);
-      const uint64_t n_win = n_ent / kWinEnts;
-      for (uint64_t j = 0; j < n_img; ++j) {   // (docs past the span have no bitmap bit either)
-        if (s.docs[j] < doc_lo) continue;
-        const uint64_t wi = (s.docs[j] - doc_lo) / (static_cast<uint64_t>(kDenseDocs) * kWinEnts);
-        if (wi < n_win) wm[wi] = std::max(wm[wi], t8[j]);
-      }
     }
     if (positions) {
       // The list's position cozy box (flash_engine_dumper.h:78-104): the bag of
@@ -742,6 +740,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
             throw std::runtime_error("bad bloom box in '" + term + "'");
           const uint8_t* bm = bx + 1 + l;
           const uint8_t* items = bm + (n + 7) / 8;
+          if (items > fend) throw std::runtime_error("bloom box bitmap of '" + term + "' out of range");
           uint64_t phys = 0;
           for (uint64_t i = 0; i < n; ++i) {
             if (!(bm[i / 8] & (0x80u >> (i % 8)))) continue;
@@ -786,11 +785,7 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
   const uint32_t sh = rel % kDenseDocs;
   if (!dense_ent_bit(e, sh)) return -1;
-#if WSR_DENSE_FMT == 2
   const uint32_t idx = dense_ent_rank(e, img.dense_rank[kRankWords * (L.bm + rel / kDenseDocs)], sh);
-#else
-  const uint32_t idx = dense_ent_rank(e, e.rank, sh);
-#endif
   const uint8_t t = img.tf8[L.tf8 + idx];
   if (t != kTf8Escape) return t;
   const uint32_t j = idx / kPackSize;

@@ -125,10 +125,8 @@ struct HostImage {
   uint32_t doc_lo = 0, doc_hi = 0;
   uint64_t docid_tf_bytes = 0;  // sum of all lists' docid+tf spans in the image
   big_vector<DenseEnt> dense;   // rank bitmaps of the dense lists
-  big_vector<uint32_t> dense_rank;   // WSR_DENSE_FMT 2: the rank of each DenseEnt, same index
+  big_vector<uint32_t> dense_rank;   // the rank record of each DenseEnt (kRankWords u32), same index
   big_vector<uint8_t> tf8;      // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
-  big_vector<uint8_t> wmax;     // per dense list and 2,048-doc window (64 bitmap entries): its
-                                // largest tf, 255 = 255 or more (entry ListDev::bm / 64 + window)
   uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
   uint32_t dense_lists = 0;
   big_vector<uint32_t> tails;   // decoded VInts last blocks (ListDev::tail)
@@ -160,10 +158,12 @@ bool host_decode_block(const uint8_t* p, const uint8_t* end, int cnt, bool delta
 
 // dense_div > 0: lists with at least span / dense_div postings in the image get
 // a rank bitmap + 1-byte tf array (0 disables them); dense_budget > 0 caps the
-// bytes of all bitmaps + tf arrays (the longest lists keep theirs).
+// bytes of all bitmaps + tf arrays (the longest lists keep theirs).  hbm_free >
+// 0 (the device's free bytes): the budget is also clamped to 90 % of it minus
+// the rest of the image, so that an image never fails to fit for its bitmaps.
 HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, int threads,
                       uint32_t dense_div = 0, bool positions = false, uint64_t dense_budget = 0,
-                      bool blooms = false);
+                      bool blooms = false, uint64_t hbm_free = 0);
 
 // Host restatement of the device's dense probe (segment kernel): tf of doc in
 // list L of the image, -1 when absent or when L has no bitmap.

@@ -23,26 +23,18 @@ struct IndexArgs {
   uint32_t doc_lo, doc_hi;  // doc-id range of this image (shard)
   double avg;               // average doc length stored in my.doc_length
   const DenseEnt* dense;    // rank bitmaps of the dense lists (ListDev::bm)
-  const uint32_t* dense_rk; // WSR_DENSE_FMT 2: their ranks (same index), else null
+  const uint32_t* dense_rk; // their rank records (same index, kRankWords u32 each)
   const uint8_t* tf8;       // their 1-byte tfs (ListDev::tf8)
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
-  float and_wpb;            // lean items of a driver with a bitmap intersect bitmaps word by
-                            // word when their doc span is <= and_wpb 32-doc words per driver
-                            // block (0 = never)
-  float merge_ratio;        // merge class: the most selective other list O1 has at most
-                            // merge_ratio times the driver's blocks (0 = never); O1 is then
-                            // decoded beside the driver and the two merged, not probed
-  uint32_t merge_min;       //   ... and the driver at least merge_min blocks
   // positions (phrase queries; null unless the engine was opened with them)
   const uint8_t* pos_blob;  // every list's position cozy box, byte-exact from my.vacuum
   const PosDev* pos_lists;  // indexed by list id
   const uint2* pos_pk;      // per full pack: byte offset from PosDev::base, bit width
   const uint32_t* pos_tail; // decoded VInts remainders
   const uint32_t* pos_start;// bag start entry of every posting, 128 slots per image block
-  const uint8_t* wmax;      // per dense list and 2,048-doc window: its largest tf (HostImage::wmax)
   // phrase bloom filters (null / 0 unless a bloom index was opened with
   // positions and bloom_factor > 0): per posting slot two 16-byte bit arrays
   // (prior, next), per list its term's two hashes; bloom_factor as
@@ -53,56 +45,35 @@ struct IndexArgs {
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
-// 4 error flags, 6 end of the lean items, 8 end of the merge items (items
-// [0, lean) run in lean_kernel, [lean, merge) in merge_kernel, the rest in
-// segment_kernel); each work queue has one head per XCD-sized shard, each on
-// its own 64-byte line (kCtrHead0 + 16*s lean, kCtrMHead0 + 16*s merge,
-// kCtrGHead0 + 16*s general), so the dequeues of the persistent workers do
-// not serialise on a single line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrMerge = 8, kCtrHead0 = 16,
+// 4 error flags, 6 end of the lean items (items [0, lean) run in lean_kernel,
+// the rest in segment_kernel); each work queue has one head per XCD-sized
+// shard, each on its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 +
+// 16*s general), so the dequeues of the persistent workers do not serialise
+// on a single line.
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16,
        kQueueShards = 8,
-       kCtrMHead0 = kCtrHead0 + 16 * kQueueShards,
-       kCtrGHead0 = kCtrMHead0 + 16 * kQueueShards,
+       kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
-// QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean / kPlanMerge
+// QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean
 constexpr uint32_t kPlanSlotMask = 0x7FFu;   // (kMaxQueryTerms <= 2048)
 constexpr int kPlanBucketShift = 12;
 constexpr uint32_t kPlanLean = 1u << 16;
-constexpr uint32_t kPlanMerge = 1u << 17;
-constexpr int kMergeWaves = 4;   // independent waves per merge_kernel workgroup
 static_assert(kMaxQueryTerms <= static_cast<int>(kPlanSlotMask) + 1, "driver slot field");
 constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
-// per-workgroup statistics written by the segment kernel (no atomics):
+// per-workgroup statistics written by the segment kernels (no atomics):
 // stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
-#ifdef WSR_PROFILE
-constexpr int kStatStride = 16;  // + section cycles: 4 dequeue/setup, 5 driver, 6 dense, 7 blocks, 8 top-k, 9 total
-#else
 constexpr int kStatStride = 4;
-#endif
 enum { kErrLimit = 1, kErrCapacity = 2, kErrExchange = 4 };
 constexpr int kMaxOwners = 1024;   // doc-range shards (ranks) of one exchange
 
-#ifndef WSR_SEG_COST
-#define WSR_SEG_COST 63
-#endif
-constexpr int kSegCost = WSR_SEG_COST;  // target block decodes per work item; bounds seg_blocks (< 64)
+// Target block decodes per work item, for every class (lean, general,
+// phrase); bounds seg_blocks (< 64).  Phrase items have been this long since
+// round 3 (5 blocks before, while every conjunctive survivor ran the position
+// check; now only the running top-k's candidates do, and longer items prune
+// more: C5 leg 3.50 -> 4.95 M q/s at 63 blocks, 16: 4.27, 32: 4.56 M,
+// profiles/r03_phrase_item_ab.txt).
+constexpr int kSegCost = 63;
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
-// phrase queries: items of kSegCost blocks as well since round 3.  Items of 5
-// blocks were kept while every conjunctive survivor ran the position check;
-// now only the running top-k's candidates do (lean_segment), and longer items
-// prune more: C5 leg 3.50 -> 4.95 M q/s at 63 blocks (16: 4.27, 32: 4.56 M),
-// profiles/r03_phrase_item_ab.txt
-#ifndef WSR_SEG_COST_PHRASE
-#define WSR_SEG_COST_PHRASE 63
-#endif
-constexpr int kSegCostPhrase = WSR_SEG_COST_PHRASE;
-static_assert(kSegCostPhrase <= kSegCost, "the event workspace is sized for kSegCost");
-// conjunctive items of the general (non-bitmap) kernel
-#ifndef WSR_SEG_COST_GENERAL
-#define WSR_SEG_COST_GENERAL 63
-#endif
-constexpr int kSegCostGeneral = WSR_SEG_COST_GENERAL;
-static_assert(kSegCostGeneral <= kSegCost, "the event workspace is sized for kSegCost");
 // item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5
@@ -155,7 +126,7 @@ constexpr int kPhraseScratch = kMaxPhraseTerms * 256;
 // plan queries (2 launches); part: per plan workgroup of kPlanThreads queries
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int merge_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
@@ -170,44 +141,12 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
                        uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st);
 int lean_kernel_occupancy();
-// merge items (QueryPlan kPlanMerge): merge_wgs workgroups of kMergeWaves waves;
-// stats of wave w at stats[w * kStatStride]
-hipError_t launch_merge(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
-                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
-                        int merge_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                        uint64_t* pub, const QueryDesc* desc, hipStream_t st);
-int merge_kernel_occupancy();
-hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
-                         const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
-                         hipStream_t st);
-// diagnostics build (-DWSR_REPLAY_PROF): replay_kernel writes 6 words per query
-// (filter cycles, finish cycles, events, candidates, insertions, items)
-hipError_t set_replay_prof(uint32_t* rows);
 // queries with k > kMaxK (their segments emitted every survivor): heap in LDS
 hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                               const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
                               hipStream_t st);
 hipError_t launch_decode_probe(const uint8_t* p, uint32_t bits, uint32_t cnt, bool delta,
                                uint32_t seed, uint32_t* out, hipStream_t st);
-// doc-range shards (multi-GPU)
-hipError_t launch_shard_reduce(const QueryIn* q, const QueryPlan* plan, int nq, Event* events,
-                               const uint32_t* ev_cnt, int32_t* scount, hipStream_t st);
-hipError_t launch_scan_counts(const int32_t* cnt, int n, int seg, uint64_t* off, int64_t* seg_total,
-                              hipStream_t st);
-hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events,
-                              const int32_t* scount, const uint64_t* off, Event* send,
-                              hipStream_t st);
-hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
-                               const uint64_t* roff, const uint64_t* rbase, const Event* recv,
-                               HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st);
-// fixed-slot exchange: pack (shard side, after launch_shard_reduce + scan) and
-// scan + replay (owner side); slot = events per (shard, owner) pair
-hipError_t launch_pack_fixed(const QueryPlan* plan, int nq, const Event* events, int32_t* scount,
-                             const uint64_t* off, int q_per_owner, uint64_t slot, Event* send,
-                             uint32_t* counters, hipStream_t st);
-hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
-                                     uint64_t* roff, uint64_t slot, const Event* recv, HitDev* hits,
-                                     int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st);
 // owner side of the fused exchange: meta[(g * nq + i) * 2] = {count, offset}
 // sent by shard g for owned query i, its events at recv + g * slot + offset
 // (meta of shard g at meta + g * meta_stride, its events at recv + g * stride)

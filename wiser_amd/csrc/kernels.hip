@@ -11,23 +11,25 @@
 //   top-k heap ................. MinPointerHeap / RankDoc / SortHeap
 //                                (query_processing.h:510-524,551-562,588-616)
 //
-// Three launches per query batch:
+// Launches per query batch:
 //   plan_*_kernel   per query pick the shortest list as driver and cut its
 //                   blocks into segments of similar cost (one thread per query),
 //                   then exclusive-scan segment counts and event capacities.
-//   segment_kernel  persistent, one wave per workgroup, segments pulled from an
-//                   atomic queue.  Per driver block (128 postings): wave-decode
-//                   doc ids (2 per lane; bit-unpack or ballot-parallel varint),
-//                   gallop each other list's block directory per lane, decode the
-//                   touched blocks into LDS once, lower_bound in LDS, decode the
-//                   tf blocks only where something matched, score survivors in
-//                   fp64 in query-term order, and keep a running top-k (one f64
-//                   per lane) to emit the survivors a heap started empty at the
-//                   segment start would insert ("events", in doc-id order).
-//   replay_kernel   one wave per query: filters the events of its segments, in
-//                   doc-id order, down to the reference heap's insertions and
-//                   applies them to a restatement of libstdc++'s push_heap /
-//                   pop_heap with the reference comparator, then SortHeap.
+//   lean_kernel     persistent, independent waves: items whose other lists all
+//                   carry a rank bitmap (the common case) -- a software pipeline
+//                   over the driver's blocks, one bitmap probe per posting.
+//   segment_kernel  persistent, one wave per workgroup, beside lean_kernel on a
+//                   second stream: the general items.  Per driver block (128
+//                   postings): wave-decode doc ids (2 per lane; bit-unpack or
+//                   ballot-parallel varint), gallop each other list's block
+//                   directory per lane, decode the touched blocks into LDS once,
+//                   lower_bound in LDS, score survivors in fp64 in query-term
+//                   order, and keep a running top-k (one f64 per lane) to emit
+//                   the survivors a heap started empty at the segment start
+//                   would insert ("events", in doc-id order).
+//   The worker that finishes a query's last item replays its events, in doc-id
+//   order, through a restatement of libstdc++'s push_heap / pop_heap with the
+//   reference comparator, then SortHeap (wide_replay_kernel for k > 64).
 //
 // Exactness of the event filter: survivor i is inserted by a heap run from
 // empty over a sequence iff fewer than k earlier survivors have a score >= s_i.
@@ -97,16 +99,11 @@ __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b 
 // A wave-uniform value kept in a vector register: for values only ever used as
 // VALU operands, so that they do not compete for the scalar registers of a
 // loop that already needs more than the 106 it can have.
-#ifndef WSR_NO_VPIN
 template <class T>
 __device__ __forceinline__ T in_vgpr(T x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-#else
-template <class T>
-__device__ __forceinline__ T in_vgpr(T x) { return x; }
-#endif
 
 // max over the lanes below this one (0 for lane 0)
 __device__ __forceinline__ uint32_t wave_excl_max(uint32_t x) {
@@ -280,23 +277,18 @@ __device__ __forceinline__ uint32_t find_block(const uint32_t* last, uint32_t cu
 // ---------------------------------------------------------- dense lists --
 // Other list B is probed through its rank bitmap when it has one and is at
 // least dense_ratio times as long as the driver (then a block decode per
-// probe would mostly decode postings nobody asks for).
-// (0: a lean item is kSegCost driver blocks, 63; with the pre-probe bound and
-// the floor refresh, longer items prune more and carry less fixed work per
-// block: main leg 26.6 -> 28.0 M q/s against 0.5, i.e. 42-block items, and
-// 27.9 M at 0.25: profiles/r02_sy_item_size_ab.txt)
-#ifndef WSR_DENSE_COST
-#define WSR_DENSE_COST 0.0f
-#endif
-constexpr float kDenseCost = WSR_DENSE_COST;   // plan cost of a bitmap probe round, in block decodes
-
+// probe would mostly decode postings nobody asks for).  A bitmap probe round
+// adds nothing to an item's plan cost: a lean item is kSegCost driver blocks
+// (with the pre-probe bound and the floor refresh, longer items prune more and
+// carry less fixed work per block: main leg 26.6 -> 28.0 M q/s against
+// 42-block items, profiles/r02_sy_item_size_ab.txt).
 __device__ __forceinline__ bool use_dense(const IndexArgs& ix, bool has_bm, uint32_t nblk_b,
                                           uint32_t nblk_driver) {
   return has_bm && static_cast<float>(nblk_b) >= ix.dense_ratio * static_cast<float>(nblk_driver);
 }
 
-// A bitmap entry as loaded for a probe: x = rank, y = mask word (WSR_DENSE_FMT
-// 2: two independent loads, one from each array; 0: one 8-byte load).
+// A bitmap entry as loaded for a probe: x = rank, y = mask word (two
+// independent loads, one from each array).
 using DenseVal = uint2;
 __device__ __forceinline__ bool dense_bit(const DenseVal v, uint32_t sh) { return (v.y >> sh) & 1u; }
 __device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
@@ -304,15 +296,8 @@ __device__ __forceinline__ uint32_t dense_rank(const DenseVal v, uint32_t sh) {
 }
 // entry e of the bitmap that starts at entry bm (ListDev::bm)
 __device__ __forceinline__ DenseVal dense_at(const IndexArgs& ix, uint64_t bm, uint32_t e) {
-#if WSR_DENSE_FMT == 2
   return make_uint2(ix.dense_rk[kRankWords * (bm + e)], ix.dense[bm + e].w);
-#else
-  return reinterpret_cast<const uint2*>(ix.dense + bm)[e];
-#endif
 }
-__device__ __forceinline__ uint32_t dense_word(const DenseVal v, uint32_t) { return v.y; }
-// an entry whose mask is m (and rank 0): 0 = no doc
-__device__ __forceinline__ DenseVal dense_fill(uint32_t m) { return make_uint2(0u, m); }
 
 // Bit of doc a in a prefetched bitmap entry; on a hit *idx = posting index.
 __device__ __forceinline__ bool dense_hit(const IndexArgs& ix, uint32_t a, const DenseVal v,
@@ -374,14 +359,14 @@ __device__ __forceinline__ const int32_t* qlist_of(const QueryIn* qs, int qi) {
 }
 
 // ----------------------------------------------------------------- plan --
-// Item order: class-major (lean items first, then merge items, then general
-// ones), then cost bucket-major, heaviest bucket first (query order inside a bucket, a query's
+// Item order: class-major (lean items first, then general ones), then cost
+// bucket-major, heaviest bucket first (query order inside a bucket, a query's
 // items consecutive), so the persistent workers take the long items first and
 // the short ones fill the tail (longest-first list scheduling).
-constexpr int kPlanKeys = 3 * kCostBuckets;   // classes: lean, merge, general
+constexpr int kPlanKeys = 2 * kCostBuckets;   // classes: lean, general
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
   const uint32_t bucket = (drv >> kPlanBucketShift) & 0xFu;
-  const uint32_t cls = (drv & kPlanLean) ? 0u : (drv & kPlanMerge) ? 1u : 2u;
+  const uint32_t cls = (drv & kPlanLean) ? 0u : 1u;
   return cls * kCostBuckets + (kCostBuckets - 1 - bucket);
 }
 
@@ -469,7 +454,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     // all of them are in flight together); longer queries: plain loops.
     uint32_t d = 0, nd = 0xFFFFFFFFu, o1 = kNoSlot, min_last = 0xFFFFFFFFu;
     float cost = 1.0f;
-    bool lean = true, merge_ok = false;
+    bool lean = true;
     if (nt <= kMaxTerms) {
       uint32_t nb[kMaxTerms], last[kMaxTerms];
       bool dn[kMaxTerms];
@@ -499,18 +484,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       for (int s = 0; s < kMaxTerms; ++s) {
         if (s >= nt || s == static_cast<int>(d)) continue;
         const bool dense = use_dense(ix, dn[s], nb[s], nd);
-        cost += dense ? kDenseCost : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+        cost += dense ? 0.0f : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
         if (!dense) lean = false;
         min_last = last[s] < min_last ? last[s] : min_last;
         if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
       }
-      // merge class: every other list but O1 has a bitmap, O1 is at most
-      // merge_ratio times as long as the driver
-      merge_ok = o1 != kNoSlot && static_cast<float>(o_nb) <= ix.merge_ratio * static_cast<float>(nd);
-#pragma unroll
-      for (int s = 0; s < kMaxTerms; ++s)
-        if (s < nt && s != static_cast<int>(d) && s != static_cast<int>(o1) && !use_dense(ix, dn[s], nb[s], nd))
-          merge_ok = false;
     } else if (ok) {
       for (int s = 0; s < nt; ++s) {
         const int32_t id = ql[s];
@@ -524,26 +502,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         if (s == static_cast<int>(d)) continue;
         const ListDev& L = ix.lists[ql[s]];
         const bool dense = use_dense(ix, L.bm != kNoDense, L.nblk, nd);
-        cost += dense ? kDenseCost : fminf(static_cast<float>(L.nblk) / nd, 64.0f);
+        cost += dense ? 0.0f : fminf(static_cast<float>(L.nblk) / nd, 64.0f);
         if (!dense) lean = false;
         min_last = L.last < min_last ? L.last : min_last;
         if (L.nblk < o_nb) { o1 = s; o_nb = L.nblk; }
       }
-      merge_ok = ok && o1 != kNoSlot && static_cast<float>(o_nb) <= ix.merge_ratio * static_cast<float>(nd);
-      for (int s = 0; merge_ok && s < nt; ++s) {
-        if (s == static_cast<int>(d) || s == static_cast<int>(o1)) continue;
-        const ListDev& L = ix.lists[ql[s]];
-        if (!use_dense(ix, L.bm != kNoDense, L.nblk, nd)) merge_ok = false;
-      }
     }
     if (ok) {
-      const bool ph = nt > 1 && (q.flags & kQueryPhrase);
-      // merge class (merge_kernel): conjunctive, two or more terms, a driver of
-      // at least merge_min blocks; it takes such queries from the lean and the
-      // general class alike
-      const bool merge = merge_ok && !ph && nd >= ix.merge_min;
-      if (merge) { lean = false; cost = 1.0f; }
-      uint32_t seg = static_cast<uint32_t>((ph ? kSegCostPhrase : (lean || merge) ? kSegCost : kSegCostGeneral) / cost);
+      uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
       // for the per-item setup): the queue hands out heavy items first
@@ -551,10 +517,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       const uint32_t ic = static_cast<uint32_t>(item_cost);
       const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
       const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u) | (merge ? kPlanMerge : 0u);
+      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u);
       p.seg_blocks = seg;
       p.n_items = (nd + seg - 1) / seg;
-      if (lean || merge) {
+      if (lean) {
         // the lean kernel's record (bases are added by plan_fill_kernel)
         // (the driver's and O1's records: a second round of loads, side by side)
         const ListDev A = ix.lists[ql[d]];
@@ -572,8 +538,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
           D.o_list = static_cast<uint32_t>(ql[o1]);
         }
         D.min_last = min_last;
-        D.a_bm = A.bm;
-        D.a_tf8 = A.tf8;
         D.ev_base = 0;
         D.item_base = 0;
         D.n_items = p.n_items;
@@ -594,9 +558,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.b_id = static_cast<float>(2.2 * A.idf);
         D.b_m = mf;
         D.b_iom = static_cast<float>(io * static_cast<double>(mf));
-        // a two-term lean query's other-term bound may use O1's per-window tf
-        // maxima instead of its list maximum (lean_segment, WSR_WIN_BOUND)
-        D.nt = static_cast<uint32_t>(nt) | ((nt == 2 && o1 != kNoSlot) ? kDescWinBound : 0u);
+        D.nt = static_cast<uint32_t>(nt);
         desc[i] = D;
       }
     }
@@ -635,7 +597,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
                                                         const PlanPart* __restrict__ part, int n_part,
                                                         uint32_t* __restrict__ counters,
                                                         uint64_t ev_capacity, uint32_t item_capacity,
-                                                        uint32_t lean_grid, uint32_t merge_grid, uint32_t seg_grid,
+                                                        uint32_t lean_grid, uint32_t seg_grid,
                                                         uint32_t* __restrict__ item_q,
                                                         uint64_t* __restrict__ pub,
                                                         QueryDesc* __restrict__ desc) {
@@ -674,13 +636,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
   }
   __syncthreads();
   uint32_t key_base[kPlanKeys];
-  uint32_t run = 0, n_lean = 0, n_merge_end = 0;
+  uint32_t run = 0, n_lean = 0;
 #pragma unroll
   for (int k = 0; k < kPlanKeys; ++k) {
     key_base[k] = run + s_key_below[k];
     run += s_key_all[k];
     if (k == kCostBuckets - 1) n_lean = run;
-    if (k == 2 * kCostBuckets - 1) n_merge_end = run;
   }
   const uint32_t total_items = run;
   const bool fits = s_cap_all <= ev_capacity && total_items <= item_capacity;
@@ -705,7 +666,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     plan[i].ev_base = cb;
     // (skipped when the plan does not fit the workspace: never written past it)
     if (fits) {
-      if (p.driver & (kPlanLean | kPlanMerge)) {
+      if (p.driver & kPlanLean) {
         desc[i].item_base = base;
         desc[i].ev_base = cb;
       }
@@ -720,7 +681,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
       if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
       counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
       counters[kCtrLean] = fits ? n_lean : 0u;
-      counters[kCtrMerge] = fits ? n_merge_end : 0u;
       counters[kCtrEvCap] = static_cast<uint32_t>(s_cap_all > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap_all);
     }
     // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
@@ -728,7 +688,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     // those first items (lean: one worker per wave; general: per workgroup).
     if (t < kQueueShards) {
       counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
-      counters[kCtrMHead0 + 16 * t] = (merge_grid + kQueueShards - 1 - t) / kQueueShards;
       counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
     }
   }
@@ -845,18 +804,12 @@ __device__ __forceinline__ double length_norm(uint32_t c4, double avg) {
 __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm) {
   // TfNormLossy (scoring.h:65-69) times idf (scoring.h:136-140)
   const double f = static_cast<double>(static_cast<int32_t>(tf));
-#ifdef WSR_DIAG_CHEAP_SCORE   // timing diagnostic only (wrong scores): no divide
-  return idf * (f + norm);
-#endif
   const double k1p1 = 1.2 + 1;
   const double tfn = (f * k1p1) / (f + norm);
   return idf * tfn;
 }
 
 // --------------------------------------------------------------- replay --
-#ifndef WSR_HANDOFF_ACQREL
-#define WSR_HANDOFF_ACQREL 0
-#endif
 // Events handed from one workgroup to another inside the segment kernel
 // (fused replay) travel with agent-scope relaxed atomics, which gfx950 issues
 // as sc1 (coherent across the XCDs' L2s) loads and stores; the hand-off itself
@@ -1164,16 +1117,10 @@ struct LdsHeapSink {
 struct HeapSink {
   WaveHeap H;
   uint32_t k = 0;
-#ifdef WSR_REPLAY_PROF   // diagnostics: events seen, candidates, insertions
-  uint32_t n_ev = 0, n_cand = 0, n_ins = 0;
-#endif
   __device__ __forceinline__ void insert(double sv, int32_t dv) {
     if (H.n < k) H.push(sv, dv);
     else if (sv > H.at(0)) { H.pop(); H.push(sv, dv); }
     else return;
-#ifdef WSR_REPLAY_PROF
-    ++n_ins;
-#endif
   }
   // one chunk of up to 64 events in doc order (lane order): the candidates
   // beat the heap's top as it stands (it only grows), each applied in turn
@@ -1181,13 +1128,6 @@ struct HeapSink {
   __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&&) {
     const double top = H.n < k ? -1.0 : H.at(0);
     uint64_t cm = __ballot(valid && sc > top);
-#ifdef WSR_REPLAY_PROF
-    n_ev += __popcll(__ballot(valid));
-    n_cand += __popcll(cm);
-#endif
-#ifdef WSR_DIAG_REPLAY_NO_HEAP   // timing diagnostic only (wrong results): stream, no heap
-    cm = 0;
-#endif
     while (cm) {
       const int fl = __builtin_ctzll(cm);
       cm &= cm - 1;
@@ -1217,9 +1157,6 @@ struct HeapSink {
   }
 };
 
-#ifdef WSR_REPLAY_PROF
-__device__ uint32_t* g_replay_prof = nullptr;   // diagnostics build: per-query replay rows
-#endif
 
 // One wave per query: the events of its segments (doc-id order) through the
 // restated heap (HeapSink::step: the heap's own insertion test).
@@ -1231,28 +1168,13 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
                                              int32_t* __restrict__ n_hits) {
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
-#ifdef WSR_REPLAY_PROF
-  const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
   HeapSink sink;
   sink.k = k;
   consume_stream<kCoherent>(
       sink, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
       [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
       [](double, int32_t) {});
-#ifdef WSR_REPLAY_PROF
-  const uint64_t t_filter = __builtin_amdgcn_s_memtime();
-#endif
   sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
-#ifdef WSR_REPLAY_PROF
-  // (unfused replay_kernel only: one row of g_replay_prof per query)
-  if ((threadIdx.x & 63) == 0 && g_replay_prof) {
-    uint32_t* o = g_replay_prof + 6 * qi;
-    o[0] = static_cast<uint32_t>(t_filter - t_start);
-    o[1] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - t_filter);
-    o[2] = sink.n_ev; o[3] = sink.n_cand; o[4] = sink.n_ins; o[5] = P.n_items;
-  }
-#endif
 }
 
 // out-of-line copy for the segment kernel (keeps its register allocation
@@ -1261,17 +1183,6 @@ __device__ __noinline__ void replay_query_call(const QueryIn* qs, const QueryPla
                                                const Event* events, const uint32_t* ev_cnt,
                                                HitDev* hits, int hit_stride, int32_t* n_hits) {
   replay_query<true>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits);
-}
-
-__global__ __launch_bounds__(64) void replay_kernel(const QueryIn* __restrict__ qs,
-                                                    const QueryPlan* __restrict__ plan, int nq,
-                                                    const Event* __restrict__ events,
-                                                    const uint32_t* __restrict__ ev_cnt,
-                                                    HitDev* __restrict__ hits, int hit_stride,
-                                                    int32_t* __restrict__ n_hits) {
-  const int qi = blockIdx.x;
-  if (qi >= nq || qs[qi].k > kMaxK) return;   // (wide queries: wide_replay_kernel)
-  replay_query<false>(qs, plan, qi, events, ev_cnt, hits, hit_stride, n_hits);
 }
 
 // Wide queries (k > kMaxK): their segments emitted every survivor; one wave
@@ -1418,9 +1329,6 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
                                             const FusedReplay& fr) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
-#ifdef WSR_DIAG_NO_REFILTER   // diagnostic: keep every event (still exact, more of them)
-  prev_pub = nullptr;
-#endif
   if (prev_pub && ev_n > 0) {
     const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double fl_end = __longlong_as_double(static_cast<long long>(
@@ -1445,15 +1353,23 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     }
     ev_n = kept;
   }
-  // The hand-off: the events went out as agent-scope (sc1, write-through)
-  // stores and the replay reads them with sc1 loads; the per-query counter is
-  // a relaxed agent-scope RMW issued after a full s_waitcnt, which retires
-  // this item's event and count stores first.  An acquire-release RMW
-  // (WSR_HANDOFF_ACQREL=1) states the same ordering in the memory model's own
-  // terms, but gfx950 implements it with a write-back of the whole L2 before
-  // the RMW and an invalidate after it, on every item: measured at 0.88 ms
-  // against 0.49 ms for the C2 high x high class and 5.8 M against 10.6 M q/s
-  // on the C3 headline, parity green both ways (profiles/r03_handoff_ab.txt).
+  // The hand-off, stated against the LLVM AMDGPU memory model's code
+  // sequences for GFX942/GFX950 (AMDGPUUsage, "Memory Model GFX942"):
+  //  * every byte the replay reads (events, counts) is written here with
+  //    `store atomic monotonic agent` = global_store sc1: written through to
+  //    the agent's point of coherence (no XCD's L2 keeps it dirty);
+  //  * `s_waitcnt vmcnt(0)` below returns only when those stores are acked at
+  //    that point, and the counter RMW (`atomicrmw monotonic agent`, sc1) is
+  //    issued after it, so it is ordered after them in the memory system;
+  //  * the finisher's loads depend on the RMW's value (control dependence, no
+  //    speculation of vector loads on GFX9) and are `load atomic monotonic
+  //    agent` = global_load sc1, which miss every non-coherent L2 line.
+  // The acquire-release RMW (the C++-model form) adds `buffer_wbl2 sc1` before
+  // and `buffer_inv sc1` after the RMW: a write-back / invalidate of the whole
+  // L2 of the issuing XCD that has nothing to do here (the only data handed
+  // over is sc1-coherent), on every item.  Measured: 0.88 against 0.49 ms for
+  // the C2 high x high class, 5.8 against 10.6 M q/s on the C3 headline,
+  // parity green both ways (profiles/r03_handoff_ab.txt).
   if (l == 0) __hip_atomic_store(&ev_cnt[item], ev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // wide queries (k > kMaxK) are replayed by wide_replay_kernel after the
   // segments; in a shard step every query is emitted here
@@ -1462,8 +1378,7 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
     block_sync<kWave>();
     uint32_t old = 0;
     if (l == 0)
-      old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, WSR_HANDOFF_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+      old = __hip_atomic_fetch_add(&fr.q_done[qi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = uni(old);
     if (old + 1 == n_items) {
       if (fr.x_send)
@@ -1477,27 +1392,7 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
 }
 
 // waves per SIMD the segment kernel is compiled for (register budget)
-#ifndef WSR_SEG_WAVES
-#define WSR_SEG_WAVES 3
-#endif
-
-// Section timers of the diagnostics build (-DWSR_PROFILE): core-clock cycles
-// per workgroup, charged to the section that ends at each WSR_T.
-#ifdef WSR_PROFILE
-#define WSR_T0()                                        \
-  uint64_t prof_t = __builtin_amdgcn_s_memtime();       \
-  const uint64_t prof_start = prof_t;                   \
-  uint32_t prof_acc[5] = {0, 0, 0, 0, 0};
-#define WSR_T(i)                                                        \
-  {                                                                     \
-    const uint64_t now = __builtin_amdgcn_s_memtime();                  \
-    prof_acc[i] += static_cast<uint32_t>(now - prof_t);                 \
-    prof_t = now;                                                       \
-  }
-#else
-#define WSR_T0()
-#define WSR_T(i)
-#endif
+constexpr int kSegWaves = 3;
 
 // ---------------------------------------------------------- phrase check --
 // Per general workgroup (kPhraseScratch words), per query term s: the image
@@ -1637,20 +1532,6 @@ __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* ql
 }
 
 // ------------------------------------------------- lean bitmap segment --
-// Stage timers of the diagnostics build (-DWSR_PROFILE): cycles charged to
-// prof[0..3] = W, C (compaction + scoring), H, D of the lean pipeline.
-#ifdef WSR_PROFILE
-#define LT0() uint64_t lt_t = __builtin_amdgcn_s_memtime();
-#define LT(i)                                                         \
-  {                                                                   \
-    const uint64_t now = __builtin_amdgcn_s_memtime();                \
-    if (prof) prof[i] += static_cast<uint32_t>(now - lt_t);          \
-    lt_t = now;                                                       \
-  }
-#else
-#define LT0()
-#define LT(i)
-#endif
 // Byte loads of the pipeline are whole aligned dwords, kept raw until the
 // consuming stage extracts the byte (an extraction next to the load would make
 // the loop wait for it in the iteration that issued it).
@@ -1682,74 +1563,6 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
   v1 = __builtin_amdgcn_alignbit(up ? w2 : w1, up ? w1 : w0, s2 & 31u) & mask;
 }
 
-// Coalesced form of pair_words (the lean pipeline): lane l loads dwords 2l and
-// 2l+1 of the pack's dword-aligned span, and only the lanes the pack reaches
-// (16 b + 8 bytes: the pack, its misalignment and the third word of the last
-// pair), so the load touches the pack's few lines once instead of 64
-// overlapping 12-byte gathers.  pick_words then hands each lane the three
-// words of its pair through the LDS crossbar (ds_bpermute, no LDS storage).
-// Widths up to 31 (a doc-id gap or tf of 2^31 or more never occurs: doc ids
-// and tfs are below 2^32 and deltas below the doc count).
-// Measured slower than the 12-byte gathers (main leg 25.3 M against 26.4 M
-// q/s, profiles/r02_sb_ab.txt): the eight ds_bpermute per block cost more than
-// the vector-memory work they save, so it is off (-DWSR_COALESCED_WORDS=1).
-#ifndef WSR_COALESCED_WORDS
-#define WSR_COALESCED_WORDS 0
-#endif
-// driver blocks between floor refreshes (0: floor read once per item).  At 8:
-// events per 4,096 C2 queries 160 k -> 98 k (high x high 584 k -> 356 k), the
-// most events of one query 3,378 -> 1,111, main leg 26.37 -> 26.53 M q/s
-// (4 is no better; profiles/r02_sc_ab.txt; 16 and 32 are within the noise,
-// with 6 % and 21 % more events: profiles/r02_su_refresh_interval_ab.txt)
-// Gathers of the bitmap probe and of O1's tf bytes only on the lanes that need
-// them (exec-masked) instead of every lane reading a dummy word
-#ifndef WSR_MASKED_GATHERS
-#define WSR_MASKED_GATHERS 0
-#endif
-#ifndef WSR_OOB_GATHERS
-#define WSR_OOB_GATHERS 0
-#endif
-#ifndef WSR_BOUND_NO_RCP   // the pre-probe bound compared without the own term's reciprocal
-#define WSR_BOUND_NO_RCP 0
-#endif
-#ifndef WSR_FLOOR_REFRESH
-#define WSR_FLOOR_REFRESH 8
-#endif
-#ifndef WSR_WIN_BOUND   // the pre-probe bound with O1's per-window tf maxima (two-term queries)
-#define WSR_WIN_BOUND 0
-#endif
-#ifndef WSR_STAGE_ORDER   // 1: the lean pipeline's stages run W, D, C, H instead of W, C, H, D
-#define WSR_STAGE_ORDER 0
-#endif
-#ifndef WSR_PUBLISH_EVERY   // driver blocks between publishes (a multiple of WSR_FLOOR_REFRESH)
-#define WSR_PUBLISH_EVERY WSR_FLOOR_REFRESH
-#endif
-__device__ __forceinline__ void pack_dwords(const uint8_t* d, uint32_t b, uint32_t l, uint32_t& r0,
-                                            uint32_t& r1) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(d, 4));
-  r0 = 0;
-  r1 = 0;
-  if (8 * l < 16 * b + 8) {
-    r0 = w[2 * l];
-    r1 = w[2 * l + 1];
-  }
-}
-
-// the words (w0, w1, w2) of the pair at bit offset bitpos of the span
-__device__ __forceinline__ void pick_words(uint32_t r0, uint32_t r1, uint32_t bitpos, uint32_t& w0,
-                                           uint32_t& w1, uint32_t& w2) {
-  const uint32_t i0 = bitpos >> 5;
-  const int src = static_cast<int>(i0 >> 1) << 2;
-  const uint32_t a0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r0)));
-  const uint32_t a1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(r1)));
-  const uint32_t c0 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src + 4, static_cast<int>(r0)));
-  const uint32_t c1 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src + 4, static_cast<int>(r1)));
-  const bool odd = i0 & 1u;
-  w0 = odd ? a1 : a0;
-  w1 = odd ? c0 : a1;
-  w2 = odd ? c1 : c0;
-}
-
 // Segment of an item whose other lists all carry rank bitmaps (the common
 // case: a short driver against long lists).  The driver's blocks stream
 // through a software pipeline, one block per stage and iteration j:
@@ -1767,30 +1580,27 @@ __device__ __forceinline__ void pick_words(uint32_t r0, uint32_t r1, uint32_t bi
 // stage waits only for loads issued one iteration earlier.  Scoring one
 // survivor per lane instead of two postings per lane keeps the f64 work
 // proportional to the survivors.
+// Driver blocks between floor refreshes.  At 8: events per 4,096 C2 queries
+// 160 k -> 98 k (high x high 584 k -> 356 k), the most events of one query
+// 3,378 -> 1,111, main leg 26.37 -> 26.53 M q/s (4 is no better,
+// profiles/r02_sc_ab.txt; 16 and 32 are within the noise, with 6 % and 21 %
+// more events: profiles/r02_su_refresh_interval_ab.txt).
+constexpr uint32_t kFloorRefresh = 8;
+// Capacity of the LDS event buffer: flushed after every chunk that added
+// events (64 since round 3: C2 leg 31.5 -> 33.2 M q/s, C4 11.8 -> 12.5 M
+// against 128, C3 headline unchanged; 4 KB less LDS per workgroup,
+// profiles/r03_knob_ab.txt).
+constexpr uint32_t kLeanEvs = 64;
 // LDS of one wave of the lean kernel (kPh: phrase instance, whose queue also
 // carries the driver's posting slot and O1's posting rank of every survivor)
-// (kAnd: the instance that may take the bitmap-intersection path; the others
-// leave out its step buffer, so that more workgroups fit a CU's LDS)
-// (WSR_LEAN_EVS: capacity of the LDS event buffer, 128 or 64; at 64 it is
-// flushed after every chunk that added events.  64 since round 3: C2 leg
-// 31.5 -> 33.2 M q/s, C4 11.8 -> 12.5 M, C3 headline unchanged; 4 KB less
-// LDS per workgroup, profiles/r03_knob_ab.txt)
-#ifndef WSR_LEAN_EVS
-#define WSR_LEAN_EVS 64
-#endif
-template <bool kPh, bool kAnd>
+template <bool kPh>
 struct LeanLdsT {
   uint32_t q[kPh ? 1536 : 1024];   // survivor queue (4 or 6 rings of 256); at item end the
                                    // replay's segment scan
-  Event evs[WSR_LEAN_EVS];   // events buffered in LDS, stored when a chunk could overflow them
-                             // and at the end
-  uint32_t bx[kAnd ? 1 + kDenseDocs / 32 : 1][kAnd ? 64 : 1];   // bitmap-intersection step: per lane its entry's
-                        // survivors (exclusive prefix), intersected word, driver and O1 (rank, word)
-  uint4 dblk[64];       // the driver's directory entries of the segment
+  Event evs[kLeanEvs];   // events buffered in LDS, stored when a chunk could overflow them
+                         // and at the end
+  uint4 dblk[64];        // the driver's directory entries of the segment
   uint32_t dmeta[64];
-#ifdef WSR_PROFILE
-  uint32_t prof[4];     // lean pipeline stage cycles (diagnostics build)
-#endif
 };
 
 // o1 == kNoSlot: single-term query, every posting of the driver survives.
@@ -1800,18 +1610,16 @@ struct LeanLdsT {
 // (the headline's and C2's batches): two terms scored inline, no wide or
 // single-term paths, so the instance keeps fewer registers (86 VGPRs, no
 // scratch, half the SGPR spill reloads of the general instance).
-template <bool kPh, bool kAnd, bool kTwo = false>
-__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, kAnd>& S, const double* norm_tab,
+template <bool kPh, bool kTwo = false>
+__device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t* ph,
-                                             bool and_path, uint32_t first_doc,
                                              uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
                                              const uint64_t* prev_pub, uint64_t* my_pub,
                                              Event* ev_out, uint32_t& ev_n,
                                              double& pt, uint32_t& pt_n,
-                                             double& last_pub, uint32_t& n_surv, uint32_t& n_dblk,
-                                             uint32_t* prof) {
+                                             double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
   const uint32_t d = kTwo ? (Q.slots & 1u) : (Q.slots & 0xFFFFu);
@@ -1821,34 +1629,18 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   const bool wide = !kTwo && k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
   const bool single = !kTwo && o1 == kNoSlot;
-  // (single term: reads go to a valid dummy word; the image may have no bitmaps)
-  // O1's bitmap (single term: reads go to a valid dummy word)
-#if WSR_DENSE_FMT == 2
-  // the probe reads the mask word alone; a hit reads its rank (H stage)
+  // O1's bitmap (single term: reads go to a valid dummy word; the image may
+  // have no bitmaps): the probe reads the mask word alone; a hit reads its
+  // rank record (H stage)
   const uint32_t* o_mk = single ? ix.blk_last : &ix.dense[Q.o_bm].w;
-#if WSR_RANK_TF
   const uint2* o_rk = single ? reinterpret_cast<const uint2*>(ix.blk_last)
                              : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
-#else
-  const uint32_t* o_rk = single ? ix.blk_last : ix.dense_rk + Q.o_bm;
-#endif
   auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_mk[e]; };
-  auto probe_fill = [&](uint32_t m) __attribute__((always_inline)) { return m; };
-  (void)probe_fill;   // (the WSR_DIAG_PROBE_NONE diagnostic)
   auto probe_bit = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) { return ((v >> sh) & 1u) != 0u; };
   // posting rank of a hit, without the rank word (added at compaction)
   auto probe_rank = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) {
     return static_cast<uint32_t>(__popc(v & ((1u << sh) - 1u)));
   };
-#else
-  const uint2* o_bm = single ? reinterpret_cast<const uint2*>(ix.blk_last)
-                             : reinterpret_cast<const uint2*>(ix.dense + Q.o_bm);
-  auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_bm[e]; };
-  auto probe_fill = [&](uint32_t m) __attribute__((always_inline)) { return dense_fill(m); };
-  (void)probe_fill;
-  auto probe_bit = [&](uint2 v, uint32_t sh) __attribute__((always_inline)) { return dense_bit(v, sh); };
-  auto probe_rank = [&](uint2 v, uint32_t sh) __attribute__((always_inline)) { return dense_rank(v, sh); };
-#endif
   const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
@@ -1873,8 +1665,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   uint64_t floor_bits =
       prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
   double pub_val = 0.0;
-#if WSR_FLOOR_REFRESH
-  // Floor refresh (every WSR_FLOOR_REFRESH driver blocks): the item publishes
+  // Floor refresh (every kFloorRefresh driver blocks): the item publishes
   // its floor as it stands (the k-th best of docs before the next item) and
   // reads the previous item's, so the items of one query, which run at once,
   // hand their thresholds down the chain while they run instead of at their
@@ -1882,7 +1673,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   // iteration waits for anyway, and consumed one refresh later.
   uint64_t floor_next = floor_bits;
   double sent = 0.0;
-#endif
   // Pre-probe pruning.  A driver posting whose score bound -- its own term,
   // exact, plus QueryDesc's bound of the other terms at its doc length -- is
   // <= the threshold known so far, max(the floor of the query's earlier items,
@@ -1894,45 +1684,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   constexpr float kPruneMargin = 0.998f;
   const float b_id = Q.b_id;
   float b_iom = Q.b_iom, b_m = Q.b_m;
-#if WSR_WIN_BOUND
-  // Windowed other-term bound (two-term queries): per driver block, O1's
-  // largest tf over the 2,048-doc windows the block's doc range touches
-  // replaces its list maximum (255 in a window: 255 or more, use the list's).
-  const bool win = (Q.nt & kDescWinBound) != 0u && ix.wmax != nullptr;
-  const float io = b_m > 0.0f ? b_iom / b_m : 0.0f;   // 2.2 idf of O1
-  const float m_list = b_m;
-  const uint8_t* o_wm = win ? ix.wmax + Q.o_bm / kWinEnts : reinterpret_cast<const uint8_t*>(ix.blk_last);
-  const uint32_t wm_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_wm) & 3u);
-  // the windows [w0, w1] of a block (directory entry e), clipped to the span
-  auto win_range = [&](const uint4& e, uint32_t& w0, uint32_t& w1) __attribute__((always_inline)) {
-    const uint32_t first = uni(e.x) > lo ? uni(e.x) - lo : 0u;
-    const uint32_t last = uni(e.y) - lo < span ? uni(e.y) - lo : (span ? span - 1 : 0u);
-    w0 = first / (kDenseDocs * kWinEnts);
-    w1 = last / (kDenseDocs * kWinEnts);
-    if (w1 < w0) w1 = w0;
-  };
-#endif
-#ifdef WSR_NO_PRUNE   // A/B diagnostic: every posting is probed
-  const float thr_s = -1.0f;
-#else
   float thr_s = wide ? -1.0f
                      : static_cast<float>(__longlong_as_double(static_cast<long long>(
                            (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_bits >> 32))) << 32) |
                            uni(static_cast<uint32_t>(floor_bits))))) * kPruneMargin;
-#endif
-#if WSR_BOUND_NO_RCP
-  // passes(t, c) == (bound(t, c) > thr_s) without the own term's reciprocal:
-  // b_id tf / (tf + nf) + o > thr  <=>  b_id tf > (thr - o) (tf + nf), as
-  // tf + nf > 0.  Rounding moves either side by a few f32 ulps of the score
-  // scale, far inside the 0.2 % threshold margin, so a dropped posting's score
-  // is still strictly below the threshold.
-  auto passes = [&](uint32_t t, uint32_t c) __attribute__((always_inline)) {
-    const float nf = static_cast<float>(norm_tab[c]);
-    const float f = static_cast<float>(t);
-    const float o = b_iom * __builtin_amdgcn_rcpf(b_m + nf);
-    return b_id * f > (thr_s - o) * (f + nf);
-  };
-#endif
   auto bound = [&](uint32_t t, uint32_t c) __attribute__((always_inline)) {
     const float nf = static_cast<float>(norm_tab[c]);
     const float f = static_cast<float>(t);
@@ -1942,8 +1697,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
   auto flush = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
     if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
-    if (WSR_LEAN_EVS > 64 && l + 64 < evb)
-      store_event_coherent(&ev_out[ev_n - evb + l + 64], S.evs[(l + 64) % WSR_LEAN_EVS]);
     __builtin_amdgcn_wave_barrier();
     evb = 0;
   };
@@ -1954,12 +1707,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     bool alive = l < n;
     const uint32_t doc = qdoc[e];
     const uint32_t c4 = qc4[e];
-    uint32_t td = qtd[e];
+    const uint32_t td = qtd[e];
     uint32_t to = qto[e];
     const uint32_t pd = kPh ? qpd[e] : 0u, po = kPh ? qpo[e] : 0u;
     __builtin_amdgcn_wave_barrier();
     qhead += n;
-#if WSR_DENSE_FMT == 2
     if (!single && __ballot(alive && (to & 0x80000000u))) {   // O1's tf bytes by rank (bit 31: a rank)
       const bool rk = alive && (to & 0x80000000u);
       uint32_t t = load_byte(o_tf8 + (rk ? (to & 0x7FFFFFFFu) : 0u));
@@ -1968,16 +1720,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         if (rk && t == kTf8Escape) t = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
       }
       if (rk) to = t;
-    }
-#else
-    if (__ballot(alive && (to & 0x80000000u))) {
-      const ListDev O = ix.lists[Q.o_list];
-      if (alive && (to & 0x80000000u)) to = dense_tf_slow(ix, O, to & 0x7FFFFFFFu);
-    }
-#endif
-    if (and_path && __ballot(alive && (td & 0x80000000u))) {   // (bitmap path: driver tf >= 255)
-      const ListDev A = ix.lists[qlist[d]];
-      if (alive && (td & 0x80000000u)) td = dense_tf_slow(ix, A, td & 0x7FFFFFFFu);
     }
     // phrase: each term's posting slot and tf, for the position check
     auto rec = [&](uint32_t s, uint32_t slot, uint32_t tf) __attribute__((always_inline)) {
@@ -2040,7 +1782,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       }
       ev_n += __popcll(am);
       evb += __popcll(am);
-      if (evb >= WSR_LEAN_EVS - 64) flush();
+      if (evb >= kLeanEvs - 64) flush();
       return;
     }
     // running top-k: candidates beat the k-th best so far and the floor of the
@@ -2051,9 +1793,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         uni(static_cast<uint32_t>(fb))));
     const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     uint64_t cm = __ballot(alive && sc > flo && (pt_n < k || sc > kth));
-#ifdef WSR_DIAG_NO_TOPK   // timing diagnostic only (wrong results): no running top-k
-    cm = 0;
-#endif
     while (cm) {
       const int fl = __builtin_ctzll(cm);
       cm &= cm - 1;
@@ -2076,13 +1815,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
         pt_n = pt_n + 1 > k ? k : pt_n + 1;
       }
     }
-    if (evb && evb >= WSR_LEAN_EVS - 64) flush();
+    if (evb && evb >= kLeanEvs - 64) flush();
     const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     const double pv = kn > flo ? kn : flo;
     pub_val = pv > pub_val ? pv : pub_val;
-#ifndef WSR_NO_PRUNE
     thr_s = static_cast<float>(pv) * kPruneMargin;
-#endif
   };
 
   // Pipeline registers, in two alternating sets: iteration j reads set X
@@ -2096,32 +1833,20 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     uint32_t w0 = 0, w1 = 0, w2 = 0;               // doc-id pack words of the next block
     uint32_t wc = 0;                               //   its doc-length codes (2 bytes of a word)
     uint32_t wt0 = 0, wt1 = 0, wt2 = 0;            //   its driver tf pack words
-#if WSR_WIN_BOUND
-    uint32_t wm = 0;                               //   O1's window tf maxima (a raw dword per lane)
-#endif
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
-#if WSR_DENSE_FMT == 2
     uint32_t de0 = 0, de1 = 0;                     // O1 bitmap mask words
-#else
-    uint2 de0 = make_uint2(0, 0), de1 = make_uint2(0, 0);   // O1 bitmap entries
-#endif
     // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
     // block, outside the image or pruned, a rank with bit 31 set is an O1 miss
     // -- so that they take no scalar lane-mask registers across the iteration)
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
-#if WSR_DENSE_FMT == 2 && WSR_RANK_TF
     uint2 hf0 = make_uint2(0, 0), hf1 = make_uint2(0, 0);   // O1 rank records (rank, 4 tfs; in flight)
-#else
-    uint32_t hf0 = 0, hf1 = 0;                     // O1 tf byte words (fmt 2: rank words; in flight)
-#endif
     uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit)
 
   };
   Regs R0, R1;
-#if !WSR_COALESCED_WORDS
   // byte shift of a pair's first value inside its aligned dword (pair_words)
   auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
     const uint32_t bit = 2 * l * bits;
@@ -2129,86 +1854,30 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
                        (bit >> 3);
     return ((a & 3u) << 3) + (bit & 7u);
   };
-#endif
-  const uint32_t tf8_mis = in_vgpr(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8) & 3u));
-#if WSR_DENSE_FMT == 2
-  (void)tf8_mis;
-#endif
-#if (WSR_OOB_GATHERS || WSR_MASKED_GATHERS || WSR_WIN_BOUND) && WSR_DENSE_FMT == 2
-#error "WSR_OOB_GATHERS / WSR_MASKED_GATHERS / WSR_WIN_BOUND need the 8-byte bitmap entries (WSR_DENSE_FMT=0)"
-#endif
-#if WSR_OOB_GATHERS
-  // Buffer views of O1's bitmap and tf bytes: a lane with nothing to fetch
-  // gives an offset past the view's end, so its load returns 0 without a
-  // memory access (the wave's other lanes still load; no branch, no exec
-  // change, so the pipeline's wait counts are the same on every path).
-  constexpr uint32_t kOob = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t r_bm =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(o_bm), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r_tf8 = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(__builtin_align_down(o_tf8, 4)), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
-#endif
 
   auto issue_words = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
     const uint32_t bi = b < b1 ? b - b0 : 0u;
     const uint32_t m = uni(S.dmeta[bi]);
     const uint4 e = S.dblk[bi];
     // (VInts tail: width 0 -> a harmless dummy read)
-#if WSR_COALESCED_WORDS
-    pack_dwords(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1);
-#else
     uint32_t sh;
     pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
-#endif
     // its doc-length codes (postings 2l, 2l+1: one line per block, plen) and
     // driver tfs, so that D can bound each posting's score before the probe
     Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
-#if WSR_WIN_BOUND
-    {
-      uint32_t w0, w1;
-      win_range(e, w0, w1);
-      Y.wm = *reinterpret_cast<const uint32_t*>(
-          __builtin_align_down(o_wm + (win ? min(w0 + l, w1) : 0u), 4));
-    }
-#endif
-#if WSR_COALESCED_WORDS
-    pack_dwords(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1);
-#else
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1, Y.wt2, sh);
-#endif
   };
-#if WSR_COALESCED_WORDS
-  // the bit offset of lane l's pair in its pack's dword-aligned span
-  auto span_bit = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
-    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + rel + 2;
-    return ((a & 3u) << 3) + 2 * l * bits;
-  };
-#endif
   auto stage_C = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // C(j-2): compaction of block j-2 (its H fields are in X)
     if (j >= b0 + 2) {
-#if WSR_DENSE_FMT == 2
       // O1 posting ranks (hits): rank word + bits below; the tf byte is read by
       // rank when the chunk is scored (flag bit 31)
-#if WSR_RANK_TF
       // (the record's tf bytes cover the word's first four postings)
       const uint32_t rk0 = X.hf0.x + X.hx0, rk1 = X.hf1.x + X.hx1;
       const uint32_t f0 = X.hx0 < 4u ? (X.hf0.y >> ((X.hx0 & 3u) << 3)) & 0xFFu : kTf8Escape;
       const uint32_t f1 = X.hx1 < 4u ? (X.hf1.y >> ((X.hx1 & 3u) << 3)) & 0xFFu : kTf8Escape;
       const uint32_t to0 = f0 != kTf8Escape ? f0 : (0x80000000u | rk0);
       const uint32_t to1 = f1 != kTf8Escape ? f1 : (0x80000000u | rk1);
-#else
-      const uint32_t rk0 = X.hf0 + X.hx0, rk1 = X.hf1 + X.hx1;
-      const uint32_t to0 = 0x80000000u | rk0, to1 = 0x80000000u | rk1;
-#endif
-#else
-      const uint32_t xs0 = ((X.hx0 + tf8_mis) & 3u) << 3, xs1 = ((X.hx1 + tf8_mis) & 3u) << 3;
-      const uint32_t f0 = single ? 0u : (X.hf0 >> xs0) & 0xFFu;
-      const uint32_t f1 = single ? 0u : (X.hf1 >> xs1) & 0xFFu;
-      const uint32_t to0 = f0 == kTf8Escape ? (0x80000000u | X.hx0) : f0;
-      const uint32_t to1 = f1 == kTf8Escape ? (0x80000000u | X.hx1) : f1;
-      const uint32_t rk0 = X.hx0, rk1 = X.hx1;
-#endif
       const bool hh0 = !(X.hx0 >> 31), hh1 = !(X.hx1 >> 31);
       const uint64_t m0 = __ballot(hh0), m1 = __ballot(hh1);
       const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
@@ -2242,28 +1911,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & probe_bit(X.de1, s1)));
       const uint32_t x0 = probe_rank(X.de0, s0);
       const uint32_t x1 = probe_rank(X.de1, s1);
-      uint32_t w;
-#if WSR_DENSE_FMT == 2
-      // the hits' rank words (O1's tf bytes are read by rank when the chunk is scored)
-      (void)w;
+      // the hits' rank records (O1's tf bytes past a word's first four postings
+      // are read by rank when the chunk is scored)
       Y.hf0 = o_rk[(h0 && !single) ? q0 / kDenseDocs : 0u];
       Y.hf1 = o_rk[(h1 && !single) ? q1 / kDenseDocs : 0u];
-#elif defined(WSR_DIAG_NO_TF8)   // timing diagnostic only (wrong tfs): no O1 tf gathers
-      Y.hf0 = 0x01010101u; Y.hf1 = 0x01010101u; (void)w;
-#else
-#if WSR_OOB_GATHERS
-      (void)w;
-      Y.hf0 = __builtin_amdgcn_raw_buffer_load_b32(r_tf8, (h0 & !single) ? ((x0 + tf8_mis) & ~3u) : kOob, 0, 0);
-      Y.hf1 = __builtin_amdgcn_raw_buffer_load_b32(r_tf8, (h1 & !single) ? ((x1 + tf8_mis) & ~3u) : kOob, 0, 0);
-#elif WSR_MASKED_GATHERS
-      // (only the hits' lanes gather: the others keep a stale word, never read)
-      if (h0 & !single) Y.hf0 = byte_word(o_tf8 + x0, &w);
-      if (h1 & !single) Y.hf1 = byte_word(o_tf8 + x1, &w);
-#else
-      Y.hf0 = byte_word(o_tf8 + ((h0 && !single) ? x0 : 0u), &w);
-      Y.hf1 = byte_word(o_tf8 + ((h1 && !single) ? x1 : 0u), &w);
-#endif
-#endif
       // (ranks are < 2^31; a single-term item's are unused)
       Y.hx0 = h0 ? (x0 & 0x7FFFFFFFu) : 0x80000000u;
       Y.hx1 = h1 ? (x1 & 0x7FFFFFFFu) : 0x80000000u;
@@ -2288,14 +1939,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
       const uint32_t cnt = live ? ((j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u) : 0u;
       uint32_t x0, x1;
-#if WSR_COALESCED_WORDS
-      uint32_t pw0, pw1, pw2;
-      const uint32_t bp = span_bit(uni(be.z), wbits);
-      pick_words(X.w0, X.w1, bp, pw0, pw1, pw2);
-      pair_values(pw0, pw1, pw2, bp & 31u, wbits, x0, x1);
-#else
       pair_values(X.w0, X.w1, X.w2, pair_shift(uni(be.z), wbits), wbits, x0, x1);
-#endif
       const uint32_t sm = x0 + x1;
       const uint32_t inc = wave_incl_scan(sm);
       uint32_t a0 = prev + (inc - sm) + x0;
@@ -2305,63 +1949,18 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
       const bool ok0 = (2 * l < cnt) & (a0 - lo < hi_rel);
       const bool ok1 = (2 * l + 1 < cnt) & (a1 - lo < hi_rel);
       uint32_t t0, t1;
-#if WSR_COALESCED_WORDS
-      const uint32_t tp = span_bit(uni(be.w), wtb);
-      pick_words(X.wt0, X.wt1, tp, pw0, pw1, pw2);
-      pair_values(pw0, pw1, pw2, tp & 31u, wtb, t0, t1);
-#else
       pair_values(X.wt0, X.wt1, X.wt2, pair_shift(uni(be.w), wtb), wtb, t0, t1);
-#endif
       if (tl) { t0 = ttf0; t1 = ttf1; }
       const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
       const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
-#if WSR_WIN_BOUND
-      if (win) {   // (wave-uniform)
-        uint32_t w0, w1;
-        win_range(be, w0, w1);
-        const uint32_t idx = min(w0 + l, w1);
-        uint32_t v = (X.wm >> (((wm_mis + idx) & 3u) << 3)) & 0xFFu;
-        if (w1 - w0 >= 64u) v = 255u;   // (wider than a wave: the list maximum)
-        const uint32_t m = umax(wave_excl_max(v), v);
-        const uint32_t mm = uni(__builtin_amdgcn_readlane(m, 63));
-        b_m = mm >= 255u ? m_list : static_cast<float>(mm);
-        b_iom = io * b_m;
-      }
-#endif
       // pre-probe pruning (above): a dropped posting is never probed
       // (branch-free: the bound of a lane past the block is computed and dropped)
-#if WSR_BOUND_NO_RCP
-      const bool p0 = ok0 & passes(t0, c0);
-      const bool p1 = ok1 & passes(t1, c1);
-#else
       const bool p0 = ok0 & (bound(t0, c0) > thr_s);
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
-#endif
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
-#if WSR_OOB_GATHERS
-      {
-        const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in0 ? ((a0 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
-        const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(r_bm, in1 ? ((a1 - lo) / kDenseDocs) * 8u : kOob, 0, 0);
-        Y.de0 = make_uint2(v0[0], v0[1]);
-        Y.de1 = make_uint2(v1[0], v1[1]);
-      }
-#elif WSR_MASKED_GATHERS
-      // (only the postings that passed the bound probe: a pruned lane keeps a
-      // stale word, which H never reads -- its doc is ~0u or outside the span)
-      if (in0) Y.de0 = o_probe((a0 - lo) / kDenseDocs);
-      if (in1) Y.de1 = o_probe((a1 - lo) / kDenseDocs);
-#elif defined(WSR_DIAG_PROBE_L2)   // timing diagnostic only (wrong hits): probes L2-resident
-      Y.de0 = o_probe(in0 ? ((a0 - lo) / kDenseDocs) & 0x3FFFu : 0u);
-      Y.de1 = o_probe(in1 ? ((a1 - lo) / kDenseDocs) & 0x3FFFu : 0u);
-#elif defined(WSR_DIAG_PROBE_NONE)   // timing diagnostic only (wrong results): no probes, no hits
-      // (k < 2^20: a zero mask the compiler cannot fold away)
-      Y.de0 = probe_fill(in0 ? (Q.k >> 20) : 0u);
-      Y.de1 = probe_fill(in1 ? (Q.k >> 20) : 0u);
-#else
       Y.de0 = o_probe(in0 ? (a0 - lo) / kDenseDocs : 0u);
       Y.de1 = o_probe(in1 ? (a1 - lo) / kDenseDocs : 0u);
-#endif
       Y.dcc = c0 | (c1 << 8);
       Y.dt0 = t0; Y.dt1 = t1;
       Y.da0 = p0 ? a0 : ~0u; Y.da1 = p1 ? a1 : ~0u;
@@ -2372,159 +1971,33 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
     }
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    LT0()
-#if WSR_FLOOR_REFRESH
-    if (((j - b0) % WSR_FLOOR_REFRESH) == WSR_FLOOR_REFRESH - 1 && !wide) {
+    if (((j - b0) % kFloorRefresh) == kFloorRefresh - 1 && !wide) {
       const uint64_t fb = (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_next >> 32))) << 32) |
                           uni(static_cast<uint32_t>(floor_next));
       if (fb > floor_bits) {
         floor_bits = fb;
-#ifndef WSR_NO_PRUNE
         const float t = static_cast<float>(__longlong_as_double(static_cast<long long>(fb))) * kPruneMargin;
         thr_s = t > thr_s ? t : thr_s;
-#endif
       }
-#ifndef WSR_DIAG_NO_PUBLISH   // diagnostic: the refresh reads floors but never publishes
-      if (my_pub && pub_val > sent && ((j - b0) % WSR_PUBLISH_EVERY) == WSR_PUBLISH_EVERY - 1) {
+      if (my_pub && pub_val > sent) {
         if (l == 0)
           __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sent = pub_val;
       }
-#endif
       if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
     // W(j+1): the doc-id words of block j+1
     issue_words(j + 1, Y);
-    LT(0)
-#if WSR_STAGE_ORDER
-    // (D, C, then H: the probes D issues get almost two iterations before H
-    // reads them, instead of the tail of one)
-    stage_D(X, Y, j);
-    LT(3)
     stage_C(X, Y, j);
-    LT(1)
     stage_H(X, Y, j);
-    LT(2)
-#else
-    stage_C(X, Y, j);
-    LT(1)
-    stage_H(X, Y, j);
-    LT(2)
     stage_D(X, Y, j);
-    LT(3)
-#endif
   };
-  if (kAnd && and_path) {
-    // Bitmap intersection: the segment's doc span, one bitmap entry
-    // (kDenseDocs docs) per lane and step; the entries of every list are
-    // ANDed, so a step costs a few loads per list whatever the driver's
-    // density.  Survivors are taken in rank order (= doc order) 64 at a time:
-    // lane l finds the entry holding survivor c*64 + l by a search over the
-    // step's prefix counts and the bit by a popcount select, and appends it to
-    // the queue.
-    constexpr uint32_t kDW = kDenseDocs / 32;   // mask words per entry
-    const uint32_t last_doc = min(uni(S.dblk[b1 - 1 - b0].y), min_last);
-    const uint32_t a_lo = first_doc > lo ? first_doc - lo : 0u;
-    uint32_t a_hi = last_doc - lo;                      // inclusive, relative
-    if (a_hi >= span) a_hi = span - 1;
-    const uint64_t a_bm = Q.a_bm;
-    const uint8_t* a_tf8 = ix.tf8 + Q.a_tf8;
-    if (span && last_doc >= lo && a_lo <= a_hi) {
-      const uint32_t w0 = a_lo / kDenseDocs, w1 = a_hi / kDenseDocs;   // inclusive entry range
-      for (uint32_t base = w0; base <= w1; base += 64) {
-        const uint32_t wi = base + l;
-        const bool live = wi <= w1;
-        const DenseVal va = dense_at(ix, a_bm, live ? wi : w0);
-        const DenseVal vo = single ? dense_fill(~0u) : dense_at(ix, Q.o_bm, live ? wi : w0);
-        uint32_t m[kDW];
-#pragma unroll
-        for (uint32_t i = 0; i < kDW; ++i) {
-          uint32_t x = live ? (dense_word(va, i) & dense_word(vo, i)) : 0u;
-          const uint32_t r0 = wi * kDenseDocs + i * 32u;   // relative doc of the word's bit 0
-          if (r0 + 31u < a_lo || r0 > a_hi) x = 0u;
-          else {
-            if (r0 < a_lo) x &= ~0u << (a_lo - r0);
-            if (a_hi < r0 + 31u) x &= (2u << (a_hi - r0)) - 1u;
-          }
-          m[i] = x;
-        }
-        for (uint32_t s = 0; s < nt; ++s) {   // the further other lists
-          uint32_t any = 0;
-#pragma unroll
-          for (uint32_t i = 0; i < kDW; ++i) any |= m[i];
-          if (s == d || s == o1 || !__ballot(any)) continue;
-          const ListDev B = ix.lists[qlist[s]];
-          const DenseVal vb = dense_at(ix, B.bm, live ? wi : w0);
-#pragma unroll
-          for (uint32_t i = 0; i < kDW; ++i) m[i] &= dense_word(vb, i);
-        }
-        uint32_t c = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < kDW; ++i) c += __popc(m[i]);
-        const uint32_t inc = wave_incl_scan(c);
-        const uint32_t total = uni(__builtin_amdgcn_readlane(inc, 63));
-        if (total == 0) continue;
-        __builtin_amdgcn_wave_barrier();
-        S.bx[0][l] = inc - c;
-#pragma unroll
-        for (uint32_t i = 0; i < kDW; ++i) S.bx[1 + i][l] = m[i];
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t c0 = 0; c0 < total; c0 += 64) {
-          const uint32_t g = c0 + l;
-          const bool has = g < total;
-          // owner lane: the last lane whose exclusive prefix is <= g
-          uint32_t ow = 0;
-#pragma unroll
-          for (uint32_t st = 32; st; st >>= 1)
-            if (S.bx[0][ow + st] <= g) ow += st;
-          uint32_t k = g - S.bx[0][ow], wd = 0, mw = S.bx[1][ow];
-#pragma unroll
-          for (uint32_t i = 1; i < kDW; ++i) {   // the word holding the k-th set bit
-            const uint32_t pc = __popc(mw);
-            if (k >= pc) { k -= pc; wd = i; mw = S.bx[1 + i][ow]; }
-          }
-          uint32_t bit = 0;
-#pragma unroll
-          for (uint32_t st = 16; st; st >>= 1) {   // k-th set bit of mw
-            const uint32_t lowc = __popc(mw & ((1u << st) - 1u));
-            if (k >= lowc) { k -= lowc; bit += st; mw >>= st; }
-          }
-          const uint32_t sh = wd * 32u + bit;
-          const uint32_t ent = has ? base + ow : w0;
-          const uint32_t doc = lo + (base + ow) * kDenseDocs + sh;
-          // (the entries again, from the cache: their ranks)
-          const uint32_t ra = dense_rank(dense_at(ix, a_bm, ent), sh);
-          const uint32_t ro = single ? 0u : dense_rank(dense_at(ix, Q.o_bm, ent), sh);
-          const uint32_t ta = load_byte(a_tf8 + (has ? ra : 0u));
-#if WSR_DENSE_FMT == 2
-          const uint32_t tb = 0u;   // (O1's tf: read by rank when the chunk is scored)
-#else
-          const uint32_t tb = single ? 0u : load_byte(o_tf8 + (has ? ro : 0u));
-#endif
-          const uint32_t cc = (has && doc < ix.n_c4) ? load_byte(ix.c4 + doc) : 0u;
-          const uint32_t e = (qtail + l) & 255u;
-          if (has) {
-            qdoc[e] = doc; qc4[e] = cc;
-            qtd[e] = ta == kTf8Escape ? (0x80000000u | ra) : ta;
-            qto[e] = (WSR_DENSE_FMT == 2 || tb == kTf8Escape) ? (0x80000000u | ro) : tb;
-            if (kPh) { qpd[e] = Q.a_blk0 * 128u + ra; qpo[e] = ro; }
-          }
-          qtail += min(64u, total - c0);
-          __builtin_amdgcn_wave_barrier();
-          if (qtail - qhead >= 64) score_chunk(64);
-        }
-      }
-    }
-    n_dblk += b1 - b0;
-  } else {
-    issue_words(b0, R0);
-    for (uint32_t j = b0; j < bend + 2; j += 2) {
-      body(R0, R1, j);
-      if (j + 1 >= bend + 2) break;
-      body(R1, R0, j + 1);
-    }
+  issue_words(b0, R0);
+  for (uint32_t j = b0; j < bend + 2; j += 2) {
+    body(R0, R1, j);
+    if (j + 1 >= bend + 2) break;
+    body(R1, R0, j + 1);
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
   if (evb) flush();
@@ -2538,7 +2011,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh, 
 // kPhrase: the batch holds phrase queries (their position check is compiled
 // only into this instance, so the conjunctive kernel keeps its registers).
 template <bool kPhrase>
-__global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
+__global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, const QueryIn* __restrict__ qs,
                                                      const QueryPlan* __restrict__ plan, int nq,
                                                      uint32_t* __restrict__ counters,
                                                      Event* __restrict__ events,
@@ -2548,15 +2021,14 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
                                                      uint64_t* __restrict__ pub,
                                                      uint32_t* __restrict__ ph_all) {
   __shared__ WaveLds S;
-  WSR_T0()
   const uint32_t l = threadIdx.x & 63;
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) S.norm[l + 64 * i] = ix.cache[l + 64 * i];
   const uint64_t lt = lanemask_lt();
-  // general items are [merge end, total): the lean and merge kernels take the others
+  // general items are [lean end, total): the lean kernel takes the others
   const uint32_t total = uni(__hip_atomic_load(&counters[kCtrItems], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrMerge], __ATOMIC_RELAXED,
+  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0, n_oblk = 0;
   // first item: this workgroup's own index; then the shard heads
@@ -2733,7 +2205,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       ++n_dblk;
       const uint32_t a0 = cs.a0, a1 = cs.a1;
       bool al0 = cs.al0, al1 = cs.al1;
-      WSR_T(1)
       double s0 = 0.0, s1 = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
       const double nrm0 = S.norm[cs.ok0 ? (cs.c0 >> ((l & 1u) << 4)) & 0xFFu : 0u];
       const double nrm1 = S.norm[cs.ok1 ? (cs.c1 >> (((l & 1u) << 4) + 8)) & 0xFFu : 0u];
@@ -2770,7 +2241,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           if (al0) s0 += bm25_term(B.idf, t0, nrm0);
           if (al1) s1 += bm25_term(B.idf, t1, nrm1);
           rec(s, B.blk0 * 128u + fi0, B.blk0 * 128u + fi1, t0, t1);
-          WSR_T(2)
           continue;
         }
         if (use_dense(ix, B.bm != kNoDense, B.nblk, A.nblk)) {
@@ -2786,7 +2256,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           if (al0) s0 += bm25_term(B.idf, t0, nrm0);
           if (al1) s1 += bm25_term(B.idf, t1, nrm1);
           rec(s, B.blk0 * 128u + x0, B.blk0 * 128u + x1, t0, t1);
-          WSR_T(2)
           continue;
         }
         const uint32_t* last = ix.blk_last + B.blk0;
@@ -2899,7 +2368,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
         rec(s, (B.blk0 + j0) * 128u + p0, (B.blk0 + j1) * 128u + p1, t0, t1);
         // advance the cursor to the furthest block queried (docs only increase)
         if (l == 0 && nd && jlast > c && s < kMaxTerms) S.cur[s] = jlast;
-        WSR_T(3)
       }
       if (__ballot(al0 || al1) == 0) return;
       if (phrase) {   // HandleTheFoundDoc: rank only docs that hold the phrase
@@ -2961,7 +2429,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
           last_pub = pv;
         }
       }
-      WSR_T(4)
     };
 
     Stage sa, sb;
@@ -2969,7 +2436,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
       issue_words(b0);
       fetch(b0, sa);
     }
-    WSR_T(0)
     for (uint32_t b = b0; b < b1 && !done; b += 2) {
       step(sa, sb, b);
       if (b + 1 >= b1 || done) break;
@@ -2983,11 +2449,6 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
     stats[blockIdx.x * kStatStride + 0] = n_surv;
     stats[blockIdx.x * kStatStride + 1] = n_dblk;
     stats[blockIdx.x * kStatStride + 2] = n_oblk;
-#ifdef WSR_PROFILE
-    for (int i = 0; i < 5; ++i) stats[blockIdx.x * kStatStride + 4 + i] = prof_acc[i];
-    stats[blockIdx.x * kStatStride + 9] =
-        static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - prof_start);
-#endif
   }
 }
 
@@ -2997,40 +2458,28 @@ __global__ __launch_bounds__(64, WSR_SEG_WAVES) void segment_kernel(IndexArgs ix
 // Workgroups of kLeanWaves independent waves: each wave dequeues and runs its
 // own items, so the only workgroup barrier is the norm-table fill at start.
 // Small LDS (LeanLds per wave + one shared norm table) and a register budget
-// of WSR_LEAN_WGS workgroups per CU keep several waves per SIMD resident, which
+// of kLeanWgs workgroups per CU keep several waves per SIMD resident, which
 // is what hides the dependent loads of short items and of the probe chains.
-// 5 workgroups (the conjunctive instance: 96 VGPRs, 31.8 KB LDS, 5 waves per
-// SIMD; the phrase / bitmap-intersection instances stay LDS-bound at 2 and 4):
-// with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against 4
-// (profiles/r02_pr2_ab.txt).
-#ifndef WSR_LEAN_WGS
-#define WSR_LEAN_WGS 5
-#endif
-#ifndef WSR_LEAN_WGS_PHRASE
-#define WSR_LEAN_WGS_PHRASE 3
-#endif
-template <bool kPh, bool kAnd, bool kTwo = false>
-__global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd ? 4 : WSR_LEAN_WGS)) void lean_kernel(
+// 5 workgroups (the conjunctive instance: 96 VGPRs, 27.7 KB LDS, 5 waves per
+// SIMD): with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against
+// 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 3 (kLeanWgsPhrase).
+constexpr int kLeanWgs = 5;
+constexpr int kLeanWgsPhrase = 3;
+template <bool kPh, bool kTwo = false>
+__global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
     uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc, uint32_t* __restrict__ ph_all) {
-  __shared__ LeanLdsT<kPh, kAnd> SW[kLeanWaves];
-#ifdef WSR_LEAN_GNORM
-  const double* norm = ix.cache;   // (read through the caches: no LDS copy)
-  const uint32_t l = threadIdx.x & 63;
-#else
+  __shared__ LeanLdsT<kPh> SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
-#endif
   // (wave-uniform; said so, so that the item indices, segment bounds and the
   // pipeline's loop counter derived from it are scalar, not per-lane values)
   const uint32_t w = uni(threadIdx.x >> 6);
-#ifndef WSR_LEAN_GNORM
   for (uint32_t i = threadIdx.x; i < 256; i += 64 * kLeanWaves) norm[i] = ix.cache[i];
   __syncthreads();
-#endif
-  LeanLdsT<kPh, kAnd>& S = SW[w];
+  LeanLdsT<kPh>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
   uint32_t* ph = kPh ? ph_all + static_cast<uint64_t>(wid) * kPhraseScratch : nullptr;
   const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
@@ -3038,16 +2487,8 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd 
   uint32_t n_surv = 0, n_dblk = 0;
   uint32_t shard = wid % kQueueShards, tried = 0;
   uint32_t item = wid;
-#ifdef WSR_PROFILE
-  uint32_t* prof = S.prof;
-  for (int i = 0; i < 4; ++i) prof[i] = 0;
-#else
-  uint32_t* prof = nullptr;
-#endif
-  WSR_T0()
   for (;;) {
     if (item >= n_lean) item = next_item(&counters[kCtrHead0], 0, n_lean, shard, tried);
-    WSR_T(3)
     if (item >= n_lean) break;
     const uint32_t qi = uni(item_q[item]);
     const QueryDesc Q = desc[qi];   // everything the item's setup needs, one record
@@ -3078,492 +2519,14 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? WSR_LEAN_WGS_PHRASE : (kAnd 
     const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
     // an other list ends before this segment: nothing in it can match
     const bool done = first_doc > Q.min_last;
-    // a driver with a bitmap and a dense segment: intersect bitmaps word by word
-    const bool and_path = ix.and_wpb > 0.0f && Q.a_bm != kNoDense && b0 < b1 &&
-                          static_cast<float>((uni(S.dblk[b1 - 1 - b0].y) - first_doc) >> 5) <
-                              ix.and_wpb * static_cast<float>(b1 - b0);
-    WSR_T(0)
     // a query of one item with fused replay: the heap runs here, no events
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
     if (!done && b0 < b1)
-      lean_segment<kPh, kAnd, kTwo>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
-                   kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
-                   ph, and_path, first_doc, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
-                   my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk, prof);
-    WSR_T(1)
-    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
-    WSR_T(2)
-    item = 0xFFFFFFFFu;
-  }
-  if (l == 0) {
-    stats[wid * kStatStride + 0] = n_surv;
-    stats[wid * kStatStride + 1] = n_dblk;
-    stats[wid * kStatStride + 2] = 0;
-#ifdef WSR_PROFILE
-    for (int i = 0; i < 5; ++i) stats[wid * kStatStride + 4 + i] = prof_acc[i];
-    stats[wid * kStatStride + 9] = static_cast<uint32_t>(__builtin_amdgcn_s_memtime() - prof_start);
-    for (int i = 0; i < 4; ++i) stats[wid * kStatStride + 10 + i] = prof[i];
-#endif
-  }
-}
-
-// ------------------------------------------------------------ merge path --
-// Items of the merge class: the driver and the most selective other list O1
-// are both decoded from their packs and merged, instead of probing O1's rank
-// bitmap once per driver posting.  At en-Wikipedia shape the bitmap probes of
-// two long lists touch about 46 cache lines per driver block (O1 holds ~1-3 %
-// of the docs, its bitmap 2 bits per doc), which is what bounds the lean
-// kernel there (TA/TD ~80 % busy, profiles/r03_c_pmc); O1's own blocks over
-// the same doc range are ~R x 200 bytes, streamed (R = O1's blocks per driver
-// block, at most WSR_MERGE_RATIO).  Reference: the intersection this replaces
-// is TwoTermNonPhraseQueryProcessor::Process / QueryProcessor::FindMatch
-// (query_processing.h:656-677,810-852) over DocIdIterator::SkipForward
-// (flash_iterators.h:181-227); the survivors, their scores and the events are
-// the lean kernel's, so the replay and its exactness argument are unchanged.
-//
-// Per driver block j (doc range (prev_j, last_j]): O1's blocks [lo_j, hi_j]
-// that overlap it are decoded into an LDS ring (block b at slot b % ring; a
-// block shared with block j-1 is not decoded again), each driver doc is
-// searched in them (which block by the ring's last docs, then lower_bound in
-// the block), and the hits join the lean kernel's survivor queue.  The words
-// of driver block j+1 and of up to kMergeG of its new O1 blocks are loaded
-// while block j is processed (two alternating register sets); more O1 blocks,
-// or a range wider than the ring, take a slower synchronous path.
-#ifndef WSR_MERGE_RING
-#define WSR_MERGE_RING 8
-#endif
-#ifndef WSR_MERGE_G
-#define WSR_MERGE_G 4
-#endif
-constexpr int kMergeRing = WSR_MERGE_RING;   // O1 blocks held decoded (a power of two)
-constexpr int kMergeG = WSR_MERGE_G;         // O1 blocks prefetched per driver block
-static_assert((kMergeRing & (kMergeRing - 1)) == 0 && kMergeG <= kMergeRing, "merge ring");
-constexpr uint32_t kMergeQ = 128;            // survivor queue entries (a ring)
-
-struct MergeLds {
-  uint32_t ring[kMergeRing * 128];   // O1 doc ids; entries past a block's count are ~0u
-  uint32_t rlast[kMergeRing];        // last doc id of the block in each slot
-  uint32_t q[4 * kMergeQ];           // survivors: doc, length code, driver tf, O1 posting (block << 7 | pos)
-  Event evs[64];
-  uint4 dblk[64];                    // the driver's directory entries of the segment
-  uint32_t dmeta[64];
-};
-
-__device__ __forceinline__ void merge_segment(const IndexArgs& ix, MergeLds& S, const double* norm_tab,
-                                              const QueryDesc& Q, const int32_t* qlist, uint32_t b0,
-                                              uint32_t b1, bool dtail, uint32_t tdoc0, uint32_t tdoc1,
-                                              uint32_t ttf0, uint32_t ttf1, const uint64_t* prev_pub,
-                                              uint64_t* my_pub, Event* ev_out, uint32_t& ev_n, double& pt,
-                                              uint32_t& pt_n, uint32_t& n_surv, uint32_t& n_dblk) {
-  const uint32_t l = threadIdx.x & 63;
-  const uint64_t lt = lanemask_lt();
-  const uint32_t d = Q.slots & 0xFFFFu, o1 = Q.slots >> 16;
-  const uint32_t nt = Q.nt & 0xFFFFu, k = Q.k;
-  const bool wide = k > static_cast<uint32_t>(kMaxK);
-  const ListDev O = ix.lists[Q.o_list];
-  const uint32_t o_blk0 = uni(O.blk0), o_nblk = uni(O.nblk), o_tcnt = uni(O.tail_cnt);
-  const uint8_t* o_blob = ix.blob + O.base;
-  const bool o_vtail = O.tail != kNoTail;
-  const uint32_t* o_tails = ix.tails + (o_vtail ? O.tail : 0ull);
-  const uint8_t* a_blob = ix.blob + Q.a_base;
-  const uint32_t lo = in_vgpr(ix.doc_lo), hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);
-  const uint32_t min_last = Q.min_last;
-  const double idf_d = in_vgpr(Q.a_idf), idf_o = in_vgpr(Q.o_idf);
-  uint32_t* qdoc = S.q;
-  uint32_t* qc4 = S.q + kMergeQ;
-  uint32_t* qtd = S.q + 2 * kMergeQ;
-  uint32_t* qpo = S.q + 3 * kMergeQ;
-  uint32_t qhead = 0, qtail = 0, evb = 0;
-  uint64_t floor_bits =
-      prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-  double pub_val = 0.0, sent = 0.0;
-
-  auto flush = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_wave_barrier();
-    if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
-    __builtin_amdgcn_wave_barrier();
-    evb = 0;
-  };
-  // score survivors qhead .. qhead + n (n <= 64, lane = doc order), then the
-  // running top-k (as lean_segment's score_chunk)
-  auto score_chunk = [&](uint32_t n) __attribute__((always_inline)) {
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t e = (qhead + l) & (kMergeQ - 1);
-    bool alive = l < n;
-    const uint32_t doc = qdoc[e];
-    const uint32_t c4 = qc4[e];
-    const uint32_t td = qtd[e];
-    const uint32_t po = qpo[e];
-    __builtin_amdgcn_wave_barrier();
-    qhead += n;
-    // O1's tf: its pack (two dependent loads per survivor), or its decoded VInts tail
-    const uint32_t ob = alive ? po >> 7 : 0u, opos = po & 127u;
-    uint32_t to = 0;
-    if (o_vtail && ob == o_nblk - 1) {
-      to = o_tails[o_tcnt + opos];
-    } else {
-      const uint32_t tb = ix.blk_meta[o_blk0 + ob] >> 8;
-      const uint32_t trel = ix.blocks[o_blk0 + ob].tf_rel;
-      to = pack_value(o_blob + trel + 2, tb ? tb : 1u, opos);
-    }
-    const double norm = norm_tab[c4 & 255u];
-    double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
-    for (uint32_t s = 0; s < nt; ++s) {
-      if (s == d) {
-        sc += bm25_term(idf_d, alive ? td : 0u, norm);
-      } else if (s == o1) {
-        sc += bm25_term(idf_o, alive ? to : 0u, norm);
-      } else {
-        const ListDev B = ix.lists[qlist[s]];
-        uint32_t t = 0, x = 0;
-        const DenseVal v = dense_load(ix, B, doc, alive);
-        alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
-        if (__ballot(alive) == 0) break;
-        sc += bm25_term(B.idf, alive ? t : 0u, norm);
-      }
-    }
-    const uint64_t am = __ballot(alive);
-    if (am == 0) return;
-    n_surv += __popcll(am);
-    if (wide) {   // all of them, in doc order (lane order), no floor
-      if (alive) {
-        Event ev;
-        ev.score = sc;
-        ev.doc = static_cast<int32_t>(doc);
-        ev.pad = 0;
-        S.evs[evb + __popcll(am & lt)] = ev;
-      }
-      ev_n += __popcll(am);
-      evb += __popcll(am);
-      flush();
-      return;
-    }
-    // the floor of the query's earlier items as it stands now (it only grows)
-    if (prev_pub) {
-      const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t fu = (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
-                          uni(static_cast<uint32_t>(fb));
-      if (fu > floor_bits) floor_bits = fu;
-    }
-    const uint64_t fb = floor_bits;
-    const double flo = __longlong_as_double(static_cast<long long>(fb));
-    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-    uint64_t cm = __ballot(alive && sc > flo && (pt_n < k || sc > kth));
-    while (cm) {
-      const int fl = __builtin_ctzll(cm);
-      cm &= cm - 1;
-      const double sv = readlane_f64(sc, fl);
-      const uint32_t dv = __builtin_amdgcn_readlane(doc, fl);
-      const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
-      if (pos < k) {
-        if (l == 0) {
-          Event ev;
-          ev.score = sv;
-          ev.doc = static_cast<int32_t>(dv);
-          ev.pad = 0;
-          S.evs[evb] = ev;
-        }
-        ++ev_n;
-        ++evb;
-        const double up = wave_shr1_f64(pt);
-        if (l > pos) pt = up;
-        else if (l == pos) pt = sv;
-        pt_n = pt_n + 1 > k ? k : pt_n + 1;
-      }
-    }
-    if (evb) flush();
-    const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
-    const double pv = kn > flo ? kn : flo;
-    pub_val = pv > pub_val ? pv : pub_val;
-    if (my_pub && pub_val > sent) {   // hand the floor down the query's chain of items
-      if (l == 0)
-        __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      sent = pub_val;
-    }
-  };
-
-  // O1 directory window: lane l holds block wb + l (last = ~0u past the list)
-  uint32_t wb = 0, w_prev = 0, w_last = ~0u, w_doc = 0, w_meta = 0;
-  auto load_window = [&](uint32_t base) __attribute__((always_inline)) {
-    wb = base;
-    const uint32_t e = base + l;
-    w_prev = 0; w_last = ~0u; w_doc = 0; w_meta = 0;
-    if (e < o_nblk) {
-      const uint4 bd = reinterpret_cast<const uint4*>(ix.blocks)[o_blk0 + e];
-      w_prev = bd.x; w_last = bd.y; w_doc = bd.z;
-      w_meta = ix.blk_meta[o_blk0 + e];
-    }
-  };
-  // first O1 block at or after wb whose last doc is >= x (o_nblk if none);
-  // slides the window forward (callers ask in nondecreasing x)
-  auto first_ge = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
-    for (;;) {
-      const uint64_t below = __ballot(w_last < x);
-      if (~below) return min(wb + static_cast<uint32_t>(__builtin_ctzll(~below)), o_nblk);
-      if (wb + 64 >= o_nblk) return o_nblk;
-      load_window(wb + 64);
-    }
-  };
-  // the window must hold block b to decode it
-  auto cover = [&](uint32_t b) __attribute__((always_inline)) {
-    if (b < wb || b >= wb + 64) load_window(b);
-  };
-  // words of O1 block b for lane l (the VInts tail: its decoded doc ids)
-  auto o1_words = [&](uint32_t b, uint32_t& x0, uint32_t& x1, uint32_t& x2) __attribute__((always_inline)) {
-    const uint32_t i = b - wb;
-    const uint32_t bits = __builtin_amdgcn_readlane(w_meta, static_cast<int>(i)) & 0xFFu;
-    if (bits) {
-      uint32_t sh;
-      pair_words(o_blob + __builtin_amdgcn_readlane(w_doc, static_cast<int>(i)) + 2, bits, l, x0, x1, x2, sh);
-    } else {   // (only the list's last block is a VInts blob)
-      x0 = 2 * l < o_tcnt ? o_tails[2 * l] : 0u;
-      x1 = 2 * l + 1 < o_tcnt ? o_tails[2 * l + 1] : 0u;
-      x2 = 0;
-    }
-  };
-  uint32_t dec_hi = 0xFFFFFFFFu;   // the highest O1 block decoded (none yet)
-  // decode O1 block b (window-resident) from its words into its ring slot
-  auto o1_decode = [&](uint32_t b, uint32_t x0, uint32_t x1, uint32_t x2) __attribute__((always_inline)) {
-    const uint32_t i = b - wb;
-    const uint32_t m = __builtin_amdgcn_readlane(w_meta, static_cast<int>(i));
-    const uint32_t bits = m & 0xFFu;
-    const uint32_t cnt = b == o_nblk - 1 ? o_tcnt : 128u;
-    uint32_t v0, v1;
-    if (bits) {
-      const uint32_t rel = __builtin_amdgcn_readlane(w_doc, static_cast<int>(i));
-      const uint32_t bit = 2 * l * bits;
-      const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_blob)) + rel + 2 + (bit >> 3);
-      uint32_t y0, y1;
-      pair_values(x0, x1, x2, ((a & 3u) << 3) + (bit & 7u), bits, y0, y1);
-      const uint32_t sm = y0 + y1;
-      const uint32_t inc = wave_incl_scan(sm);
-      v0 = __builtin_amdgcn_readlane(w_prev, static_cast<int>(i)) + (inc - sm) + y0;
-      v1 = v0 + y1;
-    } else {
-      v0 = x0;
-      v1 = x1;
-    }
-    uint32_t* r = &S.ring[(b & (kMergeRing - 1)) * 128];
-    r[2 * l] = 2 * l < cnt ? v0 : 0xFFFFFFFFu;
-    r[2 * l + 1] = 2 * l + 1 < cnt ? v1 : 0xFFFFFFFFu;
-    if (l == 0) S.rlast[b & (kMergeRing - 1)] = __builtin_amdgcn_readlane(w_last, static_cast<int>(i));
-    dec_hi = b;
-  };
-  // lower_bound of x over ring blocks [c0, c1] (resident, c1 - c0 < ring):
-  // *blk = first block whose last >= x (c1 + 1: none), *pos = slot in it
-  auto ring_find = [&](uint32_t x, uint32_t c0, uint32_t c1, uint32_t* blk, uint32_t* pos)
-      __attribute__((always_inline)) {
-    uint32_t b = c0;
-    while (b <= c1 && S.rlast[b & (kMergeRing - 1)] < x) ++b;   // (at most the ring's blocks)
-    *blk = b;
-    if (b > c1) { *pos = 128; return; }
-    *pos = lds_lower_bound(&S.ring[(b & (kMergeRing - 1)) * 128], 128, x);
-  };
-
-  // two alternating register sets: driver block words, tf words, length codes,
-  // and the words of up to kMergeG new O1 blocks
-  struct MRegs {
-    uint32_t w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0, wc = 0;
-    uint32_t o0[kMergeG], o1w[kMergeG], o2[kMergeG];
-    uint32_t ob0 = 0, on = 0;    // prefetched O1 blocks [ob0, ob0 + on)
-    uint32_t lo = 0, hi = 0;     // the O1 blocks the driver block overlaps (lo = o_nblk: none)
-  };
-  MRegs R0, R1;
-  // W(j): the words of driver block j, the O1 range it overlaps and the words
-  // of its first new O1 blocks.  The range is found here, in block order, so
-  // the window only ever moves forward for it: lo_j and hi_j are asked in the
-  // order a_first_j <= a_last_j < a_first_j+1 ... (lo_j+1 >= hi_j).
-  auto issue = [&](uint32_t j, uint32_t hi_prev, MRegs& Y) __attribute__((always_inline)) {
-    const uint32_t bi = j - b0;
-    const uint32_t m = uni(S.dmeta[bi]);
-    const uint4 e = S.dblk[bi];
-    uint32_t sh;
-    pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
-    pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.t0, Y.t1, Y.t2, sh);
-    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + j) * 32u + (l >> 1)];
-    Y.lo = first_ge(j == 0 ? 0u : uni(e.x) + 1u);
-    Y.hi = Y.lo < o_nblk ? min(first_ge(uni(e.y)), o_nblk - 1) : o_nblk;
-    // O1 blocks this driver block needs beyond those the previous one needed
-    // (hi_prev: its last; this block's range starts at or after it)
-    const uint32_t from = hi_prev == 0xFFFFFFFFu ? Y.lo : max(hi_prev + 1, Y.lo);
-    Y.ob0 = from;
-    Y.on = 0;
-    if (Y.lo < o_nblk && from <= Y.hi && from >= wb) {
-      const uint32_t want = min(Y.hi - from + 1, static_cast<uint32_t>(kMergeG));
-      const uint32_t n = min(want, wb + 64 - from);   // (inside the window)
-#pragma unroll
-      for (int g = 0; g < kMergeG; ++g)
-        if (static_cast<uint32_t>(g) < n) o1_words(from + g, Y.o0[g], Y.o1w[g], Y.o2[g]);
-      Y.on = n;
-    }
-  };
-
-  uint32_t bend = b1;
-  // block j with the words in X
-  auto body = [&](MRegs& X, MRegs& Y, uint32_t j) __attribute__((always_inline)) {
-    const uint32_t bi = j - b0;
-    const uint4 be = S.dblk[bi];
-    const uint32_t m = uni(S.dmeta[bi]);
-    // O1 blocks overlapping this driver block (found by W(j))
-    const uint32_t lo_j = X.lo, hi_j = X.hi;
-    // decode the prefetched O1 blocks (they start after the last decoded one)
-    for (uint32_t g = 0; g < X.on; ++g) {
-      const uint32_t b = X.ob0 + g;
-      if (dec_hi != 0xFFFFFFFFu && b <= dec_hi) continue;
-      cover(b);
-      uint32_t x0 = X.o0[0], x1 = X.o1w[0], x2 = X.o2[0];
-#pragma unroll
-      for (int gg = 1; gg < kMergeG; ++gg)
-        if (g == static_cast<uint32_t>(gg)) { x0 = X.o0[gg]; x1 = X.o1w[gg]; x2 = X.o2[gg]; }
-      o1_decode(b, x0, x1, x2);
-    }
-    // W(j+1): the next block's words and its first new O1 blocks
-    if (j + 1 < bend) issue(j + 1, hi_j, Y);
-    // D(j): the driver's doc ids, tfs and length codes
-    const uint32_t cnt = (j == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u;
-    uint32_t x0, x1, t0, t1;
-    {
-      const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
-      const uint32_t bit = 2 * l * wbits;
-      const uint32_t ad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + uni(be.z) + 2 + (bit >> 3);
-      pair_values(X.w0, X.w1, X.w2, ((ad & 3u) << 3) + (bit & 7u), wbits, x0, x1);
-      const uint32_t tbit = 2 * l * wtb;
-      const uint32_t at = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + uni(be.w) + 2 + (tbit >> 3);
-      pair_values(X.t0, X.t1, X.t2, ((at & 3u) << 3) + (tbit & 7u), wtb, t0, t1);
-    }
-    const uint32_t sm = x0 + x1;
-    const uint32_t inc = wave_incl_scan(sm);
-    uint32_t a0 = uni(be.x) + (inc - sm) + x0;
-    uint32_t a1 = a0 + x1;
-    const bool tl = dtail && j == b1 - 1;
-    if (tl) { a0 = tdoc0; a1 = tdoc1; t0 = ttf0; t1 = ttf1; }
-    const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
-    const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
-    const bool ok0 = (2 * l < cnt) & (a0 - lo < hi_rel);
-    const bool ok1 = (2 * l + 1 < cnt) & (a1 - lo < hi_rel);
-    ++n_dblk;
-    if (__ballot((ok0 & (a0 > min_last)) | (ok1 & (a1 > min_last)))) bend = j + 1;
-    // S(j): search in O1's blocks [lo_j, hi_j], in ring-sized chunks
-    bool h0 = false, h1 = false;
-    uint32_t p0 = 0, p1 = 0;
-    if (lo_j < o_nblk) {
-      for (uint32_t c = lo_j; c <= hi_j;) {
-        const uint32_t ce = min(hi_j, c + kMergeRing - 1);
-        // (the slow path: blocks of the chunk not decoded yet, one at a time)
-        for (uint32_t b = (dec_hi == 0xFFFFFFFFu || dec_hi < c) ? c : dec_hi + 1; b <= ce; ++b) {
-          cover(b);
-          uint32_t y0, y1, y2;
-          o1_words(b, y0, y1, y2);
-          o1_decode(b, y0, y1, y2);
-        }
-        uint32_t bb, pp;
-        if (ok0 && !h0) {
-          ring_find(a0, c, ce, &bb, &pp);
-          if (bb <= ce && pp < 128 && S.ring[(bb & (kMergeRing - 1)) * 128 + pp] == a0) { h0 = true; p0 = (bb << 7) | pp; }
-        }
-        if (ok1 && !h1) {
-          ring_find(a1, c, ce, &bb, &pp);
-          if (bb <= ce && pp < 128 && S.ring[(bb & (kMergeRing - 1)) * 128 + pp] == a1) { h1 = true; p1 = (bb << 7) | pp; }
-        }
-        c = ce + 1;
-      }
-    }
-    // C(j): hits to the survivor queue in doc order; score every full 64
-    const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
-    // (a block adds up to 128 hits to the < 64 queued: a queue that would
-    // overflow is scored first, as a partial chunk)
-    if (qtail - qhead + __popcll(m0) + __popcll(m1) > kMergeQ) score_chunk(qtail - qhead);
-    const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
-    const uint32_t r1 = r0 + (h0 ? 1u : 0u);
-    if (h0) {
-      const uint32_t e0 = r0 & (kMergeQ - 1);
-      qdoc[e0] = a0; qc4[e0] = c0; qtd[e0] = t0; qpo[e0] = p0;
-    }
-    if (h1) {
-      const uint32_t e1 = r1 & (kMergeQ - 1);
-      qdoc[e1] = a1; qc4[e1] = c1; qtd[e1] = t1; qpo[e1] = p1;
-    }
-    qtail += __popcll(m0) + __popcll(m1);
-#pragma nounroll
-    for (int cc = 0; cc < 2 && qtail - qhead >= 64; ++cc) score_chunk(64);
-  };
-
-  if (b0 < b1 && o_nblk) {
-    // the window starts at the first O1 block that can hold a doc of the segment
-    load_window(uni(find_block(ix.blk_last + o_blk0, 0, o_nblk, b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u)));
-    issue(b0, 0xFFFFFFFFu, R0);
-    for (uint32_t j = b0; j < bend; j += 2) {
-      body(R0, R1, j);
-      if (j + 1 >= bend) break;
-      body(R1, R0, j + 1);
-    }
-  }
-  if (qtail != qhead) score_chunk(qtail - qhead);
-  if (evb) flush();
-  if (my_pub && pub_val > sent && l == 0)
-    __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_wave_barrier();
-}
-
-// Persistent, workgroups of kMergeWaves independent waves (as lean_kernel):
-// each wave dequeues merge items [n_lean, n_merge) and runs merge_segment.
-#ifndef WSR_MERGE_WGS
-#define WSR_MERGE_WGS 4
-#endif
-__global__ __launch_bounds__(64 * kMergeWaves, WSR_MERGE_WGS) void merge_kernel(
-    IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
-    uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
-    uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
-    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc) {
-  __shared__ MergeLds SW[kMergeWaves];
-  __shared__ double norm[256];
-  const uint32_t l = threadIdx.x & 63;
-  const uint32_t w = uni(threadIdx.x >> 6);
-  for (uint32_t i = threadIdx.x; i < 256; i += 64 * kMergeWaves) norm[i] = ix.cache[i];
-  __syncthreads();
-  MergeLds& S = SW[w];
-  const uint32_t wid = blockIdx.x * kMergeWaves + w;
-  const uint32_t m_lo = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t m_hi = uni(__hip_atomic_load(&counters[kCtrMerge], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  uint32_t n_surv = 0, n_dblk = 0;
-  uint32_t shard = wid % kQueueShards, tried = 0;
-  uint32_t item = m_lo + wid;
-  for (;;) {
-    if (item >= m_hi) item = next_item(&counters[kCtrMHead0], m_lo, m_hi, shard, tried);
-    if (item >= m_hi) break;
-    const uint32_t qi = uni(item_q[item]);
-    const QueryDesc Q = desc[qi];
-    const uint32_t r = item - Q.item_base;
-    const uint32_t seg = Q.seg;
-    const uint32_t b0 = r * seg;
-    const uint32_t b1 = min(b0 + seg, Q.a_nblk);
-    Event* ev_out = events + Q.ev_base + static_cast<uint64_t>(r) * seg * 128;
-    uint64_t* my_pub = pub ? pub + item : nullptr;
-    const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
-    __builtin_amdgcn_wave_barrier();
-    if (b0 + l < b1) {
-      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + b0 + l];
-      S.dmeta[l] = ix.blk_meta[Q.a_blk0 + b0 + l];
-    }
-    const bool dtail = b0 < b1 && b1 == Q.a_nblk && Q.a_tail != kNoTail;
-    uint32_t tdoc0 = 0, tdoc1 = 0, ttf0 = 0, ttf1 = 0;
-    if (dtail) {
-      const uint32_t cnt = Q.a_tail_cnt;
-      const uint32_t* t = ix.tails + Q.a_tail;
-      if (2 * l < cnt) { tdoc0 = t[2 * l]; ttf0 = t[cnt + 2 * l]; }
-      if (2 * l + 1 < cnt) { tdoc1 = t[2 * l + 1]; ttf1 = t[cnt + 2 * l + 1]; }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t first_doc = b0 == 0 ? 0u : uni(S.dblk[0].x) + 1u;
-    const bool done = first_doc > Q.min_last;   // an other list ends before this segment
-    double pt = 0.0;
-    uint32_t pt_n = 0, ev_n = 0;
-    if (!done && b0 < b1)
-      merge_segment(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)), b0, b1, dtail, tdoc0, tdoc1, ttf0,
-                    ttf1, prev_pub, my_pub, ev_out, ev_n, pt, pt_n, n_surv, n_dblk);
+      lean_segment<kPh, kTwo>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
+                              kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
+                              ph, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
+                              my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
     finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
     item = 0xFFFFFFFFu;
   }
@@ -3575,122 +2538,6 @@ __global__ __launch_bounds__(64 * kMergeWaves, WSR_MERGE_WGS) void merge_kernel(
 }
 
 // ------------------------------------------------------ doc-range shards --
-// Shard side: reduce each query's segment events to the events of a heap run
-// from empty over the whole shard (a superset of the global insertions inside
-// the shard), compacted in place at the query's event base; count -> scount[q].
-__global__ __launch_bounds__(64) void shard_reduce_kernel(const QueryIn* __restrict__ qs,
-                                                          const QueryPlan* __restrict__ plan, int nq,
-                                                          Event* __restrict__ events,
-                                                          const uint32_t* __restrict__ ev_cnt,
-                                                          int32_t* __restrict__ scount) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const QueryPlan P = plan[qi];
-  const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
-  Event* out = events + P.ev_base;
-  uint32_t n = 0;
-  // writes land at out[n], below the address of every event not yet read
-  // (event g of the stream sits at or above out + g, and n <= g)
-  auto emit = [&](double sv, int32_t dv) {
-    if ((threadIdx.x & 63) == 0) { Event e; e.score = sv; e.doc = dv; e.pad = 0; out[n] = e; }
-    ++n;
-  };
-  auto count_of = [&](uint32_t r) { return ev_cnt[P.item_base + r]; };
-  auto base_of = [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; };
-  if (k > static_cast<uint32_t>(kMaxK)) {   // wide: every survivor goes to the owner
-    PassFilter F;
-    consume_stream(F, P.n_items, count_of, base_of, emit);
-  } else {
-    EventFilter F;
-    F.k = k;
-    consume_stream(F, P.n_items, count_of, base_of, emit);
-  }
-  if ((threadIdx.x & 63) == 0) scount[qi] = static_cast<int32_t>(n);
-}
-
-// Exclusive scan of cnt[0..n) -> off[0..n) (64-bit), single workgroup; the
-// total per segment of `seg` consecutive entries -> seg_total[n / seg].
-__global__ __launch_bounds__(1024) void scan_counts_kernel(const int32_t* __restrict__ cnt, int n,
-                                                           int seg, uint64_t* __restrict__ off,
-                                                           int64_t* __restrict__ seg_total) {
-  __shared__ uint64_t s[1024];
-  const int t = threadIdx.x, T = blockDim.x;
-  const int per = (n + T - 1) / T;
-  const int i0 = t * per, i1 = min(n, i0 + per);
-  uint64_t sum = 0;
-  for (int i = i0; i < i1; ++i) sum += static_cast<uint64_t>(cnt[i]);
-  s[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < T; d <<= 1) {
-    uint64_t a = t >= d ? s[t - d] : 0;
-    __syncthreads();
-    s[t] += a;
-    __syncthreads();
-  }
-  uint64_t run = s[t] - sum;
-  for (int i = i0; i < i1; ++i) { off[i] = run; run += static_cast<uint64_t>(cnt[i]); }
-  __syncthreads();
-  if (seg_total && seg > 0)
-    for (int g = t; g * seg < n; g += T) {
-      const int e = min(n, (g + 1) * seg) - 1;
-      seg_total[g] = static_cast<int64_t>(off[e] + static_cast<uint64_t>(cnt[e]) - off[g * seg]);
-    }
-}
-
-// Copy each query's compacted shard events to send[off[q]] (owner-major order).
-__global__ __launch_bounds__(64) void pack_events_kernel(const QueryPlan* __restrict__ plan, int nq,
-                                                         const Event* __restrict__ events,
-                                                         const int32_t* __restrict__ scount,
-                                                         const uint64_t* __restrict__ off,
-                                                         Event* __restrict__ send) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const Event* src = events + plan[qi].ev_base;
-  Event* dst = send + off[qi];
-  const int n = scount[qi];
-  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
-}
-
-// Owner side: for each owned query, the events every shard sent, in shard
-// (= doc-id range) order, through the filter and the heap.
-// rcount[g * nq + q], roff[g * nq + q] (offset inside shard g's block), rbase[g].
-__global__ __launch_bounds__(64) void owner_replay_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
-                                                          int n_shards,
-                                                          const int32_t* __restrict__ rcount,
-                                                          const uint64_t* __restrict__ roff,
-                                                          const uint64_t* __restrict__ rbase,
-                                                          uint64_t slot,
-                                                          const Event* __restrict__ recv,
-                                                          HitDev* __restrict__ hits, int hit_stride,
-                                                          int32_t* __restrict__ n_hits) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const int gq = q0 + qi;
-  const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
-  auto count_of = [&](uint32_t g) {   // (a negative count marks a sender's slot overflow: flagged, read as 0)
-    const int32_t c = rcount[static_cast<int64_t>(g) * nq + qi];
-    return static_cast<uint32_t>(c > 0 ? c : 0);
-  };
-  auto base_of = [&](uint32_t g) {
-    return recv + (rbase ? rbase[g] : g * slot) + roff[static_cast<int64_t>(g) * nq + qi];
-  };
-  if (k > static_cast<uint32_t>(kMaxK)) {   // wide: the heap in LDS
-    __shared__ double s_hs[kMaxKWide];
-    __shared__ int32_t s_hd[kMaxKWide];
-    LdsHeapSink sink;
-    sink.hs = s_hs;
-    sink.hd = s_hd;
-    sink.k = k;
-    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
-    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
-    return;
-  }
-  HeapSink sink;
-  sink.k = k;
-  consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
-  sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
-}
-
 // Owner side of the fused exchange (wsr_shard_step): meta[g * meta_stride +
 // 2 * i] = {count, offset} shard g sent for owned query i (count -1: the
 // sender's slot overflowed: flagged, read as empty); its events at recv +
@@ -3736,79 +2583,17 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
   }
 }
 
-// Fixed-slot exchange (no host round trip): owner o's events from this shard
-// go to send[o * slot ...] in query order; a query whose events would pass the
-// slot's end is not copied, its count becomes -1 and the error flag is set (the
-// owner's replay flags it again).  off = exclusive scan of scount over all the
-// batch's queries (scan_counts_kernel).
-__global__ __launch_bounds__(64) void pack_fixed_kernel(const QueryPlan* __restrict__ plan, int nq,
-                                                        const Event* __restrict__ events,
-                                                        int32_t* __restrict__ scount,
-                                                        const uint64_t* __restrict__ off, int q_per_owner,
-                                                        uint64_t slot, Event* __restrict__ send,
-                                                        uint32_t* __restrict__ counters) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
-  const int o = qi / q_per_owner;
-  const uint64_t rel = off[qi] - off[o * q_per_owner];
-  const int n = scount[qi];
-  if (rel + static_cast<uint64_t>(n) > slot) {
-    if (threadIdx.x == 0) {
-      scount[qi] = -1;
-      atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
-    }
-    return;
-  }
-  const Event* src = events + plan[qi].ev_base;
-  Event* dst = send + o * slot + rel;
-  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
-}
-
-// Owner side: per shard row g of rcount (n counts each), the exclusive scan of
-// its counts (negative = a sender's overflow: flagged, counted as 0).
-__global__ __launch_bounds__(1024) void scan_rows_kernel(const int32_t* __restrict__ cnt, int n,
-                                                         uint64_t* __restrict__ off,
-                                                         uint32_t* __restrict__ counters) {
-  __shared__ uint64_t s[1024];
-  const int t = threadIdx.x, T = blockDim.x;
-  const int32_t* c = cnt + static_cast<int64_t>(blockIdx.x) * n;
-  uint64_t* o = off + static_cast<int64_t>(blockIdx.x) * n;
-  const int per = (n + T - 1) / T;
-  const int i0 = t * per, i1 = min(n, i0 + per);
-  uint64_t sum = 0;
-  bool bad = false;
-  for (int i = i0; i < i1; ++i) {
-    const int32_t v = c[i];
-    bad |= v < 0;
-    sum += v > 0 ? static_cast<uint64_t>(v) : 0ull;
-  }
-  if (bad) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrExchange));
-  s[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < T; d <<= 1) {
-    const uint64_t a = t >= d ? s[t - d] : 0;
-    __syncthreads();
-    s[t] += a;
-    __syncthreads();
-  }
-  uint64_t run = s[t] - sum;
-  for (int i = i0; i < i1; ++i) {
-    o[i] = run;
-    run += c[i] > 0 ? static_cast<uint64_t>(c[i]) : 0ull;
-  }
-}
-
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int merge_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st) {
   const int n_part = std::max(1, (nq + kPlanThreads - 1) / kPlanThreads);
   hipLaunchKernelGGL(plan_query_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, ix, q, nq, plan,
                      counters, fr, desc, part);
   hipLaunchKernelGGL(plan_fill_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, nq, plan, part, n_part,
                      counters, ev_capacity, item_capacity, static_cast<uint32_t>(lean_grid),
-                     static_cast<uint32_t>(merge_grid), static_cast<uint32_t>(seg_grid), item_q, pub, desc);
+                     static_cast<uint32_t>(seg_grid), item_q, pub, desc);
   return hipGetLastError();
 }
 
@@ -3831,45 +2616,21 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st) {
   // (a persistent grid sized for the conjunctive instance: waves of a larger
   // instance that find no room start later and find the queue drained)
-  // (phrase batches: the bitmap-intersection path only when it is on, so the
-  // default phrase instance leaves out its step buffer, as the conjunctive one)
-  if (ph && ix.and_wpb > 0.0f)
-    hipLaunchKernelGGL((lean_kernel<true, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
+  if (ph)
+    hipLaunchKernelGGL((lean_kernel<true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
                        nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
-  else if (ph)
-    hipLaunchKernelGGL((lean_kernel<true, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
-                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
-  else if (ix.and_wpb > 0.0f)
+  else if (two)
     hipLaunchKernelGGL((lean_kernel<false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
                        plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
-  else if (two)
-    hipLaunchKernelGGL((lean_kernel<false, false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
-                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   else
-    hipLaunchKernelGGL((lean_kernel<false, false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
+    hipLaunchKernelGGL((lean_kernel<false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
                        plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
   return hipGetLastError();
-}
-
-hipError_t launch_merge(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
-                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
-                        int merge_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                        uint64_t* pub, const QueryDesc* desc, hipStream_t st) {
-  hipLaunchKernelGGL(merge_kernel, dim3(merge_wgs), dim3(64 * kMergeWaves), 0, st, ix, q, plan, nq, counters,
-                     events, ev_cnt, stats, fr, item_q, pub, desc);
-  return hipGetLastError();
-}
-
-int merge_kernel_occupancy() {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, merge_kernel, 64 * kMergeWaves, 0) != hipSuccess)
-    return 1;
-  return n;
 }
 
 int lean_kernel_occupancy() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false, false>, 64 * kLeanWaves, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false>, 64 * kLeanWaves, 0) != hipSuccess)
     return 1;
   return n;
 }
@@ -3883,71 +2644,10 @@ hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, c
   return hipGetLastError();
 }
 
-hipError_t set_replay_prof(uint32_t* rows) {
-#ifdef WSR_REPLAY_PROF
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_replay_prof), &rows, sizeof rows);
-#else
-  (void)rows;
-  return hipErrorNotSupported;
-#endif
-}
-
-hipError_t launch_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
-                         const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,
-                         hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(replay_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events,
-                     ev_cnt, hits, hit_stride, n_hits);
-  return hipGetLastError();
-}
-
 int segment_kernel_occupancy() {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, segment_kernel<false>, 64, 0) != hipSuccess) return 1;
   return n;
-}
-
-hipError_t launch_shard_reduce(const QueryIn* q, const QueryPlan* plan, int nq, Event* events,
-                               const uint32_t* ev_cnt, int32_t* scount, hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(shard_reduce_kernel, dim3(nq), dim3(64), 0, st, q, plan, nq, events, ev_cnt,
-                     scount);
-  return hipGetLastError();
-}
-
-hipError_t launch_scan_counts(const int32_t* cnt, int n, int seg, uint64_t* off, int64_t* seg_total,
-                              hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, st, cnt, n, seg, off, seg_total);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_events(const QueryPlan* plan, int nq, const Event* events,
-                              const int32_t* scount, const uint64_t* off, Event* send,
-                              hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_events_kernel, dim3(nq), dim3(64), 0, st, plan, nq, events, scount, off,
-                     send);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_fixed(const QueryPlan* plan, int nq, const Event* events, int32_t* scount,
-                             const uint64_t* off, int q_per_owner, uint64_t slot, Event* send,
-                             uint32_t* counters, hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_fixed_kernel, dim3(nq), dim3(64), 0, st, plan, nq, events, scount, off,
-                     q_per_owner, slot, send, counters);
-  return hipGetLastError();
-}
-
-hipError_t launch_owner_replay_fixed(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
-                                     uint64_t* roff, uint64_t slot, const Event* recv, HitDev* hits,
-                                     int hit_stride, int32_t* n_hits, uint32_t* counters, hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_rows_kernel, dim3(n_shards), dim3(1024), 0, st, rcount, nq, roff, counters);
-  hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount, roff,
-                     static_cast<const uint64_t*>(nullptr), slot, recv, hits, hit_stride, n_hits);
-  return hipGetLastError();
 }
 
 hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* meta,
@@ -3960,15 +2660,6 @@ hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shar
   if (any_wide)
     hipLaunchKernelGGL(owner_replay_meta_kernel<true>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
                        meta_stride, stride, recv, hits, hit_stride, n_hits, counters);
-  return hipGetLastError();
-}
-
-hipError_t launch_owner_replay(const QueryIn* q, int q0, int nq, int n_shards, const int32_t* rcount,
-                               const uint64_t* roff, const uint64_t* rbase, const Event* recv,
-                               HitDev* hits, int hit_stride, int32_t* n_hits, hipStream_t st) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(owner_replay_kernel, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, rcount,
-                     roff, rbase, static_cast<uint64_t>(0), recv, hits, hit_stride, n_hits);
   return hipGetLastError();
 }
 

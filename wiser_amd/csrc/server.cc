@@ -131,6 +131,10 @@ struct wsr_server {
   std::atomic<int> sleeping{kAwake};
   alignas(64) std::atomic<int> n_busy{0};
   std::atomic<bool> stop{false};
+  // callers between their stop check and their entry's publication: the
+  // dispatcher ends only when stop is set, none is in there and every
+  // claimed entry was taken (so no request is left in the ring at close)
+  alignas(64) std::atomic<int> submitting{0};
   std::thread worker, completer;
   Slot slots[kSlots];
   std::mutex fmu;                    // the launched batches, oldest first
@@ -246,7 +250,14 @@ struct wsr_server {
       const uint64_t queued = t - next;
       const int busy = n_busy.load(std::memory_order_seq_cst);
       if (queued == 0) {
-        if (stop.load()) break;   // everything submitted was launched
+        if (stop.load(std::memory_order_seq_cst)) {
+          // everything submitted was launched, unless a caller that saw stop
+          // still clear has not claimed its entry yet: wait for it
+          if (submitting.load(std::memory_order_seq_cst) == 0 && tail.load(std::memory_order_seq_cst) == next)
+            break;
+          std::this_thread::yield();
+          continue;
+        }
         doze(kWantWork, ww, t, busy, -1);
         continue;
       }
@@ -328,7 +339,11 @@ struct wsr_server {
     const int qrc = wsr_check_query(h, &q);
     if (qrc != WSR_OK) return qrc;
     if (q.k > WSR_SERVER_MAX_K) return WSR_E_LIMIT;   // the slots' result columns
-    if (stop.load(std::memory_order_relaxed)) return WSR_E_INVALID;
+    submitting.fetch_add(1, std::memory_order_seq_cst);
+    if (stop.load(std::memory_order_seq_cst)) {
+      submitting.fetch_sub(1, std::memory_order_seq_cst);
+      return WSR_E_INVALID;
+    }
     const uint64_t i = tail.fetch_add(1, std::memory_order_seq_cst);
     while (i - consumed.load(std::memory_order_acquire) >= kRing) std::this_thread::yield();   // (ring full)
     Entry& e = ring[i & (kRing - 1)];
@@ -336,6 +351,7 @@ struct wsr_server {
     e.r = r;
     e.t_enq = now_ns();
     e.seq.store(i + 1, std::memory_order_seq_cst);
+    submitting.fetch_sub(1, std::memory_order_seq_cst);
     // wake a dispatcher asleep for work, or for a full batch when this one fills it
     const int s = sleeping.load(std::memory_order_seq_cst);
     if (s == kWantWork || (s == kWantFull && i + 1 - consumed.load(std::memory_order_relaxed) >=
