@@ -170,6 +170,12 @@ int wsr_runtime_info(char* buf, int32_t cap);
 int wsr_open(const char* vacuum_dir, const wsr_open_opts* opts, wsr_handle** out);
 void wsr_close(wsr_handle* h);
 int wsr_image_info_get(wsr_handle* h, wsr_image_info* out);
+/* The same figures without a device (host only): the image wsr_open would
+ * build for the doc range [doc_lo, doc_hi) (doc_hi 0 = all) of the index in
+ * dir, with positions / blooms as wsr_open_opts and the same load-time knobs,
+ * sized but never uploaded.  threads: host threads (0 = all). */
+int wsr_image_size(const char* dir, uint32_t doc_lo, uint32_t doc_hi, int32_t positions, int32_t bloom_factor,
+                   int32_t threads, wsr_image_info* out);
 int wsr_term_count(wsr_handle* h, int32_t* out);
 int wsr_n_docs(wsr_handle* h, int32_t* out);
 /* list id (or -1) and document frequency (0 if absent) of one term */

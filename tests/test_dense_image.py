@@ -90,3 +90,26 @@ def test_dense_bitmap_tok10k(indexes):
         dense, got = _lookup(d, t, 0, 0, 128, n)
         assert not dense and set(got) == {-1}
     orc.close()
+
+
+def test_image_size_host_only(synth_small):
+    """wsr_image_size (no device): the per-buffer sizes add up; doc-range shard
+    images hold about 1/W of the blocks and of the bitmaps each, so the W
+    shards together stay within a few percent of the whole image plus the
+    per-shard directory heads; with positions the position boxes are added."""
+    import wiser_amd as w
+    d, st = synth_small
+    full = w.image_size(d, threads=4)
+    parts = ("blob_bytes", "dense_bytes", "tf8_bytes", "plen_bytes", "dir_bytes", "pos_bytes")
+    assert full["total_bytes"] == sum(full[p] for p in parts)
+    assert full["dense_lists"] > 0 and full["pos_bytes"] == 0
+    from wiser_amd.shard import shard_range
+    for world in (2, 4, 8):
+        sh = [w.image_size(d, doc_range=shard_range(st.n_docs, r, world), threads=4) for r in range(world)]
+        assert all(s["n_lists"] == full["n_lists"] for s in sh)
+        # bitmaps cover the shard's doc range only: W of them ~ one whole one
+        assert sum(s["dense_bytes"] for s in sh) <= 1.15 * full["dense_bytes"] + world * 64 * full["dense_lists"]
+        # every shard keeps the blocks that can hold its docs: ~1/W of a list's
+        # blocks, plus at most one block per list at each shard edge
+        assert sum(s["plen_bytes"] for s in sh) <= full["plen_bytes"] + world * 128 * full["n_lists"]
+        assert max(s["total_bytes"] for s in sh) < full["total_bytes"]

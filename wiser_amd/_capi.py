@@ -92,6 +92,8 @@ _sigs = {
     "wsr_open": (C.c_int, [C.c_char_p, C.POINTER(OpenOpts), C.POINTER(_P)]),
     "wsr_close": (None, [_P]),
     "wsr_image_info_get": (C.c_int, [_P, C.POINTER(ImageInfo)]),
+    "wsr_image_size": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
+                                 C.POINTER(ImageInfo)]),
     "wsr_term_count": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "wsr_n_docs": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "wsr_lookup": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

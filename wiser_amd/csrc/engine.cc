@@ -170,6 +170,37 @@ struct wsr_batch {
   bool ran = false;
 };
 
+namespace {
+// bytes dev_upload allocates for a host array (at least one element)
+template <class V>
+uint64_t dev_bytes(const V& v) {
+  return std::max<uint64_t>(v.size(), 1) * sizeof(typename V::value_type);
+}
+
+// the image's HBM buffers, per kind, as wsr_open allocates them
+wsr_image_info image_info_of(const HostImage& img, size_t n_c4) {
+  wsr_image_info o{};
+  if (img.has_blooms) o.pos_bytes += dev_bytes(img.blm) + dev_bytes(img.blm_hash);
+  if (img.has_positions)
+    o.pos_bytes += dev_bytes(img.pos_blob) + dev_bytes(img.pos_lists) + dev_bytes(img.pos_pk) +
+                   dev_bytes(img.pos_tail) + dev_bytes(img.pos_start);
+  o.dense_bytes = dev_bytes(img.dense) + dev_bytes(img.dense_rank);
+  o.tf8_bytes = dev_bytes(img.tf8);
+  o.blob_bytes = dev_bytes(img.blob);
+  o.plen_bytes = dev_bytes(img.plen);
+  o.dir_bytes = dev_bytes(img.tails) + dev_bytes(img.lists) + dev_bytes(img.blocks) + dev_bytes(img.blk_last) +
+                dev_bytes(img.blk_meta) + std::max<uint64_t>(n_c4, 1);
+  o.dense_lists = img.dense_lists;
+  o.n_lists = static_cast<uint32_t>(img.lists.size());
+  o.total_bytes = o.blob_bytes + o.dense_bytes + o.tf8_bytes + o.plen_bytes + o.dir_bytes + o.pos_bytes;
+  return o;
+}
+
+// the load-time knobs of wsr_open (environment)
+uint32_t dense_div_knob() { return static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048)); }
+uint64_t dense_budget_knob() { return static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 48) * 1e9); }
+}  // namespace
+
 extern "C" {
 
 const char* wsr_last_error(void) { return g_err.c_str(); }
@@ -180,6 +211,23 @@ int wsr_image_info_get(wsr_handle* h, wsr_image_info* out) {
   *out = h->info;
   out->total_bytes = out->blob_bytes + out->dense_bytes + out->tf8_bytes + out->plen_bytes + out->dir_bytes +
                      out->pos_bytes;
+  return WSR_OK;
+}
+
+
+int wsr_image_size(const char* dir, uint32_t doc_lo, uint32_t doc_hi, int32_t positions, int32_t bloom_factor,
+                   int32_t threads, wsr_image_info* out) {
+  if (!dir || !out) return fail(WSR_E_INVALID, "null argument");
+  try {
+    VacuumIndex idx;
+    idx.open(dir);
+    const int t = threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency());
+    const HostImage img = build_image(idx, doc_lo, doc_hi ? doc_hi : 0xFFFFFFFFu, std::min(t, 32), dense_div_knob(),
+                                      positions != 0, dense_budget_knob(), positions && bloom_factor > 0);
+    *out = image_info_of(img, idx.char4_lengths().size());
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
   return WSR_OK;
 }
 
@@ -222,8 +270,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
     // caps the bitmaps' HBM, longest lists first: 48 GB, as the 8-byte rank
     // records put the C3 stand-in's at 33 GB)
-    const uint32_t dense_div = static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048));
-    const uint64_t dense_budget = static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 48) * 1e9);
+    const uint32_t dense_div = dense_div_knob();
+    const uint64_t dense_budget = dense_budget_knob();
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
     h->positions = opts && opts->positions;
     const uint32_t bloom_factor = opts && opts->bloom_factor > 0 ? static_cast<uint32_t>(opts->bloom_factor) : 0u;

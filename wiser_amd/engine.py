@@ -379,6 +379,18 @@ class Server:
             pass
 
 
+def image_size(index_dir: str, doc_range=None, positions: bool = False, bloom_factor: int = 0,
+               threads: int = 0) -> Dict[str, int]:
+    """HBM bytes per buffer of the image wsr_open would build for index_dir (or
+    its doc range [lo, hi)), computed on the host without a device
+    (wsr_image_size)."""
+    lo, hi = doc_range or (0, 0)
+    i = _capi.ImageInfo()
+    check(lib.wsr_image_size(index_dir.encode(), lo, hi, 1 if positions else 0, bloom_factor, threads,
+                             C.byref(i)))
+    return {f: getattr(i, f) for f, _ in _capi.ImageInfo._fields_}
+
+
 def sync(engine: VacuumEngine) -> None:
     check(lib.wsr_sync(engine._h))
 
