@@ -790,10 +790,10 @@ def open_full(idx, local, threads, rank, world, dist):
     return staggered(dist, rank, world, load)
 
 
-def open_shard_engines(a, idx, rank, world, local, dist, threads, need_full):
-    """This rank's doc-range shard image (with the engine's RCCL communicator)
-    and, for the hybrid and replica forms, the full-index image."""
-    import wiser_amd as w
+def open_shard_engine(a, idx, rank, world, local, dist, threads):
+    """This rank's doc-range shard image with the engine's RCCL communicator
+    (the full-index image the hybrid and replica forms also need is opened
+    separately, open_full, after the pure doc-range form has run alone)."""
     from wiser_amd.shard import NativeShardedSearcher
     t = time.time()
 
@@ -809,9 +809,8 @@ def open_shard_engines(a, idx, rank, world, local, dist, threads, need_full):
         S = HostExchangeShardedSearcher(idx, rank, world, device=local, threads=threads, positions=False)
     else:
         S = NativeShardedSearcher(idx, rank, world, share_id, device=local, threads=threads, positions=False)
-    full = open_full(idx, local, threads, rank, world, dist) if need_full else None
-    log(f"rank {rank}: shard {S.doc_range}{' + full image' if full else ''} loaded in {time.time()-t:.1f}s")
-    return S, full
+    log(f"rank {rank}: shard {S.doc_range} loaded in {time.time()-t:.1f}s")
+    return S
 
 
 def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
@@ -1080,21 +1079,36 @@ def main():
     forms = {}      # N > 1: every form measured, reduced over ranks
     full = S = None
     t = time.time()
-    if mode == "replica":
-        full = open_full(idx, local, threads, rank, world, dist)
-        log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
-    else:
-        hb_default = max(64, 63 * world)
-        S, full = open_shard_engines(a, idx, rank, world, local, dist, threads,
-                                     need_full=(a.heavy_blocks != 0 or a.mode == "auto"))
-    load_s = round(time.time() - t, 1)
-
     def reduced(r):
         el, q, p50 = r["el"], r["queries"], r["p50"]
         if dist:
             el, q, p50 = reduce_timing(dist, el, q, p50, False, summed=True)
         return {"value": round(q / el, 1), "ms_per_step": round(el / a.steps * 1e3, 4),
                 "p50_alone_ms": round(p50, 3), "queries": int(q), "seconds": round(el, 5)}
+
+    shard_bytes = full_bytes = None
+    if mode == "replica":
+        full = open_full(idx, local, threads, rank, world, dist)
+        log(f"rank {rank}: engine loaded in {time.time()-t:.1f}s")
+    else:
+        hb_default = max(64, 63 * world)
+        S = open_shard_engine(a, idx, rank, world, local, dist, threads)
+        shard_bytes = S.engine.image_info()["total_bytes"]
+        if world > 1 and a.mode == "auto" and a.heavy_blocks != 0:
+            # the pure doc-range form first, with only this rank's shard image
+            # resident: the form an index larger than one GPU runs, and its own
+            # HBM per rank
+            r = run_shard(a, S, None, 0, lines, rank, world, dist)
+            forms["docshard"] = {**reduced(r), "parallelism": f"docshard{world}", "slot_events": r["slot"],
+                                 "shard_every": r["every"], "hbm_per_rank": shard_bytes,
+                                 "note": "every query on every shard, one ncclAllToAll per sharded step, "
+                                         "only the rank's shard image resident"}
+            r["close"]()
+        if a.heavy_blocks != 0 or a.mode == "auto":
+            full = open_full(idx, local, threads, rank, world, dist)
+    load_s = round(time.time() - t, 1)
+    if full is not None:
+        full_bytes = full.image_info()["total_bytes"]
 
     if mode == "replica":
         main_run = run_replica(a, full, idx, lines, rank, world, dist)
@@ -1118,21 +1132,12 @@ def main():
     host_ms = main_run["host_ms"]
     main_run["close"]()
     if world > 1 and a.mode == "auto":
-        # the other forms, from the same images: every query doc-range sharded
-        # (the north_star layout), and replicas (control, no collective)
-        if a.heavy_blocks != 0:
-            r = run_shard(a, S, full, 0, lines, rank, world, dist)
-            forms["docshard"] = {**reduced(r), "parallelism": f"docshard{world}", "slot_events": r["slot"],
-                                 "shard_every": r["every"],
-                                 "note": "every query on every shard, one ncclAllToAll per sharded step"}
-            r["close"]()
+        # the control, from the same full image: replicas (no collective)
         r = run_replica(a, full, idx, lines, rank, world, dist)
-        forms["replica"] = {**reduced(r), "parallelism": f"replicas{world}",
+        forms["replica"] = {**reduced(r), "parallelism": f"replicas{world}", "hbm_per_rank": full_bytes,
                             "note": "control: the full index on every GPU, each rank its own 4096 "
                                     "queries, no collective"}
         r["close"]()
-    shard_bytes = S.engine.image_info()["total_bytes"] if S is not None else None
-    full_bytes = full.image_info()["total_bytes"] if full is not None else None
     if S is not None:
         S.close()
     if full is not None:
@@ -1208,7 +1213,8 @@ def main():
                                "shard_every": main_run["every"],
                                "heavy_query_share": round(main_run["heavy_share"], 4)}
             out["hbm_per_rank"] = {"shard_image_bytes": shard_bytes, "full_image_bytes": full_bytes,
-                                   "total_bytes": (shard_bytes or 0) + (full_bytes or 0)}
+                                   "total_bytes": (shard_bytes or 0) + (full_bytes or 0),
+                                   "note": "the value's form; forms.*.hbm_per_rank: each form's own"}
         if forms:
             out["forms"] = forms
         if extra:

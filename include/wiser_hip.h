@@ -139,8 +139,9 @@ typedef struct wsr_batch_stats {
   uint64_t survivors;        /* docs in every list (scored) */
   uint64_t driver_blocks;    /* 128-posting blocks decoded from driver lists */
   uint64_t other_blocks;     /* blocks decoded from the other lists */
-  uint64_t algo_bytes;       /* sum over queries of docid+tf span bytes of its lists
-                                + survivors * 1 B + k * 12 B */
+  uint64_t algo_bytes;       /* sum over queries of docid+tf span bytes of its lists (a phrase
+                                query: + the lists' position boxes) + survivors * 1 B + k * 12 B
+                                 */
   double plan_ms, segment_ms, replay_ms;  /* HIP-event times on the engine stream */
   uint64_t events;           /* segment heap-insertion events handed to the replay */
   uint64_t max_query_events; /* the largest per-query event count of the batch */

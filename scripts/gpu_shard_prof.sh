@@ -1,0 +1,30 @@
+#!/bin/bash
+# Where a doc-range shard step's time goes, rehearsed with one rank (the whole
+# sharded path over a one-rank RCCL communicator) against the replica: bench
+# lines with host phase timers (WSR_HOST_TIMING), then rocprofv3 kernel traces
+# of the pure doc-range form and the replica.  Every GPU step has its own
+# limit; the first failure ends the script.  Usage: TAG [bench args...]
+set -eu -o pipefail
+TAG=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+O=$R/gpurun_out/$TAG
+P=/tmp/wsr_shprof_$TAG
+mkdir -p "$O" "$P"
+export TMPDIR=/tmp
+cd "$R"
+WSR_HOST_TIMING=1 timeout -k 10 400 python3 bench.py --mode shard --heavy-blocks 0 --no-extra --no-cpu \
+    --steps 1000 "$@" > "$O/shard_hb0.json" 2> "$O/shard_hb0.err"
+grep -h "wsr_shard_step host" "$O/shard_hb0.err" || true
+WSR_HOST_TIMING=1 timeout -k 10 400 python3 bench.py --mode shard --no-extra --no-cpu \
+    --steps 1000 "$@" > "$O/shard_hybrid.json" 2> "$O/shard_hybrid.err"
+grep -h "wsr_shard_step host" "$O/shard_hybrid.err" || true
+cd /tmp
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/hb0" -o hb0 -- \
+    python3 "$R/bench.py" --mode shard --heavy-blocks 0 --no-extra --no-cpu --steps 300 "$@" \
+    > "$O/prof_hb0.json" 2> "$O/prof_hb0.err"
+find "$P/hb0" -name "*kernel_stats.csv" -exec cp {} "$O/hb0_kernel_stats.csv" \;
+find "$P/hb0" -name "*kernel_trace.csv" -exec cp {} "$P/hb0_trace.csv" \;
+python3 "$R/scripts/trace_overlap.py" "$P/hb0_trace.csv" lean_kernel segment_kernel plan_query_kernel \
+    plan_fill_kernel owner_replay_meta_kernel > "$O/hb0_overlap.json"
+python3 "$R/scripts/shard_timeline.py" "$P/hb0_trace.csv" > "$O/hb0_timeline.txt" || true
+echo "hb0 trace ok"

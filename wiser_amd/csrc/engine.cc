@@ -116,6 +116,7 @@ struct wsr_handle {
   wsr_image_info info{};            // HBM bytes of the image's buffers
   std::vector<ListDev> lists;       // host copy of the directory heads
   std::vector<uint64_t> list_bytes; // docid+tf span bytes per list in this image
+  std::vector<uint64_t> pos_bytes;  // position box bytes per list (positions on)
   std::vector<BlockDev> blocks;     // host copy (debug decode)
   std::vector<uint32_t> meta;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
@@ -302,6 +303,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
       h->args.pos_pk = reinterpret_cast<const uint2*>(h->d_pos_pk);
       h->args.pos_tail = h->d_pos_tail;
       h->args.pos_start = h->d_pos_start;
+      h->pos_bytes = img.pos_list_bytes;
       std::vector<uint8_t>().swap(img.pos_blob);
       std::vector<uint32_t>().swap(img.pos_start);
     }
@@ -704,7 +706,12 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       for (int t = 0; t < d.n_terms; ++t)
         if (t != drv && !dense(t)) lean = false;
       (lean ? lean_need : gen_need) += nbmin;
-      for (int t = 0; t < d.n_terms; ++t) algo += h->list_bytes[ids[t]];
+      // every term's docid+tf span, and for a phrase query also its
+      // position box (the bags the position check reads from)
+      for (int t = 0; t < d.n_terms; ++t) {
+        algo += h->list_bytes[ids[t]];
+        if (phrase && !h->pos_bytes.empty()) algo += h->pos_bytes[ids[t]];
+      }
       algo += 12ull * d.k;
     }
   }

@@ -760,6 +760,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     for (auto& p : pos_parts) pb += (p.bytes.size() + 15) & ~15ull;
     img.pos_blob.resize(pb + 64, 0);   // tail pad: lanes read whole dwords
     img.pos_lists.resize(L, PosDev{0, 0, 0, 0});
+    img.pos_list_bytes.assign(L, 0);
     uint64_t pat = 0;
     for (int32_t id = 0; id < L; ++id) {
       PosPart& p = pos_parts[id];
@@ -768,6 +769,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       pd.pk0 = static_cast<uint32_t>(img.pos_pk.size() / 2);
       pd.npk = static_cast<uint32_t>(p.pk.size() / 2);
       pd.tail = img.pos_tail.size();
+      img.pos_list_bytes[id] = p.bytes.size();
       if (!p.bytes.empty()) std::memcpy(&img.pos_blob[pat], p.bytes.data(), p.bytes.size());
       pat += (p.bytes.size() + 15) & ~15ull;
       img.pos_pk.insert(img.pos_pk.end(), p.pk.begin(), p.pk.end());

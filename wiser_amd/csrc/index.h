@@ -139,6 +139,7 @@ struct HostImage {
   std::vector<uint32_t> pos_pk;             // per full pack: byte offset, bit width (pairs)
   std::vector<uint32_t> pos_tail;
   std::vector<uint32_t> pos_start;          // bag start entry per posting slot (as plen)
+  std::vector<uint64_t> pos_list_bytes;     // bytes of each list's position box (algorithmic bytes)
   // two-way phrase bloom filters (build_image(..., blooms = true), positions
   // images of bloom indexes whose bit arrays fit 16 bytes): per posting slot
   // (as plen) 32 bytes, its "prior" (begin) then its "next" (end) bit array,
