@@ -130,7 +130,7 @@ def parse():
                    help="skip the secondary legs (N=1 only)")
     p.add_argument("--legs", default="",
                    help="comma list of secondary legs to run (default: all of c2_synthetic_1m, "
-                        "end_to_end, c4_mixed_1to5, c5_phrase, serving, c1_snippets)")
+                        "end_to_end, c4_mixed_1to5, c5_phrase, c3_topics, serving, c1_snippets)")
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
@@ -577,12 +577,61 @@ def extra_legs(a, idx, qlog, local, threads):
         legs["c5_phrase"]["workload"] = (f"{ptag}: 10000 two-term phrase queries from the corpus's "
                                          "phrase pool (gen_synthetic_log.py:216-265), top-10")
         eng.close()
+    if want("c3_topics") and a.workload == "c3" and not (a.vacuum_dir or a.linedoc):
+        legs["c3_topics"] = topics_leg(a, local, threads)
     if want("serving"):
         legs["serving"] = serving_leg(a, idx, qlog, local, threads)
     if want("c1_snippets"):
         legs["c1_snippets"] = snippet_leg(a, local, threads)
     del c2_idx
     return legs
+
+
+TOPICS = dict(topics=128, topics_per_term=2, affinity=0.6)
+
+
+def ensure_c3_topics(a):
+    """The topic-clustered C3 stand-in (the same df histogram; doc ids in 128
+    contiguous topic ranges, every term under N/16 postings draws 60 % of its
+    docs from two home topics) and its 100k two-term log."""
+    d = os.path.join(a.index_dir, f"c3_topics_{a.c3_docs}_{a.c3_term_scale:g}")
+    qlog = os.path.join(d, "two_term_100000.log")
+    if not os.path.exists(os.path.join(d, "READY")):
+        os.makedirs(d, exist_ok=True)
+        info = in_child(
+            f"t = time.time()\n"
+            f"st = w.build_wiki_standin({d!r}, n_docs={a.c3_docs}, term_scale={a.c3_term_scale!r}, "
+            f"threads={HOST_THREADS}, **{TOPICS!r})\n"
+            f"w.gen_two_term_log({d!r}, {qlog!r}, n_queries=100000, seed=7)\n"
+            f"print(json.dumps({{'docs': st.n_docs, 'terms': st.n_terms, 'postings': st.n_postings, "
+            f"'build_s': round(time.time() - t, 1)}}))")
+        open(os.path.join(d, "READY"), "w").write("ok")
+        log(f"C3 topic-clustered stand-in built: {info}")
+    return d, qlog
+
+
+def topics_leg(a, local, threads):
+    """the headline workload on the topic-clustered stand-in
+    (ensure_c3_topics), whose terms co-occur by topic as a real corpus's do,
+    and its high x high class alone (both terms df >= 10k, the first 4096)."""
+    import wiser_amd as w
+    idx, qlog = ensure_c3_topics(a)
+    t = time.time()
+    eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
+    eng.Load()
+    load_s = round(time.time() - t, 1)
+    lines = [l.split() for l in open(qlog).read().splitlines()]
+    out = run_leg(eng, idx, [(q, False) for q in lines], a.k, a.batch, 4, a.check,
+                  0 if a.no_cpu else a.cpu_seconds / 8)
+    hh = [q for q in lines if all(eng.lookup(x)[1] >= 10000 for x in q)][:a.batch]
+    out["high_high"] = run_leg(eng, idx, [(q, False) for q in hh], a.k, a.batch, 4, a.check, 0)
+    out.update({"load_s": load_s, "image": eng.image_info(),
+                "workload": (f"C3 stand-in with topic-clustered doc ids ({TOPICS}), the same df "
+                             "histogram, its 100000 two-term AND log (gen_synthetic_log rule, seed 7), "
+                             "top-10, batches of 4096, device-resident; high_high: its first 4096 queries "
+                             "whose two terms both have df >= 10k")})
+    eng.close()
+    return out
 
 
 def snippet_leg(a, local, threads):

@@ -367,6 +367,12 @@ int wsr_build_synthetic(const char* out_dir, int64_t n_docs, int64_t vocab, doub
  * disk, so host memory does not grow with the corpus */
 int wsr_build_wiki_standin(const char* out_dir, int64_t n_docs, double term_scale, uint64_t seed,
                            int32_t threads, wsr_build_stats* st);
+/* the same df histogram with topic-clustered doc ids (writer.h WikiSpec::topics):
+ * `topics` contiguous doc-id ranges, every term under N/16 postings draws
+ * `affinity` of its docs from its `topics_per_term` home topics */
+int wsr_build_wiki_standin_topics(const char* out_dir, int64_t n_docs, double term_scale, uint64_t seed,
+                                  int32_t threads, int32_t topics, int32_t topics_per_term, double affinity,
+                                  wsr_build_stats* st);
 int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                          const char* out_path, int64_t* n_written);
 /* mixed 1-5 term AND log (AOL term-count shares; SURVEY 8d "C4") */

@@ -261,3 +261,25 @@ def test_c5_full_size_docshard8(c3_full, c3_shards8):
     bad = [(q, g[:3], x[:3]) for q, g, x in zip(qs2, got, want) if g != x]
     assert not bad, bad[:3]
     assert sum(1 for x in want if x) > len(qs2) // 2
+
+
+# ---- a topic-clustered corpus (terms co-occur by topic) ----
+@pytest.fixture(scope="module")
+def c3_topics(built, tmp_path_factory):
+    """The full-size stand-in with topic-clustered doc ids (bench.py TOPICS)."""
+    import wiser_amd as w
+    d = str(tmp_path_factory.mktemp("c3topics"))
+    st = w.build_wiki_standin(d, n_docs=5_500_000, term_scale=1.0, threads=min(16, os.cpu_count()),
+                              topics=128, topics_per_term=2, affinity=0.6)
+    log = os.path.join(d, "two_term_100000.log")
+    w.gen_two_term_log(d, log, n_queries=100_000, seed=7)
+    return d, log, st
+
+
+def test_c3_topics_full_size_logged_queries(c3_topics):
+    """2,048 queries spread over the clustered corpus's whole 100k log, top-10,
+    bit for bit against the oracle."""
+    d, log, st = c3_topics
+    assert st.n_docs == 5_500_000
+    nonempty = _check_log(d, log, 2048, stride=48)
+    assert nonempty > 100

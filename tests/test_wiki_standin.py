@@ -100,3 +100,48 @@ def test_phrase_pool_and_positions(tiny):
     # b's docs share half of the smaller list with a; 60 % of those are phrases
     assert both > 100 and 0.45 < adjacent / both < 0.8, (both, adjacent)
     orc.close()
+
+
+def test_topic_clustered_variant(tiny, tmp_path):
+    """The topic-clustered stand-in (WikiSpec::topics): the df of every term,
+    and so the histogram, equals the uniform stand-in's; a term's doc ids
+    gather in its home topics' ranges; two terms with a common home topic
+    intersect far more often than two without; deterministic."""
+    import wiser_amd as w
+    from oracle.oracle import OracleVacuum
+    d0, st0 = tiny
+    n, topics = 20_000, 16
+    d = str(tmp_path / "topics")
+    st = w.build_wiki_standin(d, n_docs=n, term_scale=0.002, threads=4, topics=topics, topics_per_term=1,
+                              affinity=0.8)
+    assert (st.n_terms, st.n_postings) == (st0.n_terms, st0.n_postings)
+    o0, o = OracleVacuum(d0), OracleVacuum(d)
+    width = n // topics
+    home = {}
+    # (a phrase pair's second word takes half its docs from the first word's)
+    seconds = {l.split()[1] for l in open(os.path.join(d, "phrases.txt")).read().splitlines()}
+    for i in range(st.n_terms):
+        t = f"w{i:08d}"
+        assert o.df(t) == o0.df(t), t
+        docs, _ = o.postings(t)
+        # (clustered while its home topic stays at most half full: df * 0.8 <= width / 2)
+        if 50 <= len(docs) and len(docs) * 0.8 <= width / 2 and t not in seconds:
+            top = max(range(topics), key=lambda k: sum(1 for x in docs if k * width <= x < (k + 1) * width))
+            share = sum(1 for x in docs if top * width <= x < (top + 1) * width) / len(docs)
+            assert share > 0.6, (t, share)   # 0.8 affinity + the uniform rest
+            home[t] = (top, set(docs))
+    same, diff = [], []
+    terms = list(home)
+    for i in range(len(terms)):
+        for j in range(i + 1, min(len(terms), i + 40)):
+            (ka, a), (kb, b) = home[terms[i]], home[terms[j]]
+            r = len(a & b) / (len(a) * len(b) / n)   # intersection over the independent expectation
+            (same if ka == kb else diff).append(r)
+    assert same and diff and sum(same) / len(same) > 4 * sum(diff) / len(diff)
+    d2 = str(tmp_path / "again")
+    w.build_wiki_standin(d2, n_docs=n, term_scale=0.002, threads=2, topics=topics, topics_per_term=1,
+                         affinity=0.8)
+    for f in ("my.vacuum", "my.doc_length"):
+        assert open(os.path.join(d, f), "rb").read() == open(os.path.join(d2, f), "rb").read(), f
+    o0.close()
+    o.close()

@@ -139,6 +139,8 @@ _sigs = {
                                       C.c_int32, C.c_int32, C.POINTER(BuildStats)]),
     "wsr_build_wiki_standin": (C.c_int, [C.c_char_p, C.c_int64, C.c_double, C.c_uint64,
                                          C.c_int32, C.POINTER(BuildStats)]),
+    "wsr_build_wiki_standin_topics": (C.c_int, [C.c_char_p, C.c_int64, C.c_double, C.c_uint64, C.c_int32,
+                                                C.c_int32, C.c_int32, C.c_double, C.POINTER(BuildStats)]),
     "wsr_gen_two_term_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                        C.POINTER(C.c_int64)]),
     "wsr_batch_ready": (C.c_int, [_P, _P]),

@@ -165,8 +165,15 @@ struct wsr_batch {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // [4]: lean kernel end
   // Each batch runs on its own streams, so consecutive batches overlap on the
   // device (one's plan and first items under the other's last items); the
-  // general kernel goes to st2, forked from and joined back into st.
-  hipStream_t st = nullptr, st2 = nullptr;
+  // general kernel goes to st2, forked from and joined back into st.  HIP maps
+  // streams to its hardware queues (GPU_MAX_HW_QUEUES, 4) round-robin in
+  // creation order, and kernels of one queue run in order: a batch creates
+  // three streams (st_pad is never used), so the lean kernels of consecutive
+  // batches land on queues 3 apart, i.e. on all four in turn, instead of
+  // alternating between two (with two streams per batch the C3 headline fell
+  // from 21.7 to 18.9 M q/s and C2 from 35.0 to 29.6 M at unchanged per-batch
+  // kernel times, profiles/r04a_bench.json).
+  hipStream_t st = nullptr, st2 = nullptr, st_pad = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   bool ran = false;
 };
@@ -603,6 +610,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&b->st_pad, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&b->fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&b->join, hipEventDisableTiming));
   } catch (const std::exception& e) {
@@ -633,6 +641,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (b->join) (void)hipEventDestroy(b->join);
   if (b->st) (void)hipStreamDestroy(b->st);
   if (b->st2) (void)hipStreamDestroy(b->st2);
+  if (b->st_pad) (void)hipStreamDestroy(b->st_pad);
   delete b;
 }
 
@@ -1522,6 +1531,28 @@ int wsr_build_wiki_standin(const char* out_dir, int64_t n_docs, double term_scal
     sp.term_scale = term_scale;
     sp.seed = seed;
     sp.threads = threads;
+    fill_stats(build_wiki_standin(sp, out_dir), st);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_build_wiki_standin_topics(const char* out_dir, int64_t n_docs, double term_scale, uint64_t seed,
+                                  int32_t threads, int32_t topics, int32_t topics_per_term, double affinity,
+                                  wsr_build_stats* st) {
+  if (!out_dir || n_docs < 16 || !(term_scale > 0) || topics < 1 || topics_per_term < 1 || topics_per_term > 16 ||
+      !(affinity >= 0 && affinity <= 1) || topics > n_docs)
+    return fail(WSR_E_INVALID, "bad arguments");
+  try {
+    WikiSpec sp;
+    sp.n_docs = n_docs;
+    sp.term_scale = term_scale;
+    sp.seed = seed;
+    sp.threads = threads;
+    sp.topics = topics;
+    sp.topics_per_term = topics_per_term;
+    sp.affinity = affinity;
     fill_stats(build_wiki_standin(sp, out_dir), st);
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());

@@ -1103,13 +1103,31 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
 
   // df distinct uniform doc ids, sorted: by rejection for rare terms, by
   // selection sampling (Knuth's algorithm S) for common ones
-  auto uniform_docs = [&](uint32_t df, std::mt19937_64& g, std::vector<uint32_t>* out) {
+  // (topic-clustered variant: a draw lands in one of the term's home topics
+  // with probability `affinity`; the term's topics come from its id)
+  const int64_t T = sp.topics > 0 ? sp.topics : 0;
+  const int K = std::max(1, sp.topics_per_term);
+  auto uniform_docs = [&](uint32_t df, std::mt19937_64& g, std::vector<uint32_t>* out, int64_t id) {
     std::vector<uint32_t>& docs = *out;
     docs.clear();
     if (static_cast<int64_t>(df) * 16 < N) {
+      // home-topic draws only while the topics' ranges stay at most half full
+      const bool clustered = T > 0 && static_cast<double>(df) * sp.affinity <= 0.5 * K * (N / T);
+      uint64_t home[16];
+      for (int j = 0; j < std::min(K, 16); ++j)
+        home[j] = mix64(sp.seed ^ (static_cast<uint64_t>(id + 1) * 0xC2B2AE3D27D4EB4Full) ^ static_cast<uint64_t>(j)) %
+                  static_cast<uint64_t>(T > 0 ? T : 1);
+      auto draw = [&]() -> uint32_t {
+        if (clustered && unit(g) < sp.affinity) {
+          const uint64_t t = home[g() % static_cast<uint64_t>(std::min(K, 16))];
+          const int64_t lo = static_cast<int64_t>(t) * N / T, hi = (static_cast<int64_t>(t) + 1) * N / T;
+          return static_cast<uint32_t>(lo + static_cast<int64_t>(g() % static_cast<uint64_t>(hi - lo)));
+        }
+        return static_cast<uint32_t>(g() % static_cast<uint64_t>(N));
+      };
       while (docs.size() < df) {
         const size_t need = df - docs.size();
-        for (size_t i = 0; i < need; ++i) docs.push_back(static_cast<uint32_t>(g() % static_cast<uint64_t>(N)));
+        for (size_t i = 0; i < need; ++i) docs.push_back(draw());
         std::sort(docs.begin(), docs.end());
         docs.erase(std::unique(docs.begin(), docs.end()), docs.end());
       }
@@ -1135,7 +1153,7 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
       {
         // (a is never a pool b itself, so this does not recurse)
         std::mt19937_64 gg(sp.seed ^ (0x9E3779B97F4A7C15ull * static_cast<uint64_t>(a + 1)));
-        uniform_docs(dfs[a], gg, &ad);
+        uniform_docs(dfs[a], gg, &ad, a);
       }
       const uint32_t c = std::min<uint32_t>(df, static_cast<uint32_t>(ad.size())) / 2;
       // c of a's docs (partial Fisher-Yates), then uniform docs not yet taken
@@ -1150,7 +1168,7 @@ BuildStats build_wiki_standin(const WikiSpec& sp, const std::string& out_dir) {
       }
       if (docs.size() > df) docs.resize(df);   // (never: unique keeps at most df)
     } else {
-      uniform_docs(df, g, &docs);
+      uniform_docs(df, g, &docs, id);
     }
     const double base = 0.3 + 5.0 * static_cast<double>(df) / static_cast<double>(N);
     tfs_out->resize(docs.size());

@@ -68,6 +68,17 @@ struct WikiSpec {
   double term_scale = 1.0;
   uint64_t seed = 0x3C3C2026ull;
   int threads = 0;
+  // Topic-clustered variant (topics > 0; 0 = the uniform stand-in above): doc
+  // ids are cut into `topics` contiguous ranges (a topic's articles sit
+  // together, as a dump's ids follow creation order by portal / category), every
+  // term below N/16 postings whose draws keep its home topics at most half full
+  // gets topics_per_term home topics (from its id) and draws `affinity` of its
+  // doc ids inside them, the rest uniformly; the df of every term, and so the
+  // df histogram, is unchanged.  Terms with a common home topic then co-occur
+  // far more often than independent draws.
+  int topics = 0;
+  int topics_per_term = 2;
+  double affinity = 0.6;
 };
 BuildStats build_wiki_standin(const WikiSpec& spec, const std::string& out_dir);
 

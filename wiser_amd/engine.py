@@ -421,12 +421,20 @@ def build_synthetic(out_dir: str, n_docs: int = 1_000_000, vocab: int = 500_000,
 
 
 def build_wiki_standin(out_dir: str, n_docs: int = 5_500_000, term_scale: float = 1.0,
-                       seed: int = 0x3C3C2026, threads: int = 0) -> _capi.BuildStats:
+                       seed: int = 0x3C3C2026, threads: int = 0, topics: int = 0,
+                       topics_per_term: int = 2, affinity: float = 0.6) -> _capi.BuildStats:
     """BASELINE configs[2] stand-in: df histogram of the reference's en-Wikipedia
-    index (tools/gen_synthetic_log.py:8-16) x term_scale over n_docs docs."""
+    index (tools/gen_synthetic_log.py:8-16) x term_scale over n_docs docs.
+    topics > 0: the topic-clustered variant (doc ids in `topics` contiguous
+    ranges, every term under N/16 postings draws `affinity` of its docs from
+    its topics_per_term home topics; the df histogram is unchanged)."""
     st = _capi.BuildStats()
-    check(lib.wsr_build_wiki_standin(out_dir.encode(), n_docs, term_scale, seed, threads,
-                                     C.byref(st)))
+    if topics > 0:
+        check(lib.wsr_build_wiki_standin_topics(out_dir.encode(), n_docs, term_scale, seed, threads, topics,
+                                                topics_per_term, affinity, C.byref(st)))
+    else:
+        check(lib.wsr_build_wiki_standin(out_dir.encode(), n_docs, term_scale, seed, threads,
+                                         C.byref(st)))
     return st
 
 
