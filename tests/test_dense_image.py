@@ -107,9 +107,58 @@ def test_image_size_host_only(synth_small):
     for world in (2, 4, 8):
         sh = [w.image_size(d, doc_range=shard_range(st.n_docs, r, world), threads=4) for r in range(world)]
         assert all(s["n_lists"] == full["n_lists"] for s in sh)
-        # bitmaps cover the shard's doc range only: W of them ~ one whole one
-        assert sum(s["dense_bytes"] for s in sh) <= 1.15 * full["dense_bytes"] + world * 64 * full["dense_lists"]
+        # bitmaps and buckets cover the shard's doc range only: W of them ~ one
+        # whole one; the buckets' offset bytes, like tf8, are one per posting
+        # of the shard's blocks, whose edge blocks also hold postings outside
+        # the range (a one-block list is in every shard it reaches)
+        edge = sum(s["tf8_bytes"] for s in sh) - full["tf8_bytes"]
+        assert sum(s["dense_bytes"] for s in sh) <= (1.15 * full["dense_bytes"] + edge +
+                                                     world * 64 * full["dense_lists"])
         # every shard keeps the blocks that can hold its docs: ~1/W of a list's
         # blocks, plus at most one block per list at each shard edge
         assert sum(s["plen_bytes"] for s in sh) <= full["plen_bytes"] + world * 128 * full["n_lists"]
         assert max(s["total_bytes"] for s in sh) < full["total_bytes"]
+
+
+@pytest.fixture(scope="module")
+def bucket_index(built, tmp_path_factory):
+    """Lists below the bucket density (1/25) with crowded buckets: "z" in docs
+    0-9, 500-519 and the last doc (one 256-doc bucket holds ten), "f" in docs
+    1000-1255 (full 64-doc buckets: every probe past the fourth posting scans
+    the offset bytes), "s" every 40th doc, "y" every other doc (a bitmap)."""
+    import wiser_amd as w
+    root = tmp_path_factory.mktemp("buckets")
+    ld = root / "b.linedoc"
+    n = 8000
+    with open(ld, "w") as f:
+        f.write("FIELDS_HEADER_INDICATOR###\tdoctitle\tbody\ttokenized\n")
+        for i in range(n):
+            toks = [f"u{i}"]
+            if i < 10 or 500 <= i < 520 or i == n - 1:
+                toks.append("z")
+            if 1000 <= i < 1256:
+                toks += ["f"] * (1 + i % 3)
+            if i % 40 == 7:
+                toks.append("s")
+            if i % 2:
+                toks.append("y")
+            f.write(f"t\t{' '.join(toks)}\t{' '.join(toks)}\n")
+    d = root / "idx"
+    d.mkdir()
+    w.build_from_linedoc(str(ld), str(d), "TOKEN_ONLY")
+    return str(d)
+
+
+def test_dense_buckets(bucket_index):
+    """Offset buckets (sparse dense lists) answer every doc id exactly as the
+    oracle, whole image and doc-range shards, crowded buckets included."""
+    from oracle.oracle import OracleVacuum
+    orc = OracleVacuum(bucket_index)
+    n = orc.n_docs()
+    for term in ("z", "f", "s", "y", "u77"):
+        for lo, hi in _shards(n) + [(1024, 1280), (1030, 1100)]:
+            dense, got = _lookup(bucket_index, term, lo, hi, 1 << 30, n)
+            exp = _expect(orc, term, lo, hi if hi else n, n)
+            assert dense or set(exp) == {-1}, (term, lo, hi)
+            assert got == exp, (term, lo, hi)
+    orc.close()

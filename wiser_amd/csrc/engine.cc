@@ -101,6 +101,7 @@ struct wsr_handle {
   double* d_cache = nullptr;
   DenseEnt* d_dense = nullptr;
   uint32_t* d_dense_rk = nullptr;   // the bitmap entries' rank records
+  uint32_t* d_bkt = nullptr;        // offset buckets (entries and offset bytes)
   uint8_t* d_tf8 = nullptr;
   uint8_t* d_plen = nullptr;
   uint32_t* d_tails = nullptr;
@@ -146,7 +147,7 @@ struct wsr_batch {
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
-  bool two_only = false;         // every query: two terms (or empty), k <= kMaxK, no phrase
+  bool two_only = false;         // every query: two terms (or empty), k <= kMaxK
   int seg_grid = 0;
   int lean_wgs = 0;
   // doc-range shard exchange (wsr_shard_step): per owner a region of {count,
@@ -192,7 +193,7 @@ wsr_image_info image_info_of(const HostImage& img, size_t n_c4) {
   if (img.has_positions)
     o.pos_bytes += dev_bytes(img.pos_blob) + dev_bytes(img.pos_lists) + dev_bytes(img.pos_pk) +
                    dev_bytes(img.pos_tail) + dev_bytes(img.pos_start);
-  o.dense_bytes = dev_bytes(img.dense) + dev_bytes(img.dense_rank);
+  o.dense_bytes = dev_bytes(img.dense) + dev_bytes(img.dense_rank) + dev_bytes(img.bkt);
   o.tf8_bytes = dev_bytes(img.tf8);
   o.blob_bytes = dev_bytes(img.blob);
   o.plen_bytes = dev_bytes(img.plen);
@@ -316,12 +317,14 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     }
     h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
     h->info.dense_bytes += dev_upload(&h->d_dense_rk, img.dense_rank);
+    h->info.dense_bytes += dev_upload(&h->d_bkt, img.bkt);
     h->info.tf8_bytes = dev_upload(&h->d_tf8, img.tf8);
     h->dense_lists = img.dense_lists;
     h->info.dense_lists = img.dense_lists;
     h->info.n_lists = static_cast<uint32_t>(img.lists.size());
     h->args.dense = h->d_dense;
     h->args.dense_rk = h->d_dense_rk;
+    h->args.bkt = reinterpret_cast<const uint2*>(h->d_bkt);
     h->args.tf8 = h->d_tf8;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
@@ -386,7 +389,7 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_meta),
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_dense_rk),
-                  static_cast<void*>(h->d_tf8),
+                  static_cast<void*>(h->d_bkt), static_cast<void*>(h->d_tf8),
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
@@ -682,7 +685,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
     has_phrase = has_phrase || phrase;
     has_wide = has_wide || s.k > kMaxK;
-    two_only = two_only && !phrase && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
+    two_only = two_only && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
@@ -711,7 +714,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
         const ListDev& L = h->lists[ids[t]];
         return L.bm != kNoDense && static_cast<float>(L.nblk) >= dense_ratio * static_cast<float>(nbmin);
       };
-      bool lean = true;
+      bool lean = !(phrase && d.n_terms > 2);   // (longer phrases: general class)
       for (int t = 0; t < d.n_terms; ++t)
         if (t != drv && !dense(t)) lean = false;
       (lean ? lean_need : gen_need) += nbmin;
@@ -745,10 +748,8 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       HIP_OK(hipMalloc(&b->d_itemq, sizeof(uint32_t) * b->item_cap));
       HIP_OK(hipMalloc(&b->d_pub, sizeof(uint64_t) * b->item_cap));
     }
-    if (has_phrase && !b->d_ph)   // general workgroups, then lean waves
-      HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch *
-                                     (static_cast<size_t>(std::max(h->gen_cap, 1)) +
-                                      static_cast<size_t>(std::max(h->lean_wgs, 1)) * kLeanWaves)));
+    if (has_phrase && !b->d_ph)   // one per general workgroup
+      HIP_OK(hipMalloc(&b->d_ph, sizeof(uint32_t) * kPhraseScratch * static_cast<size_t>(std::max(h->gen_cap, 1))));
     if (q_bytes > b->q_cap) {   // (the term table of long queries follows the QueryIn array)
       if (b->d_q) HIP_OK(hipFree(b->d_q));
       b->d_q = nullptr;
@@ -834,9 +835,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
     HIP_OK(hipEventRecord(b->join, b->st2));
     HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                        b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
-                       b->d_itemq, b->d_pub, b->d_desc,
-                       b->has_phrase ? b->d_ph + static_cast<size_t>(kPhraseScratch) * std::max(h->gen_cap, 1)
-                                     : nullptr, b->two_only, st));
+                       b->d_itemq, b->d_pub, b->d_desc, b->has_phrase, b->two_only, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));

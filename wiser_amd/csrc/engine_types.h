@@ -35,6 +35,41 @@ constexpr uint64_t kNoTail = ~0ull;
 constexpr uint64_t kNoDense = ~0ull;
 constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 
+// A list's probe structure (ListDev::bm, QueryDesc::o_bm): bits 0-55 its
+// first entry, bits 56-63 the bucket shift c (0: a rank bitmap of DenseEnt).
+//
+// Offset buckets (c = 3..8) are for lists of density below 1/kBucketDensity
+// in the image's doc range, where a bitmap costs a 128-byte line per 1,024
+// docs probed whatever the list holds: a driver a few hundred docs apart
+// fetches nearly every mask line of the range, ~8x the list's compressed
+// bytes at 1 % density (scripts/traffic_model.py).  The range is cut into
+// buckets of 2^c docs, c chosen so that a bucket holds ~2 postings; per bucket
+// one 8-byte BucketEnt {rank << 9 | count, the in-bucket
+// offsets (doc - bucket start) of its first four postings, one byte each}, and
+// after the list's entries (at byte 8 * n_buckets of its region) the in-bucket
+// offset of every posting, one byte each, for buckets of more than four.  A
+// probe reads one entry (a line covers 16 buckets: 4,096 docs at c = 8) and
+// compares four bytes at once; a hit's posting index is rank + its position,
+// and its tf comes from tf8 as for a bitmap.
+constexpr uint32_t kProbeShiftBit = 56;
+constexpr uint64_t kProbeBaseMask = (1ull << kProbeShiftBit) - 1;
+constexpr uint32_t kBucketDensity = 25;     // buckets below 4 % density, bitmaps above
+constexpr uint32_t kBucketMinShift = 3, kBucketMaxShift = 8;
+constexpr uint32_t kBucketInline = 4;       // offsets held in the entry
+inline uint32_t probe_shift(uint64_t bm) { return static_cast<uint32_t>(bm >> kProbeShiftBit); }
+inline uint64_t bucket_count(uint32_t span, uint32_t c) { return (static_cast<uint64_t>(span) + (1u << c) - 1) >> c; }
+// bucket shift for n postings over span docs (0: a bitmap): ~2 postings per bucket
+inline uint32_t bucket_shift(uint64_t n, uint32_t span) {
+  if (!span || n * kBucketDensity >= span || n >= (1u << 23)) return 0;
+  uint32_t c = kBucketMinShift;
+  while (c < kBucketMaxShift && (n << (c + 1)) <= 3ull * span) ++c;   // mean n * 2^c / span < 1.5 -> double it
+  return c;
+}
+// words (u32) of a bucket list's region: entries, then one offset byte per posting
+inline uint64_t bucket_words(uint64_t n, uint32_t span, uint32_t c) {
+  return 2 * bucket_count(span, c) + (n + 7) / 8 * 2;
+}
+
 // Dense lists (df >= span / dense_div) also carry a rank bitmap of their doc
 // ids over the image's doc range, so that a probe costs one load + a popcount
 // instead of decoding the list's blocks.  The masks and the rank records are

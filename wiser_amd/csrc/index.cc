@@ -370,6 +370,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     uint32_t tail_cnt = 0;     // postings of the image's last row
     uint64_t bytes = 0;        // docid span + tf span
     uint8_t dense = 0, vtail = 0;
+    uint8_t shift = 0;         // dense: bucket shift (0: a bitmap)
   };
   std::vector<Info> info(L);
   struct Scratch {   // per worker thread, reused from list to list
@@ -449,6 +450,23 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
           if (docs[i] >= lim && docs[i] < doc_hi) ok = false;
       }
       in.dense = ok;
+      // the probe structure follows the density inside the range (a shard's
+      // edge blocks also hold postings outside it)
+      // (block r's docs lie in (prev_doc, last]; only edge blocks are decoded)
+      uint64_t n_in = 0;
+      for (uint64_t r = r0; r < r1 && ok; ++r) {
+        const int cnt = row_cnt(in, r, nrows);
+        const bool inside = (r == 0 ? doc_lo == 0 : s.rows[r].prev_doc + 1ull >= doc_lo) && s.last[r] < lim;
+        if (inside) {
+          n_in += static_cast<uint64_t>(cnt);
+        } else {
+          uint32_t docs[kPackSize];
+          if (!host_decode_block(file + s.rows[r].doc_off, fend, cnt, true, s.rows[r].prev_doc, docs))
+            throw std::runtime_error("cannot decode a block for the dense image");
+          for (int i = 0; i < cnt; ++i) n_in += docs[i] >= doc_lo && docs[i] < lim;
+        }
+      }
+      in.shift = static_cast<uint8_t>(bucket_shift(n_in, span));
     }
   });
 
@@ -480,7 +498,8 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     });
     uint64_t used = 0;
     for (const auto& c : cand) {
-      const uint64_t bytes = n_ent * kDenseEntBytes + c.first;
+      const uint32_t sh = info[c.second].shift;
+      const uint64_t bytes = (sh ? 4 * bucket_words(c.first, span, sh) : n_ent * kDenseEntBytes) + c.first;
       if (used + bytes > dense_budget) info[c.second].dense = 0;
       else used += bytes;
     }
@@ -493,7 +512,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.lists.resize(L);
   img.list_bytes.resize(L);
   img.has_positions = positions;
-  uint64_t at = 0, nb = 0, ne = 0, ntf8 = 0, ntail = 0;
+  uint64_t at = 0, nb = 0, ne = 0, ntf8 = 0, ntail = 0, nbk = 0;
   for (int32_t id = 0; id < L; ++id) {
     const Info& in = info[id];
     ListDev& ld = img.lists[id];
@@ -512,10 +531,17 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     if (!nbl) { img.list_bytes[id] = 0; continue; }
     if (in.vtail) { ld.tail = ntail; ntail += 2ull * in.tail_cnt; }
     if (in.dense) {
-      ld.bm = ne;
+      const uint64_t n_img = (nbl - 1) * static_cast<uint64_t>(kPackSize) + in.tail_cnt;
+      if (in.shift) {   // offset buckets (nbk: in words, entries are 8-byte aligned)
+        ld.bm = (static_cast<uint64_t>(in.shift) << kProbeShiftBit) | (nbk / 2);
+        nbk += bucket_words(n_img, span, in.shift);
+        ++img.bucket_lists;
+      } else {
+        ld.bm = ne;
+        ne += n_ent;
+      }
       ld.tf8 = ntf8;
-      ne += n_ent;
-      ntf8 += (nbl - 1) * static_cast<uint64_t>(kPackSize) + in.tail_cnt;
+      ntf8 += n_img;
       ++img.dense_lists;
     }
     img.list_bytes[id] = in.bytes;
@@ -535,6 +561,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.dense.resize(ne);
   img.dense_rank.resize(kRankWords * ne);
   img.tf8.resize(ntf8);
+  img.bkt.resize(nbk);
 
   lap("pass 2 (offsets, allocation)");
   // ---- pass 3: fill in place
@@ -625,7 +652,32 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       }
     }
     img.lists[id].tfmax = tfmax;   // (this worker's own list)
-    if (in.dense) {
+    if (in.dense && in.shift) {
+      // offset buckets: per 2^c docs the rank and count of its postings and the
+      // offsets of its first four; then every posting's offset
+      const uint32_t c = in.shift, w = 1u << c;
+      const uint64_t nbkt = bucket_count(span, c);
+      uint32_t* ent = &img.bkt[2 * (ld.bm & kProbeBaseMask)];
+      uint8_t* offs = reinterpret_cast<uint8_t*>(ent + 2 * nbkt);
+      uint64_t i = 0;
+      for (uint64_t e = 0; e < nbkt; ++e) {
+        const uint64_t start = doc_lo + (e << c);
+        while (i < n_img && s.docs[i] < start) ++i;
+        uint64_t j = i;
+        uint32_t in4 = 0xFFFFFFFFu;
+        while (j < n_img && s.docs[j] < start + w) {
+          const uint32_t o = static_cast<uint32_t>(s.docs[j] - start);
+          offs[j] = static_cast<uint8_t>(o);
+          if (j - i < kBucketInline) in4 = (in4 & ~(0xFFu << (8 * (j - i)))) | (o << (8 * (j - i)));
+          ++j;
+        }
+        ent[2 * e] = static_cast<uint32_t>(i << 9 | (j - i));   // (j - i <= 2^c <= 256)
+        ent[2 * e + 1] = in4;
+      }
+      for (uint64_t j = n_img; j < (n_img + 7) / 8 * 8; ++j) offs[j] = 0;
+      uint8_t* t8 = &img.tf8[ld.tf8];
+      for (uint64_t j = 0; j < n_img; ++j) t8[j] = static_cast<uint8_t>(s.tfs[j] < kTf8Escape ? s.tfs[j] : kTf8Escape);
+    } else if (in.dense) {
       // rank bitmap: per kDenseDocs docs the doc mask and the rank record (the
       // postings before them, the tfs of the word's first four postings; 255:
       // none, or escaped)
@@ -784,10 +836,24 @@ int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc) 
   if (L.bm == kNoDense || doc < img.doc_lo || doc >= img.doc_hi) return -1;
   const uint32_t rel = doc - img.doc_lo;
   if (rel >= img.dense_span) return -1;
-  const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
-  const uint32_t sh = rel % kDenseDocs;
-  if (!dense_ent_bit(e, sh)) return -1;
-  const uint32_t idx = dense_ent_rank(e, img.dense_rank[kRankWords * (L.bm + rel / kDenseDocs)], sh);
+  uint32_t idx = 0;
+  if (const uint32_t c = probe_shift(L.bm)) {   // offset buckets: scan the bucket's offsets
+    const uint64_t base = L.bm & kProbeBaseMask;
+    const uint32_t* ent = &img.bkt[2 * (base + (rel >> c))];
+    const uint8_t* offs = reinterpret_cast<const uint8_t*>(&img.bkt[2 * (base + bucket_count(img.dense_span, c))]);
+    const uint32_t rank = ent[0] >> 9, cnt = ent[0] & 511u, o = rel & ((1u << c) - 1u);
+    bool hit = false;
+    for (uint32_t j = 0; j < cnt && !hit; ++j) {
+      const uint32_t b = j < kBucketInline ? (ent[1] >> (8 * j)) & 255u : offs[rank + j];
+      if (b == o) { hit = true; idx = rank + j; }
+    }
+    if (!hit) return -1;
+  } else {
+    const DenseEnt& e = img.dense[L.bm + rel / kDenseDocs];
+    const uint32_t sh = rel % kDenseDocs;
+    if (!dense_ent_bit(e, sh)) return -1;
+    idx = dense_ent_rank(e, img.dense_rank[kRankWords * (L.bm + rel / kDenseDocs)], sh);
+  }
   const uint8_t t = img.tf8[L.tf8 + idx];
   if (t != kTf8Escape) return t;
   const uint32_t j = idx / kPackSize;

@@ -127,8 +127,11 @@ struct HostImage {
   big_vector<DenseEnt> dense;   // rank bitmaps of the dense lists
   big_vector<uint32_t> dense_rank;   // the rank record of each DenseEnt (kRankWords u32), same index
   big_vector<uint8_t> tf8;      // 1-byte tfs of the dense lists (kTf8Escape = look up the blob)
+  big_vector<uint32_t> bkt;     // offset buckets of the sparser dense lists (engine_types.h): per
+                                // list its BucketEnts (2 words each), then its offset bytes
   uint32_t dense_span = 0;      // doc ids covered by a bitmap: [doc_lo, doc_lo + dense_span)
-  uint32_t dense_lists = 0;
+  uint32_t dense_lists = 0;     // lists with a probe structure (bitmap or buckets)
+  uint32_t bucket_lists = 0;    //   of them with buckets
   big_vector<uint32_t> tails;   // decoded VInts last blocks (ListDev::tail)
   big_vector<uint8_t> plen;     // doc-length code (Char4) of every posting: block j of the
                                 // image at [j * 128, j * 128 + 128), 0 past the length records
@@ -166,8 +169,8 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
                       uint32_t dense_div = 0, bool positions = false, uint64_t dense_budget = 0,
                       bool blooms = false, uint64_t hbm_free = 0);
 
-// Host restatement of the device's dense probe (segment kernel): tf of doc in
-// list L of the image, -1 when absent or when L has no bitmap.
+// Host restatement of the device's dense probe (bitmap or buckets): tf of doc
+// in list L of the image, -1 when absent or when L has no probe structure.
 int64_t dense_lookup_host(const HostImage& img, const ListDev& L, uint32_t doc);
 
 }  // namespace wiser

@@ -24,6 +24,7 @@ struct IndexArgs {
   double avg;               // average doc length stored in my.doc_length
   const DenseEnt* dense;    // rank bitmaps of the dense lists (ListDev::bm)
   const uint32_t* dense_rk; // their rank records (same index, kRankWords u32 each)
+  const uint2* bkt;         // offset buckets of the sparser dense lists (ListDev::bm with a shift)
   const uint8_t* tf8;       // their 1-byte tfs (ListDev::tf8)
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
@@ -134,12 +135,12 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
                            uint64_t* pub, uint32_t* ph, hipStream_t st);
 
 // lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride];
-// ph: phrase scratch (lean_wgs * kLeanWaves * kPhraseScratch u32), null without phrase queries;
-// two: every query of the batch has two terms (or none), k <= kMaxK, no phrase
+// phrase: the batch holds phrase queries (lean ones have two terms);
+// two: every query of the batch has two terms (or none) and k <= kMaxK
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st);
+                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, hipStream_t st);
 int lean_kernel_occupancy();
 // queries with k > kMaxK (their segments emitted every survivor): heap in LDS
 hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,

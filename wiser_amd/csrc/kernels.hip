@@ -331,19 +331,77 @@ __device__ __forceinline__ uint32_t dense_tf_slow(const IndexArgs& ix, const Lis
   return val;
 }
 
+// ---- offset buckets (engine_types.h): an entry v = {rank << 9 | count,
+// the first four in-bucket offsets}.  bucket_pos: the position (0..3) of
+// offset o among the first four, kBucketMiss, or kBucketScan when o lies past
+// the fourth of a bucket of more (offsets ascend): the offset bytes decide.
+// Four bytes at once: t has a zero byte where v.y's byte equals o; the lowest
+// byte the borrow test flags is always a true zero (a false flag needs a zero
+// below it), and padding bytes past the count are ruled out by position.
+constexpr uint32_t kBucketMiss = 4, kBucketScan = 5;
+__device__ __forceinline__ uint32_t bucket_pos(const uint2 v, uint32_t o) {
+  const uint32_t cnt = v.x & 511u;
+  const uint32_t t = v.y ^ (o * 0x01010101u);
+  const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
+  const uint32_t pos = z ? (static_cast<uint32_t>(__builtin_ctz(z)) >> 3) : 4u;
+  if (pos < min(cnt, kBucketInline)) return pos;
+  return (cnt > kBucketInline && o > (v.y >> 24)) ? kBucketScan : kBucketMiss;
+}
+// the offset bytes of a bucket list (after its entries)
+__device__ __forceinline__ const uint8_t* bucket_offsets(const IndexArgs& ix, uint64_t bm) {
+  const uint32_t c = static_cast<uint32_t>(bm >> kProbeShiftBit);
+  return reinterpret_cast<const uint8_t*>(ix.bkt + (bm & kProbeBaseMask) +
+                                          ((static_cast<uint64_t>(ix.dense_span) + (1u << c) - 1) >> c));
+}
+// postings 4.. of a bucket of cnt starting at posting `rank`: is one at offset o?
+__device__ __forceinline__ bool bucket_scan(const uint8_t* offs, uint32_t rank, uint32_t cnt, uint32_t o,
+                                            uint32_t* idx) {
+  for (uint32_t j = kBucketInline; j < cnt; ++j) {
+    const uint32_t b = load_byte(offs + rank + j);
+    if (b >= o) {
+      *idx = rank + j;
+      return b == o;
+    }
+  }
+  return false;
+}
+
+// A list's probe entry for doc offset rel (in: rel inside the range, else a
+// dummy read): its bitmap entry {rank, mask} or its bucket entry.  The shift
+// comes from the list record, so the branch is uniform.
+__device__ __forceinline__ DenseVal probe_at(const IndexArgs& ix, uint64_t bm, uint32_t rel, bool in) {
+  const uint32_t c = static_cast<uint32_t>(bm >> kProbeShiftBit);
+  if (c) return ix.bkt[(bm & kProbeBaseMask) + (in ? rel >> c : 0u)];
+  return dense_at(ix, bm, in ? rel / kDenseDocs : 0u);
+}
+// Doc a in a prefetched probe entry; on a hit *idx = posting index.
+__device__ __forceinline__ bool probe_hit(const IndexArgs& ix, uint64_t bm, uint32_t a, const DenseVal v,
+                                          uint32_t* idx) {
+  const uint32_t c = static_cast<uint32_t>(bm >> kProbeShiftBit);
+  if (!c) return dense_hit(ix, a, v, idx);
+  const uint32_t rel = a - ix.doc_lo;
+  if (rel >= ix.dense_span) return false;
+  const uint32_t o = rel & ((1u << c) - 1u);
+  const uint32_t pos = bucket_pos(v, o);
+  if (pos < kBucketInline) {
+    *idx = (v.x >> 9) + pos;
+    return true;
+  }
+  return pos == kBucketScan && bucket_scan(bucket_offsets(ix, bm), v.x >> 9, v.x & 511u, o, idx);
+}
+
 // Is doc a in B?  One 8-byte load (dense_load, issued early) and, on a hit,
 // the posting's rank gives its tf (dense_resolve).
 __device__ __forceinline__ DenseVal dense_load(const IndexArgs& ix, const ListDev& B, uint32_t a,
                                                bool act) {
   const uint32_t rel = a - ix.doc_lo;
-  const bool in = act && rel < ix.dense_span;
-  return dense_at(ix, B.bm, in ? rel / kDenseDocs : 0u);
+  return probe_at(ix, B.bm, rel, act && rel < ix.dense_span);
 }
 
 __device__ __forceinline__ bool dense_resolve(const IndexArgs& ix, const ListDev& B, uint32_t a,
                                               const DenseVal v, uint32_t* tf, uint32_t* pidx = nullptr) {
   uint32_t idx;
-  if (!dense_hit(ix, a, v, &idx)) return false;
+  if (!probe_hit(ix, B.bm, a, v, &idx)) return false;
   if (pidx) *pidx = idx;
   uint32_t t = ix.tf8[B.tf8 + idx];
   if (t == kTf8Escape) t = dense_tf_slow(ix, B, idx);
@@ -508,6 +566,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         if (L.nblk < o_nb) { o1 = s; o_nb = L.nblk; }
       }
     }
+    // a phrase query of more than two terms runs in the general class (the
+    // lean kernel checks positions of two-term phrases only, in registers)
+    if (nt > 2 && (q.flags & kQueryPhrase)) lean = false;
     if (ok) {
       uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
@@ -1279,6 +1340,34 @@ __device__ __noinline__ void shard_emit_call(const QueryIn* qs, const QueryPlan*
 }
 
 // ------------------------------------------------------ item plumbing --
+// Score floors of the earlier items of a query.  pub[i] is backed by k
+// survivors at or before item i (its running k-th best, or the floor it had),
+// so the largest pub of the items before this one bounds the k-th best before
+// it as well, and is at least the predecessor's alone: items of one query run
+// at once, and the predecessor's value reaches a later item only one refresh
+// per hop.  prev_pub = pub + item - 1, n_prev = the items before this one; lane
+// l loads pub[item - 1 - l] (the nearest 64), floor_max reduces over the wave.
+__device__ __forceinline__ uint64_t floor_lanes(const uint64_t* prev_pub, uint32_t n_prev) {
+  const uint32_t l = threadIdx.x & 63;
+  return (prev_pub && l < n_prev) ? __hip_atomic_load(prev_pub - l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0ull;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+  uint32_t y;
+  y = dpp<kRowShr1>(x); x = umax(x, y);
+  y = dpp<kRowShr2>(x); x = umax(x, y);
+  y = dpp<kRowShr4>(x); x = umax(x, y);
+  y = dpp<kRowShr8>(x); x = umax(x, y);
+  y = dpp<kRowBcast15, 0xA>(x); x = umax(x, y);
+  y = dpp<kRowBcast31, 0xC>(x); x = umax(x, y);
+  return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ uint64_t floor_max(uint64_t x) {
+  const uint32_t hi = wave_max(static_cast<uint32_t>(x >> 32));
+  const uint32_t lo = wave_max(static_cast<uint32_t>(x >> 32) == hi ? static_cast<uint32_t>(x) : 0u);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 // Next work item of a persistent worker over items [lo, hi), split into
 // kQueueShards round-robin shards (relative index i in shard i % kQueueShards),
 // each with its own head on its own 64-byte line; a worker starts with its own
@@ -1324,16 +1413,13 @@ __device__ __forceinline__ uint32_t next_item(uint32_t* heads, uint32_t lo, uint
 template <bool kWave>
 __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* plan, uint32_t qi,
                                             uint32_t n_items, uint32_t item,
-                                            const uint64_t* prev_pub, Event* ev_out, uint32_t ev_n,
+                                            const uint64_t* prev_pub, uint32_t n_prev, Event* ev_out, uint32_t ev_n,
                                             const Event* events, uint32_t* ev_cnt,
                                             const FusedReplay& fr) {
   const uint32_t l = threadIdx.x & 63;
   const uint64_t lt = lanemask_lt();
   if (prev_pub && ev_n > 0) {
-    const uint64_t fb = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double fl_end = __longlong_as_double(static_cast<long long>(
-        (static_cast<uint64_t>(uni(static_cast<uint32_t>(fb >> 32))) << 32) |
-        uni(static_cast<uint32_t>(fb))));
+    const double fl_end = __longlong_as_double(static_cast<long long>(floor_max(floor_lanes(prev_pub, n_prev))));
     uint32_t kept = 0;
     for (uint32_t c = 0; c < ev_n; c += 64) {
       double sc = 0.0;
@@ -1486,6 +1572,34 @@ __device__ __forceinline__ bool bloom_possible(const IndexArgs& ix, const int32_
   return true;
 }
 
+// Two-term phrase of a lean item: terms (query order) list l0 / l1, their
+// posting slots and tfs in registers.  The bloom rule of bloom_possible's
+// two-term case, then ProcessTwoTerm's merge (bag 0 shifted by one against
+// bag 1).  Inlined: the lean kernel keeps no phrase scratch.
+__device__ __forceinline__ bool phrase_match2(const IndexArgs& ix, uint32_t l0, uint32_t l1, uint32_t slot0,
+                                              uint32_t tf0, uint32_t slot1, uint32_t tf1) {
+  if (ix.bloom_factor) {
+    const uint64_t f = ix.bloom_factor;
+    const uint64_t s1 = ix.lists[l0].df, s2 = ix.lists[l1].df;
+    if (f * s1 <= s2) {
+      if (!bloom_may(ix, slot0, 1, static_cast<int32_t>(l1))) return false;
+    } else if (f * s2 < s1) {
+      if (!bloom_may(ix, slot1, 0, static_cast<int32_t>(l0))) return false;
+    }
+  }
+  const PosDev P0 = ix.pos_lists[l0], P1 = ix.pos_lists[l1];
+  PosStream s0, s1;
+  s0.init(ix, slot0, tf0);
+  s1.init(ix, slot1, tf1);
+  if (!s0.next(ix, P0) || !s1.next(ix, P1)) return false;
+  for (;;) {
+    const int32_t a = s0.cur + 1, b = s1.cur;
+    if (a == b) return true;
+    if (a < b) { if (!s0.next(ix, P0)) return false; }
+    else if (!s1.next(ix, P1)) return false;
+  }
+}
+
 __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* qlist, uint32_t nt,
                                           const uint32_t* ph, uint32_t v) {
   if (ix.bloom_factor && !bloom_possible(ix, qlist, nt, ph, v)) return false;
@@ -1606,17 +1720,24 @@ struct LeanLdsT {
 // o1 == kNoSlot: single-term query, every posting of the driver survives.
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
-// kTwo: every item of the launch is a two-term, k <= kMaxK, non-phrase query
-// (the headline's and C2's batches): two terms scored inline, no wide or
-// single-term paths, so the instance keeps fewer registers (86 VGPRs, no
+// kTwo: every item of the launch is a two-term, k <= kMaxK query (the
+// headline's, C2's and C5's batches): two terms scored inline, no wide or
+// single-term paths, so the instance keeps fewer registers (90 VGPRs, no
 // scratch, half the SGPR spill reloads of the general instance).
-template <bool kPh, bool kTwo = false>
+// kPh: the batch holds phrase queries; a lean one has two terms (the plan
+// sends longer phrases to the general class), the driver and O1, whose
+// posting slots and tfs ride in the survivor queue, so the position check
+// (phrase_match2) runs on registers with no scratch.
+// kBk: O1 carries offset buckets (the item's QueryDesc::o_bm has a shift):
+// D loads its bucket entry, H matches the offset and loads the hit's tf word,
+// C resolves the rare probe past a bucket's fourth posting from its offset
+// bytes.  The same pipeline otherwise.
+template <bool kPh, bool kTwo = false, bool kBk = false>
 __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
-                                             bool phrase, uint32_t* ph,
-                                             uint32_t b0, uint32_t b1, bool dtail,
+                                             bool phrase, uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
-                                             const uint64_t* prev_pub, uint64_t* my_pub,
+                                             const uint64_t* prev_pub, uint32_t n_prev, uint64_t* my_pub,
                                              Event* ev_out, uint32_t& ev_n,
                                              double& pt, uint32_t& pt_n,
                                              double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
@@ -1628,13 +1749,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   // k > kMaxK: every survivor is an event; the replay's heap in LDS decides
   const bool wide = !kTwo && k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
-  const bool single = !kTwo && o1 == kNoSlot;
+  const bool single = !kTwo && !kBk && o1 == kNoSlot;
   // O1's bitmap (single term: reads go to a valid dummy word; the image may
   // have no bitmaps): the probe reads the mask word alone; a hit reads its
   // rank record (H stage)
-  const uint32_t* o_mk = single ? ix.blk_last : &ix.dense[Q.o_bm].w;
-  const uint2* o_rk = single ? reinterpret_cast<const uint2*>(ix.blk_last)
-                             : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
+  const uint32_t* o_mk = (single || kBk) ? ix.blk_last : &ix.dense[Q.o_bm].w;
+  const uint2* o_rk = (single || kBk) ? reinterpret_cast<const uint2*>(ix.blk_last)
+                                      : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
   auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_mk[e]; };
   auto probe_bit = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) { return ((v >> sh) & 1u) != 0u; };
   // posting rank of a hit, without the rank word (added at compaction)
@@ -1642,6 +1763,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     return static_cast<uint32_t>(__popc(v & ((1u << sh) - 1u)));
   };
   const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
+  // buckets (kBk): entries, shift and offset bytes of O1
+  const uint32_t bsh = kBk ? static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit) : 0u;
+  const uint2* o_bk = kBk ? ix.bkt + (Q.o_bm & kProbeBaseMask) : nullptr;
+  const uint8_t* o_off = kBk ? bucket_offsets(ix, Q.o_bm) : nullptr;
+  const uint32_t o_tf8_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8)) & 3u;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
   const uint32_t lo = in_vgpr(ix.doc_lo), span = in_vgpr(ix.dense_span);
@@ -1662,16 +1788,15 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   // here; the segment's own k-th best is published once, at the end; events
   // stay in LDS until 64 are pending (a chunk adds at most 64).  The final
   // re-filter in finish_item applies the floor as it stands at the end.
-  uint64_t floor_bits =
-      prev_pub ? __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+  uint64_t floor_bits = prev_pub ? floor_max(floor_lanes(prev_pub, n_prev)) : 0ull;
   double pub_val = 0.0;
   // Floor refresh (every kFloorRefresh driver blocks): the item publishes
   // its floor as it stands (the k-th best of docs before the next item) and
-  // reads the previous item's, so the items of one query, which run at once,
-  // hand their thresholds down the chain while they run instead of at their
-  // ends.  The load is issued just before a block's pack loads, which the next
-  // iteration waits for anyway, and consumed one refresh later.
-  uint64_t floor_next = floor_bits;
+  // reads the earlier items' (floor_lanes), so the items of one query, which
+  // run at once, hand their thresholds on while they run instead of at their
+  // ends.  The loads are issued just before a block's pack loads, which the
+  // next iteration waits for anyway, and consumed one refresh later.
+  uint64_t floor_next = 0;   // per lane: one earlier item's pub
   double sent = 0.0;
   // Pre-probe pruning.  A driver posting whose score bound -- its own term,
   // exact, plus QueryDesc's bound of the other terms at its doc length -- is
@@ -1721,10 +1846,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       }
       if (rk) to = t;
     }
-    // phrase: each term's posting slot and tf, for the position check
-    auto rec = [&](uint32_t s, uint32_t slot, uint32_t tf) __attribute__((always_inline)) {
-      if (kPh && phrase && alive) { ph[s * 256 + l] = slot; ph[s * 256 + 128 + l] = tf; }
-    };
     const double norm = norm_tab[c4 & 255u];
     double sc = 0.0;   // BM25 accumulated in query-term order (scoring.h:133-144)
     if constexpr (kTwo) {   // the two terms in query order: the driver's slot first or second
@@ -1734,11 +1855,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     for (uint32_t s = 0; s < (kTwo ? 0u : nt); ++s) {
       if (s == d) {
         sc += bm25_term(idf_d, alive ? td : 0u, norm);
-        rec(s, pd, td);
         if (single) break;
       } else if (s == o1) {
         sc += bm25_term(idf_o, alive ? to : 0u, norm);
-        rec(s, o_slot0 + po, to);
       } else {
         const ListDev B = ix.lists[qlist[s]];
         uint32_t t = 0, x = 0;
@@ -1746,7 +1865,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
         alive = alive && dense_resolve(ix, B, doc, v, &t, &x);
         if (__ballot(alive) == 0) break;
         sc += bm25_term(B.idf, alive ? t : 0u, norm);
-        rec(s, B.blk0 * 128u + x, t);
       }
     }
     // HandleTheFoundDoc: a phrase query ranks only docs that hold the phrase.
@@ -1764,8 +1882,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
         const double kth0 = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
         need = alive && sc > flo0 && (pt_n < k || sc > kth0);
       }
-      if (__ballot(need)) {
-        if (need) need = phrase_match(ix, qlist, nt, ph, l);
+      if (__ballot(need)) {   // (a lean phrase query has two terms: the driver and O1)
+        const uint32_t so = o_slot0 + po;
+        if (need)
+          need = d == 0 ? phrase_match2(ix, qlist[0], qlist[1], pd, td, so, to)
+                        : phrase_match2(ix, qlist[0], qlist[1], so, to, pd, td);
       }
       alive = need;
     }
@@ -1836,14 +1957,16 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     // D: a decoded block and its loads in flight
     uint32_t da0 = ~0u, da1 = ~0u, dcc = 0;        // docs, doc-length codes (c0 | c1 << 8)
     uint32_t dt0 = 0, dt1 = 0;                     // driver tfs
-    uint32_t de0 = 0, de1 = 0;                     // O1 bitmap mask words
+    std::conditional_t<kBk, uint2, uint32_t> de0{}, de1{};   // O1 bitmap mask words / bucket entries
     // (per-lane flags ride in the values -- a doc of ~0u is a posting past the
     // block, outside the image or pruned, a rank with bit 31 set is an O1 miss
     // -- so that they take no scalar lane-mask registers across the iteration)
     // H: the block decoded one iteration earlier, with its O1 hits
     uint32_t ha0 = 0, ha1 = 0, hc0 = 0, hc1 = 0, ht0 = 0, ht1 = 0;   // docs, length codes, driver tfs
     uint2 hf0 = make_uint2(0, 0), hf1 = make_uint2(0, 0);   // O1 rank records (rank, 4 tfs; in flight)
-    uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit)
+                                                            // kBk: the hit's tf word, the bucket count
+    uint32_t hx0 = 0x80000000u, hx1 = 0x80000000u; // O1 posting ranks (bit 31: no hit; kBk: bit 30,
+                                                   // the bucket's rank, its offsets to scan)
 
   };
   Regs R0, R1;
@@ -1873,12 +1996,32 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       // O1 posting ranks (hits): rank word + bits below; the tf byte is read by
       // rank when the chunk is scored (flag bit 31)
       // (the record's tf bytes cover the word's first four postings)
-      const uint32_t rk0 = X.hf0.x + X.hx0, rk1 = X.hf1.x + X.hx1;
-      const uint32_t f0 = X.hx0 < 4u ? (X.hf0.y >> ((X.hx0 & 3u) << 3)) & 0xFFu : kTf8Escape;
-      const uint32_t f1 = X.hx1 < 4u ? (X.hf1.y >> ((X.hx1 & 3u) << 3)) & 0xFFu : kTf8Escape;
+      uint32_t rk0, rk1, f0, f1, hx0 = X.hx0, hx1 = X.hx1;
+      if constexpr (kBk) {
+        // probes past a bucket's fourth posting (rare): its offset bytes
+        const bool s0 = (hx0 >> 30) == 1u, s1 = (hx1 >> 30) == 1u;
+        if (__ballot(s0 || s1)) {
+          const uint32_t m = (1u << bsh) - 1u;
+          uint32_t i0 = 0, i1 = 0;
+          if (s0) hx0 = bucket_scan(o_off, hx0 & 0x3FFFFFFFu, X.hf0.y, (X.ha0 - lo) & m, &i0) ? (i0 | 0x40000000u)
+                                                                                             : 0x80000000u;
+          if (s1) hx1 = bucket_scan(o_off, hx1 & 0x3FFFFFFFu, X.hf1.y, (X.ha1 - lo) & m, &i1) ? (i1 | 0x40000000u)
+                                                                                             : 0x80000000u;
+        }
+        // (a scanned hit, bit 30, reads its tf by rank when scored)
+        rk0 = hx0 & 0x3FFFFFFFu;
+        rk1 = hx1 & 0x3FFFFFFFu;
+        f0 = (hx0 & 0x40000000u) ? kTf8Escape : (X.hf0.x >> (((o_tf8_mis + rk0) & 3u) << 3)) & 0xFFu;
+        f1 = (hx1 & 0x40000000u) ? kTf8Escape : (X.hf1.x >> (((o_tf8_mis + rk1) & 3u) << 3)) & 0xFFu;
+      } else {
+        rk0 = X.hf0.x + hx0;
+        rk1 = X.hf1.x + hx1;
+        f0 = hx0 < 4u ? (X.hf0.y >> ((hx0 & 3u) << 3)) & 0xFFu : kTf8Escape;
+        f1 = hx1 < 4u ? (X.hf1.y >> ((hx1 & 3u) << 3)) & 0xFFu : kTf8Escape;
+      }
       const uint32_t to0 = f0 != kTf8Escape ? f0 : (0x80000000u | rk0);
       const uint32_t to1 = f1 != kTf8Escape ? f1 : (0x80000000u | rk1);
-      const bool hh0 = !(X.hx0 >> 31), hh1 = !(X.hx1 >> 31);
+      const bool hh0 = !(hx0 >> 31), hh1 = !(hx1 >> 31);
       const uint64_t m0 = __ballot(hh0), m1 = __ballot(hh1);
       const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
       const uint32_t r1 = r0 + (hh0 ? 1u : 0u);
@@ -1903,7 +2046,28 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   auto stage_H = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     // H(j-1): block j-1 (D fields in X): O1 hits, its driver tfs and length
     // codes extracted, into Y's H fields
-    {
+    if constexpr (kBk) {
+      const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
+      const uint32_t m = (1u << bsh) - 1u;
+      const bool v0 = (X.da0 != ~0u) & (q0 < span), v1 = (X.da1 != ~0u) & (q1 < span);
+      const uint32_t ps0 = bucket_pos(X.de0, q0 & m), ps1 = bucket_pos(X.de1, q1 & m);
+      const bool h0 = v0 & (ps0 < kBucketInline), h1 = v1 & (ps1 < kBucketInline);
+      const bool sc0 = v0 & (ps0 == kBucketScan), sc1 = v1 & (ps1 == kBucketScan);
+      const uint32_t r0 = X.de0.x >> 9, r1 = X.de1.x >> 9;
+      const uint32_t k0 = r0 + (h0 ? ps0 : 0u), k1 = r1 + (h1 ? ps1 : 0u);
+      // the hit's tf byte, as its aligned word
+      Y.hf0.x = *reinterpret_cast<const uint32_t*>(__builtin_align_down(o_tf8 + (h0 ? k0 : 0u), 4));
+      Y.hf1.x = *reinterpret_cast<const uint32_t*>(__builtin_align_down(o_tf8 + (h1 ? k1 : 0u), 4));
+      Y.hf0.y = X.de0.x & 511u;
+      Y.hf1.y = X.de1.x & 511u;
+      Y.hx0 = h0 ? k0 : sc0 ? (0x40000000u | r0) : 0x80000000u;
+      Y.hx1 = h1 ? k1 : sc1 ? (0x40000000u | r1) : 0x80000000u;
+      Y.ha0 = X.da0; Y.ha1 = X.da1;
+      Y.hc0 = X.dcc & 0xFFu;
+      Y.hc1 = X.dcc >> 8;
+      Y.ht0 = X.dt0;
+      Y.ht1 = X.dt1;
+    } else {
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
       // (bitwise, not short-circuit: the compiler would branch on each term)
@@ -1959,8 +2123,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
       const bool in0 = !single & p0 & (a0 - lo < span);
       const bool in1 = !single & p1 & (a1 - lo < span);
-      Y.de0 = o_probe(in0 ? (a0 - lo) / kDenseDocs : 0u);
-      Y.de1 = o_probe(in1 ? (a1 - lo) / kDenseDocs : 0u);
+      if constexpr (kBk) {
+        Y.de0 = o_bk[in0 ? (a0 - lo) >> bsh : 0u];
+        Y.de1 = o_bk[in1 ? (a1 - lo) >> bsh : 0u];
+      } else {
+        Y.de0 = o_probe(in0 ? (a0 - lo) / kDenseDocs : 0u);
+        Y.de1 = o_probe(in1 ? (a1 - lo) / kDenseDocs : 0u);
+      }
       Y.dcc = c0 | (c1 << 8);
       Y.dt0 = t0; Y.dt1 = t1;
       Y.da0 = p0 ? a0 : ~0u; Y.da1 = p1 ? a1 : ~0u;
@@ -1972,8 +2141,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   };
   auto body = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
     if (((j - b0) % kFloorRefresh) == kFloorRefresh - 1 && !wide) {
-      const uint64_t fb = (static_cast<uint64_t>(uni(static_cast<uint32_t>(floor_next >> 32))) << 32) |
-                          uni(static_cast<uint32_t>(floor_next));
+      const uint64_t fb = floor_max(floor_next);
       if (fb > floor_bits) {
         floor_bits = fb;
         const float t = static_cast<float>(__longlong_as_double(static_cast<long long>(fb))) * kPruneMargin;
@@ -1985,7 +2153,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sent = pub_val;
       }
-      if (prev_pub) floor_next = __hip_atomic_load(prev_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      floor_next = floor_lanes(prev_pub, n_prev);
     }
     // W(j+1): the doc-id words of block j+1
     issue_words(j + 1, Y);
@@ -2178,8 +2346,8 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
       const uint32_t r0 = g.a0 - ix.doc_lo, r1 = g.a1 - ix.doc_lo;
       const bool d0 = fo_dense && g.al0 && r0 < ix.dense_span;
       const bool d1 = fo_dense && g.al1 && r1 < ix.dense_span;
-      g.p0 = dense_at(ix, f_bm, d0 ? r0 / kDenseDocs : 0u);
-      g.p1 = dense_at(ix, f_bm, d1 ? r1 / kDenseDocs : 0u);
+      g.p0 = probe_at(ix, f_bm, r0, d0);
+      g.p1 = probe_at(ix, f_bm, r1, d1);
     };
     auto flush_events = [&](uint32_t n) __attribute__((always_inline)) {
       __builtin_amdgcn_wave_barrier();
@@ -2195,8 +2363,8 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
       bool fh0 = false, fh1 = false;
       uint32_t fi0 = 0, fi1 = 0;
       if (fo_dense) {
-        fh0 = cs.al0 && dense_hit(ix, cs.a0, cs.p0, &fi0);
-        fh1 = cs.al1 && dense_hit(ix, cs.a1, cs.p1, &fi1);
+        fh0 = cs.al0 && probe_hit(ix, f_bm, cs.a0, cs.p0, &fi0);
+        fh1 = cs.al1 && probe_hit(ix, f_bm, cs.a1, cs.p1, &fi1);
       }
       const uint32_t ft0 = f_tf8[fh0 ? fi0 : 0u], ft1 = f_tf8[fh1 ? fi1 : 0u];
       const uint64_t floor_bits =
@@ -2442,7 +2610,7 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
       step(sb, sa, b + 1);
     }
     if (evb) flush_events(evb);
-    finish_item<false>(qs, plan, qi, P.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
+    finish_item<false>(qs, plan, qi, P.n_items, item, prev_pub, r, ev_out, ev_n, events, ev_cnt, fr);
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
@@ -2464,13 +2632,13 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
 // SIMD): with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against
 // 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 3 (kLeanWgsPhrase).
 constexpr int kLeanWgs = 5;
-constexpr int kLeanWgsPhrase = 3;
+constexpr int kLeanWgsPhrase = 4;
 template <bool kPh, bool kTwo = false>
 __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
     uint32_t* __restrict__ stats, FusedReplay fr, const uint32_t* __restrict__ item_q,
-    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc, uint32_t* __restrict__ ph_all) {
+    uint64_t* __restrict__ pub, const QueryDesc* __restrict__ desc) {
   __shared__ LeanLdsT<kPh> SW[kLeanWaves];
   __shared__ double norm[256];
   const uint32_t l = threadIdx.x & 63;
@@ -2481,7 +2649,6 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
   __syncthreads();
   LeanLdsT<kPh>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
-  uint32_t* ph = kPh ? ph_all + static_cast<uint64_t>(wid) * kPhraseScratch : nullptr;
   const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT));
   uint32_t n_surv = 0, n_dblk = 0;
@@ -2522,12 +2689,18 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
     // a query of one item with fused replay: the heap runs here, no events
     double pt = 0.0, last_pub = 0.0;
     uint32_t pt_n = 0, ev_n = 0;
-    if (!done && b0 < b1)
-      lean_segment<kPh, kTwo>(ix, S, norm, Q, qlist_of(qs, static_cast<int>(qi)),
-                              kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase),
-                              ph, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, prev_pub,
-                              my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
-    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, ev_out, ev_n, events, ev_cnt, fr);
+    if (!done && b0 < b1) {
+      const bool phrase =
+          kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
+      const int32_t* ql = qlist_of(qs, static_cast<int>(qi));
+      if (uni(static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit)))   // O1 has offset buckets
+        lean_segment<kPh, kTwo, true>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
+                                      prev_pub, r, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
+      else
+        lean_segment<kPh, kTwo, false>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
+                                       prev_pub, r, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
+    }
+    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, r, ev_out, ev_n, events, ev_cnt, fr);
     item = 0xFFFFFFFFu;
   }
   if (l == 0) {
@@ -2613,18 +2786,22 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, uint32_t* ph, bool two, hipStream_t st) {
+                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, hipStream_t st) {
   // (a persistent grid sized for the conjunctive instance: waves of a larger
   // instance that find no room start later and find the queue drained)
-  if (ph)
-    hipLaunchKernelGGL((lean_kernel<true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q, plan,
-                       nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+  const dim3 g(lean_wgs), b(64 * kLeanWaves);
+  if (phrase && two)
+    hipLaunchKernelGGL((lean_kernel<true, true>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
+                       stats, fr, item_q, pub, desc);
+  else if (phrase)
+    hipLaunchKernelGGL((lean_kernel<true, false>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
+                       stats, fr, item_q, pub, desc);
   else if (two)
-    hipLaunchKernelGGL((lean_kernel<false, true>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
-                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+    hipLaunchKernelGGL((lean_kernel<false, true>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
+                       stats, fr, item_q, pub, desc);
   else
-    hipLaunchKernelGGL((lean_kernel<false>), dim3(lean_wgs), dim3(64 * kLeanWaves), 0, st, ix, q,
-                       plan, nq, counters, events, ev_cnt, stats, fr, item_q, pub, desc, ph);
+    hipLaunchKernelGGL((lean_kernel<false, false>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
+                       stats, fr, item_q, pub, desc);
   return hipGetLastError();
 }
 
