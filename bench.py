@@ -143,6 +143,9 @@ def parse():
                         "rank's full-index image (0: every query is sharded; -1, the default: "
                         "max(64, 63 * N), so that each shard's part of a sharded query is at "
                         "least one full work item)")
+    p.add_argument("--shard-group", type=int, default=4,
+                   help="N>1 shards: heavy batches of this many consecutive steps share one "
+                        "all-to-all (wsr_shard_steps)")
     p.add_argument("--shard-every", type=int, default=0,
                    help="N>1 shards: the heavy queries of this many consecutive steps go through "
                         "one sharded step (a heavy batch every that many steps; 0, the default: "
@@ -948,12 +951,25 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     max_hq = max(1, max(st[1] for st in steps))
     slot = slot_for_fill(fill, max_hq)
 
+    # heavy batches of up to --shard-group consecutive steps (of one shape)
+    # go through one all-to-all: its host cost is paid once per group
+    pend = []
+
+    def flush():
+        if pend:
+            S.steps([x for x, _ in pend], pend[0][1], slot)
+            pend.clear()
+
     def step(i, fetch=False):
         hb, hq, _, cb, _ = steps[i % nb]
         if cb:
             cb.run()
         if hb:
-            S.step(hb, hq, slot)
+            if pend and pend[0][1] != hq:
+                flush()
+            pend.append((hb, hq))
+            if fetch or len(pend) >= max(1, a.shard_group):
+                flush()
         if fetch:
             return (S.fetch_owned(hb, hq) if hb else None), (cb.fetch() if cb else None)
         return None
@@ -965,6 +981,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
 
     for s_ in range(a.warmup):
         step(s_)
+    flush()
     sync_all()
     lat = []
     for i in range(nb):
@@ -977,6 +994,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     t0 = time.perf_counter()
     for s_ in range(a.steps):
         step(s_)
+    flush()
     host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     sync_all()
     el = time.perf_counter() - t0
@@ -1150,7 +1168,7 @@ def main():
             r = run_shard(a, S, None, 0, lines, rank, world, dist)
             forms["docshard"] = {**reduced(r), "parallelism": f"docshard{world}", "slot_events": r["slot"],
                                  "shard_every": r["every"], "hbm_per_rank": shard_bytes,
-                                 "note": "every query on every shard, one ncclAllToAll per sharded step, "
+                                 "note": f"every query on every shard, one ncclAllToAll per {a.shard_group} sharded steps, "
                                          "only the rank's shard image resident"}
             r["close"]()
         if a.heavy_blocks != 0 or a.mode == "auto":
@@ -1253,13 +1271,14 @@ def main():
         out["host_enqueue_ms_per_step"] = round(host_ms, 4)
         if mode != "replica":
             kind = ("one ncclAllToAll of per-owner regions ({count, offset} pairs + fixed event slot) over "
-                    "xGMI per sharded step (wsr_shard_step), no host round trip inside a step")
+                    f"xGMI per group of {a.shard_group} sharded steps (wsr_shard_steps), no host round trip "
+                    "inside a step")
             if a.exchange == "gloo" and world > 1:
                 kind = ("REHEARSAL: fused emit / owner replay with the slots moved by gloo through "
                         "host memory (not the RCCL path's speed)")
             out["exchange"] = {"kind": kind, "slot_events": main_run["slot"],
                                "heavy_blocks": main_run["heavy_blocks"],
-                               "shard_every": main_run["every"],
+                               "shard_every": main_run["every"], "shard_group": a.shard_group,
                                "heavy_query_share": round(main_run["heavy_share"], 4)}
             out["hbm_per_rank"] = {"shard_image_bytes": shard_bytes, "full_image_bytes": full_bytes,
                                    "total_bytes": (shard_bytes or 0) + (full_bytes or 0),

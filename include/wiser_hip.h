@@ -306,6 +306,13 @@ int wsr_comm_unique_id(uint8_t* id /* WSR_COMM_ID_BYTES */);
 int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device, wsr_comm** out);
 void wsr_comm_close(wsr_comm* c);
 int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot);
+/* A step group: n batches of world * q_per_owner queries each, every one
+ * emitted into its region of each owner's run of n regions (in the first
+ * batch's exchange buffers), then ONE ncclAllToAll of the runs and the n owner
+ * replays.  The same results as n wsr_shard_step calls, with one collective's
+ * host cost instead of n. */
+int wsr_shard_steps(wsr_handle* h, wsr_batch* const* b, int32_t n, wsr_comm* c, int32_t q_per_owner,
+                    int64_t slot);
 /* wsr_shard_step's two device halves with the transfer left to the caller (a
  * multi-rank rehearsal on one GPU, where RCCL refuses two ranks, or a host
  * exchange): the engine's own region buffers, in the exact layout the step's

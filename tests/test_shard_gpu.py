@@ -171,6 +171,41 @@ def test_native_rccl_step_one_rank(synth_small):
     S.close()
 
 
+def test_native_rccl_step_groups(synth_small):
+    """wsr_shard_steps: groups of batches through one ncclAllToAll (regions
+    of every batch in the first one's buffers), groups of changing size and
+    leader in flight one after another: equal to the oracle."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import NativeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_groups.log")
+    w.gen_two_term_log(d, log, n_queries=1024, seed=17)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    S = NativeShardedSearcher(d, 0, 1, share_id=lambda x: x)
+    eng = S.engine
+    n = 256
+    parts = [qs[i * n:(i + 1) * n] for i in range(4)]
+    bs = []
+    for part in parts:
+        arr = (_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=10))[0] for q in part])
+        b = w.ResidentBatch(eng, n, 10)
+        b.upload(arr)
+        bs.append(b)
+    o = OracleVacuum(d)
+    exp = [[o.search(q, 10)[0] for q in part] for part in parts]
+    for order in ([0, 1, 2], [3], [1, 3, 0, 2], [2, 0], [0, 1, 2, 3]):
+        S.steps([bs[i] for i in order], n, 64 * n)
+    for b, e in zip(bs, exp):
+        hits, nh = S.fetch_owned(b, n)
+        got = [[(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] for i in range(n)]
+        assert got == e
+    for b in bs:
+        b.close()
+    S.close()
+
+
 @pytest.mark.parametrize("world,k", [(2, 10), (3, 10), (8, 10), (3, 200)])
 def test_step_regions_equal_oracle(synth_small, world, k):
     """The native step's region layout (in-region meta, region stride, one

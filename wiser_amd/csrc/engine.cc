@@ -1242,38 +1242,47 @@ static uint64_t region_events_of(int32_t q_per_owner, int64_t slot) {
   return (static_cast<uint64_t>(q_per_owner) + 1) / 2 + static_cast<uint64_t>(slot);
 }
 
-// First half of a shard step: size the region buffers and run the batch with
-// fused emission into the send regions (owner o's region at o * region).
-static int step_emit(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot) {
+static int check_step(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot) {
   if (!h || !b || W < 1 || q_per_owner <= 0 || slot <= 0 || static_cast<int64_t>(q_per_owner) * W != b->nq)
     return fail(WSR_E_INVALID, "bad shard_step arguments (the batch must hold world * q_per_owner queries)");
   if (W > kMaxOwners) return fail(WSR_E_LIMIT, "more than kMaxOwners ranks");
   if (static_cast<uint64_t>(slot) > 0xFFFFFFFFull) return fail(WSR_E_LIMIT, "slot over 2^32 events");
-  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
-  const uint64_t region = region_events_of(q_per_owner, slot);
-  try {
-    HIP_OK(hipSetDevice(h->device));
-    const uint64_t need = region * W;
-    if (need > b->x_slots || W != b->x_pairs) {
-      if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));
-      if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
-      if (b->d_xrecv) HIP_OK(hipFree(b->d_xrecv));
-      b->d_xsend = b->d_xrecv = nullptr;
-      HIP_OK(hipMalloc(&b->d_xsend, sizeof(Event) * need));
-      HIP_OK(hipMalloc(&b->d_xrecv, sizeof(Event) * need));
-      b->x_slots = need;
-      b->x_pairs = W;
-    }
-    if (!b->xev[0]) {
-      HIP_OK(hipEventCreateWithFlags(&b->xev[0], hipEventDisableTiming));
-      HIP_OK(hipEventCreateWithFlags(&b->xev[1], hipEventDisableTiming));
-    }
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
+  return WSR_OK;
+}
+
+// The events that order a shard step's exchange against the batch's runs.
+static void ensure_xev(wsr_batch* b) {
+  if (!b->xev[0]) {
+    HIP_OK(hipEventCreateWithFlags(&b->xev[0], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&b->xev[1], hipEventDisableTiming));
   }
-  const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));   // int32 per region
-  const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), b->d_xsend + meta_events, region,
-                     reinterpret_cast<int32_t*>(b->d_xsend), meta_stride};
+}
+
+// The exchange buffers of b: send and receive, need events each.
+static void ensure_xbuf(wsr_batch* b, uint64_t need, int W) {
+  if (need > b->x_slots || W != b->x_pairs) {
+    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));
+    if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
+    if (b->d_xrecv) HIP_OK(hipFree(b->d_xrecv));
+    b->d_xsend = b->d_xrecv = nullptr;
+    HIP_OK(hipMalloc(&b->d_xsend, sizeof(Event) * need));
+    HIP_OK(hipMalloc(&b->d_xrecv, sizeof(Event) * need));
+    b->x_slots = need;
+    b->x_pairs = W;
+  }
+  ensure_xev(b);
+}
+
+// First half of a shard step: run the batch with fused emission into the
+// send regions, owner o's region at send + o * owner_stride events (one
+// batch: its own buffer, owner_stride = region; a step group: the group's
+// buffer, this batch's region within every owner's run of regions).
+static int step_emit_into(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot, Event* send,
+                          uint64_t owner_stride) {
+  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
+  const uint64_t meta_stride = owner_stride * (sizeof(Event) / sizeof(int32_t));   // int32 per owner
+  const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), send + meta_events, owner_stride,
+                     reinterpret_cast<int32_t*>(send), meta_stride};
   const int rc = batch_run(h, b, &se);
   if (rc == WSR_OK) {
     b->x_world = W;
@@ -1283,21 +1292,45 @@ static int step_emit(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, in
   return rc;
 }
 
-// Second half: the owner replay of this rank's queries over the receive
-// regions (region g = what shard g sent this owner), on stream st.
-static int step_replay(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, int64_t slot,
-                       hipStream_t st) {
-  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
+static int step_emit(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot) {
+  if (int rc = check_step(h, b, W, q_per_owner, slot)) return rc;
   const uint64_t region = region_events_of(q_per_owner, slot);
-  const uint64_t meta_stride = region * (sizeof(Event) / sizeof(int32_t));
-  return owner_replay_meta_on(h, b, rank * q_per_owner, q_per_owner, W,
-                              reinterpret_cast<const int32_t*>(b->d_xrecv), meta_stride, region,
-                              b->d_xrecv + meta_events, st);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    ensure_xbuf(b, region * W, W);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  return step_emit_into(h, b, W, q_per_owner, slot, b->d_xsend, region);
 }
 
-int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
-  if (!c) return fail(WSR_E_INVALID, "null communicator");
+// Second half: the owner replay of this rank's queries over the receive
+// regions (region g = what shard g sent this owner, at recv + g *
+// owner_stride events), on stream st.
+static int step_replay_from(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, const Event* recv,
+                            uint64_t owner_stride, hipStream_t st) {
+  const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
+  const uint64_t meta_stride = owner_stride * (sizeof(Event) / sizeof(int32_t));
+  return owner_replay_meta_on(h, b, rank * q_per_owner, q_per_owner, W, reinterpret_cast<const int32_t*>(recv),
+                              meta_stride, owner_stride, recv + meta_events, st);
+}
+
+static int step_replay(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, int64_t slot,
+                       hipStream_t st) {
+  return step_replay_from(h, b, rank, W, q_per_owner, b->d_xrecv, region_events_of(q_per_owner, slot), st);
+}
+
+// A step group: n batches of the same shape, each emitted into its region of
+// every owner's run of n regions in the first batch's buffers, then ONE
+// ncclAllToAll of the runs and the n owner replays, on the communicator's
+// stream.  The collective's host cost (~0.1-0.2 ms a call under load, more
+// than a whole step's kernels) is paid once per group.
+int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c, int32_t q_per_owner,
+                    int64_t slot) {
+  if (!c || !bs || n < 1) return fail(WSR_E_INVALID, "bad shard_steps arguments");
   const int W = c->world;
+  for (int i = 0; i < n; ++i)
+    if (int rc = check_step(h, bs[i], W, q_per_owner, slot)) return rc;
   uint64_t t0 = c->timing ? now_ns() : 0;
   auto lap = [&](int i) {
     if (!c->timing) return;
@@ -1305,27 +1338,51 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
     c->t_ns[i] += t - t0;
     t0 = t;
   };
-  int rc = step_emit(h, b, W, q_per_owner, slot);
-  if (rc) return rc;
-  lap(0);
+  wsr_batch* b0 = bs[0];
   const uint64_t region = region_events_of(q_per_owner, slot);
+  const uint64_t run = region * static_cast<uint64_t>(n);   // events per owner
   try {
-    HIP_OK(hipEventRecord(b->xev[0], b->st));
-    HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
-    const ncclResult_t r = ncclAllToAll(b->d_xsend, b->d_xrecv, region * (sizeof(Event) / sizeof(uint64_t)),
+    HIP_OK(hipSetDevice(h->device));
+    ensure_xbuf(b0, run * W, W);
+    for (int i = 1; i < n; ++i) {
+      ensure_xev(bs[i]);
+      // the group's buffers: b0's previous exchange must be done with them
+      if (b0->x_pending) HIP_OK(hipStreamWaitEvent(bs[i]->st, b0->xev[1], 0));
+    }
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  for (int i = 0; i < n; ++i) {
+    if (int rc = step_emit_into(h, bs[i], W, q_per_owner, slot, b0->d_xsend + region * i, run)) return rc;
+  }
+  lap(0);
+  try {
+    for (int i = 0; i < n; ++i) {
+      HIP_OK(hipEventRecord(bs[i]->xev[0], bs[i]->st));
+      HIP_OK(hipStreamWaitEvent(c->stream, bs[i]->xev[0], 0));
+    }
+    const ncclResult_t r = ncclAllToAll(b0->d_xsend, b0->d_xrecv, run * (sizeof(Event) / sizeof(uint64_t)),
                                         ncclUint64, c->comm, c->stream);
     if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   lap(2);
-  rc = step_replay(h, b, c->rank, W, q_per_owner, slot, c->stream);
-  if (rc) return rc;
-  if (hipEventRecord(b->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
-  b->x_pending = true;
+  for (int i = 0; i < n; ++i) {
+    if (int rc = step_replay_from(h, bs[i], c->rank, W, q_per_owner, b0->d_xrecv + region * i, run, c->stream))
+      return rc;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (hipEventRecord(bs[i]->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
+    bs[i]->x_pending = true;
+  }
   lap(3);
-  ++c->steps;
+  c->steps += static_cast<uint64_t>(n);
   return WSR_OK;
+}
+
+int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot) {
+  return wsr_shard_steps(h, &b, 1, c, q_per_owner, slot);
 }
 
 int wsr_shard_step_regions(int32_t q_per_owner, int64_t slot, uint64_t* region_bytes) {

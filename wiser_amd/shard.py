@@ -108,6 +108,12 @@ class NativeShardedSearcher:
         results of the owned slice stay in HBM (fetch_owned reads them)."""
         check(lib.wsr_shard_step(self.engine._h, b._b, self._c, qpr, slot))
 
+    def steps(self, bs, qpr: int, slot: int):
+        """A step group (wsr_shard_steps): the batches bs, each of world * qpr
+        queries, through one all-to-all."""
+        arr = (C.c_void_p * len(bs))(*[b._b for b in bs])
+        check(lib.wsr_shard_steps(self.engine._h, arr, len(bs), self._c, qpr, slot))
+
     def max_fill(self, b) -> int:
         tot = (C.c_int64 * self.world)()
         check(lib.wsr_shard_fill(self.engine._h, b._b, self.world, tot))
@@ -159,6 +165,10 @@ class HostExchangeShardedSearcher:
         check(lib.wsr_shard_step_replay(self.engine._h, b._b, self.rank, W, qpr, slot,
                                         C.c_void_p(recv.data_ptr())))
         self._keep[(id(b), b.nq)] = (b, send, recv)   # alive until the replay has run
+
+    def steps(self, bs, qpr: int, slot: int):
+        for b in bs:   # (one host exchange per batch: the rehearsal has no collective to share)
+            self.step(b, qpr, slot)
 
     def max_fill(self, b) -> int:
         tot = (C.c_int64 * self.world)()
