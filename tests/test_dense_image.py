@@ -122,31 +122,8 @@ def test_image_size_host_only(synth_small):
 
 @pytest.fixture(scope="module")
 def bucket_index(built, tmp_path_factory):
-    """Lists below the bucket density (1/25) with crowded buckets: "z" in docs
-    0-9, 500-519 and the last doc (one 256-doc bucket holds ten), "f" in docs
-    1000-1255 (full 64-doc buckets: every probe past the fourth posting scans
-    the offset bytes), "s" every 40th doc, "y" every other doc (a bitmap)."""
-    import wiser_amd as w
-    root = tmp_path_factory.mktemp("buckets")
-    ld = root / "b.linedoc"
-    n = 8000
-    with open(ld, "w") as f:
-        f.write("FIELDS_HEADER_INDICATOR###\tdoctitle\tbody\ttokenized\n")
-        for i in range(n):
-            toks = [f"u{i}"]
-            if i < 10 or 500 <= i < 520 or i == n - 1:
-                toks.append("z")
-            if 1000 <= i < 1256:
-                toks += ["f"] * (1 + i % 3)
-            if i % 40 == 7:
-                toks.append("s")
-            if i % 2:
-                toks.append("y")
-            f.write(f"t\t{' '.join(toks)}\t{' '.join(toks)}\n")
-    d = root / "idx"
-    d.mkdir()
-    w.build_from_linedoc(str(ld), str(d), "TOKEN_ONLY")
-    return str(d)
+    from bucket_corpus import build_bucket_index
+    return build_bucket_index(tmp_path_factory.mktemp("buckets"))
 
 
 def test_dense_buckets(bucket_index):
@@ -155,8 +132,8 @@ def test_dense_buckets(bucket_index):
     from oracle.oracle import OracleVacuum
     orc = OracleVacuum(bucket_index)
     n = orc.n_docs()
-    for term in ("z", "f", "s", "y", "u77"):
-        for lo, hi in _shards(n) + [(1024, 1280), (1030, 1100)]:
+    for term in ("g", "s", "z", "y", "u77"):
+        for lo, hi in _shards(n) + [(6400, 6464), (6410, 20000), (12801, 30000)]:
             dense, got = _lookup(bucket_index, term, lo, hi, 1 << 30, n)
             exp = _expect(orc, term, lo, hi if hi else n, n)
             assert dense or set(exp) == {-1}, (term, lo, hi)

@@ -43,26 +43,35 @@ constexpr uint8_t kTf8Escape = 255;   // tf >= 255: read the tf blob instead
 // docs probed whatever the list holds: a driver a few hundred docs apart
 // fetches nearly every mask line of the range, ~8x the list's compressed
 // bytes at 1 % density (scripts/traffic_model.py).  The range is cut into
-// buckets of 2^c docs, c chosen so that a bucket holds ~2 postings; per bucket
+// buckets of 2^c docs, c chosen so that a bucket holds 1-2 postings on
+// average (below 2.5 % density that is >= 64 docs: an entry line covers at
+// least as many docs as a mask line); per bucket
 // one 8-byte BucketEnt {rank << 9 | count, the in-bucket
 // offsets (doc - bucket start) of its first four postings, one byte each}, and
 // after the list's entries (at byte 8 * n_buckets of its region) the in-bucket
 // offset of every posting, one byte each, for buckets of more than four.  A
 // probe reads one entry (a line covers 16 buckets: 4,096 docs at c = 8) and
 // compares four bytes at once; a hit's posting index is rank + its position,
-// and its tf comes from tf8 as for a bitmap.
+// and its tf comes from tf8 as for a bitmap.  A probe past the fourth posting
+// of a larger bucket reads the next offset bytes (one 8-byte window: counts up
+// to 9 cost no further wait); past the ninth it walks them.  A list whose
+// postings crowd (more than 1/1024 of its buckets over kBucketWindow, as a
+// topic-clustered term's do) keeps a bitmap: every wave would walk.
 constexpr uint32_t kProbeShiftBit = 56;
 constexpr uint64_t kProbeBaseMask = (1ull << kProbeShiftBit) - 1;
-constexpr uint32_t kBucketDensity = 25;     // buckets below 4 % density, bitmaps above
+constexpr uint32_t kBucketDensity = 40;     // buckets below 2.5 % density, bitmaps above
 constexpr uint32_t kBucketMinShift = 3, kBucketMaxShift = 8;
 constexpr uint32_t kBucketInline = 4;       // offsets held in the entry
+constexpr uint32_t kBucketWindow = 9;       // counts served without a walk
+constexpr uint32_t kBucketCrowdedDiv = 1024;   // more crowded buckets than 1/this: a bitmap
 inline uint32_t probe_shift(uint64_t bm) { return static_cast<uint32_t>(bm >> kProbeShiftBit); }
 inline uint64_t bucket_count(uint32_t span, uint32_t c) { return (static_cast<uint64_t>(span) + (1u << c) - 1) >> c; }
-// bucket shift for n postings over span docs (0: a bitmap): ~2 postings per bucket
+// bucket shift for n postings over span docs (0: a bitmap): 1-2 postings per bucket
 inline uint32_t bucket_shift(uint64_t n, uint32_t span) {
-  if (!span || n * kBucketDensity >= span || n >= (1u << 23)) return 0;
+  // (ranks travel in 23 bits; a shard image's edge blocks add < 256 postings)
+  if (!span || n * kBucketDensity >= span || n >= (1u << 23) - 1024) return 0;
   uint32_t c = kBucketMinShift;
-  while (c < kBucketMaxShift && (n << (c + 1)) <= 3ull * span) ++c;   // mean n * 2^c / span < 1.5 -> double it
+  while (c < kBucketMaxShift && (n << (c + 1)) <= 2ull * span) ++c;   // doubled, the mean stays <= 2
   return c;
 }
 // words (u32) of a bucket list's region: entries, then one offset byte per posting

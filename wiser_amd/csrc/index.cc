@@ -467,6 +467,23 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         }
       }
       in.shift = static_cast<uint8_t>(bucket_shift(n_in, span));
+      if (in.shift) {   // crowded buckets (postings clustered in the range): a bitmap
+        const uint32_t c = in.shift;
+        uint64_t crowded = 0, run = 0, cur = ~0ull;
+        for (uint64_t r = r0; r < r1; ++r) {
+          uint32_t docs[kPackSize];
+          const int cnt = row_cnt(in, r, nrows);
+          if (!host_decode_block(file + s.rows[r].doc_off, fend, cnt, true, s.rows[r].prev_doc, docs))
+            throw std::runtime_error("cannot decode a block for the dense image");
+          for (int i = 0; i < cnt; ++i) {
+            if (docs[i] < doc_lo || docs[i] >= lim) continue;
+            const uint64_t bk = (docs[i] - doc_lo) >> c;
+            if (bk != cur) { cur = bk; run = 0; }
+            if (++run == kBucketWindow + 1) ++crowded;
+          }
+        }
+        if (crowded * kBucketCrowdedDiv > bucket_count(span, c)) in.shift = 0;
+      }
     }
   });
 
@@ -561,7 +578,8 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.dense.resize(ne);
   img.dense_rank.resize(kRankWords * ne);
   img.tf8.resize(ntf8);
-  img.bkt.resize(nbk);
+  img.bkt.resize(nbk + 4);   // (+16 B: the last list's 8-byte offset windows)
+  for (uint64_t i = nbk; i < nbk + 4; ++i) img.bkt[i] = 0;
 
   lap("pass 2 (offsets, allocation)");
   // ---- pass 3: fill in place

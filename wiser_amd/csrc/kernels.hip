@@ -353,10 +353,10 @@ __device__ __forceinline__ const uint8_t* bucket_offsets(const IndexArgs& ix, ui
   return reinterpret_cast<const uint8_t*>(ix.bkt + (bm & kProbeBaseMask) +
                                           ((static_cast<uint64_t>(ix.dense_span) + (1u << c) - 1) >> c));
 }
-// postings 4.. of a bucket of cnt starting at posting `rank`: is one at offset o?
+// postings j0.. of a bucket of cnt starting at posting `rank`: is one at offset o?
 __device__ __forceinline__ bool bucket_scan(const uint8_t* offs, uint32_t rank, uint32_t cnt, uint32_t o,
-                                            uint32_t* idx) {
-  for (uint32_t j = kBucketInline; j < cnt; ++j) {
+                                            uint32_t* idx, uint32_t j0 = kBucketInline) {
+  for (uint32_t j = j0; j < cnt; ++j) {
     const uint32_t b = load_byte(offs + rank + j);
     if (b >= o) {
       *idx = rank + j;
@@ -1768,6 +1768,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   const uint2* o_bk = kBk ? ix.bkt + (Q.o_bm & kProbeBaseMask) : nullptr;
   const uint8_t* o_off = kBk ? bucket_offsets(ix, Q.o_bm) : nullptr;
   const uint32_t o_tf8_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8)) & 3u;
+  const uint32_t o_off_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_off)) & 3u;
   const uint8_t* a_blob = ix.blob + Q.a_base;
   uint32_t evb = 0;
   const uint32_t lo = in_vgpr(ix.doc_lo), span = in_vgpr(ix.dense_span);
@@ -1998,15 +1999,29 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       // (the record's tf bytes cover the word's first four postings)
       uint32_t rk0, rk1, f0, f1, hx0 = X.hx0, hx1 = X.hx1;
       if constexpr (kBk) {
-        // probes past a bucket's fourth posting (rare): its offset bytes
+        // probes past a bucket's fourth posting: the window of its next offset
+        // bytes loaded in H (bit 30; count in bits 23-29), a walk past it
         const bool s0 = (hx0 >> 30) == 1u, s1 = (hx1 >> 30) == 1u;
         if (__ballot(s0 || s1)) {
           const uint32_t m = (1u << bsh) - 1u;
-          uint32_t i0 = 0, i1 = 0;
-          if (s0) hx0 = bucket_scan(o_off, hx0 & 0x3FFFFFFFu, X.hf0.y, (X.ha0 - lo) & m, &i0) ? (i0 | 0x40000000u)
-                                                                                             : 0x80000000u;
-          if (s1) hx1 = bucket_scan(o_off, hx1 & 0x3FFFFFFFu, X.hf1.y, (X.ha1 - lo) & m, &i1) ? (i1 | 0x40000000u)
-                                                                                             : 0x80000000u;
+          auto resolve = [&](uint32_t hx, uint2 win, uint32_t doc) __attribute__((always_inline)) {
+            const uint32_t rk = hx & 0x7FFFFFu, cn = (hx >> 23) & 127u, o = (doc - lo) & m;
+            const uint32_t mis = (o_off_mis + rk + kBucketInline) & 3u, avail = 8u - mis;
+            const uint64_t w = ((static_cast<uint64_t>(win.y) << 32) | win.x) >> (mis << 3);
+            const uint64_t t = w ^ (o * 0x0101010101010101ull);
+            const uint64_t z = (t - 0x0101010101010101ull) & ~t & 0x8080808080808080ull;
+            const uint32_t pos = z ? static_cast<uint32_t>(__builtin_ctzll(z)) >> 3 : 8u;
+            if (pos < min(cn - kBucketInline, avail)) return (rk + kBucketInline + pos) | 0x40000000u;
+            if (cn - kBucketInline > avail && o > ((w >> ((avail - 1) << 3)) & 0xFFu)) {
+              // past the window (the count is exact below 127)
+              const uint32_t c = cn < 127u ? cn : (o_bk[(doc - lo) >> bsh].x & 511u);
+              uint32_t i = 0;
+              if (bucket_scan(o_off, rk, c, o, &i, kBucketInline + avail)) return i | 0x40000000u;
+            }
+            return 0x80000000u;
+          };
+          if (s0) hx0 = resolve(hx0, X.hf0, X.ha0);
+          if (s1) hx1 = resolve(hx1, X.hf1, X.ha1);
         }
         // (a scanned hit, bit 30, reads its tf by rank when scored)
         rk0 = hx0 & 0x3FFFFFFFu;
@@ -2055,13 +2070,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       const bool sc0 = v0 & (ps0 == kBucketScan), sc1 = v1 & (ps1 == kBucketScan);
       const uint32_t r0 = X.de0.x >> 9, r1 = X.de1.x >> 9;
       const uint32_t k0 = r0 + (h0 ? ps0 : 0u), k1 = r1 + (h1 ? ps1 : 0u);
-      // the hit's tf byte, as its aligned word
-      Y.hf0.x = *reinterpret_cast<const uint32_t*>(__builtin_align_down(o_tf8 + (h0 ? k0 : 0u), 4));
-      Y.hf1.x = *reinterpret_cast<const uint32_t*>(__builtin_align_down(o_tf8 + (h1 ? k1 : 0u), 4));
-      Y.hf0.y = X.de0.x & 511u;
-      Y.hf1.y = X.de1.x & 511u;
-      Y.hx0 = h0 ? k0 : sc0 ? (0x40000000u | r0) : 0x80000000u;
-      Y.hx1 = h1 ? k1 : sc1 ? (0x40000000u | r1) : 0x80000000u;
+      // a hit: its tf byte, as its aligned word; a probe past the fourth
+      // posting: the next 8 offset bytes (two aligned words)
+      const uint32_t* p0 = reinterpret_cast<const uint32_t*>(
+          sc0 ? __builtin_align_down(o_off + r0 + kBucketInline, 4) : __builtin_align_down(o_tf8 + (h0 ? k0 : 0u), 4));
+      const uint32_t* p1 = reinterpret_cast<const uint32_t*>(
+          sc1 ? __builtin_align_down(o_off + r1 + kBucketInline, 4) : __builtin_align_down(o_tf8 + (h1 ? k1 : 0u), 4));
+      Y.hf0.x = p0[0];
+      Y.hf1.x = p1[0];
+      Y.hf0.y = p0[1];
+      Y.hf1.y = p1[1];
+      const uint32_t n0 = min(X.de0.x & 511u, 127u), n1 = min(X.de1.x & 511u, 127u);
+      Y.hx0 = h0 ? k0 : sc0 ? (0x40000000u | (n0 << 23) | r0) : 0x80000000u;
+      Y.hx1 = h1 ? k1 : sc1 ? (0x40000000u | (n1 << 23) | r1) : 0x80000000u;
       Y.ha0 = X.da0; Y.ha1 = X.da1;
       Y.hc0 = X.dcc & 0xFFu;
       Y.hc1 = X.dcc >> 8;
