@@ -39,7 +39,7 @@ def test_bucket_probes_equal_oracle(bucket_index, div, k, monkeypatch):
     eng.Load()
     res = eng.SearchBatch([w.SearchQuery(q, n_results=k) for q in qs])
     for q, r in zip(qs, res):
-        assert [(x.doc_id, x.score) for x in r.entries] == o.search(q, k)[0], q
+        assert [(x.doc_id, x.doc_score) for x in r.entries] == o.search(q, k)[0], q
     eng.close()
     o.close()
 
