@@ -559,6 +559,9 @@ def extra_legs(a, idx, qlog, local, threads):
                                         0 if a.no_cpu else a.cpu_seconds / 4)
         legs["c4_mixed_1to5"]["workload"] = (f"{tag}: 20000 AND queries of 1-5 terms (AOL term-count "
                                              "shares, gen_synthetic_log group rule, seed 7), top-10")
+        pmc = load_pmc("c4") if a.workload == "c3" and not (a.vacuum_dir or a.linedoc) else None
+        if pmc:
+            legs["c4_mixed_1to5"]["roofline"].update(pmc)
         eng.close()
     if want("c5_phrase"):
         pidx = idx
@@ -579,6 +582,9 @@ def extra_legs(a, idx, qlog, local, threads):
         legs["c5_phrase"]["image"] = eng.image_info()
         legs["c5_phrase"]["workload"] = (f"{ptag}: 10000 two-term phrase queries from the corpus's "
                                          "phrase pool (gen_synthetic_log.py:216-265), top-10")
+        pmc = load_pmc("c5") if pidx == idx and a.workload == "c3" and not (a.vacuum_dir or a.linedoc) else None
+        if pmc:
+            legs["c5_phrase"]["roofline"].update(pmc)
         eng.close()
     if want("c3_topics") and a.workload == "c3" and not (a.vacuum_dir or a.linedoc):
         legs["c3_topics"] = topics_leg(a, local, threads)

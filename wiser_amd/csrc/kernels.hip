@@ -366,6 +366,24 @@ __device__ __forceinline__ bool bucket_scan(const uint8_t* offs, uint32_t rank, 
   return false;
 }
 
+// The window of a bucket's next eight offset bytes (postings 4..) as two
+// aligned words w0, w1 from offs + rank + 4: is o among its first
+// min(cnt - 4, available) bytes?  (its position, < 8; kWindowMiss; or, past
+// a window that holds fewer than the remaining count with o beyond its last
+// byte, kWindowScan: walk from `*next`.)
+constexpr uint32_t kWindowMiss = 8, kWindowScan = 9;
+__device__ __forceinline__ uint32_t bucket_window(uint32_t w0, uint32_t w1, uint32_t mis, uint32_t cnt, uint32_t o,
+                                                  uint32_t* next) {
+  const uint32_t avail = 8u - mis;
+  const uint64_t w = ((static_cast<uint64_t>(w1) << 32) | w0) >> (mis << 3);
+  const uint64_t t = w ^ (o * 0x0101010101010101ull);
+  const uint64_t z = (t - 0x0101010101010101ull) & ~t & 0x8080808080808080ull;
+  const uint32_t pos = z ? static_cast<uint32_t>(__builtin_ctzll(z)) >> 3 : 8u;
+  if (pos < min(cnt - kBucketInline, avail)) return pos;
+  *next = kBucketInline + avail;
+  return (cnt - kBucketInline > avail && o > ((w >> ((avail - 1) << 3)) & 0xFFu)) ? kWindowScan : kWindowMiss;
+}
+
 // A list's probe entry for doc offset rel (in: rel inside the range, else a
 // dummy read): its bitmap entry {rank, mask} or its bucket entry.  The shift
 // comes from the list record, so the branch is uniform.
@@ -383,11 +401,24 @@ __device__ __forceinline__ bool probe_hit(const IndexArgs& ix, uint64_t bm, uint
   if (rel >= ix.dense_span) return false;
   const uint32_t o = rel & ((1u << c) - 1u);
   const uint32_t pos = bucket_pos(v, o);
+  const uint32_t rank = v.x >> 9;
   if (pos < kBucketInline) {
-    *idx = (v.x >> 9) + pos;
+    *idx = rank + pos;
     return true;
   }
-  return pos == kBucketScan && bucket_scan(bucket_offsets(ix, bm), v.x >> 9, v.x & 511u, o, idx);
+  if (pos != kBucketScan) return false;
+  // the next eight offset bytes at once, a walk past them
+  const uint8_t* offs = bucket_offsets(ix, bm);
+  const uint8_t* p = offs + rank + kBucketInline;
+  const uint32_t* wp = reinterpret_cast<const uint32_t*>(__builtin_align_down(p, 4));
+  uint32_t next = 0;
+  const uint32_t wpos = bucket_window(wp[0], wp[1], static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)) & 3u,
+                                      v.x & 511u, o, &next);
+  if (wpos < 8u) {
+    *idx = rank + kBucketInline + wpos;
+    return true;
+  }
+  return wpos == kWindowScan && bucket_scan(offs, rank, v.x & 511u, o, idx, next);
 }
 
 // Is doc a in B?  One 8-byte load (dense_load, issued early) and, on a hit,
@@ -2006,17 +2037,13 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
           const uint32_t m = (1u << bsh) - 1u;
           auto resolve = [&](uint32_t hx, uint2 win, uint32_t doc) __attribute__((always_inline)) {
             const uint32_t rk = hx & 0x7FFFFFu, cn = (hx >> 23) & 127u, o = (doc - lo) & m;
-            const uint32_t mis = (o_off_mis + rk + kBucketInline) & 3u, avail = 8u - mis;
-            const uint64_t w = ((static_cast<uint64_t>(win.y) << 32) | win.x) >> (mis << 3);
-            const uint64_t t = w ^ (o * 0x0101010101010101ull);
-            const uint64_t z = (t - 0x0101010101010101ull) & ~t & 0x8080808080808080ull;
-            const uint32_t pos = z ? static_cast<uint32_t>(__builtin_ctzll(z)) >> 3 : 8u;
-            if (pos < min(cn - kBucketInline, avail)) return (rk + kBucketInline + pos) | 0x40000000u;
-            if (cn - kBucketInline > avail && o > ((w >> ((avail - 1) << 3)) & 0xFFu)) {
-              // past the window (the count is exact below 127)
+            uint32_t next = 0;
+            const uint32_t pos = bucket_window(win.x, win.y, (o_off_mis + rk + kBucketInline) & 3u, cn, o, &next);
+            if (pos < 8u) return (rk + kBucketInline + pos) | 0x40000000u;
+            if (pos == kWindowScan) {   // past the window (the count is exact below 127)
               const uint32_t c = cn < 127u ? cn : (o_bk[(doc - lo) >> bsh].x & 511u);
               uint32_t i = 0;
-              if (bucket_scan(o_off, rk, c, o, &i, kBucketInline + avail)) return i | 0x40000000u;
+              if (bucket_scan(o_off, rk, c, o, &i, next)) return i | 0x40000000u;
             }
             return 0x80000000u;
           };
