@@ -981,6 +981,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
         return None
 
     def sync_all():
+        S.flush()   # (a host-exchange rehearsal's last exchange)
         w.sync(S.engine)
         if full:
             w.sync(full)

@@ -329,6 +329,13 @@ int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_pe
                         void* host_send);
 int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
                           int64_t slot, const void* host_recv);
+/* wsr_shard_step_emit without the wait: the copy to host_send (page-locked,
+ * wsr_pinned_alloc) is enqueued on the batch's stream; wsr_batch_stream_sync
+ * waits for it, so a caller overlaps one batch's host exchange with the next
+ * batch's kernels. */
+int wsr_shard_step_emit_async(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                              void* host_send);
+int wsr_batch_stream_sync(wsr_handle* h, wsr_batch* b);
 
 /* Decode one block of a list on the device (test hook for the decoder):
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */

@@ -206,6 +206,46 @@ def test_native_rccl_step_groups(synth_small):
     S.close()
 
 
+def test_host_exchange_pipelined(synth_small):
+    """HostExchangeShardedSearcher (the gloo rehearsal's searcher): each step
+    enqueues its emission and then finishes the step before it (exchange,
+    replay), the same batch twice in a row included; a one-rank gloo group in
+    this process.  Equal to the oracle."""
+    import torch.distributed as dist
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import HostExchangeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_hostx.log")
+    w.gen_two_term_log(d, log, n_queries=1024, seed=19)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:29613", rank=0, world_size=1)
+    try:
+        S = HostExchangeShardedSearcher(d, 0, 1)
+        eng = S.engine
+        n = 256
+        parts = [qs[i * n:(i + 1) * n] for i in range(4)]
+        bs = []
+        for part in parts:
+            arr = (_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=10))[0] for q in part])
+            b = w.ResidentBatch(eng, n, 10)
+            b.upload(arr)
+            bs.append(b)
+        for i in (0, 1, 2, 3, 3, 1, 0, 2):
+            S.step(bs[i], n, 64 * n)
+        o = OracleVacuum(d)
+        for b, part in zip(bs, parts):
+            hits, nh = S.fetch_owned(b, n)
+            got = [[(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])] for i in range(n)]
+            assert got == [o.search(q, 10)[0] for q in part]
+        for b in bs:
+            b.close()
+        S.close()
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("world,k", [(2, 10), (3, 10), (8, 10), (3, 200)])
 def test_step_regions_equal_oracle(synth_small, world, k):
     """The native step's region layout (in-region meta, region stride, one

@@ -1391,19 +1391,35 @@ int wsr_shard_step_regions(int32_t q_per_owner, int64_t slot, uint64_t* region_b
   return WSR_OK;
 }
 
-int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
-                        void* host_send) {
+static int shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                           void* host_send, bool wait) {
   if (!host_send) return fail(WSR_E_INVALID, "null host buffer");
   const int rc = step_emit(h, b, world, q_per_owner, slot);
   if (rc) return rc;
   try {
     HIP_OK(hipMemcpyAsync(host_send, b->d_xsend, sizeof(Event) * region_events_of(q_per_owner, slot) * world,
                           hipMemcpyDeviceToHost, b->st));
-    HIP_OK(hipStreamSynchronize(b->st));
+    if (wait) HIP_OK(hipStreamSynchronize(b->st));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   return WSR_OK;
+}
+
+int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                        void* host_send) {
+  return shard_step_emit(h, b, world, q_per_owner, slot, host_send, true);
+}
+
+int wsr_shard_step_emit_async(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
+                              void* host_send) {
+  return shard_step_emit(h, b, world, q_per_owner, slot, host_send, false);
+}
+
+int wsr_batch_stream_sync(wsr_handle* h, wsr_batch* b) {
+  if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  const hipError_t e = hipStreamSynchronize(b->st);
+  return e == hipSuccess ? WSR_OK : fail(WSR_E_HIP, hipGetErrorString(e));
 }
 
 int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,

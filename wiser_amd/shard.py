@@ -114,6 +114,9 @@ class NativeShardedSearcher:
         arr = (C.c_void_p * len(bs))(*[b._b for b in bs])
         check(lib.wsr_shard_steps(self.engine._h, arr, len(bs), self._c, qpr, slot))
 
+    def flush(self):
+        """(every step is enqueued whole: nothing is held back on the host)"""
+
     def max_fill(self, b) -> int:
         tot = (C.c_int64 * self.world)()
         check(lib.wsr_shard_fill(self.engine._h, b._b, self.world, tot))
@@ -153,18 +156,46 @@ class HostExchangeShardedSearcher:
                                    doc_range=self.doc_range if world > 1 else None, positions=positions)
         self.engine.Load()
         self._keep = {}
+        self._send = {}       # per batch: its page-locked send regions (pointer, bytes)
+        self._pending = None  # the step whose exchange waits for the next step's launch
 
     def step(self, b, qpr: int, slot: int):
-        import torch
+        """Enqueue the batch's emission (the copy of its send regions to
+        page-locked memory included), then finish the previous step: wait for
+        its copy, exchange, replay.  So one step's host exchange runs while the
+        next step's kernels do."""
         W = self.world
         rb = C.c_uint64()
         check(lib.wsr_shard_step_regions(qpr, slot, C.byref(rb)))
-        send = torch.empty(W * rb.value // 8, dtype=torch.int64)
-        check(lib.wsr_shard_step_emit(self.engine._h, b._b, W, qpr, slot, C.c_void_p(send.data_ptr())))
-        recv = exchange_regions(send, W, self.group)
-        check(lib.wsr_shard_step_replay(self.engine._h, b._b, self.rank, W, qpr, slot,
+        nbytes = W * rb.value
+        if self._pending is not None and self._pending[0] is b:
+            self.flush()   # (its send buffer is about to be rewritten)
+        ptr, have = self._send.get(id(b), (None, 0))
+        if have < nbytes:
+            lib.wsr_pinned_free(ptr)
+            p = C.c_void_p()
+            check(lib.wsr_pinned_alloc(nbytes, C.byref(p)))
+            ptr = p.value
+            self._send[id(b)] = (ptr, nbytes)
+        check(lib.wsr_shard_step_emit_async(self.engine._h, b._b, W, qpr, slot, C.c_void_p(ptr)))
+        prev, self._pending = self._pending, (b, qpr, slot, ptr, nbytes)
+        if prev is not None:
+            self._finish(*prev)
+
+    def _finish(self, b, qpr, slot, ptr, nbytes):
+        import torch
+        check(lib.wsr_batch_stream_sync(self.engine._h, b._b))
+        send = torch.frombuffer((C.c_char * nbytes).from_address(ptr), dtype=torch.int64)
+        recv = exchange_regions(send, self.world, self.group)
+        check(lib.wsr_shard_step_replay(self.engine._h, b._b, self.rank, self.world, qpr, slot,
                                         C.c_void_p(recv.data_ptr())))
-        self._keep[(id(b), b.nq)] = (b, send, recv)   # alive until the replay has run
+        self._keep[(id(b), b.nq)] = (b, recv)   # alive until the replay has run
+
+    def flush(self):
+        """Finish the step still waiting for its exchange."""
+        prev, self._pending = self._pending, None
+        if prev is not None:
+            self._finish(*prev)
 
     def steps(self, bs, qpr: int, slot: int):
         for b in bs:   # (one host exchange per batch: the rehearsal has no collective to share)
@@ -176,11 +207,16 @@ class HostExchangeShardedSearcher:
         return max(tot)
 
     def fetch_owned(self, b, qpr: int):
+        self.flush()
         hits = (_capi.Hit * (qpr * b.stride))()
         nh = (C.c_int32 * qpr)()
         check(lib.wsr_batch_fetch_range(self.engine._h, b._b, self.rank * qpr, qpr, hits, nh))
         return hits, nh
 
     def close(self):
+        self.flush()
         self._keep.clear()
+        for ptr, _ in self._send.values():
+            lib.wsr_pinned_free(ptr)
+        self._send.clear()
         self.engine.close()
