@@ -28,7 +28,7 @@ for counters in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_32B_sum"
 done
 python3 "$R/scripts/pmc_bytes.py" "$P/calib" > "$O/calib_bytes.txt"
 cat "$O/calib_bytes.txt"
-python3 "$R/scripts/pmc_bytes.py" "$P/pmc" lean_kernel,segment_kernel "$O/pmc_segment.json"
+python3 "$R/scripts/pmc_bytes.py" "$P/pmc" lean_kernel,segment_kernel "$O/pmc_segment.json" "$O/pmc_pass1.json"
 python3 "$R/scripts/pmc_bytes.py" "$P/pmc" > "$O/pmc_all_kernels.txt"
 echo done
 # the sharded path rehearsed with one rank: where a step's time goes

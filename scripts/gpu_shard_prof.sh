@@ -28,3 +28,14 @@ python3 "$R/scripts/trace_overlap.py" "$P/hb0_trace.csv" lean_kernel segment_ker
     plan_fill_kernel owner_replay_meta_kernel > "$O/hb0_overlap.json"
 python3 "$R/scripts/shard_timeline.py" "$P/hb0_trace.csv" > "$O/hb0_timeline.txt" || true
 echo "hb0 trace ok"
+# two ranks on this one GPU: the gloo rehearsal of every N > 1 form (hybrid,
+# pure doc-range, replicas), host exchange pipelined behind the next step
+cd "$R"
+timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --exchange gloo --steps 400 --warmup 20 --no-cpu "$@" \
+    > "$O/n2_gloo.json" 2> "$O/n2_gloo.err"
+python3 - "$O/n2_gloo.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print("n2 gloo value", d["value"], {k: v.get("value") for k, v in (d.get("forms") or {}).items()})
+PY
