@@ -1,0 +1,33 @@
+#!/bin/bash
+# One-rank RCCL rehearsal of the sharded forms under several settings (A/B of
+# the exchange stream's priority and the step-group size), with host phase
+# timers.  Every GPU step has its own limit; the first failure ends the
+# script.  Usage: TAG
+set -eu -o pipefail
+TAG=$1
+R=$(cd "$(dirname "$0")/.." && pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+run() {   # name env-assignments... -- bench args...
+  local name=$1; shift
+  local envs=()
+  while [ "$1" != "--" ]; do envs+=("$1"); shift; done
+  shift
+  env "${envs[@]}" WSR_HOST_TIMING=1 timeout -k 10 300 python3 bench.py --mode shard --no-extra --no-cpu \
+      --steps 1000 "$@" > "$O/$name.json" 2> "$O/$name.err"
+  python3 - "$O/$name.json" "$name" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], "value", d["value"], "ms/step", d["ms_per_step"], "host", d.get("host_enqueue_ms_per_step"))
+PY
+  grep -h "wsr_shard_step host" "$O/$name.err" || true
+}
+run replica X=1 -- --mode replica
+run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
+run hb0_g4_noprio WSR_COMM_PRIORITY=0 -- --heavy-blocks 0 --shard-group 4
+run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
+run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
+run hyb_g4 X=1 -- --shard-group 4
+run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
+run hyb_g8 X=1 -- --shard-group 8
