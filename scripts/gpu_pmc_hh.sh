@@ -20,7 +20,7 @@ while read -r counters; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --pmc $counters --output-format csv -d "$P/pass$i" -o pmc -- \
       python3 "$R/scripts/diag_types.py" $WIKI --only high-high > "$O/pass$i.txt" 2> "$O/pass$i.err" \
-      && echo "pass $i ok: $counters" || { echo "pass $i failed: $counters"; tail -3 "$O/pass$i.err"; }
+      && echo "pass $i ok: $counters" || { echo "pass $i failed: $counters"; tail -3 "$O/pass$i.err"; exit 1; }
 done < "$R/scripts/counters_hh.txt"
 python3 "$R/scripts/pmc_summary.py" "$P" > "$O/pmc_hh.json"
 python3 -c "
