@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <cstdlib>
@@ -159,6 +160,11 @@ struct wsr_batch {
   int x_pairs = 0;
   hipEvent_t xev[2] = {nullptr, nullptr};   // emission done -> comm stream; exchange done -> replay
   bool x_pending = false;   // a shard step's exchange + owner replay (xev[1]) not yet joined
+  // exchanges asked of the communicator's worker thread for this batch, and
+  // those it has enqueued (xev[1] recorded): xev[1] is only waited on once
+  // they agree (x_join)
+  uint64_t x_req = 0;
+  std::atomic<uint64_t> x_enq{0};
   bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
   int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
   int64_t x_slot = 0;           //     and slot (the replay half must match them)
@@ -178,6 +184,13 @@ struct wsr_batch {
   hipEvent_t fork = nullptr, join = nullptr;
   bool ran = false;
 };
+// Is a shard step's exchange of b outstanding?  First wait until the
+// communicator's worker has enqueued every exchange asked of it for b, so
+// that xev[1] is the record to wait on.
+static bool x_join(wsr_batch* b) {
+  while (b->x_enq.load(std::memory_order_acquire) != b->x_req) std::this_thread::yield();
+  return b->x_pending;
+}
 
 namespace {
 // bytes dev_upload allocates for a host array (at least one element)
@@ -626,6 +639,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
 
 void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (!b) return;
+  if (x_join(b)) (void)hipEventSynchronize(b->xev[1]);   // a shard step's exchange reads its buffers
   if (b->st) (void)hipStreamSynchronize(b->st);
   if (b->st2) (void)hipStreamSynchronize(b->st2);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
@@ -731,7 +745,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     if (ev_need > b->ev_cap) {
       if (b->d_events) HIP_OK(hipFree(b->d_events));
       b->ev_cap = ev_need + ev_need / 4 + 4096;
@@ -791,6 +805,7 @@ struct ShardEmit {
 
 static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se = nullptr);
 
+
 int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
 
 // One run of the batch: plan, then the lean and general segment kernels on
@@ -805,7 +820,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
     hipStream_t st = b->st;
     // the previous shard step's exchange and owner replay (on the communicator's
     // stream) read this batch's buffers and write its results
-    if (b->x_pending) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));
+    if (x_join(b)) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));
     b->x_pending = false;
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * (kNumCounters + (se ? se->owners : 0)), st));
     FusedReplay fr{b->d_qdone, b->d_hits, b->stride, b->d_nhits};
@@ -880,7 +895,7 @@ static int batch_fetch(wsr_handle* h, wsr_batch* b, wsr_hit* hits, int32_t* n_hi
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
-    if (b->x_pending) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));   // a shard step's exchange + replay
     HIP_OK(hipMemcpyAsync(b->h_ctr, b->d_ctr, sizeof(uint32_t) * kNumCounters, hipMemcpyDeviceToHost, st));
     if (b->nq && !(host_pinned(hits) && host_pinned(n_hits))) {
       // pageable destinations: a queued copy into them is staged by the runtime
@@ -942,7 +957,7 @@ int wsr_batch_ready(wsr_handle* h, wsr_batch* b) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   if (!b->ran) return 0;
   hipError_t e = hipEventQuery(b->ev[3]);   // recorded after the batch's last kernel
-  if (e == hipSuccess && b->x_pending) e = hipEventQuery(b->xev[1]);   // and a shard step's replay
+  if (e == hipSuccess && x_join(b)) e = hipEventQuery(b->xev[1]);   // and a shard step's replay
   if (e == hipSuccess) return 1;
   if (e == hipErrorNotReady) return 0;
   return fail(WSR_E_HIP, hipGetErrorString(e));
@@ -953,7 +968,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
   std::lock_guard<std::mutex> g(h->mu);
   try {
     HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
@@ -1118,7 +1133,7 @@ int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     // the segment kernels' per-owner fill counters
     std::vector<uint32_t> fill(n_owners);
     HIP_OK(hipMemcpy(fill.data(), b->d_ctr + kNumCounters, sizeof(uint32_t) * n_owners, hipMemcpyDeviceToHost));
@@ -1140,6 +1155,19 @@ int wsr_batch_stream(wsr_handle* h, wsr_batch* b, void** stream) {
 // (the same order on every rank), whatever batch stream it serves: a step's
 // pack is joined into it by an event and its replay waits for it by another,
 // so consecutive batches still overlap their kernels.
+// The exchange half of a step group (the collective and the owner replays)
+// is enqueued by the communicator's own worker thread: an ncclAllToAll call
+// can hold its caller for milliseconds while the device is busy (RCCL's host
+// side waits for its earlier work: 0.13-0.23 ms of host time per step in the
+// hybrid rehearsal, the loop host-bound, profiles/r04g/), and the caller's
+// next batches must not wait behind it.  Jobs run in submission order, so
+// every rank issues its collectives in the same order.
+struct XJob {
+  wsr_handle* h;
+  std::vector<wsr_batch*> bs;
+  int32_t qpr;
+  int64_t slot;
+};
 struct wsr_comm {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
@@ -1147,13 +1175,89 @@ struct wsr_comm {
   // WSR_HOST_TIMING=1: host time per phase of wsr_shard_step (enqueue only),
   // printed to stderr when the communicator closes
   bool timing = false;
-  uint64_t steps = 0, t_ns[4] = {0, 0, 0, 0};   // run, (unused), rccl, replay
+  uint64_t steps = 0, t_ns[4] = {0, 0, 0, 0};   // run, submit, rccl (worker), replay (worker)
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<XJob> jobs;   // (FIFO)
+  size_t head = 0;
+  bool stop = false;
+  std::atomic<int> err{WSR_OK};   // the worker's first failure, reported by the next call
+  std::string err_msg;
 };
 
 static uint64_t now_ns() {
   return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                    std::chrono::steady_clock::now().time_since_epoch())
                                    .count());
+}
+
+static int step_replay_from(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, const Event* recv,
+                            uint64_t owner_stride, hipStream_t st);
+
+// One job: wait for the group's emissions, one ncclAllToAll of the owners'
+// runs of regions (in the first batch's buffers), the owner replays, and the
+// end event of every batch; then each batch's enqueue count moves (x_join).
+static void run_xjob(wsr_comm* c, const XJob& j) {
+  const int W = c->world;
+  wsr_batch* b0 = j.bs[0];
+  const uint64_t region = (static_cast<uint64_t>(j.qpr) + 1) / 2 + static_cast<uint64_t>(j.slot);
+  const uint64_t run = region * j.bs.size();
+  uint64_t t0 = c->timing ? now_ns() : 0;
+  int rc = WSR_OK;
+  std::string msg;
+  try {
+    HIP_OK(hipSetDevice(c->device));
+    for (wsr_batch* b : j.bs) HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
+    const ncclResult_t r = ncclAllToAll(b0->d_xsend, b0->d_xrecv, run * (sizeof(Event) / sizeof(uint64_t)),
+                                        ncclUint64, c->comm, c->stream);
+    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+  } catch (const std::exception& e) {
+    rc = WSR_E_HIP;
+    msg = e.what();
+  }
+  uint64_t t1 = c->timing ? now_ns() : 0;
+  for (size_t i = 0; i < j.bs.size() && rc == WSR_OK; ++i) {
+    rc = step_replay_from(j.h, j.bs[i], c->rank, W, j.qpr, b0->d_xrecv + region * i, run, c->stream);
+    if (rc) msg = g_err;
+  }
+  for (wsr_batch* b : j.bs) {
+    if (rc == WSR_OK && hipEventRecord(b->xev[1], c->stream) != hipSuccess) {
+      rc = WSR_E_HIP;
+      msg = "hipEventRecord failed";
+    }
+    b->x_pending = true;
+    b->x_enq.fetch_add(1, std::memory_order_release);
+  }
+  if (rc != WSR_OK) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->err.load() == WSR_OK) {
+      c->err_msg = msg;
+      c->err.store(rc);
+    }
+  }
+  if (c->timing) {
+    const uint64_t t2 = now_ns();
+    c->t_ns[2] += t1 - t0;
+    c->t_ns[3] += t2 - t1;
+  }
+}
+
+static void exchange_worker(wsr_comm* c) {
+  for (;;) {
+    XJob j;
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv.wait(lk, [&] { return c->stop || c->head < c->jobs.size(); });
+      if (c->head == c->jobs.size()) return;   // (stop, and drained)
+      j = std::move(c->jobs[c->head++]);
+      if (c->head == c->jobs.size()) {
+        c->jobs.clear();
+        c->head = 0;
+      }
+    }
+    run_xjob(c, j);
+  }
 }
 
 int wsr_comm_unique_id(uint8_t* id) {
@@ -1175,12 +1279,13 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   std::memcpy(&u, id, sizeof u);
   const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
   if (r != ncclSuccess) return fail(WSR_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  // the exchange stream waits on every step's segment kernels: at high
-  // priority it gets a hardware queue of its own, so its waits do not hold up
-  // batch streams that share a queue with it (+3 % on the one-rank rehearsal,
-  // profiles/r02_v_shard_variants.txt; WSR_COMM_PRIORITY=0 turns it off)
+  // exchange stream priority (WSR_COMM_PRIORITY=1: high).  Normal since
+  // round 4: at high priority the owner replays' thousands of one-wave
+  // workgroups are dispatched ahead of the next batches' persistent kernels;
+  // one-rank rehearsal 15.6 -> 16.7 M q/s every query sharded, 12.7 -> 15.4 M
+  // hybrid (profiles/r04g/; round 2 had measured +3 % for high)
   int lo_prio = 0, hi_prio = 0;
-  const bool prio = env_number("WSR_COMM_PRIORITY", 1) != 0 &&
+  const bool prio = env_number("WSR_COMM_PRIORITY", 0) != 0 &&
                     hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
   if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
             : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
@@ -1192,16 +1297,25 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   c->device = device;
   const char* ht = std::getenv("WSR_HOST_TIMING");
   c->timing = ht && *ht && *ht != '0';
+  wsr_comm* cp = c.get();
+  cp->worker = std::thread([cp] { exchange_worker(cp); });
   *out = c.release();
   return WSR_OK;
 }
 
 void wsr_comm_close(wsr_comm* c) {
   if (!c) return;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->stop = true;
+  }
+  c->cv.notify_one();
+  if (c->worker.joinable()) c->worker.join();
   if (c->timing && c->steps)
-    std::fprintf(stderr, "wsr_shard_step host us/step over %llu steps: run %.1f rccl %.1f replay %.1f\n",
+    std::fprintf(stderr, "wsr_shard_step host us/step over %llu steps: run %.1f submit %.1f rccl %.1f replay %.1f "
+                 "(rccl and replay: the exchange worker)\n",
                  static_cast<unsigned long long>(c->steps), c->t_ns[0] / 1e3 / c->steps,
-                 c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps);
+                 c->t_ns[1] / 1e3 / c->steps, c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1261,7 +1375,7 @@ static void ensure_xev(wsr_batch* b) {
 // The exchange buffers of b: send and receive, need events each.
 static void ensure_xbuf(wsr_batch* b, uint64_t need, int W) {
   if (need > b->x_slots || W != b->x_pairs) {
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));
     if (b->d_xsend) HIP_OK(hipFree(b->d_xsend));
     if (b->d_xrecv) HIP_OK(hipFree(b->d_xrecv));
     b->d_xsend = b->d_xrecv = nullptr;
@@ -1328,6 +1442,10 @@ static int step_replay(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_p
 int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c, int32_t q_per_owner,
                     int64_t slot) {
   if (!c || !bs || n < 1) return fail(WSR_E_INVALID, "bad shard_steps arguments");
+  if (const int e = c->err.load()) {   // an earlier exchange of this communicator failed
+    std::lock_guard<std::mutex> g(c->mu);
+    return fail(e, "exchange worker: " + c->err_msg);
+  }
   const int W = c->world;
   for (int i = 0; i < n; ++i)
     if (int rc = check_step(h, bs[i], W, q_per_owner, slot)) return rc;
@@ -1347,36 +1465,25 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
     for (int i = 1; i < n; ++i) {
       ensure_xev(bs[i]);
       // the group's buffers: b0's previous exchange must be done with them
-      if (b0->x_pending) HIP_OK(hipStreamWaitEvent(bs[i]->st, b0->xev[1], 0));
+      if (x_join(b0)) HIP_OK(hipStreamWaitEvent(bs[i]->st, b0->xev[1], 0));
     }
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   for (int i = 0; i < n; ++i) {
     if (int rc = step_emit_into(h, bs[i], W, q_per_owner, slot, b0->d_xsend + region * i, run)) return rc;
+    if (hipEventRecord(bs[i]->xev[0], bs[i]->st) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
   }
   lap(0);
-  try {
-    for (int i = 0; i < n; ++i) {
-      HIP_OK(hipEventRecord(bs[i]->xev[0], bs[i]->st));
-      HIP_OK(hipStreamWaitEvent(c->stream, bs[i]->xev[0], 0));
-    }
-    const ncclResult_t r = ncclAllToAll(b0->d_xsend, b0->d_xrecv, run * (sizeof(Event) / sizeof(uint64_t)),
-                                        ncclUint64, c->comm, c->stream);
-    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
-  } catch (const std::exception& e) {
-    return fail(WSR_E_HIP, e.what());
+  // the exchange half: the communicator's worker thread enqueues it
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    XJob j{h, std::vector<wsr_batch*>(bs, bs + n), q_per_owner, slot};
+    for (int i = 0; i < n; ++i) ++bs[i]->x_req;
+    c->jobs.push_back(std::move(j));
   }
-  lap(2);
-  for (int i = 0; i < n; ++i) {
-    if (int rc = step_replay_from(h, bs[i], c->rank, W, q_per_owner, b0->d_xrecv + region * i, run, c->stream))
-      return rc;
-  }
-  for (int i = 0; i < n; ++i) {
-    if (hipEventRecord(bs[i]->xev[1], c->stream) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
-    bs[i]->x_pending = true;
-  }
-  lap(3);
+  c->cv.notify_one();
+  lap(1);
   c->steps += static_cast<uint64_t>(n);
   return WSR_OK;
 }
@@ -1446,7 +1553,7 @@ int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, w
   try {
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
     if (ctr[kCtrError])
@@ -1508,7 +1615,7 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                                     static_cast<size_t>(kStatStride) * rows);
   try {
     HIP_OK(hipStreamSynchronize(b->st));
-    if (b->x_pending) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
+    if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     HIP_OK(hipMemcpy(out, b->d_stats, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
