@@ -1394,6 +1394,9 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   return __builtin_amdgcn_readlane(x, 63);
 }
 __device__ __forceinline__ uint64_t floor_max(uint64_t x) {
+  // (volatile: the reduction stays inside the caller's refresh branch; the
+  // compiler would otherwise run it speculatively on every driver block)
+  asm volatile("" : "+v"(x));
   const uint32_t hi = wave_max(static_cast<uint32_t>(x >> 32));
   const uint32_t lo = wave_max(static_cast<uint32_t>(x >> 32) == hi ? static_cast<uint32_t>(x) : 0u);
   return (static_cast<uint64_t>(hi) << 32) | lo;
