@@ -336,6 +336,10 @@ int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t wor
 int wsr_shard_step_emit_async(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
                               void* host_send);
 int wsr_batch_stream_sync(wsr_handle* h, wsr_batch* b);
+/* Driver blocks per work item at most for this batch's runs (1..63, default
+ * 63): shorter items cut a batch's latency (its longest item) at some cost in
+ * throughput; the serving front end's batches use WSR_SERVER_ITEM_BLOCKS. */
+int wsr_batch_set_item_blocks(wsr_handle* h, wsr_batch* b, int32_t blocks);
 
 /* Decode one block of a list on the device (test hook for the decoder):
  * out[0..128) receives the block's values (doc ids when which == 0, tf when 1). */

@@ -124,6 +124,7 @@ _sigs = {
     "wsr_shard_steps": (C.c_int, [_P, _P, C.c_int32, _P, C.c_int32, C.c_int64]),
     "wsr_shard_step_emit_async": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_batch_stream_sync": (C.c_int, [_P, _P]),
+    "wsr_batch_set_item_blocks": (C.c_int, [_P, _P, C.c_int32]),
     "wsr_shard_step_regions": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint64)]),
     "wsr_shard_step_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_shard_step_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),

@@ -149,6 +149,7 @@ struct wsr_batch {
   bool has_phrase = false;       // the uploaded queries include a phrase query
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   bool two_only = false;         // every query: two terms (or empty), k <= kMaxK
+  uint32_t seg_cap = kSegCost;   // driver blocks per work item at most (wsr_batch_set_item_blocks)
   int seg_grid = 0;
   int lean_wgs = 0;
   // doc-range shard exchange (wsr_shard_step): per owner a region of {count,
@@ -341,6 +342,7 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.tf8 = h->d_tf8;
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
+    h->args.seg_cap = kSegCost;
     h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
     h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
@@ -835,7 +837,9 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
       fr.x_qpr = se->qpr;
     }
     HIP_OK(hipEventRecord(b->ev[0], st));
-    HIP_OK(launch_plan(h->args, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
+    IndexArgs pa = h->args;   // (the batch's item length)
+    pa.seg_cap = b->seg_cap;
+    HIP_OK(launch_plan(pa, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
                        kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq, b->d_pub, b->d_desc,
                        b->d_part, st));
@@ -1521,6 +1525,12 @@ int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_pe
 int wsr_shard_step_emit_async(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_per_owner, int64_t slot,
                               void* host_send) {
   return shard_step_emit(h, b, world, q_per_owner, slot, host_send, false);
+}
+
+int wsr_batch_set_item_blocks(wsr_handle* h, wsr_batch* b, int32_t blocks) {
+  if (!h || !b || blocks < 1 || blocks > kSegCost) return fail(WSR_E_INVALID, "item blocks must be 1..63");
+  b->seg_cap = static_cast<uint32_t>(blocks);
+  return WSR_OK;
 }
 
 int wsr_batch_stream_sync(wsr_handle* h, wsr_batch* b) {

@@ -28,6 +28,8 @@ struct IndexArgs {
   const uint8_t* tf8;       // their 1-byte tfs (ListDev::tf8)
   uint32_t dense_span;      // bitmaps cover doc ids [doc_lo, doc_lo + dense_span)
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
+  uint32_t seg_cap;         // driver blocks per work item at most (kSegCost; the batch's own, see
+                            // wsr_batch_set_item_blocks: a latency-bound caller takes shorter items)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
   // positions (phrase queries; null unless the engine was opened with them)

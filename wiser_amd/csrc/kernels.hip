@@ -602,6 +602,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     if (nt > 2 && (q.flags & kQueryPhrase)) lean = false;
     if (ok) {
       uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
+      seg = seg > ix.seg_cap ? ix.seg_cap : seg;
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
       // for the per-item setup): the queue hands out heavy items first

@@ -378,8 +378,13 @@ int wsr_server_open(wsr_handle* h, int32_t max_batch, int32_t window_us, wsr_ser
   s->window_ns = static_cast<int64_t>(window_us) * 1000;
   s->ring.reset(new Entry[wsr_server::kRing]);
   if (const char* e = std::getenv("WSR_SERVER_DEPTH")) s->depth = std::max(1, std::min(wsr_server::kSlots, std::atoi(e)));
+  int item_blocks = 63;
+  if (const char* e = std::getenv("WSR_SERVER_ITEM_BLOCKS")) item_blocks = std::max(1, std::min(63, std::atoi(e)));
   for (auto& sl : s->slots) {
     int rc = wsr_batch_create(h, max_batch, WSR_SERVER_MAX_K, &sl.b);
+    // shorter work items: a batch's latency is its longest item's, and the
+    // server's batches are latency-bound (WSR_SERVER_ITEM_BLOCKS)
+    if (rc == WSR_OK) rc = wsr_batch_set_item_blocks(h, sl.b, item_blocks);
     if (rc != WSR_OK) {
       for (auto& x : s->slots)
         if (x.b) wsr_batch_destroy(h, x.b);
