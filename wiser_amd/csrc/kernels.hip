@@ -2600,8 +2600,35 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
           al0 = al0 && s0 > flo0 && (pt_n < k || s0 > kth0);
           al1 = al1 && s1 > flo0 && (pt_n < k || s1 > kth0);
         }
-        if (al0) al0 = phrase_match(ix, qlist, nt, ph, 2 * l);
-        if (al1) al1 = phrase_match(ix, qlist, nt, ph, 2 * l + 1);
+        // the candidates of both halves compacted onto the wave's lanes, one
+        // check each (two passes of divergent position walks become one when
+        // they are at most 64); two-term phrases take the inline check
+        const uint64_t m0 = __ballot(al0), m1 = __ballot(al1);
+        const uint32_t n0 = __popcll(m0), nc = n0 + __popcll(m1);
+        const uint32_t c0 = __popcll(m0 & lanemask_lt()), c1 = n0 + __popcll(m1 & lanemask_lt());
+        bool r0 = false, r1 = false;
+        for (uint32_t base = 0; base < nc; base += 64) {
+          const uint32_t c = base + l;
+          bool ok = false;
+          if (c < nc) {
+            // value of candidate c: the (c)-th set lane of m0 (value 2l), else of m1 (2l + 1)
+            const uint64_t m = c < n0 ? m0 : m1;
+            uint32_t want = c < n0 ? c : c - n0, pos = 0;
+            for (uint32_t step = 32; step; step >>= 1) {   // lowest pos with want + 1 set bits at or below
+              const uint32_t below = __popcll(m & ((2ull << (pos + step - 1)) - 1ull));
+              if (below <= want) pos += step;
+            }
+            const uint32_t v = 2 * pos + (c < n0 ? 0u : 1u);
+            ok = nt == 2 ? phrase_match2(ix, static_cast<uint32_t>(qlist[0]), static_cast<uint32_t>(qlist[1]), ph[v],
+                                         ph[128 + v], ph[256 + v], ph[384 + v])
+                         : phrase_match(ix, qlist, nt, ph, v);
+          }
+          const uint64_t res = __ballot(ok);
+          if (al0 && c0 >= base && c0 < base + 64) r0 = (res >> (c0 - base)) & 1ull;
+          if (al1 && c1 >= base && c1 < base + 64) r1 = (res >> (c1 - base)) & 1ull;
+        }
+        al0 = r0;
+        al1 = r1;
         if (__ballot(al0 || al1) == 0) return;
       }
       n_surv += __popcll(__ballot(al0)) + __popcll(__ballot(al1));
