@@ -772,11 +772,11 @@ def serving_leg(a, idx, qlog, local, threads):
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
     out = {}
-    # (8 clients x 640 / 768 and 6 x 768: the final sweep's best points on the
-    # box's 16-core share, profiles/r03_serve_sweep_final.txt: 5.7 / 6.3 / 5.5 M
-    # q/s at p50 0.90 / 0.91 / 0.82 ms; more client threads oversubscribe the
-    # share beside the dispatcher, the completer and HIP's threads)
-    for clients, depth, window in ((8, 640, 1000), (8, 768, 1000), (6, 768, 1000), (4, 64, 100)):
+    # (8 clients x 640 / 768, 7 x 704 and 6 x 768: around the best points of
+    # the sweeps on the box's 16-core share, profiles/r03_serve_sweep_final.txt,
+    # r04l/serve.jsonl: 5.0-6.3 M q/s at p50 0.9-1.07 ms; more client threads
+    # oversubscribe the share beside the dispatcher, the completer and HIP's)
+    for clients, depth, window in ((8, 640, 1000), (8, 768, 1000), (7, 704, 1000), (6, 768, 1000), (4, 64, 100)):
         srv = w.Server(eng, max_batch=a.batch, window_us=window)
         st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
         srv.close()

@@ -220,7 +220,7 @@ wsr_image_info image_info_of(const HostImage& img, size_t n_c4) {
 }
 
 // the load-time knobs of wsr_open (environment)
-uint32_t dense_div_knob() { return static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 2048)); }
+uint32_t dense_div_knob() { return static_cast<uint32_t>(env_number("WSR_DENSE_DIV", 8192)); }
 uint64_t dense_budget_knob() { return static_cast<uint64_t>(env_number("WSR_DENSE_BUDGET_GB", 48) * 1e9); }
 }  // namespace
 
@@ -286,13 +286,15 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     uint32_t lo = opts ? opts->doc_lo : 0, hi = opts ? opts->doc_hi : 0;
     if (hi == 0) hi = 0xFFFFFFFFu;
     int threads = opts && opts->threads > 0 ? opts->threads : static_cast<int>(std::thread::hardware_concurrency());
-    // dense-list bitmaps: lists with >= span/div postings (WSR_DENSE_DIV, 0 = off);
-    // probed by bitmap when >= ratio x the driver's blocks (WSR_DENSE_RATIO)
-    // (1024: every list that is at least 1/1024 of the doc range -- on the
-    // en-Wikipedia-shaped C3 corpus this halves the mixed batch against 128,
-    // on C2 it is neutral, profiles/r02_d_dense_sweep.txt; WSR_DENSE_BUDGET_GB
-    // caps the bitmaps' HBM, longest lists first: 48 GB, as the 8-byte rank
-    // records put the C3 stand-in's at 33 GB)
+    // probe structures (bitmaps, offset buckets): lists with >= span/div
+    // postings (WSR_DENSE_DIV, 0 = off), probed when >= ratio x the driver's
+    // blocks (WSR_DENSE_RATIO).  8192 since round 4's buckets made a sparse
+    // list's structure cheap (~6 B per posting + 8 B per 256 docs): on the C3
+    // stand-in C5 6.1 -> 10.1 M q/s against 2048 (its phrases' lists become
+    // lean), headline and C4 within 1 %, image 10.1 -> 14.0 GB (16384 and
+    // 32768: C5 the same, headline +0.4 %, 17.6 / 23.0 GB;
+    // profiles/r04k/, r04l/).  WSR_DENSE_BUDGET_GB caps their HBM, longest
+    // lists first (48 GB)
     const uint32_t dense_div = dense_div_knob();
     const uint64_t dense_budget = dense_budget_knob();
     const float dense_ratio = static_cast<float>(env_number("WSR_DENSE_RATIO", 1.0));
@@ -1288,11 +1290,16 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   // workgroups are dispatched ahead of the next batches' persistent kernels;
   // one-rank rehearsal 15.6 -> 16.7 M q/s every query sharded, 12.7 -> 15.4 M
   // hybrid (profiles/r04g/; round 2 had measured +3 % for high)
+  // WSR_COMM_PRIORITY=2: normal priority on a hardware queue of its own (a
+  // stream with a CU mask, every CU set, is not mapped onto the shared
+  // queues), so the exchange stream's waits hold up no batch stream
   int lo_prio = 0, hi_prio = 0;
-  const bool prio = env_number("WSR_COMM_PRIORITY", 0) != 0 &&
-                    hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
-  if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
-            : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+  const int mode = static_cast<int>(env_number("WSR_COMM_PRIORITY", 0));
+  const bool prio = mode == 1 && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+  std::vector<uint32_t> all_cus(16, 0xFFFFFFFFu);   // (bits past the CU count are ignored)
+  if ((mode == 2 ? hipExtStreamCreateWithCUMask(&c->stream, static_cast<uint32_t>(all_cus.size()), all_cus.data())
+       : prio    ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
+                 : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     (void)ncclCommDestroy(c->comm);
     return fail(WSR_E_HIP, "hipStreamCreate failed");
   }
