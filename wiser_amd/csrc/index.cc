@@ -740,14 +740,14 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       const uint64_t p0 = s.rows[0].pos_off;
       const uint64_t npk = total / kPackSize, rem = total % kPackSize;
       std::vector<uint64_t> blob_at(npk + (rem ? 1 : 0));
+      std::vector<uint32_t> width(npk);
       uint64_t pa = p0;
       for (uint64_t k = 0; k < npk; ++k) {
         const uint8_t* b = file + pa;
         if (b + 2 > fend || b[0] != kPackMagic || b[1] < 1 || b[1] > 32)
           throw std::runtime_error("bad position pack in '" + term + "'");
         blob_at[k] = pa;
-        pt.pk.push_back(static_cast<uint32_t>(pa - p0));
-        pt.pk.push_back(b[1]);
+        width[k] = b[1];
         pa += 2 + 16ull * b[1];
       }
       if (rem) {
@@ -765,10 +765,26 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         if (s.rows[r].pos_off != blob_at[e / kPackSize] || s.rows[r].pos_idx != e % kPackSize)
           throw std::runtime_error("skip row position pointer disagrees with the box of '" + term + "'");
       }
-      pt.bytes.assign(file + p0, file + pa);
+      // The image keeps the slice of the box its blocks' bags lie in: packs
+      // [k0, k1) and the VInts remainder when the slice reaches it, entries
+      // renumbered from pack k0 (a doc-range shard holds a fraction of each
+      // box; the whole image keeps all of it)
+      const uint64_t e_lo = cum[r0 * kPackSize], e_hi = cum[std::min<uint64_t>(n, r1 * kPackSize)];
+      const uint64_t k0 = std::min<uint64_t>(e_lo / kPackSize, npk);
+      const uint64_t k1 = std::min<uint64_t>((e_hi + kPackSize - 1) / kPackSize, npk);
+      const bool with_tail = rem && e_hi > npk * kPackSize;
+      const uint64_t b_lo = k0 < blob_at.size() ? blob_at[k0] : pa;
+      const uint64_t b_hi = k1 < blob_at.size() ? blob_at[k1] : pa;
+      for (uint64_t k = k0; k < k1; ++k) {
+        pt.pk.push_back(static_cast<uint32_t>(blob_at[k] - b_lo));
+        pt.pk.push_back(width[k]);
+      }
+      if (!with_tail) pt.tail.clear();
+      pt.bytes.assign(file + b_lo, file + std::max(b_lo, b_hi));
+      const uint64_t e0 = k0 * kPackSize;
       for (uint64_t r = r0; r < r1; ++r)
         for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
-          img.pos_start[(ld.blk0 + r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i]);
+          img.pos_start[(ld.blk0 + r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i] - e0);
     }
     if (with_blm) {
       // The list's two bloom sections (flash_engine_dumper.h:620-646): the 8
