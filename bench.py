@@ -544,6 +544,12 @@ def extra_legs(a, idx, qlog, local, threads):
         return not chosen or name in chosen
 
     c2_idx = None
+    # serving first: its closed loop of host threads is the leg most sensitive
+    # to what earlier legs left in the process (in a fresh process the same
+    # points run 20-40 % faster than after the others, profiles/r04m_bench.json
+    # against r04n/serve_points.jsonl)
+    if want("serving"):
+        legs["serving"] = serving_leg(a, idx, qlog, local, threads)
     if want("c2_synthetic_1m") and not (a.workload == "c2" and not (a.vacuum_dir or a.linedoc)):
         legs["c2_synthetic_1m"] = c2_leg(a, local, threads)
     if want("end_to_end"):
@@ -589,8 +595,6 @@ def extra_legs(a, idx, qlog, local, threads):
         eng.close()
     if want("c3_topics") and a.workload == "c3" and not (a.vacuum_dir or a.linedoc):
         legs["c3_topics"] = topics_leg(a, local, threads)
-    if want("serving"):
-        legs["serving"] = serving_leg(a, idx, qlog, local, threads)
     if want("c1_snippets"):
         legs["c1_snippets"] = snippet_leg(a, local, threads)
     del c2_idx
@@ -772,11 +776,11 @@ def serving_leg(a, idx, qlog, local, threads):
     for i, t in enumerate(lines):
         arr[i] = eng.resolve(w.SearchQuery(t, n_results=a.k))[0]
     out = {}
-    # (8 clients x 640 / 768, 7 x 704 and 6 x 768: around the best points of
-    # the sweeps on the box's 16-core share, profiles/r03_serve_sweep_final.txt,
-    # r04l/serve.jsonl: 5.0-6.3 M q/s at p50 0.9-1.07 ms; more client threads
+    # (7 x 704, 6 x 768, 5 x 960 and 8 x 640 in flight: around the best points
+    # of the sweeps on the box's 16-core share, profiles/r04n/serve_points.jsonl:
+    # 6.1 / 5.2 / 5.1 M q/s at p50 0.85 / 0.88 / 0.94 ms; more client threads
     # oversubscribe the share beside the dispatcher, the completer and HIP's)
-    for clients, depth, window in ((8, 640, 1000), (8, 768, 1000), (7, 704, 1000), (6, 768, 1000), (4, 64, 100)):
+    for clients, depth, window in ((7, 704, 1000), (6, 768, 1000), (5, 960, 1000), (8, 640, 1000), (4, 64, 100)):
         srv = w.Server(eng, max_batch=a.batch, window_us=window)
         st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
         srv.close()

@@ -31,5 +31,3 @@ run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
 run hyb_g4 X=1 -- --shard-group 4
 run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
 run hyb_g8 X=1 -- --shard-group 8
-run hb0_g4_own WSR_COMM_PRIORITY=2 -- --heavy-blocks 0 --shard-group 4
-run hyb_g4_own WSR_COMM_PRIORITY=2 -- --shard-group 4

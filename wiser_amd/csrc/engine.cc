@@ -1290,16 +1290,14 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   // workgroups are dispatched ahead of the next batches' persistent kernels;
   // one-rank rehearsal 15.6 -> 16.7 M q/s every query sharded, 12.7 -> 15.4 M
   // hybrid (profiles/r04g/; round 2 had measured +3 % for high)
-  // WSR_COMM_PRIORITY=2: normal priority on a hardware queue of its own (a
-  // stream with a CU mask, every CU set, is not mapped onto the shared
-  // queues), so the exchange stream's waits hold up no batch stream
+  // (a stream with a full CU mask, i.e. a hardware queue of its own at normal
+  // priority, was slower again: 16.5 / 14.2 M against 17.0 / 15.6 M,
+  // profiles/r04n/)
   int lo_prio = 0, hi_prio = 0;
-  const int mode = static_cast<int>(env_number("WSR_COMM_PRIORITY", 0));
-  const bool prio = mode == 1 && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
-  std::vector<uint32_t> all_cus(16, 0xFFFFFFFFu);   // (bits past the CU count are ignored)
-  if ((mode == 2 ? hipExtStreamCreateWithCUMask(&c->stream, static_cast<uint32_t>(all_cus.size()), all_cus.data())
-       : prio    ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
-                 : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+  const bool prio = env_number("WSR_COMM_PRIORITY", 0) != 0 &&
+                    hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+  if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
+            : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     (void)ncclCommDestroy(c->comm);
     return fail(WSR_E_HIP, "hipStreamCreate failed");
   }
