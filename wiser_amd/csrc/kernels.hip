@@ -2796,7 +2796,6 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
 // g * stride + offset.
 // kWide: the queries with k > kMaxK, heap in LDS (a separate instance, so the
 // common one reserves no LDS for it).
-constexpr int kOwnerReplayWgs = 1024;
 template <bool kWide>
 __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
                                                                int n_shards, const int32_t* __restrict__ meta,
@@ -2805,13 +2804,11 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
                                                                HitDev* __restrict__ hits, int hit_stride,
                                                                int32_t* __restrict__ n_hits,
                                                                uint32_t* __restrict__ counters) {
-  // (a grid of at most kOwnerReplayWgs one-wave workgroups, each looping over
-  // queries: one workgroup per query flooded the dispatcher with thousands of
-  // tiny workgroups ahead of the next batches' persistent grids)
-  for (int qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
   const int gq = q0 + qi;
   const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
-  if ((k > static_cast<uint32_t>(kMaxK)) != kWide) continue;
+  if ((k > static_cast<uint32_t>(kMaxK)) != kWide) return;
   const uint32_t l = threadIdx.x & 63;
   auto meta_of = [&](uint32_t g) { return meta + g * meta_stride + 2ull * static_cast<uint32_t>(qi); };
   for (uint32_t g = l; g < static_cast<uint32_t>(n_shards); g += 64)   // (up to kMaxOwners shards)
@@ -2835,7 +2832,6 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
-  }
   }
 }
 
@@ -2915,11 +2911,10 @@ hipError_t launch_owner_replay_meta(const QueryIn* q, int q0, int nq, int n_shar
                                     int hit_stride, int32_t* n_hits, uint32_t* counters, bool any_wide,
                                     hipStream_t st) {
   if (nq <= 0) return hipSuccess;
-  const dim3 g(static_cast<unsigned>(std::min(nq, kOwnerReplayWgs)));
-  hipLaunchKernelGGL(owner_replay_meta_kernel<false>, g, dim3(64), 0, st, q, q0, nq, n_shards, meta,
+  hipLaunchKernelGGL(owner_replay_meta_kernel<false>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
                      meta_stride, stride, recv, hits, hit_stride, n_hits, counters);
   if (any_wide)
-    hipLaunchKernelGGL(owner_replay_meta_kernel<true>, g, dim3(64), 0, st, q, q0, nq, n_shards, meta,
+    hipLaunchKernelGGL(owner_replay_meta_kernel<true>, dim3(nq), dim3(64), 0, st, q, q0, nq, n_shards, meta,
                        meta_stride, stride, recv, hits, hit_stride, n_hits, counters);
   return hipGetLastError();
 }
