@@ -1,7 +1,7 @@
 #!/bin/bash
 # One-rank RCCL rehearsal of the sharded forms under several settings (A/B of
 # the exchange stream's priority and the step-group size), with host phase
-# timers.  Every GPU step has its own limit; the first failure ends the
+# timers (SET=queues: the hardware-queue count instead).  Every GPU step has its own limit; the first failure ends the
 # script.  Usage: TAG
 set -eu -o pipefail
 TAG=$1
@@ -23,11 +23,22 @@ print(sys.argv[2], "value", d["value"], "ms/step", d["ms_per_step"], "host", d.g
 PY
   grep -h "wsr_shard_step host" "$O/$name.err" || true
 }
-run replica X=1 -- --mode replica
-run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
-run hb0_g4_noprio WSR_COMM_PRIORITY=0 -- --heavy-blocks 0 --shard-group 4
-run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
-run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
-run hyb_g4 X=1 -- --shard-group 4
-run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
-run hyb_g8 X=1 -- --shard-group 8
+case "${SET:-default}" in
+queues)   # hardware queues per process (HIP's default 4): do barrier packets of
+          # cross-stream waits in shared queues serialise the batches?
+  for q in 4 8 16; do
+    run replica_q$q GPU_MAX_HW_QUEUES=$q -- --mode replica
+    run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
+    run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
+  done ;;
+*)
+  run replica X=1 -- --mode replica
+  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g4_noprio WSR_COMM_PRIORITY=0 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
+  run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
+  run hyb_g4 X=1 -- --shard-group 4
+  run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
+  run hyb_g8 X=1 -- --shard-group 8
+  ;;
+esac
