@@ -1,7 +1,7 @@
 #!/bin/bash
 # One-rank RCCL rehearsal of the sharded forms under several settings (A/B of
 # the exchange stream's priority and the step-group size), with host phase
-# timers (SET=queues: the hardware-queue count instead).  Every GPU step has its own limit; the first failure ends the
+# timers (SET=queues: the hardware-queue count instead; SET=variants VARIANTS="a b": diagnostic builds).  Every GPU step has its own limit; the first failure ends the
 # script.  Usage: TAG
 set -eu -o pipefail
 TAG=$1
@@ -30,6 +30,12 @@ queues)   # hardware queues per process (HIP's default 4): do barrier packets of
     run replica_q$q GPU_MAX_HW_QUEUES=$q -- --mode replica
     run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
     run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
+  done ;;
+variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
+  run replica X=1 -- --mode replica
+  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
+  for v in ${VARIANTS:-}; do
+    run hb0_g4_$v WISER_HIP_LIB=$R/wiser_amd/_lib/variants/$v.so -- --heavy-blocks 0 --shard-group 4 --check 0
   done ;;
 *)
   run replica X=1 -- --mode replica
