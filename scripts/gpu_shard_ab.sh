@@ -21,7 +21,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[2], "value", d["value"], "ms/step", d["ms_per_step"], "host", d.get("host_enqueue_ms_per_step"))
 PY
-  grep -h "wsr_shard_step host" "$O/$name.err" || true
+  grep -h "wsr_shard_step host\|wsr_comm exchange stream" "$O/$name.err" || true
 }
 case "${SET:-default}" in
 queues)   # hardware queues per process (HIP's default 4): do barrier packets of
@@ -31,6 +31,11 @@ queues)   # hardware queues per process (HIP's default 4): do barrier packets of
     run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
     run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
   done ;;
+prio)   # the exchange stream's priority: low against normal
+  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g4_low WSR_COMM_PRIORITY=low -- --heavy-blocks 0 --shard-group 4
+  run hyb_g4 X=1 -- --shard-group 4
+  run hyb_g4_low WSR_COMM_PRIORITY=low -- --shard-group 4 ;;
 variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
@@ -40,11 +45,11 @@ variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
 *)
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
-  run hb0_g4_noprio WSR_COMM_PRIORITY=0 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g4_noprio WSR_COMM_PRIORITY=normal -- --heavy-blocks 0 --shard-group 4
   run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
   run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
   run hyb_g4 X=1 -- --shard-group 4
-  run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
+  run hyb_g4_noprio WSR_COMM_PRIORITY=normal -- --shard-group 4
   run hyb_g8 X=1 -- --shard-group 8
   ;;
 esac
