@@ -31,11 +31,6 @@ queues)   # hardware queues per process (HIP's default 4): do barrier packets of
     run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
     run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
   done ;;
-prio)   # the exchange stream's priority: low against normal
-  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
-  run hb0_g4_low WSR_COMM_PRIORITY=low -- --heavy-blocks 0 --shard-group 4
-  run hyb_g4 X=1 -- --shard-group 4
-  run hyb_g4_low WSR_COMM_PRIORITY=low -- --shard-group 4 ;;
 variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
@@ -45,11 +40,11 @@ variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
 *)
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
-  run hb0_g4_noprio WSR_COMM_PRIORITY=normal -- --heavy-blocks 0 --shard-group 4
+  run hb0_g4_noprio WSR_COMM_PRIORITY=0 -- --heavy-blocks 0 --shard-group 4
   run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
   run hb0_g1 X=1 -- --heavy-blocks 0 --shard-group 1
   run hyb_g4 X=1 -- --shard-group 4
-  run hyb_g4_noprio WSR_COMM_PRIORITY=normal -- --shard-group 4
+  run hyb_g4_noprio WSR_COMM_PRIORITY=0 -- --shard-group 4
   run hyb_g8 X=1 -- --shard-group 8
   ;;
 esac

@@ -1285,21 +1285,19 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   std::memcpy(&u, id, sizeof u);
   const ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
   if (r != ncclSuccess) return fail(WSR_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  // exchange stream priority (WSR_COMM_PRIORITY: "high" or 1, "low", else
-  // normal).  Normal since round 4: at high priority the owner replays'
-  // thousands of one-wave workgroups are dispatched ahead of the next
-  // batches' persistent kernels; one-rank rehearsal 15.6 -> 16.7 M q/s every
-  // query sharded, 12.7 -> 15.4 M hybrid (profiles/r04g/; round 2 had
-  // measured +3 % for high)
+  // exchange stream priority (WSR_COMM_PRIORITY=1: high).  Normal since
+  // round 4: at high priority the owner replays' thousands of one-wave
+  // workgroups are dispatched ahead of the next batches' persistent kernels;
+  // one-rank rehearsal 15.6 -> 16.7 M q/s every query sharded, 12.7 -> 15.4 M
+  // hybrid (profiles/r04g/; round 2 had measured +3 % for high)
   // (a stream with a full CU mask, i.e. a hardware queue of its own at normal
   // priority, was slower again: 16.5 / 14.2 M against 17.0 / 15.6 M,
-  // profiles/r04n/)
-  const char* pv = std::getenv("WSR_COMM_PRIORITY");
-  const std::string pname = pv ? pv : "";
-  const int want = (pname == "high" || pname == "1") ? 1 : pname == "low" ? -1 : 0;
+  // profiles/r04n/; low priority was slower still: 16.3 / 12.9 M against
+  // 16.7 / 15.3 M, profiles/r04s/)
   int lo_prio = 0, hi_prio = 0;
-  const bool prio = want != 0 && hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
-  if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, want > 0 ? hi_prio : lo_prio)
+  const bool prio = env_number("WSR_COMM_PRIORITY", 0) != 0 &&
+                    hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) == hipSuccess;
+  if ((prio ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_prio)
             : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
     (void)ncclCommDestroy(c->comm);
     return fail(WSR_E_HIP, "hipStreamCreate failed");
@@ -1309,9 +1307,6 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   c->device = device;
   const char* ht = std::getenv("WSR_HOST_TIMING");
   c->timing = ht && *ht && *ht != '0';
-  if (c->timing)
-    std::fprintf(stderr, "wsr_comm exchange stream priority %s (range %d..%d)\n",
-                 prio ? (want > 0 ? "high" : "low") : "normal", lo_prio, hi_prio);
   wsr_comm* cp = c.get();
   cp->worker = std::thread([cp] { exchange_worker(cp); });
   *out = c.release();
