@@ -928,14 +928,20 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
             every = int(ev.item())
     every = max(1, min(every, nb))
     # every rank builds the same global heavy batches from the same log split
+    # One shape for every heavy batch (q_per_owner = the largest heavy batch,
+    # the rest padded with empty queries): --shard-group batches go through one
+    # all-to-all only when their shapes agree (every rank computes the same
+    # split of the same log, so the shape is common).
+    heavy_parts = {j: [sum((heavy_of(jj, g) for jj in range(j, min(nb, j + every))), []) for g in range(world)]
+                   for j in range(0, nb, every)}
+    hq_all = max((len(p) for parts in heavy_parts.values() for p in parts), default=0)
     steps = []   # per batch index: (heavy ResidentBatch or None, q_per_owner, heavy chunk,
                  #                   cheap ResidentBatch or None, cheap chunk)
     for j in range(nb):
         hb, hq, hchunk = None, 0, []
         if j % every == 0:
-            group = range(j, min(nb, j + every))
-            parts = [sum((heavy_of(jj, g) for jj in group), []) for g in range(world)]
-            hq = max(len(p) for p in parts)
+            parts = heavy_parts[j]
+            hq = hq_all if any(parts) else 0
             if hq:
                 for p in parts:
                     hchunk += p + [[]] * (hq - len(p))   # (an empty query: an empty result)

@@ -31,12 +31,12 @@ queues)   # hardware queues per process (HIP's default 4): do barrier packets of
     run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
     run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
   done ;;
-hostwait)   # the exchange worker waits for the group's emissions on the host
-  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
-  run hb0_g4_hw WSR_XCHG_HOST_WAIT=1 -- --heavy-blocks 0 --shard-group 4
+hyb)   # the hybrid's step groups and heavy-batch cadence
+  run replica X=1 -- --mode replica
+  run hyb_g1 X=1 -- --shard-group 1
   run hyb_g4 X=1 -- --shard-group 4
-  run hyb_g4_hw WSR_XCHG_HOST_WAIT=1 -- --shard-group 4
-  run hyb_g8_hw WSR_XCHG_HOST_WAIT=1 -- --shard-group 8 ;;
+  run hyb_g8 X=1 -- --shard-group 8
+  run hyb_g4_e4 X=1 -- --shard-group 4 --shard-every 4 ;;
 variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
