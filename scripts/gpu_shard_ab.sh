@@ -36,7 +36,10 @@ hyb)   # the hybrid's step groups and heavy-batch cadence
   run hyb_g1 X=1 -- --shard-group 1
   run hyb_g4 X=1 -- --shard-group 4
   run hyb_g8 X=1 -- --shard-group 8
-  run hyb_g4_e4 X=1 -- --shard-group 4 --shard-every 4 ;;
+  run hyb_g4_e4 X=1 -- --shard-group 4 --shard-every 4
+  run hyb_g8_e4 X=1 -- --shard-group 8 --shard-every 4
+  run hyb_g4_e8 X=1 -- --shard-group 4 --shard-every 8
+  run hyb_g2_e8 X=1 -- --shard-group 2 --shard-every 8 ;;
 variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4

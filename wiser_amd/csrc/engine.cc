@@ -1181,9 +1181,7 @@ struct wsr_comm {
   // WSR_HOST_TIMING=1: host time per phase of wsr_shard_step (enqueue only),
   // printed to stderr when the communicator closes
   bool timing = false;
-  // run, submit, rccl (worker), replay (worker), host wait (worker)
-  uint64_t steps = 0, t_ns[5] = {0, 0, 0, 0, 0};
-  bool host_wait = false;   // WSR_XCHG_HOST_WAIT=1: the worker waits for the group's emissions on the host
+  uint64_t steps = 0, t_ns[4] = {0, 0, 0, 0};   // run, submit, rccl (worker), replay (worker)
   std::thread worker;
   std::mutex mu;
   std::condition_variable cv;
@@ -1211,17 +1209,17 @@ static void run_xjob(wsr_comm* c, const XJob& j) {
   wsr_batch* b0 = j.bs[0];
   const uint64_t region = (static_cast<uint64_t>(j.qpr) + 1) / 2 + static_cast<uint64_t>(j.slot);
   const uint64_t run = region * j.bs.size();
-  uint64_t tw = c->timing ? now_ns() : 0, t0 = tw;
+  uint64_t t0 = c->timing ? now_ns() : 0;
   int rc = WSR_OK;
   std::string msg;
   try {
     HIP_OK(hipSetDevice(c->device));
-    if (c->host_wait) {
-      for (wsr_batch* b : j.bs) HIP_OK(hipEventSynchronize(b->xev[0]));
-      if (c->timing) t0 = now_ns();
-    } else {
-      for (wsr_batch* b : j.bs) HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
-    }
+    // (the device waits for the emissions, not this thread: waiting on the
+    // host first makes the collective's own call short, 2-8 us, but the loop
+    // no faster -- the enqueueing thread is held by full hardware queues
+    // either way, and the exchange starts later: 16.8 -> 15.3 M q/s every
+    // query sharded, profiles/r04t/)
+    for (wsr_batch* b : j.bs) HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
     const ncclResult_t r = ncclAllToAll(b0->d_xsend, b0->d_xrecv, run * (sizeof(Event) / sizeof(uint64_t)),
                                         ncclUint64, c->comm, c->stream);
     if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
@@ -1253,7 +1251,6 @@ static void run_xjob(wsr_comm* c, const XJob& j) {
     const uint64_t t2 = now_ns();
     c->t_ns[2] += t1 - t0;
     c->t_ns[3] += t2 - t1;
-    c->t_ns[4] += t0 - tw;
   }
 }
 
@@ -1315,7 +1312,6 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   c->device = device;
   const char* ht = std::getenv("WSR_HOST_TIMING");
   c->timing = ht && *ht && *ht != '0';
-  c->host_wait = env_number("WSR_XCHG_HOST_WAIT", 0) != 0;
   wsr_comm* cp = c.get();
   cp->worker = std::thread([cp] { exchange_worker(cp); });
   *out = c.release();
@@ -1332,10 +1328,9 @@ void wsr_comm_close(wsr_comm* c) {
   if (c->worker.joinable()) c->worker.join();
   if (c->timing && c->steps)
     std::fprintf(stderr, "wsr_shard_step host us/step over %llu steps: run %.1f submit %.1f rccl %.1f replay %.1f "
-                 "wait %.1f (rccl, replay and wait: the exchange worker)\n",
+                 "(rccl and replay: the exchange worker)\n",
                  static_cast<unsigned long long>(c->steps), c->t_ns[0] / 1e3 / c->steps,
-                 c->t_ns[1] / 1e3 / c->steps, c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps,
-                 c->t_ns[4] / 1e3 / c->steps);
+                 c->t_ns[1] / 1e3 / c->steps, c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
