@@ -913,15 +913,17 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     # (its own plan and segment launches, the RCCL call, the owner replay), so
     # with few heavy queries per step (0.7 % of the log at N = 8) a step per
     # batch makes the loop host-bound (profiles/r02_sm_shard_every.txt: 0.22 ms
-    # of host time per 0.15 ms step); grouped, heavy batches keep ~1024 queries
-    # per rank and the light batches run every step.
+    # of host time per 0.15 ms step); grouped, heavy batches keep ~4096 queries
+    # per rank (a whole batch; one-rank hybrid rehearsal, C3: 16.3 M q/s at
+    # ~1024 per heavy batch, 18.0 M at ~4096, profiles/r04v/) and the light
+    # batches run every step.
     def heavy_of(j, g):
         chunk = lines[g * per_rank + j * B: g * per_rank + (j + 1) * B]
         return [q for q in chunk if is_heavy(q)]
     every = a.shard_every
     if every <= 0:
         per_step = max(1, sum(len(heavy_of(j, rank)) for j in range(nb)) // nb)
-        every = max(1, min(nb, -(-1024 // per_step)))
+        every = max(1, min(nb, -(-4096 // per_step)))
         if dist is not None:   # one cadence for every rank (the collective pairs up)
             ev = torch.tensor([float(every)])
             dist.all_reduce(ev, op=dist.ReduceOp.MAX)

@@ -307,12 +307,19 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
 void wsr_comm_close(wsr_comm* c);
 int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner, int64_t slot);
 /* A step group: n batches of world * q_per_owner queries each, every one
- * emitted into its region of each owner's run of n regions (in the first
- * batch's exchange buffers), then ONE ncclAllToAll of the runs and the n owner
- * replays.  The same results as n wsr_shard_step calls, with one collective's
- * host cost instead of n. */
+ * emitted into its region of each owner's run of n regions (in one of the
+ * communicator's exchange buffer sets), then ONE ncclAllToAll of the runs and
+ * the n owner replays.  The same results as n wsr_shard_step calls, with one
+ * collective's host cost instead of n.  The owner replays are deferred by
+ * default (WSR_REPLAY_DEFER=0: not) into the lean kernels of the step group
+ * two groups later; a fetch, wsr_batch_ready or the batch's next run enqueues
+ * a still-pending one first.  The communicator's calls (steps, flush, and the
+ * joins of its batches) come from one thread. */
 int wsr_shard_steps(wsr_handle* h, wsr_batch* const* b, int32_t n, wsr_comm* c, int32_t q_per_owner,
                     int64_t slot);
+/* enqueue every deferred owner replay of the communicator (before timing the
+ * whole job on a device synchronize, or closing) */
+int wsr_comm_flush(wsr_comm* c);
 /* wsr_shard_step's two device halves with the transfer left to the caller (a
  * multi-rank rehearsal on one GPU, where RCCL refuses two ranks, or a host
  * exchange): the engine's own region buffers, in the exact layout the step's

@@ -31,15 +31,14 @@ queues)   # hardware queues per process (HIP's default 4): do barrier packets of
     run hb0_g4_q$q GPU_MAX_HW_QUEUES=$q -- --heavy-blocks 0 --shard-group 4
     run hyb_g4_q$q GPU_MAX_HW_QUEUES=$q -- --shard-group 4
   done ;;
-hyb)   # the hybrid's step groups and heavy-batch cadence
+defer)   # owner replays deferred into later lean kernels (default) or not
   run replica X=1 -- --mode replica
-  run hyb_g1 X=1 -- --shard-group 1
+  run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g4_nodefer WSR_REPLAY_DEFER=0 -- --heavy-blocks 0 --shard-group 4
+  run hb0_g8 X=1 -- --heavy-blocks 0 --shard-group 8
   run hyb_g4 X=1 -- --shard-group 4
-  run hyb_g8 X=1 -- --shard-group 8
-  run hyb_g4_e4 X=1 -- --shard-group 4 --shard-every 4
-  run hyb_g8_e4 X=1 -- --shard-group 8 --shard-every 4
-  run hyb_g4_e8 X=1 -- --shard-group 4 --shard-every 8
-  run hyb_g2_e8 X=1 -- --shard-group 2 --shard-every 8 ;;
+  run hyb_g4_nodefer WSR_REPLAY_DEFER=0 -- --shard-group 4
+  run hyb_g2 X=1 -- --shard-group 2 ;;
 variants)   # diagnostic builds (scripts/build_variant.py), parity unchecked
   run replica X=1 -- --mode replica
   run hb0_g4 X=1 -- --heavy-blocks 0 --shard-group 4

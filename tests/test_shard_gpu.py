@@ -206,6 +206,60 @@ def test_native_rccl_step_groups(synth_small):
     S.close()
 
 
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_native_rccl_deferred_replay(synth_small, monkeypatch, defer):
+    """Owner replays deferred into later groups' lean kernels (the default)
+    and not (WSR_REPLAY_DEFER=0): 14 step groups of changing size over five
+    batches -- one of k = 100, whose replay needs the LDS heap and so is never
+    deferred -- more groups than exchange buffer sets, batches stepped again
+    while their replay is pending; then a flush and every fetch.  Equal to the
+    oracle."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import NativeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    monkeypatch.setenv("WSR_REPLAY_DEFER", defer)
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_defer.log")
+    w.gen_two_term_log(d, log, n_queries=1280, seed=23)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    S = NativeShardedSearcher(d, 0, 1, share_id=lambda x: x)
+    eng = S.engine
+    n = 256
+    ks = [10, 10, 10, 10, 100]
+    parts = [qs[i * n:(i + 1) * n] for i in range(5)]
+    bs = []
+    for part, k in zip(parts, ks):
+        arr = (_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=k))[0] for q in part])
+        b = w.ResidentBatch(eng, n, k)
+        b.upload(arr)
+        bs.append(b)
+    o = OracleVacuum(d)
+    exp = [[o.search(q, k)[0] for q in part] for part, k in zip(parts, ks)]
+    groups = [[0, 1], [2, 3], [4], [0, 1, 2], [3, 4], [1], [2, 0], [4, 3, 1], [0], [1, 2, 3, 4], [0, 4], [2],
+              [3], [1, 0]]
+    for g in groups:
+        S.steps([bs[i] for i in g], n, 64 * n)
+    S.flush()
+    w.sync(eng)
+    for b, e, k in zip(bs, exp, ks):
+        hits, nh = S.fetch_owned(b, n)
+        got = [[(hits[i * b.stride + j].doc_id, hits[i * b.stride + j].score) for j in range(nh[i])]
+               for i in range(n)]
+        assert got == e
+    # again, fetched straight after the steps (the fetch enqueues what is pending)
+    for g in groups[:5]:
+        S.steps([bs[i] for i in g], n, 64 * n)
+    for b, e in zip(bs, exp):
+        hits, nh = S.fetch_owned(b, n)
+        got = [[(hits[i * b.stride + j].doc_id, hits[i * b.stride + j].score) for j in range(nh[i])]
+               for i in range(n)]
+        assert got == e
+    for b in bs:
+        b.close()
+    S.close()
+
+
 def test_host_exchange_pipelined(synth_small):
     """HostExchangeShardedSearcher (the gloo rehearsal's searcher): each step
     enqueues its emission and then finishes the step before it (exchange,

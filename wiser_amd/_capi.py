@@ -120,6 +120,7 @@ _sigs = {
     "wsr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_close": (None, [_P]),
+    "wsr_comm_flush": (C.c_int, [_P]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
     "wsr_shard_steps": (C.c_int, [_P, _P, C.c_int32, _P, C.c_int32, C.c_int64]),
     "wsr_shard_step_emit_async": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),

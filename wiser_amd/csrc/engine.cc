@@ -13,6 +13,7 @@
 #include <cstring>
 #include <memory>
 #include <cstdlib>
+#include <deque>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -166,6 +167,9 @@ struct wsr_batch {
   // they agree (x_join)
   uint64_t x_req = 0;
   std::atomic<uint64_t> x_enq{0};
+  // a step group's owner replay of this batch deferred (wsr_shard_steps) and
+  // not yet enqueued: x_join has x_comm enqueue it first
+  wsr_comm* x_comm = nullptr;
   bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
   int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
   int64_t x_slot = 0;           //     and slot (the replay half must match them)
@@ -185,10 +189,13 @@ struct wsr_batch {
   hipEvent_t fork = nullptr, join = nullptr;
   bool ran = false;
 };
-// Is a shard step's exchange of b outstanding?  First wait until the
-// communicator's worker has enqueued every exchange asked of it for b, so
-// that xev[1] is the record to wait on.
+static void replay_flush(wsr_comm* c, const wsr_batch* upto);
+// Is a shard step's exchange of b outstanding?  First wait until every
+// exchange and owner replay asked for b is enqueued (by the communicator's
+// worker, or, deferred, by a later step group: enqueued now if still
+// pending), so that xev[1] is the record to wait on.
 static bool x_join(wsr_batch* b) {
+  if (b->x_comm) replay_flush(b->x_comm, b);
   while (b->x_enq.load(std::memory_order_acquire) != b->x_req) std::this_thread::yield();
   return b->x_pending;
 }
@@ -807,7 +814,7 @@ struct ShardEmit {
   uint64_t meta_stride;
 };
 
-static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se = nullptr);
+static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se = nullptr, const OwnerJob* oj = nullptr);
 
 
 int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
@@ -816,8 +823,9 @@ int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
 // two streams; the worker that finishes a query's last item replays it
 // (se == nullptr) or emits its reduced events into the owner's exchange
 // region (a shard step).  Wide queries (k > kMaxK) of a plain run are
-// replayed by one more launch after the segments.
-static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
+// replayed by one more launch after the segments.  oj: an earlier step
+// group's owner replay for the lean kernel's tail (its exchange is done).
+static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const OwnerJob* oj) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   try {
     HIP_OK(hipSetDevice(h->device));
@@ -837,6 +845,10 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se) {
       fr.x_stride = se->stride;
       fr.x_meta_stride = se->meta_stride;
       fr.x_qpr = se->qpr;
+    }
+    if (oj) {
+      fr.oj = *oj;
+      fr.oj.claim = b->d_ctr + kCtrReplay;   // (zeroed above)
     }
     HIP_OK(hipEventRecord(b->ev[0], st));
     IndexArgs pa = h->args;   // (the batch's item length)
@@ -1168,11 +1180,38 @@ int wsr_batch_stream(wsr_handle* h, wsr_batch* b, void** stream) {
 // hybrid rehearsal, the loop host-bound, profiles/r04g/), and the caller's
 // next batches must not wait behind it.  Jobs run in submission order, so
 // every rank issues its collectives in the same order.
-struct XJob {
+//
+// A group's owner replays are deferred (WSR_REPLAY_DEFER, default 1) into the
+// lean kernels of the step group kReplayLag groups later: each of its
+// batches' lean kernel, its own items done, replays one batch of the earlier
+// group (OwnerJob).  A separate owner replay launch -- thousands of one-wave,
+// latency-bound workgroups per batch beside the persistent lean kernels --
+// cost more than its work (one-rank rehearsal 16.8 M q/s with it, 20.9 M with
+// the replay dropped, profiles/r04r/).  Whatever needs a deferred replay's
+// results first (a fetch, the batch's next run, wsr_comm_flush) enqueues it
+// on the communicator's stream instead (replay_flush).
+struct XGroup {
   wsr_handle* h;
   std::vector<wsr_batch*> bs;
   int32_t qpr;
   int64_t slot;
+  int xs;                              // its exchange buffers: c->xs[xs]
+  bool defer;
+  std::vector<hipEvent_t> wait_done;   // the slot's previous replays (before the all-to-all)
+  std::vector<uint8_t> queued;         // deferred: bs[i]'s replay enqueued
+  std::atomic<bool> enq{false};        // the worker has enqueued the all-to-all (and, not deferred, the replays)
+};
+using XJob = std::shared_ptr<XGroup>;
+constexpr int kXSlots = 4;       // exchange buffer sets in rotation
+constexpr size_t kReplayLag = 2;  // groups between a group's exchange and its deferred replays
+struct XSlot {
+  Event* send = nullptr;
+  Event* recv = nullptr;
+  uint64_t events = 0;
+  hipEvent_t xa = nullptr;            // the last all-to-all out of this slot done (comm stream)
+  std::vector<hipEvent_t> done;       // its group's owner replays done, one per batch
+  size_t n_done = 0;                  // (recorded)
+  std::shared_ptr<XGroup> last;       // the group that used it last
 };
 struct wsr_comm {
   ncclComm_t comm = nullptr;
@@ -1190,7 +1229,19 @@ struct wsr_comm {
   bool stop = false;
   std::atomic<int> err{WSR_OK};   // the worker's first failure, reported by the next call
   std::string err_msg;
+  XSlot xs[kXSlots];
+  uint64_t n_groups = 0;
+  bool defer = true;
+  std::deque<std::shared_ptr<XGroup>> pend;   // deferred groups, oldest first (the calling thread's)
 };
+
+static void set_comm_err(wsr_comm* c, int rc, const std::string& msg) {
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->err.load() == WSR_OK) {
+    c->err_msg = msg;
+    c->err.store(rc);
+  }
+}
 
 static uint64_t now_ns() {
   return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -1201,12 +1252,13 @@ static uint64_t now_ns() {
 static int step_replay_from(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, const Event* recv,
                             uint64_t owner_stride, hipStream_t st);
 
-// One job: wait for the group's emissions, one ncclAllToAll of the owners'
-// runs of regions (in the first batch's buffers), the owner replays, and the
-// end event of every batch; then each batch's enqueue count moves (x_join).
-static void run_xjob(wsr_comm* c, const XJob& j) {
+// One job: wait for the group's emissions (and for the slot's previous
+// replays), one ncclAllToAll of the owners' runs of regions, then -- not
+// deferred -- the owner replays and the end event of every batch.
+static void run_xjob(wsr_comm* c, const XJob& jp) {
+  XGroup& j = *jp;
+  XSlot& S = c->xs[j.xs];
   const int W = c->world;
-  wsr_batch* b0 = j.bs[0];
   const uint64_t region = (static_cast<uint64_t>(j.qpr) + 1) / 2 + static_cast<uint64_t>(j.slot);
   const uint64_t run = region * j.bs.size();
   uint64_t t0 = c->timing ? now_ns() : 0;
@@ -1220,33 +1272,33 @@ static void run_xjob(wsr_comm* c, const XJob& j) {
     // either way, and the exchange starts later: 16.8 -> 15.3 M q/s every
     // query sharded, profiles/r04t/)
     for (wsr_batch* b : j.bs) HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
-    const ncclResult_t r = ncclAllToAll(b0->d_xsend, b0->d_xrecv, run * (sizeof(Event) / sizeof(uint64_t)),
+    for (hipEvent_t e : j.wait_done) HIP_OK(hipStreamWaitEvent(c->stream, e, 0));
+    const ncclResult_t r = ncclAllToAll(S.send, S.recv, run * (sizeof(Event) / sizeof(uint64_t)),
                                         ncclUint64, c->comm, c->stream);
     if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+    HIP_OK(hipEventRecord(S.xa, c->stream));
   } catch (const std::exception& e) {
     rc = WSR_E_HIP;
     msg = e.what();
   }
   uint64_t t1 = c->timing ? now_ns() : 0;
-  for (size_t i = 0; i < j.bs.size() && rc == WSR_OK; ++i) {
-    rc = step_replay_from(j.h, j.bs[i], c->rank, W, j.qpr, b0->d_xrecv + region * i, run, c->stream);
-    if (rc) msg = g_err;
-  }
-  for (wsr_batch* b : j.bs) {
-    if (rc == WSR_OK && hipEventRecord(b->xev[1], c->stream) != hipSuccess) {
-      rc = WSR_E_HIP;
-      msg = "hipEventRecord failed";
+  if (!j.defer) {
+    for (size_t i = 0; i < j.bs.size() && rc == WSR_OK; ++i) {
+      rc = step_replay_from(j.h, j.bs[i], c->rank, W, j.qpr, S.recv + region * i, run, c->stream);
+      if (rc) msg = g_err;
+      else if (hipEventRecord(j.bs[i]->xev[1], c->stream) != hipSuccess ||
+               hipEventRecord(S.done[i], c->stream) != hipSuccess) {
+        rc = WSR_E_HIP;
+        msg = "hipEventRecord failed";
+      }
     }
-    b->x_pending = true;
-    b->x_enq.fetch_add(1, std::memory_order_release);
-  }
-  if (rc != WSR_OK) {
-    std::lock_guard<std::mutex> g(c->mu);
-    if (c->err.load() == WSR_OK) {
-      c->err_msg = msg;
-      c->err.store(rc);
+    for (wsr_batch* b : j.bs) {
+      b->x_pending = rc == WSR_OK;
+      b->x_enq.fetch_add(1, std::memory_order_release);
     }
   }
+  if (rc != WSR_OK) set_comm_err(c, rc, msg);
+  j.enq.store(true, std::memory_order_release);
   if (c->timing) {
     const uint64_t t2 = now_ns();
     c->t_ns[2] += t1 - t0;
@@ -1312,6 +1364,7 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   c->device = device;
   const char* ht = std::getenv("WSR_HOST_TIMING");
   c->timing = ht && *ht && *ht != '0';
+  c->defer = env_number("WSR_REPLAY_DEFER", 1) != 0;
   wsr_comm* cp = c.get();
   cp->worker = std::thread([cp] { exchange_worker(cp); });
   *out = c.release();
@@ -1320,6 +1373,7 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
 
 void wsr_comm_close(wsr_comm* c) {
   if (!c) return;
+  (void)wsr_comm_flush(c);   // (every deferred replay enqueued before the worker stops)
   {
     std::lock_guard<std::mutex> g(c->mu);
     c->stop = true;
@@ -1332,6 +1386,13 @@ void wsr_comm_close(wsr_comm* c) {
                  static_cast<unsigned long long>(c->steps), c->t_ns[0] / 1e3 / c->steps,
                  c->t_ns[1] / 1e3 / c->steps, c->t_ns[2] / 1e3 / c->steps, c->t_ns[3] / 1e3 / c->steps);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (XSlot& S : c->xs) {
+    for (size_t i = 0; i < S.n_done; ++i) (void)hipEventSynchronize(S.done[i]);   // (replays in lean kernels)
+    for (hipEvent_t e : S.done) (void)hipEventDestroy(e);
+    if (S.xa) (void)hipEventDestroy(S.xa);
+    if (S.send) (void)hipFree(S.send);
+    if (S.recv) (void)hipFree(S.recv);
+  }
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1407,12 +1468,12 @@ static void ensure_xbuf(wsr_batch* b, uint64_t need, int W) {
 // batch: its own buffer, owner_stride = region; a step group: the group's
 // buffer, this batch's region within every owner's run of regions).
 static int step_emit_into(wsr_handle* h, wsr_batch* b, int W, int32_t q_per_owner, int64_t slot, Event* send,
-                          uint64_t owner_stride) {
+                          uint64_t owner_stride, const OwnerJob* oj = nullptr) {
   const uint64_t meta_events = (static_cast<uint64_t>(q_per_owner) + 1) / 2;
   const uint64_t meta_stride = owner_stride * (sizeof(Event) / sizeof(int32_t));   // int32 per owner
   const ShardEmit se{W, q_per_owner, static_cast<uint64_t>(slot), send + meta_events, owner_stride,
                      reinterpret_cast<int32_t*>(send), meta_stride};
-  const int rc = batch_run(h, b, &se);
+  const int rc = batch_run(h, b, &se, oj);
   if (rc == WSR_OK) {
     b->x_world = W;
     b->x_qpr = q_per_owner;
@@ -1449,11 +1510,75 @@ static int step_replay(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_p
   return step_replay_from(h, b, rank, W, q_per_owner, b->d_xrecv, region_events_of(q_per_owner, slot), st);
 }
 
+// A deferred group's replays not yet enqueued go to the communicator's
+// stream (after its all-to-all, which the worker has enqueued first).
+static void flush_group(wsr_comm* c, XGroup& g) {
+  while (!g.enq.load(std::memory_order_acquire)) std::this_thread::yield();
+  XSlot& S = c->xs[g.xs];
+  const uint64_t region = region_events_of(g.qpr, g.slot), run = region * g.bs.size();
+  int rc = c->err.load() == WSR_OK ? WSR_OK : WSR_E_HIP;
+  for (size_t i = 0; i < g.bs.size(); ++i) {
+    if (g.queued[i]) continue;
+    g.queued[i] = 1;
+    wsr_batch* b = g.bs[i];
+    if (rc == WSR_OK) {
+      rc = step_replay_from(g.h, b, c->rank, c->world, g.qpr, S.recv + region * i, run, c->stream);
+      if (rc) set_comm_err(c, rc, g_err);
+      else if (hipEventRecord(b->xev[1], c->stream) != hipSuccess ||
+               hipEventRecord(S.done[i], c->stream) != hipSuccess) {
+        rc = WSR_E_HIP;
+        set_comm_err(c, rc, "hipEventRecord failed");
+      }
+    }
+    b->x_pending = rc == WSR_OK;
+    b->x_comm = nullptr;
+    b->x_enq.fetch_add(1, std::memory_order_release);
+  }
+  S.n_done = g.bs.size();
+}
+
+// Enqueue the deferred replays of every pending group up to the one holding
+// `upto` (all of them: upto null), oldest first.
+static void replay_flush(wsr_comm* c, const wsr_batch* upto) {
+  if (upto) {
+    bool held = false;
+    for (const auto& g : c->pend)
+      for (size_t i = 0; i < g->bs.size(); ++i) held = held || (!g->queued[i] && g->bs[i] == upto);
+    if (!held) return;
+  }
+  while (!c->pend.empty()) {
+    std::shared_ptr<XGroup> g = c->pend.front();
+    c->pend.pop_front();
+    bool has = false;
+    for (size_t i = 0; i < g->bs.size(); ++i) has = has || (!g->queued[i] && g->bs[i] == upto);
+    flush_group(c, *g);
+    if (has) return;
+  }
+}
+
+int wsr_comm_flush(wsr_comm* c) {
+  if (!c) return fail(WSR_E_INVALID, "null argument");
+  try {
+    HIP_OK(hipSetDevice(c->device));
+    replay_flush(c, nullptr);
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  if (const int e = c->err.load()) {
+    std::lock_guard<std::mutex> g(c->mu);
+    return fail(e, "exchange: " + c->err_msg);
+  }
+  return WSR_OK;
+}
+
 // A step group: n batches of the same shape, each emitted into its region of
-// every owner's run of n regions in the first batch's buffers, then ONE
-// ncclAllToAll of the runs and the n owner replays, on the communicator's
-// stream.  The collective's host cost (~0.1-0.2 ms a call under load, more
-// than a whole step's kernels) is paid once per group.
+// every owner's run of n regions in one of the communicator's exchange buffer
+// sets, then ONE ncclAllToAll of the runs on the communicator's stream.  The
+// collective's host cost (~0.1-0.2 ms a call under load, more than a whole
+// step's kernels) is paid once per group.  The group's owner replays run on
+// the communicator's stream too, or (deferred, the default) in the lean
+// kernels of the group kReplayLag groups later: batch i of this group replays
+// batch i of that one after its own items.
 int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c, int32_t q_per_owner,
                     int64_t slot) {
   if (!c || !bs || n < 1) return fail(WSR_E_INVALID, "bad shard_steps arguments");
@@ -1462,8 +1587,11 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
     return fail(e, "exchange worker: " + c->err_msg);
   }
   const int W = c->world;
-  for (int i = 0; i < n; ++i)
+  for (int i = 0; i < n; ++i) {
     if (int rc = check_step(h, bs[i], W, q_per_owner, slot)) return rc;
+    for (int j = 0; j < i; ++j)
+      if (bs[j] == bs[i]) return fail(WSR_E_INVALID, "a batch twice in one step group");
+  }
   uint64_t t0 = c->timing ? now_ns() : 0;
   auto lap = [&](int i) {
     if (!c->timing) return;
@@ -1471,32 +1599,117 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
     c->t_ns[i] += t - t0;
     t0 = t;
   };
-  wsr_batch* b0 = bs[0];
   const uint64_t region = region_events_of(q_per_owner, slot);
   const uint64_t run = region * static_cast<uint64_t>(n);   // events per owner
+  const int xs = static_cast<int>(c->n_groups % kXSlots);
+  XSlot& S = c->xs[xs];
+  std::shared_ptr<XGroup> P;   // the group whose replays this one's lean kernels take
+  std::vector<OwnerJob> oj(static_cast<size_t>(n));
   try {
     HIP_OK(hipSetDevice(h->device));
-    ensure_xbuf(b0, run * W, W);
-    for (int i = 1; i < n; ++i) {
+    // this group's batches: their own earlier replays enqueued first
+    for (int i = 0; i < n; ++i) {
       ensure_xev(bs[i]);
-      // the group's buffers: b0's previous exchange must be done with them
-      if (x_join(b0)) HIP_OK(hipStreamWaitEvent(bs[i]->st, b0->xev[1], 0));
+      if (bs[i]->x_comm) replay_flush(c, bs[i]);
+    }
+    // the slot: its previous group's all-to-all and replays enqueued (their
+    // end events are what this group's emission and exchange wait for)
+    if (S.last) {
+      for (size_t i = 0; i < S.last->queued.size(); ++i)
+        if (!S.last->queued[i]) replay_flush(c, S.last->bs[i]);
+      while (!S.last->enq.load(std::memory_order_acquire)) std::this_thread::yield();
+    }
+    const uint64_t need = run * static_cast<uint64_t>(W);
+    if (need > S.events) {
+      if (S.last) {
+        HIP_OK(hipEventSynchronize(S.xa));
+        for (size_t i = 0; i < S.n_done; ++i) HIP_OK(hipEventSynchronize(S.done[i]));
+        S.last.reset();
+        S.n_done = 0;
+      }
+      if (S.send) HIP_OK(hipFree(S.send));
+      if (S.recv) HIP_OK(hipFree(S.recv));
+      S.send = S.recv = nullptr;
+      S.events = 0;
+      HIP_OK(hipMalloc(&S.send, sizeof(Event) * need));
+      HIP_OK(hipMalloc(&S.recv, sizeof(Event) * need));
+      S.events = need;
+    }
+    if (!S.xa) HIP_OK(hipEventCreateWithFlags(&S.xa, hipEventDisableTiming));
+    while (S.done.size() < static_cast<size_t>(n)) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      S.done.push_back(e);
+    }
+    // the deferred replays this group's lean kernels take
+    if (c->defer && c->pend.size() >= kReplayLag) {
+      P = c->pend.front();
+      c->pend.pop_front();
+      while (!P->enq.load(std::memory_order_acquire)) std::this_thread::yield();
+      const XSlot& SP = c->xs[P->xs];
+      const uint64_t rP = region_events_of(P->qpr, P->slot), runP = rP * P->bs.size();
+      const uint64_t meta_events = (static_cast<uint64_t>(P->qpr) + 1) / 2;
+      for (size_t i = 0; i < P->bs.size() && i < static_cast<size_t>(n); ++i) {
+        const wsr_batch* pb = P->bs[i];
+        if (P->queued[i]) continue;
+        if (pb->has_wide) continue;   // (the LDS heap: on the communicator's stream)
+        const Event* recv = SP.recv + rP * i;
+        oj[i] = OwnerJob{pb->d_q, reinterpret_cast<const int32_t*>(recv), recv + meta_events, pb->d_hits,
+                         pb->d_nhits, pb->d_ctr, nullptr, runP * (sizeof(Event) / sizeof(int32_t)), runP,
+                         c->rank * P->qpr, P->qpr, W, pb->stride};
+      }
     }
   } catch (const std::exception& e) {
     return fail(WSR_E_HIP, e.what());
   }
   for (int i = 0; i < n; ++i) {
-    if (int rc = step_emit_into(h, bs[i], W, q_per_owner, slot, b0->d_xsend + region * i, run)) return rc;
-    if (hipEventRecord(bs[i]->xev[0], bs[i]->st) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
+    wsr_batch* b = bs[i];
+    const OwnerJob* job = oj[i].nq > 0 ? &oj[i] : nullptr;
+    try {
+      if (S.last) HIP_OK(hipStreamWaitEvent(b->st, S.xa, 0));   // the slot's last all-to-all read its send buffer
+      if (job) HIP_OK(hipStreamWaitEvent(b->st, c->xs[P->xs].xa, 0));
+    } catch (const std::exception& e) {
+      return fail(WSR_E_HIP, e.what());
+    }
+    if (int rc = step_emit_into(h, b, W, q_per_owner, slot, S.send + region * i, run, job)) return rc;
+    if (hipEventRecord(b->xev[0], b->st) != hipSuccess) return fail(WSR_E_HIP, "hipEventRecord failed");
+    if (job) {
+      wsr_batch* pb = P->bs[static_cast<size_t>(i)];
+      if (hipEventRecord(pb->xev[1], b->st) != hipSuccess ||
+          hipEventRecord(c->xs[P->xs].done[static_cast<size_t>(i)], b->st) != hipSuccess)
+        return fail(WSR_E_HIP, "hipEventRecord failed");
+      pb->x_pending = true;
+      pb->x_comm = nullptr;
+      P->queued[static_cast<size_t>(i)] = 1;
+      pb->x_enq.fetch_add(1, std::memory_order_release);
+    }
   }
+  // the rest of P (more batches than this group, or wide ones): the
+  // communicator's stream
+  if (P) flush_group(c, *P);
   lap(0);
   // the exchange half: the communicator's worker thread enqueues it
+  auto g = std::make_shared<XGroup>();
+  g->h = h;
+  g->bs.assign(bs, bs + n);
+  g->qpr = q_per_owner;
+  g->slot = slot;
+  g->xs = xs;
+  g->defer = c->defer;
+  g->queued.assign(static_cast<size_t>(n), g->defer ? 0 : 1);
+  if (S.last) g->wait_done.assign(S.done.begin(), S.done.begin() + static_cast<std::ptrdiff_t>(S.n_done));
+  S.last = g;
+  S.n_done = 0;
+  ++c->n_groups;
   {
-    std::lock_guard<std::mutex> g(c->mu);
-    XJob j{h, std::vector<wsr_batch*>(bs, bs + n), q_per_owner, slot};
-    for (int i = 0; i < n; ++i) ++bs[i]->x_req;
-    c->jobs.push_back(std::move(j));
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (int i = 0; i < n; ++i) {
+      ++bs[i]->x_req;
+      if (g->defer) bs[i]->x_comm = c;
+    }
+    c->jobs.push_back(g);
   }
+  if (g->defer) c->pend.push_back(g);
   c->cv.notify_one();
   lap(1);
   c->steps += static_cast<uint64_t>(n);

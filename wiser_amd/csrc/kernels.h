@@ -49,11 +49,11 @@ struct IndexArgs {
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
 // 4 error flags, 6 end of the lean items (items [0, lean) run in lean_kernel,
-// the rest in segment_kernel); each work queue has one head per XCD-sized
+// the rest in segment_kernel), 8 a deferred owner replay's claims; each work queue has one head per XCD-sized
 // shard, each on its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 +
 // 16*s general), so the dequeues of the persistent workers do not serialise
 // on a single line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16,
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrReplay = 8, kCtrHead0 = 16,
        kQueueShards = 8,
        kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
@@ -94,6 +94,22 @@ constexpr float kItemFixedCost = 4.0f;
 // the owner's fill counter, and records {count, offset} for the query
 // (count -1 and kErrExchange when the slot is full).  No reduce, scan or pack
 // launch is left between the segment kernels and the exchange.
+// A deferred owner replay (wsr_shard_steps): after their own items, the waves
+// of a lean kernel claim owned queries of an earlier step group's exchange and
+// replay them -- owner_replay_meta_kernel's work without its launch (nq 0:
+// none).  Only batches without wide queries are deferred.
+struct OwnerJob {
+  const QueryIn* qs;      // the replayed batch's queries; owned ones from q0
+  const int32_t* meta;    // {count, offset} of owned query i from shard g at meta + g * meta_stride + 2 * i
+  const Event* recv;      // shard g's events at recv + g * stride + offset
+  HitDev* hits;
+  int32_t* n_hits;
+  uint32_t* counters;     // the replayed batch's (error flags)
+  uint32_t* claim;        // the next owned query to replay (zeroed with the lean batch's counters)
+  uint64_t meta_stride, stride;
+  int32_t q0, nq, n_shards, hit_stride;
+};
+
 struct FusedReplay {
   uint32_t* q_done;
   HitDev* hits;
@@ -108,6 +124,7 @@ struct FusedReplay {
   uint64_t x_stride;    // events between owners' slots
   uint64_t x_meta_stride;   // int32 between owners' meta blocks
   int32_t x_qpr;        // queries per owner
+  OwnerJob oj;          // (lean kernel only)
   __device__ int32_t* meta_of(uint32_t q) const {
     const uint32_t o = q / static_cast<uint32_t>(x_qpr);
     return x_meta + o * x_meta_stride + 2ull * (q - o * static_cast<uint32_t>(x_qpr));

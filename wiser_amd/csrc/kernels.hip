@@ -2700,6 +2700,12 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
 }
 
 
+// (below, with the owner replay kernel)
+__device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t* meta, const Event* recv,
+                                               HitDev* hits, int32_t* n_hits, uint32_t* counters,
+                                               uint32_t* claim, uint64_t meta_stride, uint64_t stride,
+                                               int32_t q0, int32_t nq, int32_t n_shards, int32_t hit_stride);
+
 // ----------------------------------------------------------- lean kernel --
 // Items whose other lists all carry rank bitmaps (and single-term items).
 // Workgroups of kLeanWaves independent waves: each wave dequeues and runs its
@@ -2782,6 +2788,9 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
     finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, r, ev_out, ev_n, events, ev_cnt, fr);
     item = 0xFFFFFFFFu;
   }
+  if (fr.oj.nq > 0)   // an earlier step group's owner replay, deferred into this kernel's tail
+    owner_replay_tail(fr.oj.qs, fr.oj.meta, fr.oj.recv, fr.oj.hits, fr.oj.n_hits, fr.oj.counters, fr.oj.claim,
+                      fr.oj.meta_stride, fr.oj.stride, fr.oj.q0, fr.oj.nq, fr.oj.n_shards, fr.oj.hit_stride);
   if (l == 0) {
     stats[wid * kStatStride + 0] = n_surv;
     stats[wid * kStatStride + 1] = n_dblk;
@@ -2797,15 +2806,11 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
 // kWide: the queries with k > kMaxK, heap in LDS (a separate instance, so the
 // common one reserves no LDS for it).
 template <bool kWide>
-__global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
-                                                               int n_shards, const int32_t* __restrict__ meta,
-                                                               uint64_t meta_stride, uint64_t stride,
-                                                               const Event* __restrict__ recv,
-                                                               HitDev* __restrict__ hits, int hit_stride,
-                                                               int32_t* __restrict__ n_hits,
-                                                               uint32_t* __restrict__ counters) {
-  const int qi = blockIdx.x;
-  if (qi >= nq) return;
+__device__ __forceinline__ void owner_replay_query(const QueryIn* __restrict__ qs, int qi, int q0, int n_shards,
+                                                   const int32_t* __restrict__ meta, uint64_t meta_stride,
+                                                   uint64_t stride, const Event* __restrict__ recv,
+                                                   HitDev* __restrict__ hits, int hit_stride,
+                                                   int32_t* __restrict__ n_hits, uint32_t* __restrict__ counters) {
   const int gq = q0 + qi;
   const uint32_t k = uni(qs[gq].k > 0 ? static_cast<uint32_t>(qs[gq].k) : 0u);
   if ((k > static_cast<uint32_t>(kMaxK)) != kWide) return;
@@ -2832,6 +2837,37 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+  }
+}
+
+template <bool kWide>
+__global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __restrict__ qs, int q0, int nq,
+                                                               int n_shards, const int32_t* __restrict__ meta,
+                                                               uint64_t meta_stride, uint64_t stride,
+                                                               const Event* __restrict__ recv,
+                                                               HitDev* __restrict__ hits, int hit_stride,
+                                                               int32_t* __restrict__ n_hits,
+                                                               uint32_t* __restrict__ counters) {
+  const int qi = blockIdx.x;
+  if (qi >= nq) return;
+  owner_replay_query<kWide>(qs, qi, q0, n_shards, meta, meta_stride, stride, recv, hits, hit_stride, n_hits,
+                            counters);
+}
+
+// The deferred form (OwnerJob): a lean kernel's wave, its items done, claims
+// owned queries one at a time until none is left.  Out of line, fields as
+// values (see shard_emit_call), so the lean kernel's registers are its own.
+__device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t* meta, const Event* recv,
+                                               HitDev* hits, int32_t* n_hits, uint32_t* counters,
+                                               uint32_t* claim, uint64_t meta_stride, uint64_t stride,
+                                               int32_t q0, int32_t nq, int32_t n_shards, int32_t hit_stride) {
+  for (;;) {
+    uint32_t qi = 0;
+    if ((threadIdx.x & 63) == 0) qi = atomicAdd(claim, 1u);
+    qi = uni(qi);
+    if (qi >= static_cast<uint32_t>(nq)) break;
+    owner_replay_query<false>(qs, static_cast<int>(qi), q0, n_shards, meta, meta_stride, stride, recv, hits,
+                              hit_stride, n_hits, counters);
   }
 }
 

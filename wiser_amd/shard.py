@@ -115,7 +115,9 @@ class NativeShardedSearcher:
         check(lib.wsr_shard_steps(self.engine._h, arr, len(bs), self._c, qpr, slot))
 
     def flush(self):
-        """(every step is enqueued whole: nothing is held back on the host)"""
+        """Enqueue every deferred owner replay (wsr_comm_flush): after it, a
+        device synchronize covers all the work of the steps so far."""
+        check(lib.wsr_comm_flush(self._c))
 
     def max_fill(self, b) -> int:
         tot = (C.c_int64 * self.world)()
