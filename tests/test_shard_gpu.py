@@ -212,52 +212,61 @@ def test_native_rccl_deferred_replay(synth_small, monkeypatch, defer):
     and not (WSR_REPLAY_DEFER=0): 14 step groups of changing size over five
     batches -- one of k = 100, whose replay needs the LDS heap and so is never
     deferred -- more groups than exchange buffer sets, batches stepped again
-    while their replay is pending; then a flush and every fetch.  Equal to the
+    while their replay is pending; then a flush and every fetch, and again
+    with fetches straight after the steps.  Each phase runs a query set the
+    batches did not hold before, so a replay left undone shows.  Equal to the
     oracle."""
     import wiser_amd as w
     from wiser_amd import _capi
-    from wiser_amd.shard import NativeShardedSearcher
+    from wiser_amd.shard import NativeShardedSearcher, slot_for_fill
     from oracle.oracle import OracleVacuum
     monkeypatch.setenv("WSR_REPLAY_DEFER", defer)
     d, _ = synth_small
     log = os.path.join(d, "qshard_defer.log")
-    w.gen_two_term_log(d, log, n_queries=1280, seed=23)
+    w.gen_two_term_log(d, log, n_queries=3 * 1280, seed=23)
     qs = [l.split() for l in open(log).read().splitlines()]
     S = NativeShardedSearcher(d, 0, 1, share_id=lambda x: x)
     eng = S.engine
     n = 256
     ks = [10, 10, 10, 10, 100]
-    parts = [qs[i * n:(i + 1) * n] for i in range(5)]
-    bs = []
-    for part, k in zip(parts, ks):
-        arr = (_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=k))[0] for q in part])
-        b = w.ResidentBatch(eng, n, k)
-        b.upload(arr)
-        bs.append(b)
     o = OracleVacuum(d)
-    exp = [[o.search(q, k)[0] for q in part] for part, k in zip(parts, ks)]
+    sets = [[qs[(5 * s + i) * n:(5 * s + i + 1) * n] for i in range(5)] for s in range(3)]
+    bs = [w.ResidentBatch(eng, n, k) for k in ks]
+
+    def upload(parts):
+        for b, part, k in zip(bs, parts, ks):
+            b.upload((_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=k))[0] for q in part]))
+        return [[o.search(q, k)[0] for q in part] for part, k in zip(parts, ks)]
+
+    def check(exp):
+        for b, e in zip(bs, exp):
+            hits, nh = S.fetch_owned(b, n)
+            got = [[(hits[i * b.stride + j].doc_id, hits[i * b.stride + j].score) for j in range(nh[i])]
+                   for i in range(n)]
+            assert got == e
+
     groups = [[0, 1], [2, 3], [4], [0, 1, 2], [3, 4], [1], [2, 0], [4, 3, 1], [0], [1, 2, 3, 4], [0, 4], [2],
               [3], [1, 0]]
-    for g in groups:
-        S.steps([bs[i] for i in g], n, 64 * n)
-    S.flush()
-    w.sync(eng)
-    for b, e, k in zip(bs, exp, ks):
-        hits, nh = S.fetch_owned(b, n)
-        got = [[(hits[i * b.stride + j].doc_id, hits[i * b.stride + j].score) for j in range(nh[i])]
-               for i in range(n)]
-        assert got == e
-    # again, fetched straight after the steps (the fetch enqueues what is pending)
-    for g in groups[:5]:
-        S.steps([bs[i] for i in g], n, 64 * n)
-    for b, e in zip(bs, exp):
-        hits, nh = S.fetch_owned(b, n)
-        got = [[(hits[i * b.stride + j].doc_id, hits[i * b.stride + j].score) for j in range(nh[i])]
-               for i in range(n)]
-        assert got == e
-    for b in bs:
-        b.close()
-    S.close()
+    try:
+        # the slot from a first pass (the k = 100 batch sends every survivor)
+        upload(sets[0])
+        for b in bs:
+            S.steps([b], n, 1 << 20)
+        slot = slot_for_fill(max(S.max_fill(b) for b in bs), n)
+        exp = upload(sets[1])
+        for g in groups:
+            S.steps([bs[i] for i in g], n, slot)
+        S.flush()
+        w.sync(eng)
+        check(exp)
+        exp = upload(sets[2])
+        for g in groups[:5]:
+            S.steps([bs[i] for i in g], n, slot)
+        check(exp)
+    finally:
+        for b in bs:
+            b.close()
+        S.close()
 
 
 def test_host_exchange_pipelined(synth_small):

@@ -846,10 +846,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
       fr.x_meta_stride = se->meta_stride;
       fr.x_qpr = se->qpr;
     }
-    if (oj) {
-      fr.oj = *oj;
-      fr.oj.claim = b->d_ctr + kCtrReplay;   // (zeroed above)
-    }
+    if (oj) fr.oj = *oj;
     HIP_OK(hipEventRecord(b->ev[0], st));
     IndexArgs pa = h->args;   // (the batch's item length)
     pa.seg_cap = b->seg_cap;
@@ -1655,7 +1652,7 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
         if (pb->has_wide) continue;   // (the LDS heap: on the communicator's stream)
         const Event* recv = SP.recv + rP * i;
         oj[i] = OwnerJob{pb->d_q, reinterpret_cast<const int32_t*>(recv), recv + meta_events, pb->d_hits,
-                         pb->d_nhits, pb->d_ctr, nullptr, runP * (sizeof(Event) / sizeof(int32_t)), runP,
+                         pb->d_nhits, pb->d_ctr, runP * (sizeof(Event) / sizeof(int32_t)), runP,
                          c->rank * P->qpr, P->qpr, W, pb->stride};
       }
     }

@@ -49,11 +49,11 @@ struct IndexArgs {
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
 // 4 error flags, 6 end of the lean items (items [0, lean) run in lean_kernel,
-// the rest in segment_kernel), 8 a deferred owner replay's claims; each work queue has one head per XCD-sized
+// the rest in segment_kernel); each work queue has one head per XCD-sized
 // shard, each on its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 +
 // 16*s general), so the dequeues of the persistent workers do not serialise
 // on a single line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrReplay = 8, kCtrHead0 = 16,
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16,
        kQueueShards = 8,
        kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
@@ -95,9 +95,9 @@ constexpr float kItemFixedCost = 4.0f;
 // (count -1 and kErrExchange when the slot is full).  No reduce, scan or pack
 // launch is left between the segment kernels and the exchange.
 // A deferred owner replay (wsr_shard_steps): after their own items, the waves
-// of a lean kernel claim owned queries of an earlier step group's exchange and
-// replay them -- owner_replay_meta_kernel's work without its launch (nq 0:
-// none).  Only batches without wide queries are deferred.
+// of a lean kernel replay owned queries of an earlier step group's exchange --
+// owner_replay_meta_kernel's work without its launch (nq 0: none).  Only
+// batches without wide queries are deferred.
 struct OwnerJob {
   const QueryIn* qs;      // the replayed batch's queries; owned ones from q0
   const int32_t* meta;    // {count, offset} of owned query i from shard g at meta + g * meta_stride + 2 * i
@@ -105,7 +105,6 @@ struct OwnerJob {
   HitDev* hits;
   int32_t* n_hits;
   uint32_t* counters;     // the replayed batch's (error flags)
-  uint32_t* claim;        // the next owned query to replay (zeroed with the lean batch's counters)
   uint64_t meta_stride, stride;
   int32_t q0, nq, n_shards, hit_stride;
 };

@@ -2703,8 +2703,9 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
 // (below, with the owner replay kernel)
 __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t* meta, const Event* recv,
                                                HitDev* hits, int32_t* n_hits, uint32_t* counters,
-                                               uint32_t* claim, uint64_t meta_stride, uint64_t stride,
-                                               int32_t q0, int32_t nq, int32_t n_shards, int32_t hit_stride);
+                                               uint32_t wave, uint32_t waves, uint64_t meta_stride,
+                                               uint64_t stride, int32_t q0, int32_t nq, int32_t n_shards,
+                                               int32_t hit_stride);
 
 // ----------------------------------------------------------- lean kernel --
 // Items whose other lists all carry rank bitmaps (and single-term items).
@@ -2789,8 +2790,9 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
     item = 0xFFFFFFFFu;
   }
   if (fr.oj.nq > 0)   // an earlier step group's owner replay, deferred into this kernel's tail
-    owner_replay_tail(fr.oj.qs, fr.oj.meta, fr.oj.recv, fr.oj.hits, fr.oj.n_hits, fr.oj.counters, fr.oj.claim,
-                      fr.oj.meta_stride, fr.oj.stride, fr.oj.q0, fr.oj.nq, fr.oj.n_shards, fr.oj.hit_stride);
+    owner_replay_tail(fr.oj.qs, fr.oj.meta, fr.oj.recv, fr.oj.hits, fr.oj.n_hits, fr.oj.counters, wid,
+                      gridDim.x * kLeanWaves, fr.oj.meta_stride, fr.oj.stride, fr.oj.q0, fr.oj.nq,
+                      fr.oj.n_shards, fr.oj.hit_stride);
   if (l == 0) {
     stats[wid * kStatStride + 0] = n_surv;
     stats[wid * kStatStride + 1] = n_dblk;
@@ -2854,21 +2856,39 @@ __global__ __launch_bounds__(64) void owner_replay_meta_kernel(const QueryIn* __
                             counters);
 }
 
-// The deferred form (OwnerJob): a lean kernel's wave, its items done, claims
-// owned queries one at a time until none is left.  Out of line, fields as
-// values (see shard_emit_call), so the lean kernel's registers are its own.
+// The deferred form (OwnerJob): a lean kernel's waves, their items done,
+// replay owned queries wave, wave + waves, ...  Out of line, fields as values
+// (see shard_emit_call), so the lean kernel's registers are its own; the
+// arguments come in VGPRs and are made wave-uniform first (readfirstlane), so
+// the loop is a scalar one.  (A first form claimed queries with lane 0's
+// atomicAdd + readfirstlane on VGPR arguments: the loop compiled as a
+// divergent one and never ended on the GPU; a static stride needs neither.)
+__device__ __forceinline__ const void* uni_ptr(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  return reinterpret_cast<const void*>(static_cast<uint64_t>(uni(static_cast<uint32_t>(v))) |
+                                       (static_cast<uint64_t>(uni(static_cast<uint32_t>(v >> 32))) << 32));
+}
 __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t* meta, const Event* recv,
                                                HitDev* hits, int32_t* n_hits, uint32_t* counters,
-                                               uint32_t* claim, uint64_t meta_stride, uint64_t stride,
-                                               int32_t q0, int32_t nq, int32_t n_shards, int32_t hit_stride) {
-  for (;;) {
-    uint32_t qi = 0;
-    if ((threadIdx.x & 63) == 0) qi = atomicAdd(claim, 1u);
-    qi = uni(qi);
-    if (qi >= static_cast<uint32_t>(nq)) break;
-    owner_replay_query<false>(qs, static_cast<int>(qi), q0, n_shards, meta, meta_stride, stride, recv, hits,
-                              hit_stride, n_hits, counters);
-  }
+                                               uint32_t wave, uint32_t waves, uint64_t meta_stride,
+                                               uint64_t stride, int32_t q0, int32_t nq, int32_t n_shards,
+                                               int32_t hit_stride) {
+  qs = static_cast<const QueryIn*>(uni_ptr(qs));
+  meta = static_cast<const int32_t*>(uni_ptr(meta));
+  recv = static_cast<const Event*>(uni_ptr(recv));
+  hits = static_cast<HitDev*>(const_cast<void*>(uni_ptr(hits)));
+  n_hits = static_cast<int32_t*>(const_cast<void*>(uni_ptr(n_hits)));
+  counters = static_cast<uint32_t*>(const_cast<void*>(uni_ptr(counters)));
+  const uint32_t w0 = uni(wave), nw = uni(waves), n = uni(static_cast<uint32_t>(nq));
+  const uint64_t ms = static_cast<uint64_t>(uni(static_cast<uint32_t>(meta_stride))) |
+                      (static_cast<uint64_t>(uni(static_cast<uint32_t>(meta_stride >> 32))) << 32);
+  const uint64_t st = static_cast<uint64_t>(uni(static_cast<uint32_t>(stride))) |
+                      (static_cast<uint64_t>(uni(static_cast<uint32_t>(stride >> 32))) << 32);
+  const int32_t b0 = static_cast<int32_t>(uni(static_cast<uint32_t>(q0)));
+  const int32_t ns = static_cast<int32_t>(uni(static_cast<uint32_t>(n_shards)));
+  const int32_t hs = static_cast<int32_t>(uni(static_cast<uint32_t>(hit_stride)));
+  for (uint32_t qi = w0; qi < n; qi += nw)
+    owner_replay_query<false>(qs, static_cast<int>(qi), b0, ns, meta, ms, st, recv, hits, hs, n_hits, counters);
 }
 
 // ------------------------------------------------------------ launchers --
