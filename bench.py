@@ -144,7 +144,7 @@ def parse():
                         "rank's full-index image (0: every query is sharded; -1, the default: "
                         "max(64, 63 * N), so that each shard's part of a sharded query is at "
                         "least one full work item)")
-    p.add_argument("--shard-group", type=int, default=4,
+    p.add_argument("--shard-group", type=int, default=8,
                    help="N>1 shards: heavy batches of this many consecutive steps share one "
                         "all-to-all (wsr_shard_steps)")
     p.add_argument("--shard-every", type=int, default=0,
