@@ -163,7 +163,8 @@ def in_child(code):
     """Run `code` (Python, with `w` = wiser_amd) in a child process and return
     the JSON it prints last.  Index builds run there: the writer's many
     threads and gigabytes of short-lived host memory stay out of the process
-    whose HIP calls the timed loops measure (see snapshot)."""
+    whose HIP calls the timed loops measure (see snapshot); so does the
+    serving leg (its own HIP runtime, as a server process has)."""
     prog = f"import sys, json, time\nsys.path.insert(0, {ROOT!r})\nimport wiser_amd as w\n{code}"
     r = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True)
     if r.returncode != 0:
@@ -544,12 +545,15 @@ def extra_legs(a, idx, qlog, local, threads):
         return not chosen or name in chosen
 
     c2_idx = None
-    # serving first: its closed loop of host threads is the leg most sensitive
-    # to what earlier legs left in the process (in a fresh process the same
-    # points run 20-40 % faster than after the others, profiles/r04m_bench.json
-    # against r04n/serve_points.jsonl)
+    # serving in a process of its own, as a server runs: its closed loop of host
+    # threads is the leg most sensitive to what the timed loops before it left in
+    # this process (the same points ran 20-40 % faster in a fresh process,
+    # profiles/r04m_bench.json and r04f1/ against r04n/serve_points.jsonl)
     if want("serving"):
-        legs["serving"] = serving_leg(a, idx, qlog, local, threads)
+        legs["serving"] = in_child(
+            "import bench\nfrom types import SimpleNamespace\n"
+            f"out = bench.serving_leg(SimpleNamespace(batch={a.batch}, k={a.k}), {idx!r}, {qlog!r}, "
+            f"{local}, {threads})\nprint(json.dumps(out))")
     if want("c2_synthetic_1m") and not (a.workload == "c2" and not (a.vacuum_dir or a.linedoc)):
         legs["c2_synthetic_1m"] = c2_leg(a, local, threads)
     if want("end_to_end"):
