@@ -784,6 +784,11 @@ def serving_leg(a, idx, qlog, local, threads):
     # of the sweeps on the box's 16-core share, profiles/r04n/serve_points.jsonl:
     # 6.1 / 5.2 / 5.1 M q/s at p50 0.85 / 0.88 / 0.94 ms; more client threads
     # oversubscribe the share beside the dispatcher, the completer and HIP's)
+    # (a first, unrecorded second of load: the first server of a process ran
+    # its first point 20 % below the same point later, profiles/r04s2/)
+    srv = w.Server(eng, max_batch=a.batch, window_us=1000)
+    srv.bench(arr, n_clients=7, depth=704, seconds=1.0)
+    srv.close()
     for clients, depth, window in ((7, 704, 1000), (6, 768, 1000), (5, 960, 1000), (8, 640, 1000), (4, 64, 100)):
         srv = w.Server(eng, max_batch=a.batch, window_us=window)
         st = srv.bench(arr, n_clients=clients, depth=depth, seconds=3.0)
