@@ -993,8 +993,8 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
         if cb:
             cb.run()
         if hb:
-            if pend and pend[0][1] != hq:
-                flush()
+            if pend and (pend[0][1] != hq or any(x is hb for x, _ in pend)):
+                flush()   # (a group holds one shape, and each batch once)
             pend.append((hb, hq))
             if fetch or len(pend) >= max(1, a.shard_group):
                 flush()
