@@ -314,7 +314,8 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
  * default (WSR_REPLAY_DEFER=0: not) into the lean kernels of the step group
  * two groups later; a fetch, wsr_batch_ready or the batch's next run enqueues
  * a still-pending one first.  The communicator's calls (steps, flush, and the
- * joins of its batches) come from one thread. */
+ * joins of its batches) come from one thread; close the communicator before
+ * the engine handles whose batches it stepped. */
 int wsr_shard_steps(wsr_handle* h, wsr_batch* const* b, int32_t n, wsr_comm* c, int32_t q_per_owner,
                     int64_t slot);
 /* enqueue every deferred owner replay of the communicator (before timing the
