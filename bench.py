@@ -46,7 +46,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Per-launch fabric bytes of the segment phase (scripts/gpu_prof.sh,
 # scripts/pmc_bytes.py), one profile per workload: attached to lines of that
 # workload only, with the file named in roofline.traffic_source.
-PMC_PROFILES = {"c3": "r04e_pmc_segment_c3.json", "c2": "r03d_pmc_segment_c2.json",
+PMC_PROFILES = {"c3": "r04fp_pmc_segment_c3.json", "c2": "r03d_pmc_segment_c2.json",
                 "c4": "r04e_pmc_segment_c4.json", "c5": "r04e_pmc_segment_c5.json"}
 DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
 DEFERRED = []   # oracle work (parity checks, CPU baselines) run after every timed loop
