@@ -758,16 +758,35 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     plan[i].item_base = base;
     plan[i].ev_base = cb;
     // (skipped when the plan does not fit the workspace: never written past it)
-    if (fits) {
-      if (p.driver & kPlanLean) {
-        desc[i].item_base = base;
-        desc[i].ev_base = cb;
-      }
-      for (uint32_t j = 0; j < p.n_items; ++j) {
-        item_q[base + j] = static_cast<uint32_t>(i);
-        if (pub) pub[base + j] = 0;
-      }
+    if (fits && (p.driver & kPlanLean)) {
+      desc[i].item_base = base;
+      desc[i].ev_base = cb;
     }
+  }
+  // The workgroup's items (item -> query, zeroed floor), spread over all its
+  // threads: item j of the workgroup's run belongs to the last query whose
+  // first item is at or before j (a binary search over the scan in LDS), so a
+  // query of hundreds of items is not stored by its own thread alone.
+  __shared__ ScanLds<1> S1;
+  __shared__ uint32_t s_off[kPlanThreads + 1], s_base[kPlanThreads];
+  const uint32_t mine[1] = {(i < nq && fits) ? p.n_items : 0u};
+  uint32_t off[1], n_run[1];
+  uint64_t u_ex, u_tot;
+  block_excl_scan_n<1>(mine, 0ull, off, n_run, u_ex, u_tot, S1);
+  s_off[t] = off[0];
+  s_base[t] = base;
+  if (t == 0) s_off[kPlanThreads] = n_run[0];
+  __syncthreads();
+  for (uint32_t j = t; j < n_run[0]; j += kPlanThreads) {
+    uint32_t lo = 0, hi = kPlanThreads;   // s_off[lo] <= j < s_off[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_off[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t slot = s_base[lo] + (j - s_off[lo]);
+    item_q[slot] = blockIdx.x * blockDim.x + lo;
+    if (pub) pub[slot] = 0;
   }
   if (blockIdx.x == 0) {
     if (t == 0) {
