@@ -544,43 +544,22 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     uint32_t d = 0, nd = 0xFFFFFFFFu, o1 = kNoSlot, min_last = 0xFFFFFFFFu;
     float cost = 1.0f;
     bool lean = true;
-    // (up to kMaxTerms terms: the lean record's inputs from the same round of
-    // loads -- slots 0 and 1 whole, so that a two-term query's driver and O1
-    // records need no second round -- and the pre-probe bound's idf / tf bound)
-    ListDev L01[2];
-    bool have_rec = false;
-    double io_reg = 0.0;
-    uint32_t mm_reg = 0;
     if (nt <= kMaxTerms) {
-      uint32_t nb[kMaxTerms], last[kMaxTerms], tfm[kMaxTerms];
-      double idf[kMaxTerms];
+      uint32_t nb[kMaxTerms], last[kMaxTerms];
       bool dn[kMaxTerms];
 #pragma unroll
       for (int s = 0; s < kMaxTerms; ++s) {
         nb[s] = 0xFFFFFFFFu;
         last[s] = 0xFFFFFFFFu;
-        tfm[s] = 0;
-        idf[s] = 0.0;
         dn[s] = false;
         const int32_t id = q.list[s];
         const bool in = s < nt;
         if (in && (id < 0 || static_cast<uint32_t>(id) >= ix.n_lists)) ok = false;
         if (in && id >= 0 && static_cast<uint32_t>(id) < ix.n_lists) {
-          if (s < 2) {
-            L01[s] = ix.lists[id];
-            nb[s] = L01[s].nblk;
-            dn[s] = L01[s].bm != kNoDense;
-            last[s] = L01[s].last;
-            idf[s] = L01[s].idf;
-            tfm[s] = L01[s].tfmax;
-          } else {
-            const ListDev& L = ix.lists[id];
-            nb[s] = L.nblk;
-            dn[s] = L.bm != kNoDense;
-            last[s] = L.last;
-            idf[s] = L.idf;
-            tfm[s] = L.tfmax;
-          }
+          const ListDev& L = ix.lists[id];
+          nb[s] = L.nblk;
+          dn[s] = L.bm != kNoDense;
+          last[s] = L.last;
         }
       }
 #pragma unroll
@@ -598,10 +577,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         if (!dense) lean = false;
         min_last = last[s] < min_last ? last[s] : min_last;
         if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
-        io_reg += 2.2 * idf[s];
-        mm_reg = tfm[s] > mm_reg ? tfm[s] : mm_reg;
       }
-      have_rec = d < 2 && (o1 < 2 || o1 == kNoSlot);
     } else if (ok) {
       for (int s = 0; s < nt; ++s) {
         const int32_t id = ql[s];
@@ -640,7 +616,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       if (lean) {
         // the lean kernel's record (bases are added by plan_fill_kernel)
         // (the driver's and O1's records: a second round of loads, side by side)
-        const ListDev A = have_rec ? (d == 0 ? L01[0] : L01[1]) : ix.lists[ql[d]];
+        const ListDev A = ix.lists[ql[d]];
         QueryDesc D;
         D.a_base = A.base;
         D.a_tail = A.tail;
@@ -650,7 +626,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.a_tail_cnt = A.tail_cnt;
         D.o_bm = 0; D.o_tf8 = 0; D.o_idf = 0.0; D.o_list = 0;
         if (o1 != kNoSlot) {
-          const ListDev O = have_rec ? (o1 == 0 ? L01[0] : L01[1]) : ix.lists[ql[o1]];
+          const ListDev O = ix.lists[ql[o1]];
           D.o_bm = O.bm; D.o_tf8 = O.tf8; D.o_idf = O.idf;
           D.o_list = static_cast<uint32_t>(ql[o1]);
         }
@@ -663,15 +639,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         D.k = static_cast<uint32_t>(q.k);
         // pre-probe score bound: the other terms' BM25 parts are at most
         // sum(2.2 idf) * M / (M + norm) with M their largest tf bound
-        double io = io_reg;
-        uint32_t mm = mm_reg;
-        if (nt > kMaxTerms) {
-          for (int s = 0; s < nt; ++s) {
-            if (s == static_cast<int>(d)) continue;
-            const ListDev& L = ix.lists[ql[s]];
-            io += 2.2 * L.idf;
-            mm = L.tfmax > mm ? L.tfmax : mm;
-          }
+        double io = 0.0;
+        uint32_t mm = 0;
+        for (int s = 0; s < nt; ++s) {
+          if (s == static_cast<int>(d)) continue;
+          const ListDev& L = ix.lists[ql[s]];
+          io += 2.2 * L.idf;
+          mm = L.tfmax > mm ? L.tfmax : mm;
         }
         const float mf = o1 != kNoSlot ? static_cast<float>(mm) : 1.0f;
         D.b_id = static_cast<float>(2.2 * A.idf);
