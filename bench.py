@@ -1008,16 +1008,16 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
         if full:
             w.sync(full)
 
-    for s_ in range(a.warmup):
-        step(s_)
-    flush()
-    sync_all()
-    lat = []
+    lat = []   # one step at a time (p50_alone), every batch once before the clock
     for i in range(nb):
         barrier()
         t0 = time.perf_counter()
         step(i, fetch=True)
         lat.append((time.perf_counter() - t0) * 1e3)
+    # the W warmup steps right before the clock
+    for s_ in range(a.warmup):
+        step(s_)
+    flush()
     barrier()
     sync_all()
     t0 = time.perf_counter()
@@ -1068,15 +1068,15 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
         batches.append(b)
         chunks.append(chunk)
     nb = len(batches)
-    for s in range(a.warmup):
-        batches[s % nb].run()
-    w.sync(eng)
-    lat = []
+    lat = []   # one batch at a time (p50_alone), every batch once before the clock
     for b in batches:
         t0 = time.perf_counter()
         b.run()
         b.fetch()
         lat.append((time.perf_counter() - t0) * 1e3)
+    # the W warmup steps right before the clock (the device busy, as in the loop)
+    for s in range(a.warmup):
+        batches[s % nb].run()
     if dist:
         dist.barrier()
     w.sync(eng)
