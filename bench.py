@@ -150,7 +150,7 @@ def parse():
     p.add_argument("--shard-every", type=int, default=0,
                    help="N>1 shards: the heavy queries of this many consecutive steps go through "
                         "one sharded step (a heavy batch every that many steps; 0, the default: "
-                        "enough steps for about 1024 heavy queries per rank, at most the log's "
+                        "enough steps for about 4096 heavy queries per rank, at most the log's "
                         "batches)")
     return p.parse_args()
 

@@ -47,7 +47,7 @@ def summary(ws):
 
 def main():
     sys.argv = [sys.argv[0]]
-    a = bench.parse_args()
+    a = bench.parse()
     idx, qlog, _ = bench.ensure_c3(a)
     lines = [l.split() for l in open(qlog).read().splitlines()]
     eng = w.VacuumEngine(idx, device=0, threads=16, positions=False)
