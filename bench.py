@@ -144,6 +144,9 @@ def parse():
                         "rank's full-index image (0: every query is sharded; -1, the default: "
                         "max(64, 63 * N), so that each shard's part of a sharded query is at "
                         "least one full work item)")
+    p.add_argument("--item-blocks", type=int, default=0,
+                   help="driver blocks per work item at most for the headline batches "
+                        "(wsr_batch_set_item_blocks; 0: the engine's default)")
     p.add_argument("--shard-group", type=int, default=8,
                    help="N>1 shards: heavy batches of this many consecutive steps share one "
                         "all-to-all (wsr_shard_steps)")
@@ -1064,6 +1067,9 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
     for s in range(0, len(mine), a.batch):
         chunk = mine[s:s + a.batch]
         b = w.ResidentBatch(eng, a.batch, a.k)
+        if a.item_blocks:
+            from wiser_amd._capi import check as _check, lib as _lib
+            _check(_lib.wsr_batch_set_item_blocks(eng._h, b._b, a.item_blocks))
         b.upload(resolve(eng, chunk, a.k))
         batches.append(b)
         chunks.append(chunk)
