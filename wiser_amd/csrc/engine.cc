@@ -352,7 +352,6 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->args.dense_span = img.dense_span;
     h->args.dense_ratio = dense_ratio;
     h->args.seg_cap = kSegCost;
-    h->args.hit_cost = static_cast<float>(env_number("WSR_HIT_COST", 0));
     h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
     h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;

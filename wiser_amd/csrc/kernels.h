@@ -30,8 +30,6 @@ struct IndexArgs {
   float dense_ratio;        // probe list B by bitmap when nblk(B) >= dense_ratio * nblk(driver)
   uint32_t seg_cap;         // driver blocks per work item at most (kSegCost; the batch's own, see
                             // wsr_batch_set_item_blocks: a latency-bound caller takes shorter items)
-  float hit_cost;           // plan cost of a probed list per unit of its density in the image (its
-                            // hits: scoring and events per driver posting; WSR_HIT_COST)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
   // positions (phrase queries; null unless the engine was opened with them)

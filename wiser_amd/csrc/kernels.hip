@@ -573,8 +573,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       for (int s = 0; s < kMaxTerms; ++s) {
         if (s >= nt || s == static_cast<int>(d)) continue;
         const bool dense = use_dense(ix, dn[s], nb[s], nd);
-        cost += dense ? ix.hit_cost * fminf(128.0f * static_cast<float>(nb[s]) / static_cast<float>(ix.dense_span), 1.0f)
-                      : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
+        cost += dense ? 0.0f : fminf(static_cast<float>(nb[s]) / nd, 64.0f);
         if (!dense) lean = false;
         min_last = last[s] < min_last ? last[s] : min_last;
         if (nb[s] < o_nb) { o1 = s; o_nb = nb[s]; }
@@ -592,8 +591,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
         if (s == static_cast<int>(d)) continue;
         const ListDev& L = ix.lists[ql[s]];
         const bool dense = use_dense(ix, L.bm != kNoDense, L.nblk, nd);
-        cost += dense ? ix.hit_cost * fminf(128.0f * static_cast<float>(L.nblk) / static_cast<float>(ix.dense_span), 1.0f)
-                      : fminf(static_cast<float>(L.nblk) / nd, 64.0f);
+        cost += dense ? 0.0f : fminf(static_cast<float>(L.nblk) / nd, 64.0f);
         if (!dense) lean = false;
         min_last = L.last < min_last ? L.last : min_last;
         if (L.nblk < o_nb) { o1 = s; o_nb = L.nblk; }
