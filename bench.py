@@ -30,6 +30,7 @@ value = queries completed by all ranks / max-over-ranks wall time (weak scaling)
 """
 import argparse
 import ctypes as C
+import hashlib
 import json
 import math
 import os
@@ -48,6 +49,21 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # workload only, with the file named in roofline.traffic_source.
 PMC_PROFILES = {"c3": "r04fp_pmc_segment_c3.json", "c2": "r03d_pmc_segment_c2.json",
                 "c4": "r04e_pmc_segment_c4.json", "c5": "r04e_pmc_segment_c5.json"}
+# The sources a counter profile describes (the kernels, their launch and the
+# image they read): scripts/pmc_bytes.py records their hash in the profile and
+# load_pmc attaches its traffic only to a run of sources that hash the same.
+PMC_SRC = ("wiser_amd/csrc/kernels.hip", "wiser_amd/csrc/kernels.h", "wiser_amd/csrc/engine_types.h",
+           "wiser_amd/csrc/engine.cc", "wiser_amd/csrc/index.cc", "wiser_amd/csrc/index.h")
+
+
+def src_sha(root=ROOT):
+    """sha256 (16 hex digits) of the PMC_SRC files, names and contents."""
+    h = hashlib.sha256()
+    for f in PMC_SRC:
+        h.update(f.encode())
+        with open(os.path.join(root, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 DIAG = {}   # host-side diagnostics of the timed loop (rank 0's)
 DEFERRED = []   # oracle work (parity checks, CPU baselines) run after every timed loop
 
@@ -1023,6 +1039,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     flush()
     barrier()
     sync_all()
+    cs0 = S.comm_stats() if hasattr(S, "comm_stats") else None
     t0 = time.perf_counter()
     for s_ in range(a.steps):
         step(s_)
@@ -1030,6 +1047,11 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
     host_ms = (time.perf_counter() - t0) / max(1, a.steps) * 1e3
     sync_all()
     el = time.perf_counter() - t0
+    comm = None
+    if cs0 is not None:   # what the timed loop's step groups really were
+        cs1 = S.comm_stats()
+        comm = {k: cs1[k] - cs0[k] for k in cs1}
+        comm["mean_group"] = round(comm["steps"] / max(1, comm["groups"]), 3)
     snaps = []
     for i, (hb, hq, hchunk, cb, cheap) in enumerate(steps):   # error flags (a slot overflow among
         hres = S.fetch_owned(hb, hq) if hb else None         # them) of every last step
@@ -1052,7 +1074,7 @@ def run_shard(a, S, full, heavy_blocks, lines, rank, world, dist):
                     x.close()
     return {"queries": queries, "el": el, "p50": statistics.median(lat), "snaps": snaps,
             "slot": slot, "heavy_share": share, "heavy_blocks": heavy_blocks, "every": every,
-            "host_ms": host_ms,
+            "host_ms": host_ms, "comm": comm,
             "batches": [st[3] for st in steps if st[3]] or [st[0] for st in steps if st[0]],
             "engine": full if (full and any(st[3] for st in steps)) else S.engine, "close": close}
 
@@ -1112,6 +1134,17 @@ def run_replica(a, eng, idx, lines, rank, world, dist):
             "host_ms": host_ms, "batches": batches, "engine": eng, "close": close}
 
 
+def group_note(a, comm):
+    """How the timed loop's sharded steps were exchanged, from the
+    communicator's own counters (a group holds each batch once, so it can be
+    smaller than --shard-group)."""
+    if not comm:
+        return f"one host exchange per sharded step (gloo rehearsal, --shard-group {a.shard_group} unused)"
+    return (f"one ncclAllToAll per {comm['mean_group']} sharded steps on average ({comm['groups']} groups, "
+            f"{comm['steps']} steps; --shard-group {a.shard_group} at most), owner replays: "
+            f"{comm['replays_in_lean']} in later lean kernels, {comm['replays_on_stream']} on the exchange stream")
+
+
 def reduce_timing(dist, el, queries, p50, on_gpu, summed):
     """Max wall time and p50 over ranks; queries summed (replicas) or as is."""
     import torch
@@ -1137,7 +1170,11 @@ def load_pmc(workload):
         return None
     try:
         pm = json.load(open(path))
-        out = {"traffic": pm["hbm_bytes_per_launch"], "traffic_source": name,
+        here = src_sha()
+        if pm.get("src_sha") != here:   # profiled on other kernel sources: not this build's bytes
+            return {"traffic": None, "traffic_stale": name,
+                    "traffic_note": f"profile of sources {pm.get('src_sha')}, running {here}"}
+        out = {"traffic": pm["hbm_bytes_per_launch"], "traffic_source": name, "traffic_src_sha": here,
                "traffic_fetch_size_raw": pm["per_launch"].get("FETCH_SIZE", 0.0) * 1024}
         if "algo_bytes_per_launch" in pm:   # the profiled run's own algorithmic bytes
             out["traffic_over_algo"] = round(pm["hbm_bytes_per_launch"] / pm["algo_bytes_per_launch"], 3)
@@ -1202,9 +1239,9 @@ def main():
             # HBM per rank
             r = run_shard(a, S, None, 0, lines, rank, world, dist)
             forms["docshard"] = {**reduced(r), "parallelism": f"docshard{world}", "slot_events": r["slot"],
-                                 "shard_every": r["every"], "hbm_per_rank": shard_bytes,
-                                 "note": f"every query on every shard, one ncclAllToAll per {a.shard_group} sharded steps, "
-                                         "only the rank's shard image resident"}
+                                 "shard_every": r["every"], "hbm_per_rank": shard_bytes, "comm": r["comm"],
+                                 "note": "every query on every shard, only the rank's shard image resident; "
+                                         + group_note(a, r["comm"])}
             r["close"]()
         if a.heavy_blocks != 0 or a.mode == "auto":
             full = open_full(idx, local, threads, rank, world, dist)
@@ -1305,15 +1342,16 @@ def main():
         # host time to enqueue the timed steps: close to ms_per_step = launch-bound
         out["host_enqueue_ms_per_step"] = round(host_ms, 4)
         if mode != "replica":
-            kind = ("one ncclAllToAll of per-owner regions ({count, offset} pairs + fixed event slot) over "
-                    f"xGMI per group of {a.shard_group} sharded steps (wsr_shard_steps), no host round trip "
-                    "inside a step")
+            kind = ("ncclAllToAll of per-owner regions ({count, offset} pairs + fixed event slot) over "
+                    "xGMI per step group (wsr_shard_steps), no host round trip inside a step: "
+                    + group_note(a, main_run["comm"]))
             if a.exchange == "gloo" and world > 1:
                 kind = ("REHEARSAL: fused emit / owner replay with the slots moved by gloo through "
                         "host memory (not the RCCL path's speed)")
             out["exchange"] = {"kind": kind, "slot_events": main_run["slot"],
                                "heavy_blocks": main_run["heavy_blocks"],
                                "shard_every": main_run["every"], "shard_group": a.shard_group,
+                               "comm": main_run["comm"],
                                "heavy_query_share": round(main_run["heavy_share"], 4)}
             out["hbm_per_rank"] = {"shard_image_bytes": shard_bytes, "full_image_bytes": full_bytes,
                                    "total_bytes": (shard_bytes or 0) + (full_bytes or 0),

@@ -313,14 +313,23 @@ int wsr_shard_step(wsr_handle* h, wsr_batch* b, wsr_comm* c, int32_t q_per_owner
  * collective's host cost instead of n.  The owner replays are deferred by
  * default (WSR_REPLAY_DEFER=0: not) into the lean kernels of the step group
  * two groups later; a fetch, wsr_batch_ready or the batch's next run enqueues
- * a still-pending one first.  The communicator's calls (steps, flush, and the
- * joins of its batches) come from one thread; close the communicator before
- * the engine handles whose batches it stepped. */
+ * a still-pending one first.  A batch may be fetched, run or destroyed on
+ * another thread than the one issuing steps (the communicator's lock orders
+ * the deferred replays); close the communicator before the engine handles
+ * whose batches it stepped. */
 int wsr_shard_steps(wsr_handle* h, wsr_batch* const* b, int32_t n, wsr_comm* c, int32_t q_per_owner,
                     int64_t slot);
 /* enqueue every deferred owner replay of the communicator (before timing the
  * whole job on a device synchronize, or closing) */
 int wsr_comm_flush(wsr_comm* c);
+/* What the communicator's step groups did so far: groups (collectives) and
+ * steps (batches), and where each batch's owner replay ran -- in a later
+ * group's lean kernel (deferred) or on the communicator's stream (not
+ * deferred, wide queries, flushed by a fetch / flush / the batch's next step). */
+typedef struct wsr_comm_stats {
+  int64_t groups, steps, replays_in_lean, replays_on_stream;
+} wsr_comm_stats;
+int wsr_comm_stats_get(wsr_comm* c, wsr_comm_stats* out);
 /* wsr_shard_step's two device halves with the transfer left to the caller (a
  * multi-rank rehearsal on one GPU, where RCCL refuses two ranks, or a host
  * exchange): the engine's own region buffers, in the exact layout the step's
@@ -359,6 +368,11 @@ int wsr_debug_decode_block(wsr_handle* h, int32_t list_id, int32_t block, int32_
  * out may be NULL to query. */
 int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_words,
                        int32_t* n_wg, int32_t* stride);
+
+/* Fault injection (tests of the error paths): the next n batch runs -- plain
+ * or the emission of a shard step -- fail with WSR_E_HIP before they enqueue
+ * anything.  n = 0 clears it. */
+int wsr_debug_fail_runs(int32_t n);
 
 /* Host-only check of the dense-list image (no GPU): builds the image of
  * [doc_lo, doc_hi) (doc_hi 0 = all) with the given dense_div and looks each doc
@@ -404,6 +418,11 @@ int wsr_gen_two_term_log(const char* index_dir, int64_t n_queries, uint64_t seed
 /* mixed 1-5 term AND log (AOL term-count shares; SURVEY 8d "C4") */
 int wsr_gen_mixed_log(const char* index_dir, int64_t n_queries, uint64_t seed,
                       const char* out_path, int64_t* n_written);
+/* single-term log (tools/gen_synthetic_log.py:171-189, the run_exp.py:116-117
+ * workloads type_single.docfreq_high / _low): terms drawn with replacement from
+ * the df group, high != 0: df >= 10^4, else df < 10^4 */
+int wsr_gen_single_term_log(const char* index_dir, int32_t high, int64_t n_queries, uint64_t seed,
+                            const char* out_path, int64_t* n_written);
 /* phrase log (tools/gen_synthetic_log.py:254-265) from a synthetic index's
  * phrase pool: one "t1 t2" per line, in double quotes */
 int wsr_gen_phrase_log(const char* index_dir, int64_t n_queries, uint64_t seed,

@@ -15,8 +15,12 @@ are recorded beside the counter bytes.
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def load(pmc_dir):
@@ -62,6 +66,7 @@ if __name__ == "__main__":
                 tot[x] += v
     res = {"kernels": per, "per_launch": dict(tot),
            "hbm_bytes_per_launch": tot.get("read_bytes", 0.0) + tot.get("write_bytes", 0.0),
+           "src_sha": __import__("bench").src_sha(),   # the profiled sources (bench.load_pmc checks it)
            "formula": "read = 128*RDREQ_128B + 32*RDREQ_32B + 64*(RDREQ - both); "
                       "write = 64*WRREQ_64B + 32*(WRREQ - WRREQ_64B) (TCC_EA0, all channels)"}
     if len(sys.argv) > 4:

@@ -269,6 +269,50 @@ def test_native_rccl_deferred_replay(synth_small, monkeypatch, defer):
         S.close()
 
 
+def test_native_rccl_failed_group_flushes_predecessor(synth_small, monkeypatch):
+    """a step group whose emission fails after it has taken the
+    deferred replays of an earlier group must still enqueue them: the earlier
+    group's batches are then fetched (bit-exact) and destroyed without waiting
+    forever in x_join.  The failure is injected (wsr_debug_fail_runs)."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd._capi import lib
+    from wiser_amd.shard import NativeShardedSearcher, slot_for_fill
+    from oracle.oracle import OracleVacuum
+    monkeypatch.setenv("WSR_REPLAY_DEFER", "1")
+    d, _ = synth_small
+    log = os.path.join(d, "qshard_fail.log")
+    w.gen_two_term_log(d, log, n_queries=4 * 256, seed=29)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    S = NativeShardedSearcher(d, 0, 1, share_id=lambda x: x)
+    eng = S.engine
+    n = 256
+    o = OracleVacuum(d)
+    bs = [w.ResidentBatch(eng, n, 10) for _ in range(3)]
+    try:
+        parts = [qs[i * n:(i + 1) * n] for i in range(3)]
+        for b, part in zip(bs, parts):
+            b.upload((_capi.Query * n)(*[eng.resolve(w.SearchQuery(q, n_results=10))[0] for q in part]))
+        S.steps([bs[0]], n, 1 << 20)
+        slot = slot_for_fill(S.max_fill(bs[0]), n)
+        S.steps([bs[0]], n, slot)   # group 0
+        S.steps([bs[1]], n, slot)   # group 1
+        lib.wsr_debug_fail_runs(1)
+        try:
+            with pytest.raises(RuntimeError):
+                S.steps([bs[2]], n, slot)   # takes group 0's replays, then fails
+        finally:
+            lib.wsr_debug_fail_runs(0)
+        for i in (0, 1):
+            hits, nh = S.fetch_owned(bs[i], n)
+            got = [[(hits[q * 10 + j].doc_id, hits[q * 10 + j].score) for j in range(nh[q])] for q in range(n)]
+            assert got == [o.search(q, 10)[0] for q in parts[i]]
+    finally:
+        for b in bs:
+            b.close()
+        S.close()
+
+
 def test_host_exchange_pipelined(synth_small):
     """HostExchangeShardedSearcher (the gloo rehearsal's searcher): each step
     enqueues its emission and then finishes the step before it (exchange,

@@ -66,6 +66,11 @@ class ServeStats(C.Structure):
                 ("handoff_ms", C.c_double)]
 
 
+class CommStats(C.Structure):
+    _fields_ = [("groups", C.c_int64), ("steps", C.c_int64), ("replays_in_lean", C.c_int64),
+                ("replays_on_stream", C.c_int64)]
+
+
 class BuildStats(C.Structure):
     _fields_ = [("n_docs", C.c_int64), ("n_terms", C.c_int64), ("n_postings", C.c_int64),
                 ("vacuum_bytes", C.c_int64), ("docs_char4_ge_0x80", C.c_int64),
@@ -121,6 +126,7 @@ _sigs = {
     "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_close": (None, [_P]),
     "wsr_comm_flush": (C.c_int, [_P]),
+    "wsr_comm_stats_get": (C.c_int, [_P, C.POINTER(CommStats)]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),
     "wsr_shard_steps": (C.c_int, [_P, _P, C.c_int32, _P, C.c_int32, C.c_int64]),
     "wsr_shard_step_emit_async": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
@@ -131,6 +137,7 @@ _sigs = {
     "wsr_shard_step_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "wsr_debug_fail_runs": (C.c_int, [C.c_int32]),
     "wsr_debug_decode_block": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]),
     "wsr_debug_dense_lookup": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p,
@@ -159,6 +166,8 @@ _sigs = {
                                    C.c_double, C.POINTER(ServeStats)]),
     "wsr_gen_mixed_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                     C.POINTER(C.c_int64)]),
+    "wsr_gen_single_term_log": (C.c_int, [C.c_char_p, C.c_int32, C.c_int64, C.c_uint64, C.c_char_p,
+                                          C.POINTER(C.c_int64)]),
     "wsr_gen_phrase_log": (C.c_int, [C.c_char_p, C.c_int64, C.c_uint64, C.c_char_p,
                                      C.POINTER(C.c_int64)]),
     "wsr_snippet": (C.c_int, [_P, C.POINTER(Query), C.c_int32, C.c_int32, C.c_char_p, C.c_int32,

@@ -168,8 +168,10 @@ struct wsr_batch {
   uint64_t x_req = 0;
   std::atomic<uint64_t> x_enq{0};
   // a step group's owner replay of this batch deferred (wsr_shard_steps) and
-  // not yet enqueued: x_join has x_comm enqueue it first
-  wsr_comm* x_comm = nullptr;
+  // not yet enqueued: x_join has x_comm enqueue it first (atomic: a fetch on
+  // one thread may race a step group on another; the communicator's pend_mu
+  // orders what the two do with the group)
+  std::atomic<wsr_comm*> x_comm{nullptr};
   bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
   int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
   int64_t x_slot = 0;           //     and slot (the replay half must match them)
@@ -195,7 +197,7 @@ static void replay_flush(wsr_comm* c, const wsr_batch* upto);
 // worker, or, deferred, by a later step group: enqueued now if still
 // pending), so that xev[1] is the record to wait on.
 static bool x_join(wsr_batch* b) {
-  if (b->x_comm) replay_flush(b->x_comm, b);
+  if (wsr_comm* c = b->x_comm.load(std::memory_order_acquire)) replay_flush(c, b);
   while (b->x_enq.load(std::memory_order_acquire) != b->x_req) std::this_thread::yield();
   return b->x_pending;
 }
@@ -825,8 +827,17 @@ int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
 // region (a shard step).  Wide queries (k > kMaxK) of a plain run are
 // replayed by one more launch after the segments.  oj: an earlier step
 // group's owner replay for the lean kernel's tail (its exchange is done).
+static std::atomic<int32_t> g_fail_runs{0};   // wsr_debug_fail_runs
+
+int wsr_debug_fail_runs(int32_t n) {
+  g_fail_runs.store(n > 0 ? n : 0);
+  return WSR_OK;
+}
+
 static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const OwnerJob* oj) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
+  for (int32_t f = g_fail_runs.load(); f > 0;)
+    if (g_fail_runs.compare_exchange_weak(f, f - 1)) return fail(WSR_E_HIP, "injected run failure");
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
@@ -1228,8 +1239,15 @@ struct wsr_comm {
   std::string err_msg;
   XSlot xs[kXSlots];
   uint64_t n_groups = 0;
+  std::atomic<int64_t> replays_lean{0}, replays_stream{0};   // wsr_comm_stats
   bool defer = true;
-  std::deque<std::shared_ptr<XGroup>> pend;   // deferred groups, oldest first (the calling thread's)
+  // deferred groups, oldest first.  pend, XGroup::queued and the batches'
+  // x_comm are changed by wsr_shard_steps and by whatever flushes a deferred
+  // replay (x_join inside a fetch, upload, run or destroy; wsr_comm_flush),
+  // which may run on other threads: pend_mu orders them (recursive: a step
+  // group flushes its own batches' earlier replays).
+  std::deque<std::shared_ptr<XGroup>> pend;
+  std::recursive_mutex pend_mu;
 };
 
 static void set_comm_err(wsr_comm* c, int rc, const std::string& msg) {
@@ -1293,6 +1311,7 @@ static void run_xjob(wsr_comm* c, const XJob& jp) {
       b->x_pending = rc == WSR_OK;
       b->x_enq.fetch_add(1, std::memory_order_release);
     }
+    c->replays_stream.fetch_add(static_cast<int64_t>(j.bs.size()));
   }
   if (rc != WSR_OK) set_comm_err(c, rc, msg);
   j.enq.store(true, std::memory_order_release);
@@ -1517,6 +1536,7 @@ static void flush_group(wsr_comm* c, XGroup& g) {
   for (size_t i = 0; i < g.bs.size(); ++i) {
     if (g.queued[i]) continue;
     g.queued[i] = 1;
+    c->replays_stream.fetch_add(1);
     wsr_batch* b = g.bs[i];
     if (rc == WSR_OK) {
       rc = step_replay_from(g.h, b, c->rank, c->world, g.qpr, S.recv + region * i, run, c->stream);
@@ -1528,7 +1548,7 @@ static void flush_group(wsr_comm* c, XGroup& g) {
       }
     }
     b->x_pending = rc == WSR_OK;
-    b->x_comm = nullptr;
+    b->x_comm.store(nullptr, std::memory_order_release);
     b->x_enq.fetch_add(1, std::memory_order_release);
   }
   S.n_done = g.bs.size();
@@ -1537,6 +1557,7 @@ static void flush_group(wsr_comm* c, XGroup& g) {
 // Enqueue the deferred replays of every pending group up to the one holding
 // `upto` (all of them: upto null), oldest first.
 static void replay_flush(wsr_comm* c, const wsr_batch* upto) {
+  std::lock_guard<std::recursive_mutex> lk(c->pend_mu);
   if (upto) {
     bool held = false;
     for (const auto& g : c->pend)
@@ -1565,6 +1586,16 @@ int wsr_comm_flush(wsr_comm* c) {
     std::lock_guard<std::mutex> g(c->mu);
     return fail(e, "exchange: " + c->err_msg);
   }
+  return WSR_OK;
+}
+
+int wsr_comm_stats_get(wsr_comm* c, wsr_comm_stats* out) {
+  if (!c || !out) return fail(WSR_E_INVALID, "null argument");
+  std::lock_guard<std::recursive_mutex> lk(c->pend_mu);
+  out->groups = static_cast<int64_t>(c->n_groups);
+  out->steps = static_cast<int64_t>(c->steps);
+  out->replays_in_lean = c->replays_lean.load();
+  out->replays_on_stream = c->replays_stream.load();
   return WSR_OK;
 }
 
@@ -1598,16 +1629,27 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
   };
   const uint64_t region = region_events_of(q_per_owner, slot);
   const uint64_t run = region * static_cast<uint64_t>(n);   // events per owner
+  std::lock_guard<std::recursive_mutex> pend_lock(c->pend_mu);
   const int xs = static_cast<int>(c->n_groups % kXSlots);
   XSlot& S = c->xs[xs];
   std::shared_ptr<XGroup> P;   // the group whose replays this one's lean kernels take
+  // Once P is off pend, every exit enqueues what its lean kernels did not
+  // take on the communicator's stream: on an early error return its batches
+  // would otherwise wait in x_join for replays nobody can find any more.
+  struct FlushRest {
+    wsr_comm* c;
+    std::shared_ptr<XGroup>& P;
+    ~FlushRest() {
+      if (P) flush_group(c, *P);
+    }
+  } flush_rest{c, P};
   std::vector<OwnerJob> oj(static_cast<size_t>(n));
   try {
     HIP_OK(hipSetDevice(h->device));
     // this group's batches: their own earlier replays enqueued first
     for (int i = 0; i < n; ++i) {
       ensure_xev(bs[i]);
-      if (bs[i]->x_comm) replay_flush(c, bs[i]);
+      if (bs[i]->x_comm.load(std::memory_order_acquire)) replay_flush(c, bs[i]);
     }
     // the slot: its previous group's all-to-all and replays enqueued (their
     // end events are what this group's emission and exchange wait for)
@@ -1676,14 +1718,16 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
           hipEventRecord(c->xs[P->xs].done[static_cast<size_t>(i)], b->st) != hipSuccess)
         return fail(WSR_E_HIP, "hipEventRecord failed");
       pb->x_pending = true;
-      pb->x_comm = nullptr;
+      pb->x_comm.store(nullptr, std::memory_order_release);
       P->queued[static_cast<size_t>(i)] = 1;
+      c->replays_lean.fetch_add(1);
       pb->x_enq.fetch_add(1, std::memory_order_release);
     }
   }
   // the rest of P (more batches than this group, or wide ones): the
   // communicator's stream
   if (P) flush_group(c, *P);
+  P.reset();
   lap(0);
   // the exchange half: the communicator's worker thread enqueues it
   auto g = std::make_shared<XGroup>();
@@ -1702,7 +1746,7 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
     std::lock_guard<std::mutex> lk(c->mu);
     for (int i = 0; i < n; ++i) {
       ++bs[i]->x_req;
-      if (g->defer) bs[i]->x_comm = c;
+      if (g->defer) bs[i]->x_comm.store(c, std::memory_order_release);
     }
     c->jobs.push_back(g);
   }
@@ -1987,6 +2031,18 @@ int wsr_gen_mixed_log(const char* index_dir, int64_t n_queries, uint64_t seed,
   if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
   try {
     int64_t n = gen_mixed_log(index_dir, n_queries, seed, out_path);
+    if (n_written) *n_written = n;
+  } catch (const std::exception& e) {
+    return fail(WSR_E_IO, e.what());
+  }
+  return WSR_OK;
+}
+
+int wsr_gen_single_term_log(const char* index_dir, int32_t high, int64_t n_queries, uint64_t seed,
+                      const char* out_path, int64_t* n_written) {
+  if (!index_dir || !out_path) return fail(WSR_E_INVALID, "null argument");
+  try {
+    int64_t n = gen_single_term_log(index_dir, high != 0, n_queries, seed, out_path);
     if (n_written) *n_written = n;
   } catch (const std::exception& e) {
     return fail(WSR_E_IO, e.what());

@@ -1407,6 +1407,17 @@ int64_t gen_mixed_log(const std::string& dir, int64_t n_queries, uint64_t seed,
   return static_cast<int64_t>(out.size());
 }
 
+int64_t gen_single_term_log(const std::string& dir, bool high, int64_t n_queries, uint64_t seed,
+                            const std::string& out_path) {
+  std::vector<std::string> low, hi;
+  df_groups(dir, &low, &hi);
+  const auto& grp = high ? hi : low;
+  std::mt19937_64 g(seed);
+  std::ofstream f(out_path, std::ios::trunc);
+  for (int64_t i = 0; i < n_queries; ++i) f << grp[g() % grp.size()] << "\n";
+  return n_queries;
+}
+
 int64_t gen_phrase_log(const std::string& dir, int64_t n_queries, uint64_t seed,
                        const std::string& out_path) {
   std::ifstream in(dir + "/phrases.txt");

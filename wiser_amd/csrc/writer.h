@@ -96,6 +96,14 @@ int64_t gen_two_term_log(const std::string& index_dir, int64_t n_queries, uint64
 int64_t gen_mixed_log(const std::string& index_dir, int64_t n_queries, uint64_t seed,
                       const std::string& out_path);
 
+// Single-term query log restating tools/gen_synthetic_log.py:171-189
+// (single_term_queries, the run_exp.py:116-117 workloads
+// type_single.docfreq_high / _low): n terms drawn with replacement
+// (rand_items_from_set, :47-58) from the whole df group, "high" (df >= 10^4)
+// or "low" (df < 10^4).
+int64_t gen_single_term_log(const std::string& index_dir, bool high, int64_t n_queries, uint64_t seed,
+                            const std::string& out_path);
+
 // Phrase query log restating tools/gen_synthetic_log.py:254-265: n phrases
 // drawn without replacement from the index's phrase pool (phrases.txt, written
 // by build_synthetic), one per line in double quotes.

@@ -453,6 +453,15 @@ def gen_mixed_log(index_dir: str, out_path: str, n_queries: int = 20_000, seed: 
     return n.value
 
 
+def gen_single_term_log(index_dir: str, out_path: str, high: bool, n_queries: int = 20_000, seed: int = 7) -> int:
+    """Single-term queries of one df group (tools/gen_synthetic_log.py:171-189;
+    run_exp.py:116-117's type_single.docfreq_high / _low)."""
+    n = C.c_int64()
+    check(lib.wsr_gen_single_term_log(index_dir.encode(), 1 if high else 0, n_queries, seed, out_path.encode(),
+                                      C.byref(n)))
+    return n.value
+
+
 def gen_phrase_log(index_dir: str, out_path: str, n_queries: int = 10_000, seed: int = 7) -> int:
     """tools/gen_synthetic_log.py:254-265 over a synthetic index's phrase pool."""
     n = C.c_int64()

@@ -125,10 +125,24 @@ class NativeShardedSearcher:
         return max(tot)
 
     def fetch_owned(self, b, qpr: int):
+        """The owned slice's results.  No flush first: the fetch joins the
+        batch's own deferred owner replay (x_join enqueues it, under the
+        communicator's lock, from whatever thread fetches), and only that one."""
         hits = (_capi.Hit * (qpr * b.stride))()
         nh = (C.c_int32 * qpr)()
         check(lib.wsr_batch_fetch_range(self.engine._h, b._b, self.rank * qpr, qpr, hits, nh))
         return hits, nh
+
+    def sync_all(self):
+        """Every step so far finished on the device (both searchers have it)."""
+        self.flush()
+        check(lib.wsr_sync(self.engine._h))
+
+    def comm_stats(self) -> dict:
+        """Step groups, steps, and where the owner replays ran (wsr_comm_stats_get)."""
+        st = _capi.CommStats()
+        check(lib.wsr_comm_stats_get(self._c, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in st._fields_}
 
     def close(self):
         if self._c:
@@ -207,6 +221,11 @@ class HostExchangeShardedSearcher:
         tot = (C.c_int64 * self.world)()
         check(lib.wsr_shard_fill(self.engine._h, b._b, self.world, tot))
         return max(tot)
+
+    def sync_all(self):
+        """Every step so far finished on the device (both searchers have it)."""
+        self.flush()
+        check(lib.wsr_sync(self.engine._h))
 
     def fetch_owned(self, b, qpr: int):
         self.flush()
