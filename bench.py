@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # scripts/pmc_bytes.py), one profile per workload: attached to lines of that
 # workload only, with the file named in roofline.traffic_source.
 PMC_PROFILES = {"c3": "r04fp_pmc_segment_c3.json", "c2": "r03d_pmc_segment_c2.json",
-                "c4": "r04e_pmc_segment_c4.json", "c5": "r04e_pmc_segment_c5.json"}
+                "c4_mixed_1to5": "r04e_pmc_segment_c4.json", "c5_phrase": "r04e_pmc_segment_c5.json"}
 # The sources a counter profile describes (the kernels, their launch and the
 # image they read): scripts/pmc_bytes.py records their hash in the profile and
 # load_pmc attaches its traffic only to a run of sources that hash the same.
@@ -147,7 +147,8 @@ def parse():
                    help="skip the secondary legs (N=1 only)")
     p.add_argument("--legs", default="",
                    help="comma list of secondary legs to run (default: all of c2_synthetic_1m, "
-                        "end_to_end, c4_mixed_1to5, c5_phrase, c3_topics, serving, c1_snippets)")
+                        "end_to_end, c4_mixed_1to5, single_high, single_low, c5_phrase, realistic_mix, "
+                        "c3_topics, serving, c1_snippets)")
     p.add_argument("--c3-docs", type=int, default=5_500_000)
     p.add_argument("--c3-term-scale", type=float, default=1.0)
     p.add_argument("--check", type=int, default=256, help="queries checked against the oracle")
@@ -300,14 +301,15 @@ def snapshot(idx, chunk, hits, nh, k, n, phrase=False):
     every bench check runs after all timed loops, on results of the last run."""
     got = [[(hits[i * k + j].doc_id, hits[i * k + j].score) for j in range(nh[i])]
            for i in range(min(n, len(chunk)))]
-    return {"idx": idx, "chunk": [list(t) for t in chunk[:n]], "got": got, "k": k, "phrase": phrase}
+    phrases = list(phrase[:n]) if isinstance(phrase, (list, tuple)) else [bool(phrase)] * len(got)
+    return {"idx": idx, "chunk": [list(t) for t in chunk[:n]], "got": got, "k": k, "phrases": phrases}
 
 
 def verify_snapshot(snap):
     from oracle.oracle import OracleVacuum
     orc = OracleVacuum(snap["idx"])
-    for terms, got in zip(snap["chunk"], snap["got"]):
-        want, _ = orc.search(terms, snap["k"], phrase=snap["phrase"])
+    for terms, got, ph in zip(snap["chunk"], snap["got"], snap["phrases"]):
+        want, _ = orc.search(terms, snap["k"], phrase=ph)
         if got != want:
             raise SystemExit(f"parity failure on {terms}: {got[:3]} vs {want[:3]}")
     orc.close()
@@ -427,7 +429,7 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
         hits, nh = b.fetch()
     snaps = []
     if check:   # batch 0's last timed run, checked after every timed loop (snapshot)
-        snaps.append(snapshot(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=bool(chunks[0][0][1])))
+        snaps.append(snapshot(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=[p for _, p in chunks[0]]))
     nq = len(items) * passes
     for b in batches:
         b.close()
@@ -550,6 +552,46 @@ def end_to_end_leg(a, idx, qlog, local, threads):
     return out
 
 
+# Legs over the headline index: its log (in a.index_dir), what it is, whether
+# the engine needs positions.  The single-term legs are the reference's
+# run_exp.py:116-117 workloads (type_single.docfreq_high / _low,
+# gen_synthetic_log.py:171-189); realistic_mix is its mixed log
+# (query_pool.h:363-375, run_exp.py:119 "type_realistic"): 10 % phrases among
+# the 1-5-term AND mix in the same batches.
+LEG_LOGS = {
+    "c4_mixed_1to5": ("mixed_{tag}_20000.log", "w.gen_mixed_log({idx!r}, {log!r}, n_queries=20000, seed=7)",
+                      False, "{tag}: 20000 AND queries of 1-5 terms (AOL term-count shares, gen_synthetic_log "
+                             "group rule, seed 7), top-10"),
+    "c5_phrase": ("phrase_{tag}_10000.log", "w.gen_phrase_log({idx!r}, {log!r}, n_queries=10000, seed=7)",
+                  True, "{tag}: 10000 two-term phrase queries from the corpus's phrase pool "
+                        "(gen_synthetic_log.py:216-265), top-10"),
+    "single_high": ("single_high_{tag}_20000.log",
+                    "w.gen_single_term_log({idx!r}, {log!r}, True, n_queries=20000, seed=7)",
+                    False, "{tag}: 20000 single-term queries of the df >= 10^4 group (run_exp.py:116 "
+                           "type_single.docfreq_high, gen_synthetic_log.py:171-189), top-10"),
+    "single_low": ("single_low_{tag}_20000.log",
+                   "w.gen_single_term_log({idx!r}, {log!r}, False, n_queries=20000, seed=7)",
+                   False, "{tag}: 20000 single-term queries of the df < 10^4 group (run_exp.py:117 "
+                          "type_single.docfreq_low), top-10"),
+    "realistic_mix": ("realistic_{tag}_20000.log",
+                      "w.gen_realistic_log({idx!r}, {log!r}, n_queries=20000, phrase_share=0.1, seed=7)",
+                      True, "{tag}: 20000 queries, 10 % two-term phrases among the 1-5-term AND mix in the "
+                            "same batches (query_pool.h:363-375 format), top-10"),
+}
+
+
+def leg_items(a, idx, name):
+    """-> (items [(terms, is_phrase)], workload text, positions) of a LEG_LOGS leg
+    (its log written first when missing, in a child process)."""
+    import wiser_amd as w
+    fname, gen, positions, what = LEG_LOGS[name]
+    tag = os.path.basename(idx.rstrip("/"))
+    log = os.path.join(a.index_dir, fname.format(tag=tag))
+    if not os.path.exists(log):
+        in_child(gen.format(idx=idx, log=log) + "\nprint('{}')")
+    return w.read_query_log(log), what.format(tag=tag), positions
+
+
 def extra_legs(a, idx, qlog, local, threads):
     """The other legs of one N = 1 run: C2 (configs[1]) as a leg of its own,
     then over the headline index: the whole Search chain from strings
@@ -577,45 +619,52 @@ def extra_legs(a, idx, qlog, local, threads):
         legs["c2_synthetic_1m"] = c2_leg(a, local, threads)
     if want("end_to_end"):
         legs["end_to_end"] = end_to_end_leg(a, idx, qlog, local, threads)
-    tag = os.path.basename(idx.rstrip("/"))
-    if want("c4_mixed_1to5"):
-        mixed = os.path.join(a.index_dir, f"mixed_{tag}_20000.log")
-        if not os.path.exists(mixed):
-            in_child(f"w.gen_mixed_log({idx!r}, {mixed!r}, n_queries=20000, seed=7)\nprint('{{}}')")
-        eng = w.VacuumEngine(idx, device=local, threads=threads, positions=False)
-        eng.Load()
-        items = [(l.split(), False) for l in open(mixed).read().splitlines()]
-        legs["c4_mixed_1to5"] = run_leg(eng, idx, items, a.k, a.batch, 4, a.check,
-                                        0 if a.no_cpu else a.cpu_seconds / 4)
-        legs["c4_mixed_1to5"]["workload"] = (f"{tag}: 20000 AND queries of 1-5 terms (AOL term-count "
-                                             "shares, gen_synthetic_log group rule, seed 7), top-10")
-        pmc = load_pmc("c4") if a.workload == "c3" and not (a.vacuum_dir or a.linedoc) else None
+    synthetic = a.workload == "c3" and not (a.vacuum_dir or a.linedoc)
+    has_pool = os.path.exists(os.path.join(idx, "phrases.txt"))
+    engines = {}
+
+    def engine(positions):   # one engine per positions setting, shared by the legs
+        if positions not in engines:
+            e = w.VacuumEngine(idx, device=local, threads=threads, positions=positions)
+            t = time.time()
+            e.Load()
+            engines[positions] = (e, round(time.time() - t, 1))
+        return engines[positions]
+
+    for name in ("c4_mixed_1to5", "single_high", "single_low", "c5_phrase", "realistic_mix"):
+        if not want(name) or (LEG_LOGS[name][2] and not has_pool and name == "realistic_mix"):
+            continue
+        lidx = idx
+        if name == "c5_phrase" and not has_pool:   # (the pool of a synthetic corpus)
+            lidx = c2_idx = ensure_c2(a)[0]
+        items, what, positions = leg_items(a, lidx, name)
+        if lidx == idx:
+            eng, load_s = engine(positions)
+        else:
+            eng = w.VacuumEngine(lidx, device=local, threads=threads, positions=positions)
+            t = time.time()
+            eng.Load()
+            load_s = round(time.time() - t, 1)
+        leg = run_leg(eng, lidx, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 4)
+        leg["workload"] = what
+        if positions:
+            leg["load_s"] = load_s
+            leg["image"] = eng.image_info()
+        pmc = load_pmc(name) if (lidx == idx and synthetic) else None
         if pmc:
-            legs["c4_mixed_1to5"]["roofline"].update(pmc)
-        eng.close()
-    if want("c5_phrase"):
-        pidx = idx
-        if not os.path.exists(os.path.join(idx, "phrases.txt")):
-            pidx = c2_idx = ensure_c2(a)[0]   # (the pool of a synthetic corpus)
-        ptag = os.path.basename(pidx.rstrip("/"))
-        phr = os.path.join(a.index_dir, f"phrase_{ptag}_10000.log")
-        if not os.path.exists(phr):
-            in_child(f"w.gen_phrase_log({pidx!r}, {phr!r}, n_queries=10000, seed=7)\nprint('{{}}')")
-        t = time.time()
-        eng = w.VacuumEngine(pidx, device=local, threads=threads, positions=True)
-        eng.Load()
-        load_s = round(time.time() - t, 1)
-        items = w.read_query_log(phr)
-        legs["c5_phrase"] = run_leg(eng, pidx, items, a.k, a.batch, 4, a.check,
-                                    0 if a.no_cpu else a.cpu_seconds / 4)
-        legs["c5_phrase"]["load_s"] = load_s
-        legs["c5_phrase"]["image"] = eng.image_info()
-        legs["c5_phrase"]["workload"] = (f"{ptag}: 10000 two-term phrase queries from the corpus's "
-                                         "phrase pool (gen_synthetic_log.py:216-265), top-10")
-        pmc = load_pmc("c5") if pidx == idx and a.workload == "c3" and not (a.vacuum_dir or a.linedoc) else None
-        if pmc:
-            legs["c5_phrase"]["roofline"].update(pmc)
-        eng.close()
+            leg["roofline"].update(pmc)
+        if lidx != idx:
+            eng.close()
+        legs[name] = leg
+    if "realistic_mix" in legs and "c4_mixed_1to5" in legs and "c5_phrase" in legs:
+        # the share-weighted pure legs: the time per query of 90 % AND mix and 10 % phrases
+        items, _, _ = leg_items(a, idx, "realistic_mix")
+        f = sum(1 for _, ph in items if ph) / len(items)
+        exp = 1.0 / ((1 - f) / legs["c4_mixed_1to5"]["value"] + f / legs["c5_phrase"]["value"])
+        legs["realistic_mix"]["weighted_pure_legs"] = round(exp, 1)
+        legs["realistic_mix"]["vs_weighted_pure_legs"] = round(legs["realistic_mix"]["value"] / exp, 3)
+    for e, _ in engines.values():
+        e.close()
     if want("c3_topics") and a.workload == "c3" and not (a.vacuum_dir or a.linedoc):
         legs["c3_topics"] = topics_leg(a, local, threads)
     if want("c1_snippets"):

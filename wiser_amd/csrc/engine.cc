@@ -106,6 +106,7 @@ struct wsr_handle {
   uint32_t* d_bkt = nullptr;        // offset buckets (entries and offset bytes)
   uint8_t* d_tf8 = nullptr;
   uint8_t* d_plen = nullptr;
+  float* d_bmax = nullptr;
   uint32_t* d_tails = nullptr;
   uint8_t* d_pos_blob = nullptr;    // positions (opened with wsr_open_opts::positions)
   PosDev* d_pos_lists = nullptr;
@@ -221,7 +222,7 @@ wsr_image_info image_info_of(const HostImage& img, size_t n_c4) {
   o.blob_bytes = dev_bytes(img.blob);
   o.plen_bytes = dev_bytes(img.plen);
   o.dir_bytes = dev_bytes(img.tails) + dev_bytes(img.lists) + dev_bytes(img.blocks) + dev_bytes(img.blk_last) +
-                dev_bytes(img.blk_meta) + std::max<uint64_t>(n_c4, 1);
+                dev_bytes(img.blk_meta) + dev_bytes(img.bmax) + std::max<uint64_t>(n_c4, 1);
   o.dense_lists = img.dense_lists;
   o.n_lists = static_cast<uint32_t>(img.lists.size());
   o.total_bytes = o.blob_bytes + o.dense_bytes + o.tf8_bytes + o.plen_bytes + o.dir_bytes + o.pos_bytes;
@@ -357,6 +358,8 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->info.blob_bytes = dev_upload(&h->d_blob, img.blob);
     h->info.plen_bytes = dev_upload(&h->d_plen, img.plen);
     h->args.plen = h->d_plen;
+    h->info.dir_bytes += dev_upload(&h->d_bmax, img.bmax);
+    h->args.bmax = h->d_bmax;
     h->info.dir_bytes += dev_upload(&h->d_tails, img.tails);
     h->args.tails = h->d_tails;
     h->info.dir_bytes += dev_upload(&h->d_lists, img.lists);
@@ -416,7 +419,7 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_c4), static_cast<void*>(h->d_cache),
                   static_cast<void*>(h->d_dense), static_cast<void*>(h->d_dense_rk),
                   static_cast<void*>(h->d_bkt), static_cast<void*>(h->d_tf8),
-                  static_cast<void*>(h->d_plen), static_cast<void*>(h->d_tails),
+                  static_cast<void*>(h->d_plen), static_cast<void*>(h->d_bmax), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
                   static_cast<void*>(h->d_pos_start), static_cast<void*>(h->d_blm),

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <fcntl.h>
 #include <fstream>
+#include <limits>
 #include <mutex>
 #include <stdexcept>
 #include <sys/mman.h>
@@ -364,6 +365,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   const uint32_t span = span_end > doc_lo ? static_cast<uint32_t>(span_end - doc_lo) : 0u;
   const uint64_t n_ent = (static_cast<uint64_t>(span) + kDenseDocs - 1) / kDenseDocs;   // entries per bitmap
   const std::vector<uint8_t>& c4 = idx.char4_lengths();
+  const double* norm = idx.bm25_cache();   // Bm25Similarity cache_ (scoring.h:85-90)
   struct Info {            // pass 1: the list's share of the image
     uint32_t r0 = 0, r1 = 0;   // image rows [r0, r1); r0 >= r1: no docs in the image
     uint32_t fcnt = 0;         // postings of the list's final row
@@ -489,14 +491,14 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
 
   lap("pass 1 (sizes)");
   if (hbm_free) {
-    // the rest of the image: blob, directory and plen (152 B per block),
+    // the rest of the image: blob, directory, plen and bmax (156 B per block),
     // decoded tails, blooms (positions are not sized yet: the 10 % margin)
     uint64_t other = static_cast<uint64_t>(std::max(idx.n_docs(), 0));
     for (int32_t id = 0; id < L; ++id) {
       const Info& in = info[id];
       if (in.r1 <= in.r0) continue;
       const uint64_t nbl = in.r1 - in.r0;
-      other += in.bytes + nbl * (sizeof(BlockDev) + 8 + kPackSize) + (in.vtail ? 8ull * in.tail_cnt : 0);
+      other += in.bytes + nbl * (sizeof(BlockDev) + 12 + kPackSize) + (in.vtail ? 8ull * in.tail_cnt : 0);
       if (blooms && positions) other += nbl * kPackSize * 32;
     }
     const uint64_t cap = hbm_free / 10 * 9;
@@ -574,6 +576,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   img.blk_last.resize(nb);
   img.blk_meta.resize(nb);
   img.plen.resize(nb * kPackSize);
+  img.bmax.resize(nb);
   img.tails.resize(ntail);
   img.dense.resize(ne);
   img.dense_rank.resize(kRankWords * ne);
@@ -653,13 +656,21 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       for (int i = 0; i < cnt; ++i) o[i] = docs[i] < c4.size() ? c4[docs[i]] : 0;
       for (int i = cnt; i < kPackSize; ++i) o[i] = 0;
       const bool last_vints = in.vtail && r + 1 == nrows;
-      if (in.dense || last_vints) {
-        if (!host_decode_block(pf, fend, cnt, false, 0, tfs))
-          throw std::runtime_error("cannot decode the tfs of '" + idx.term(id) + "'");
-        for (int i = 0; i < cnt; ++i) tfmax = std::max(tfmax, tfs[i]);
-      } else {
-        tfmax = std::max(tfmax, bf == 0 ? ~0u : bf >= 32 ? ~0u : (1u << bf) - 1u);
+      if (!host_decode_block(pf, fend, cnt, false, 0, tfs))
+        throw std::runtime_error("cannot decode the tfs of '" + idx.term(id) + "'");
+      // the block's largest TfNormLossy, by the kernels' operations in their
+      // order (f64), then rounded up to f32 so that idf times it never falls
+      // below a score of the block
+      double bm = 0.0;
+      for (int i = 0; i < cnt; ++i) {
+        tfmax = std::max(tfmax, tfs[i]);
+        const double f = static_cast<double>(static_cast<int32_t>(tfs[i]));
+        const double t = (f * (1.2 + 1)) / (f + norm[o[i]]);
+        bm = t > bm ? t : bm;
       }
+      float bmf = static_cast<float>(bm);
+      if (static_cast<double>(bmf) < bm) bmf = std::nextafter(bmf, std::numeric_limits<float>::infinity());
+      img.bmax[j] = bmf;
       if (last_vints) {   // the list's VInts tail, decoded once (the kernels read it as words)
         std::memcpy(&img.tails[ld.tail], docs, cnt * sizeof(uint32_t));
         std::memcpy(&img.tails[ld.tail + cnt], tfs, cnt * sizeof(uint32_t));

@@ -135,6 +135,9 @@ struct HostImage {
   big_vector<uint32_t> tails;   // decoded VInts last blocks (ListDev::tail)
   big_vector<uint8_t> plen;     // doc-length code (Char4) of every posting: block j of the
                                 // image at [j * 128, j * 128 + 128), 0 past the length records
+  big_vector<float> bmax;       // per block: the largest TfNormLossy (tf * 2.2) / (tf + cache_[c4])
+                                // of its postings (scoring.h:65-69), f32 rounded up: idf times it
+                                // bounds every score of the block (single-term block skipping)
   // positions (build_image(..., positions = true)): see PosDev
   bool has_positions = false;
   std::vector<uint8_t> pos_blob;

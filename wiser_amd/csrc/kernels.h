@@ -31,6 +31,7 @@ struct IndexArgs {
   uint32_t seg_cap;         // driver blocks per work item at most (kSegCost; the batch's own, see
                             // wsr_batch_set_item_blocks: a latency-bound caller takes shorter items)
   const uint8_t* plen;      // doc-length code of each posting, 128 per block (HostImage::plen)
+  const float* bmax;        // per block: its largest TfNormLossy, f32 rounded up (HostImage::bmax)
   const uint32_t* tails;    // decoded VInts last blocks (ListDev::tail)
   // positions (phrase queries; null unless the engine was opened with them)
   const uint8_t* pos_blob;  // every list's position cozy box, byte-exact from my.vacuum

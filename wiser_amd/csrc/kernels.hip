@@ -1289,6 +1289,25 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
   sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
 }
 
+// A one-item query's events straight from the lean kernel's LDS buffer (lane
+// i = event i, doc order, n <= 64) through the restated heap.  Out of line, so
+// the lean kernel's registers are its own; every uniform argument is made
+// wave-uniform at entry (a callee's arguments arrive in VGPRs: the heap's
+// loops must not compile as divergent ones).
+__device__ __noinline__ void replay_lds_call(double sc, int32_t dc, uint32_t n, uint32_t k, HitDev* out,
+                                             int32_t* n_out) {
+  const uint64_t o = reinterpret_cast<uint64_t>(out), no = reinterpret_cast<uint64_t>(n_out);
+  out = reinterpret_cast<HitDev*>(static_cast<uint64_t>(uni(static_cast<uint32_t>(o))) |
+                                  (static_cast<uint64_t>(uni(static_cast<uint32_t>(o >> 32))) << 32));
+  n_out = reinterpret_cast<int32_t*>(static_cast<uint64_t>(uni(static_cast<uint32_t>(no))) |
+                                     (static_cast<uint64_t>(uni(static_cast<uint32_t>(no >> 32))) << 32));
+  n = uni(n);
+  HeapSink sink;
+  sink.k = uni(k);
+  sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
+  sink.finish(out, n_out);
+}
+
 // out-of-line copy for the segment kernel (keeps its register allocation
 // independent of the replay code; called once per query)
 __device__ __noinline__ void replay_query_call(const QueryIn* qs, const QueryPlan* plan, int qi,
@@ -1771,7 +1790,7 @@ struct LeanLdsT {
   uint32_t dmeta[64];
 };
 
-// o1 == kNoSlot: single-term query, every posting of the driver survives.
+// (single-term items run single_segment: every item here has an O1.)
 // tdoc/ttf: the driver's VInts tail block (doc ids, tfs; 2 per lane) when
 // dtail, used for block b1 - 1.
 // kTwo: every item of the launch is a two-term, k <= kMaxK query (the
@@ -1791,8 +1810,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t b0, uint32_t b1, bool dtail,
                                              uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
-                                             const uint64_t* prev_pub, uint32_t n_prev, uint64_t* my_pub,
-                                             Event* ev_out, uint32_t& ev_n,
+                                             uint64_t floor0, const uint64_t* prev_pub, uint32_t n_prev,
+                                             uint64_t* my_pub,
+                                             Event* ev_out, uint32_t& ev_n, uint32_t& evb,
                                              double& pt, uint32_t& pt_n,
                                              double& last_pub, uint32_t& n_surv, uint32_t& n_dblk) {
   const uint32_t l = threadIdx.x & 63;
@@ -1803,20 +1823,19 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   // k > kMaxK: every survivor is an event; the replay's heap in LDS decides
   const bool wide = !kTwo && k > static_cast<uint32_t>(kMaxK);
   const uint32_t min_last = in_vgpr(Q.min_last);
-  const bool single = !kTwo && !kBk && o1 == kNoSlot;
-  // O1's bitmap (single term: reads go to a valid dummy word; the image may
-  // have no bitmaps): the probe reads the mask word alone; a hit reads its
-  // rank record (H stage)
-  const uint32_t* o_mk = (single || kBk) ? ix.blk_last : &ix.dense[Q.o_bm].w;
-  const uint2* o_rk = (single || kBk) ? reinterpret_cast<const uint2*>(ix.blk_last)
-                                      : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
+  // O1's bitmap (buckets: reads go to a valid dummy word; the image may have
+  // no bitmaps): the probe reads the mask word alone; a hit reads its rank
+  // record (H stage)
+  const uint32_t* o_mk = kBk ? ix.blk_last : &ix.dense[Q.o_bm].w;
+  const uint2* o_rk = kBk ? reinterpret_cast<const uint2*>(ix.blk_last)
+                          : reinterpret_cast<const uint2*>(ix.dense_rk) + Q.o_bm;
   auto o_probe = [&](uint32_t e) __attribute__((always_inline)) { return o_mk[e]; };
   auto probe_bit = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) { return ((v >> sh) & 1u) != 0u; };
   // posting rank of a hit, without the rank word (added at compaction)
   auto probe_rank = [&](uint32_t v, uint32_t sh) __attribute__((always_inline)) {
     return static_cast<uint32_t>(__popc(v & ((1u << sh) - 1u)));
   };
-  const uint8_t* o_tf8 = single ? reinterpret_cast<const uint8_t*>(ix.blk_last) : ix.tf8 + Q.o_tf8;
+  const uint8_t* o_tf8 = ix.tf8 + Q.o_tf8;
   // buckets (kBk): entries, shift and offset bytes of O1
   const uint32_t bsh = kBk ? static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit) : 0u;
   const uint2* o_bk = kBk ? ix.bkt + (Q.o_bm & kProbeBaseMask) : nullptr;
@@ -1824,7 +1843,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   const uint32_t o_tf8_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_tf8)) & 3u;
   const uint32_t o_off_mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(o_off)) & 3u;
   const uint8_t* a_blob = ix.blob + Q.a_base;
-  uint32_t evb = 0;
   const uint32_t lo = in_vgpr(ix.doc_lo), span = in_vgpr(ix.dense_span);
   const uint32_t hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);   // docs a with a - lo < hi_rel are in the image
   const double idf_d = in_vgpr(Q.a_idf), idf_o = in_vgpr(Q.o_idf);
@@ -1843,7 +1861,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
   // here; the segment's own k-th best is published once, at the end; events
   // stay in LDS until 64 are pending (a chunk adds at most 64).  The final
   // re-filter in finish_item applies the floor as it stands at the end.
-  uint64_t floor_bits = prev_pub ? floor_max(floor_lanes(prev_pub, n_prev)) : 0ull;
+  uint64_t floor_bits = prev_pub ? floor_max(floor0) : 0ull;   // (floor0: the caller's floor_lanes)
   double pub_val = 0.0;
   // Floor refresh (every kFloorRefresh driver blocks): the item publishes
   // its floor as it stands (the k-th best of docs before the next item) and
@@ -1892,7 +1910,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     const uint32_t pd = kPh ? qpd[e] : 0u, po = kPh ? qpo[e] : 0u;
     __builtin_amdgcn_wave_barrier();
     qhead += n;
-    if (!single && __ballot(alive && (to & 0x80000000u))) {   // O1's tf bytes by rank (bit 31: a rank)
+    if (__ballot(alive && (to & 0x80000000u))) {   // O1's tf bytes by rank (bit 31: a rank)
       const bool rk = alive && (to & 0x80000000u);
       uint32_t t = load_byte(o_tf8 + (rk ? (to & 0x7FFFFFFFu) : 0u));
       if (__ballot(rk && t == kTf8Escape)) {
@@ -1910,7 +1928,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     for (uint32_t s = 0; s < (kTwo ? 0u : nt); ++s) {
       if (s == d) {
         sc += bm25_term(idf_d, alive ? td : 0u, norm);
-        if (single) break;
       } else if (s == o1) {
         sc += bm25_term(idf_o, alive ? to : 0u, norm);
       } else {
@@ -1949,6 +1966,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     if (am == 0) return;
     n_surv += __popcll(am);
     if (wide) {   // all of them, in doc order (lane order), no floor
+      if (evb + __popcll(am) > kLeanEvs) flush();
       if (alive) {
         Event ev;
         ev.score = sc;
@@ -1958,7 +1976,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       }
       ev_n += __popcll(am);
       evb += __popcll(am);
-      if (evb >= kLeanEvs - 64) flush();
       return;
     }
     // running top-k: candidates beat the k-th best so far and the floor of the
@@ -1976,6 +1993,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       const uint32_t dv = __builtin_amdgcn_readlane(doc, fl);
       const uint32_t pos = __popcll(__ballot(l < pt_n && pt >= sv));
       if (pos < k) {
+        if (evb == kLeanEvs) flush();
         if (l == 0) {
           Event ev;
           ev.score = sv;
@@ -1991,7 +2009,6 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
         pt_n = pt_n + 1 > k ? k : pt_n + 1;
       }
     }
-    if (evb && evb >= kLeanEvs - 64) flush();
     const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
     const double pv = kn > flo ? kn : flo;
     pub_val = pv > pub_val ? pv : pub_val;
@@ -2142,15 +2159,15 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t s0 = q0 % kDenseDocs, s1 = q1 % kDenseDocs;
       // (bitwise, not short-circuit: the compiler would branch on each term)
-      const bool h0 = (X.da0 != ~0u) & (single | ((q0 < span) & probe_bit(X.de0, s0)));
-      const bool h1 = (X.da1 != ~0u) & (single | ((q1 < span) & probe_bit(X.de1, s1)));
+      const bool h0 = (X.da0 != ~0u) & (q0 < span) & probe_bit(X.de0, s0);
+      const bool h1 = (X.da1 != ~0u) & (q1 < span) & probe_bit(X.de1, s1);
       const uint32_t x0 = probe_rank(X.de0, s0);
       const uint32_t x1 = probe_rank(X.de1, s1);
       // the hits' rank records (O1's tf bytes past a word's first four postings
       // are read by rank when the chunk is scored)
-      Y.hf0 = o_rk[(h0 && !single) ? q0 / kDenseDocs : 0u];
-      Y.hf1 = o_rk[(h1 && !single) ? q1 / kDenseDocs : 0u];
-      // (ranks are < 2^31; a single-term item's are unused)
+      Y.hf0 = o_rk[h0 ? q0 / kDenseDocs : 0u];
+      Y.hf1 = o_rk[h1 ? q1 / kDenseDocs : 0u];
+      // (ranks are < 2^31)
       Y.hx0 = h0 ? (x0 & 0x7FFFFFFFu) : 0x80000000u;
       Y.hx1 = h1 ? (x1 & 0x7FFFFFFFu) : 0x80000000u;
 
@@ -2192,8 +2209,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       // (branch-free: the bound of a lane past the block is computed and dropped)
       const bool p0 = ok0 & (bound(t0, c0) > thr_s);
       const bool p1 = ok1 & (bound(t1, c1) > thr_s);
-      const bool in0 = !single & p0 & (a0 - lo < span);
-      const bool in1 = !single & p1 & (a1 - lo < span);
+      const bool in0 = p0 & (a0 - lo < span);
+      const bool in1 = p1 & (a1 - lo < span);
       if constexpr (kBk) {
         Y.de0 = o_bk[in0 ? (a0 - lo) >> bsh : 0u];
         Y.de1 = o_bk[in1 ? (a1 - lo) >> bsh : 0u];
@@ -2239,10 +2256,187 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     body(R1, R0, j + 1);
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
-  if (evb) flush();
+  // (the last evb events stay in S.evs: the item's end re-filters or replays
+  // them from there, finish_lean_item)
   if (my_pub && pub_val > last_pub && l == 0)
     __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  last_pub = pub_val;
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------ single-term segment --
+// A single-term item (SingleTermQueryProcessor::Process, query_processing.h:
+// 620-642: every posting of the list is scored and offered to the heap).
+// A posting's score is its own term's, so the threshold known before it -- the
+// floor of the query's earlier items and the item's own running k-th best --
+// rules whole blocks out: a block whose bound, idf x its largest TfNormLossy
+// (IndexArgs::bmax, f32 rounded up at load), is at most that threshold holds no
+// heap insertion and is skipped with no load at all.  The blocks that remain
+// are read in one round each (doc-id and tf pack words, the doc-length line),
+// the next remaining block's loads in flight while one is scored; inside a
+// block each posting's own bound (its tf and length, f32) leaves only the
+// candidates for the f64 score and the running top-k.  Safety of the f32
+// bounds: as the lean pipeline's pre-probe pruning (kPruneMargin).
+template <bool kPh>
+__device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
+                                               const QueryDesc& Q, uint32_t b0, uint32_t b1, bool dtail,
+                                               uint32_t tdoc0, uint32_t tdoc1, uint32_t ttf0, uint32_t ttf1,
+                                               uint64_t floor0, const uint64_t* prev_pub, uint32_t n_prev,
+                                               uint64_t* my_pub, Event* ev_out, uint32_t& ev_n, uint32_t& evb, double& pt,
+                                               uint32_t& pt_n, double& last_pub, uint32_t& n_surv,
+                                               uint32_t& n_dblk) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t k = Q.k;
+  const bool wide = k > static_cast<uint32_t>(kMaxK);   // every posting is an event
+  constexpr float kPruneMargin = 0.998f;
+  const uint8_t* a_blob = ix.blob + Q.a_base;
+  const uint32_t lo = in_vgpr(ix.doc_lo), hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);
+  const double idf = Q.a_idf;
+  const float b_id = Q.b_id, idf_f = static_cast<float>(Q.a_idf);
+  // this item's block bounds, one per lane (blocks b0 + l)
+  const float bmax = b0 + l < b1 ? ix.bmax[Q.a_blk0 + b0 + l] * idf_f : 0.0f;
+  uint64_t floor_bits = prev_pub ? floor_max(floor0) : 0ull;   // (floor0: the caller's floor_lanes)
+  auto as_f64 = [](uint64_t b) __attribute__((always_inline)) {
+    return __longlong_as_double(static_cast<long long>(
+        (static_cast<uint64_t>(uni(static_cast<uint32_t>(b >> 32))) << 32) | uni(static_cast<uint32_t>(b))));
+  };
+  double flo = as_f64(floor_bits);
+  float thr_s = wide ? -1.0f : static_cast<float>(flo) * kPruneMargin;
+  double pub_val = 0.0, sent = 0.0;
+  uint64_t floor_next = 0;
+  uint32_t n_done = 0;
+  // the first block at or after b whose bound passes the threshold (b1: none)
+  auto next_block = [&](uint32_t b) __attribute__((always_inline)) {
+    const uint64_t m = __ballot(b0 + l >= b && bmax > thr_s);
+    return m ? b0 + static_cast<uint32_t>(__builtin_ctzll(m)) : b1;
+  };
+  struct Regs {
+    uint32_t w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0, wc = 0, b = 0;
+  };
+  auto issue = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
+    const uint32_t bi = b < b1 ? b - b0 : 0u;
+    const uint32_t m = uni(S.dmeta[bi]);
+    const uint4 e = S.dblk[bi];
+    uint32_t sh;
+    pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
+    pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.t0, Y.t1, Y.t2, sh);
+    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
+    Y.b = b;
+  };
+  auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
+    const uint32_t bit = 2 * l * bits;
+    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a_blob)) + rel + 2 + (bit >> 3);
+    return ((a & 3u) << 3) + (bit & 7u);
+  };
+  auto flush = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    if (l < evb) store_event_coherent(&ev_out[ev_n - evb + l], S.evs[l]);
+    __builtin_amdgcn_wave_barrier();
+    evb = 0;
+  };
+  // score block X.b (its loads were issued one block earlier)
+  auto score = [&](const Regs& X) __attribute__((always_inline)) {
+    const uint32_t b = X.b, bi = b - b0;
+    const uint4 be = S.dblk[bi];
+    const uint32_t m = uni(S.dmeta[bi]);
+    const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
+    const uint32_t cnt = (b == Q.a_nblk - 1) ? Q.a_tail_cnt : 128u;
+    uint32_t x0, x1, t0, t1;
+    pair_values(X.w0, X.w1, X.w2, pair_shift(uni(be.z), wbits), wbits, x0, x1);
+    pair_values(X.t0, X.t1, X.t2, pair_shift(uni(be.w), wtb), wtb, t0, t1);
+    const uint32_t sm = x0 + x1;
+    const uint32_t inc = wave_incl_scan(sm);
+    uint32_t a0 = uni(be.x) + (inc - sm) + x0;
+    uint32_t a1 = a0 + x1;
+    if (dtail && b == b1 - 1) { a0 = tdoc0; a1 = tdoc1; t0 = ttf0; t1 = ttf1; }
+    const uint32_t c0 = (X.wc >> ((l & 1u) << 4)) & 0xFFu;
+    const uint32_t c1 = (X.wc >> (((l & 1u) << 4) + 8)) & 0xFFu;
+    const float nf0 = static_cast<float>(norm_tab[c0]), nf1 = static_cast<float>(norm_tab[c1]);
+    const float f0 = static_cast<float>(t0), f1 = static_cast<float>(t1);
+    const bool p0 = (2 * l < cnt) & (a0 - lo < hi_rel) & (b_id * f0 * __builtin_amdgcn_rcpf(f0 + nf0) > thr_s);
+    const bool p1 = (2 * l + 1 < cnt) & (a1 - lo < hi_rel) & (b_id * f1 * __builtin_amdgcn_rcpf(f1 + nf1) > thr_s);
+    ++n_dblk;
+    const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+    if ((m0 | m1) == 0) return;
+    n_surv += __popcll(m0) + __popcll(m1);
+    // BM25 of the one term (scoring.h:133-144: summed from 0.0)
+    double s0 = 0.0, s1 = 0.0;
+    s0 += bm25_term(idf, p0 ? t0 : 0u, norm_tab[p0 ? c0 : 0u]);
+    s1 += bm25_term(idf, p1 ? t1 : 0u, norm_tab[p1 ? c1 : 0u]);
+    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    // candidates in doc order: lane by lane, posting 2l before 2l + 1
+    uint64_t cm0 = __ballot(p0 && (wide || (s0 > flo && (pt_n < k || s0 > kth))));
+    uint64_t cm1 = __ballot(p1 && (wide || (s1 > flo && (pt_n < k || s1 > kth))));
+    while (cm0 | cm1) {
+      const int fl = __builtin_ctzll(cm0 | cm1);
+      const bool second = !((cm0 >> fl) & 1);
+      if (second) cm1 &= cm1 - 1; else cm0 &= ~(1ull << fl);
+      const double sv = readlane_f64(second ? s1 : s0, fl);
+      const uint32_t dv = __builtin_amdgcn_readlane(second ? a1 : a0, fl);
+      const uint32_t pos = wide ? 0u : __popcll(__ballot(l < pt_n && pt >= sv));
+      if (wide || pos < k) {
+        if (evb == kLeanEvs) flush();
+        if (l == 0) {
+          Event e;
+          e.score = sv;
+          e.doc = static_cast<int32_t>(dv);
+          e.pad = 0;
+          S.evs[evb] = e;
+        }
+        ++ev_n;
+        ++evb;
+        if (!wide) {
+          const double up = wave_shr1_f64(pt);
+          if (l > pos) pt = up;
+          else if (l == pos) pt = sv;
+          pt_n = pt_n + 1 > k ? k : pt_n + 1;
+        }
+      }
+    }
+    if (!wide) {
+      const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+      const double pv = kn > flo ? kn : flo;
+      pub_val = pv > pub_val ? pv : pub_val;
+      thr_s = static_cast<float>(pv) * kPruneMargin;
+    }
+  };
+  auto refresh = [&]() __attribute__((always_inline)) {
+    if (wide || ++n_done % kFloorRefresh) return;
+    const uint64_t fb = floor_max(floor_next);
+    if (fb > floor_bits) {
+      floor_bits = fb;
+      flo = as_f64(fb);
+      const float t = static_cast<float>(flo) * kPruneMargin;
+      thr_s = t > thr_s ? t : thr_s;
+    }
+    if (my_pub && pub_val > sent) {
+      if (l == 0)
+        __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      sent = pub_val;
+    }
+    floor_next = floor_lanes(prev_pub, n_prev);
+  };
+  Regs R0, R1;
+  uint32_t b = next_block(b0);
+  issue(b, R0);
+  while (b < b1) {
+    b = next_block(b + 1);
+    issue(b, R1);
+    score(R0);
+    refresh();
+    if (R1.b >= b1) break;
+    b = next_block(b + 1);
+    issue(b, R0);
+    score(R1);
+    refresh();
+    if (R0.b >= b1) break;
+  }
+  // (the last evb events stay in S.evs for finish_lean_item)
+  if (my_pub && pub_val > last_pub && l == 0)
+    __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   last_pub = pub_val;
   __builtin_amdgcn_wave_barrier();
 }
@@ -2772,8 +2966,9 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
     uint64_t* my_pub = pub ? pub + item : nullptr;
     const uint64_t* prev_pub = (pub && r > 0) ? pub + item - 1 : nullptr;
 
-    // the segment's directory entries and the driver's decoded VInts tail:
-    // one round of loads
+    // the segment's directory entries, the driver's decoded VInts tail and
+    // the earlier items' score floors (floor_lanes): one round of loads
+    const uint64_t floor0 = floor_lanes(prev_pub, r);
     __builtin_amdgcn_wave_barrier();
     if (b0 + l < b1) {
       S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + b0 + l];
@@ -2793,19 +2988,66 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
     const bool done = first_doc > Q.min_last;
     // a query of one item with fused replay: the heap runs here, no events
     double pt = 0.0, last_pub = 0.0;
-    uint32_t pt_n = 0, ev_n = 0;
+    uint32_t pt_n = 0, ev_n = 0, evb = 0;   // events of the item; the last evb of them still in S.evs
     if (!done && b0 < b1) {
       const bool phrase =
           kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
       const int32_t* ql = qlist_of(qs, static_cast<int>(qi));
-      if (uni(static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit)))   // O1 has offset buckets
+      if (!kTwo && (Q.slots >> 16) == kNoSlot)   // one term
+        single_segment<kPh>(ix, S, norm, Q, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, floor0, prev_pub, r, my_pub,
+                            ev_out,
+                            ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
+      else if (uni(static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit)))   // O1 has offset buckets
         lean_segment<kPh, kTwo, true>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
-                                      prev_pub, r, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
+                                      floor0, prev_pub, r, my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
       else
         lean_segment<kPh, kTwo, false>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
-                                       prev_pub, r, my_pub, ev_out, ev_n, pt, pt_n, last_pub, n_surv, n_dblk);
+                                       floor0, prev_pub, r, my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
     }
-    finish_item<true>(qs, plan, qi, Q.n_items, item, prev_pub, r, ev_out, ev_n, events, ev_cnt, fr);
+    // The item's end from the events still in LDS where it can (finish_item
+    // otherwise): every event of the item is there when ev_n == evb.
+    __builtin_amdgcn_wave_barrier();
+    const bool in_lds = ev_n == evb;
+    double esc = 0.0;
+    int32_t edc = 0;
+    if (l < evb) {
+      esc = S.evs[l].score;
+      edc = S.evs[l].doc;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (in_lds && Q.n_items == 1 && fr.q_done && !fr.x_send && Q.k <= static_cast<uint32_t>(kMaxK)) {
+      // a query of one item: its events are the query's whole stream, in doc
+      // order; the restated heap replays them here (replay_query's HeapSink)
+      // with no store, count hand-off or reload
+      replay_lds_call(esc, edc, evb, Q.k, fr.hits + static_cast<int64_t>(qi) * fr.hit_stride, &fr.n_hits[qi]);
+      if (l == 0) ev_cnt[item] = ev_n;   // (batch statistics)
+    } else {
+      const uint64_t* refilter = prev_pub;
+      if (in_lds && prev_pub && ev_n > 0) {
+        // finish_item's re-filter against the earlier items' floor, on the
+        // LDS copy: only the kept events are stored
+        const double fl_end =
+            __longlong_as_double(static_cast<long long>(floor_max(floor_lanes(prev_pub, r))));
+        const bool keep = l < evb && esc > fl_end;
+        const uint64_t km = __ballot(keep);
+        if (keep) {
+          Event e;
+          e.score = esc;
+          e.doc = edc;
+          e.pad = 0;
+          store_event_coherent(&ev_out[__popcll(km & lanemask_lt())], e);
+        }
+        ev_n = __popcll(km);
+        refilter = nullptr;
+      } else if (l < evb) {   // the rest of the item's events, after those stored before
+        Event e;
+        e.score = esc;
+        e.doc = edc;
+        e.pad = 0;
+        store_event_coherent(&ev_out[ev_n - evb + l], e);
+      }
+      finish_item<true>(qs, plan, qi, Q.n_items, item, refilter, r, ev_out, ev_n, events, ev_cnt, fr);
+    }
     item = 0xFFFFFFFFu;
   }
   if (fr.oj.nq > 0)   // an earlier step group's owner replay, deferred into this kernel's tail

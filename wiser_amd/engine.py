@@ -470,6 +470,30 @@ def gen_phrase_log(index_dir: str, out_path: str, n_queries: int = 10_000, seed:
     return n.value
 
 
+def gen_realistic_log(index_dir: str, out_path: str, n_queries: int = 20_000, phrase_share: float = 0.1,
+                      seed: int = 7) -> int:
+    """One stream of the reference's mixed log (query_pool.h:363-375: quoted
+    phrase lines among plain lines; run_exp.py's "type_realistic"): a share of
+    two-term phrases from the index's phrase pool among 1-5-term AND queries
+    (gen_mixed_log), interleaved in a seeded random order."""
+    import os
+    import random
+    n_ph = int(round(n_queries * phrase_share))
+    tmp_m, tmp_p = out_path + ".and.tmp", out_path + ".phr.tmp"
+    gen_mixed_log(index_dir, tmp_m, n_queries=n_queries - n_ph, seed=seed)
+    lines = open(tmp_m).read().splitlines()
+    if n_ph:
+        gen_phrase_log(index_dir, tmp_p, n_queries=n_ph, seed=seed + 1)
+        lines += open(tmp_p).read().splitlines()
+    for t in (tmp_m, tmp_p):
+        if os.path.exists(t):
+            os.remove(t)
+    random.Random(seed).shuffle(lines)
+    with open(out_path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return len(lines)
+
+
 def read_query_log(path: str):
     """-> [(terms, is_phrase)]: one query per line, a phrase in double quotes"""
     out = []
