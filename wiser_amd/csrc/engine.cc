@@ -150,10 +150,12 @@ struct wsr_batch {
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
-  bool two_only = false;         // every query: two terms (or empty), k <= kMaxK
+  bool two_conj = false;         // every conjunctive query: two terms (or empty), k <= kMaxK
+  bool two_ph = false;           // every phrase query: k <= kMaxK (a lean one has two terms)
   uint32_t seg_cap = kSegCost;   // driver blocks per work item at most (wsr_batch_set_item_blocks)
   int seg_grid = 0;
-  int lean_wgs = 0;
+  int lean_wgs = 0;      // the conjunctive lean instance's grid
+  int lean_wgs_ph = 0;   // the phrase instance's (batches with phrase queries)
   // doc-range shard exchange (wsr_shard_step): per owner a region of {count,
   // offset} pairs + an event slot, owner-major to send, shard-major received;
   // allocated on first use
@@ -638,7 +640,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
-                                      (std::max(h->grid, 1) + kLeanWaves * std::max(h->lean_wgs, 1))));
+                                      (std::max(h->grid, 1) + 2 * kLeanWaves * std::max(h->lean_wgs, 1))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
@@ -702,9 +704,9 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   uint64_t ev_need = 0, items_need = 0, algo = 0;
   // the device's class rule (plan_query_kernel), restated to size the two
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
-  uint64_t lean_need = 0, gen_need = 0;
+  uint64_t lean_need = 0, lean_need_ph = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
-  bool has_phrase = false, has_wide = false, two_only = true;
+  bool has_phrase = false, has_wide = false, two_conj = true, two_ph = true;
   std::vector<int32_t> ids;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
@@ -715,7 +717,8 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     const bool phrase = (s.flags & WSR_QUERY_PHRASE) && s.n_terms > 1;
     has_phrase = has_phrase || phrase;
     has_wide = has_wide || s.k > kMaxK;
-    two_only = two_only && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
+    if (phrase) two_ph = two_ph && s.k <= kMaxK;
+    else two_conj = two_conj && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
@@ -747,7 +750,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       bool lean = !(phrase && d.n_terms > 2);   // (longer phrases: general class)
       for (int t = 0; t < d.n_terms; ++t)
         if (t != drv && !dense(t)) lean = false;
-      (lean ? lean_need : gen_need) += nbmin;
+      (lean ? (phrase ? lean_need_ph : lean_need) : gen_need) += nbmin;
       // every term's docid+tf span, and for a phrase query also its
       // position box (the bags the position check reads from)
       for (int t = 0; t < d.n_terms; ++t) {
@@ -796,12 +799,15 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->nq = nq;
   b->has_phrase = has_phrase;
   b->has_wide = has_wide;
-  b->two_only = two_only;
+  b->two_conj = two_conj;
+  b->two_ph = two_ph;
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
       1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
+  b->lean_wgs_ph = static_cast<int>(std::max<uint64_t>(
+      1, std::min<uint64_t>(h->lean_wgs, (lean_need_ph + kLeanWaves - 1) / kLeanWaves)));
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -866,7 +872,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     pa.seg_cap = b->seg_cap;
     HIP_OK(launch_plan(pa, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       kLeanWaves * b->lean_wgs, b->seg_grid, fr, b->d_itemq, b->d_pub, b->d_desc,
+                       kLeanWaves * b->lean_wgs, kLeanWaves * b->lean_wgs_ph, b->seg_grid, fr, b->d_itemq,
+                       b->d_pub, b->d_desc,
                        b->d_part, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
@@ -876,10 +883,21 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
                            b->has_phrase ? b->d_ph : nullptr, b->st2));
+    uint32_t* lean_stats = b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid;
+    if (b->has_phrase) {
+      // the lean phrase queries' items in the phrase instance (its position
+      // check and registers), after the general kernel on the second stream;
+      // the conjunctive lean items keep the conjunctive instance's occupancy
+      // (a deferred owner replay runs in the conjunctive launch only)
+      FusedReplay frp = fr;
+      frp.oj = OwnerJob{};
+      HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
+                         lean_stats + static_cast<size_t>(kStatStride) * kLeanWaves * b->lean_wgs,
+                         b->lean_wgs_ph, frp, b->d_itemq, b->d_pub, b->d_desc, true, b->two_ph, b->st2));
+    }
     HIP_OK(hipEventRecord(b->join, b->st2));
-    HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                       b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid, b->lean_wgs, fr,
-                       b->d_itemq, b->d_pub, b->d_desc, b->has_phrase, b->two_only, st));
+    HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
+                       b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
@@ -1000,7 +1018,7 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     if (x_join(b)) HIP_OK(hipEventSynchronize(b->xev[1]));   // a shard step's exchange + replay
     uint32_t ctr[kNumCounters];
     HIP_OK(hipMemcpy(ctr, b->d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
-    const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
+    const int rows = b->seg_grid + kLeanWaves * (b->lean_wgs + (b->has_phrase ? b->lean_wgs_ph : 0));
     std::vector<uint32_t> ws(static_cast<size_t>(kStatStride) * rows);
     HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     uint64_t sv = 0, db = 0, ob = 0;
@@ -1884,8 +1902,8 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                        int32_t* n_wg, int32_t* stride) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
-  // general workgroups, then lean waves
-  const int rows = b->seg_grid + kLeanWaves * b->lean_wgs;
+  // general workgroups, then lean waves (the conjunctive instance's, then the phrase instance's)
+  const int rows = b->seg_grid + kLeanWaves * (b->lean_wgs + (b->has_phrase ? b->lean_wgs_ph : 0));
   if (n_wg) *n_wg = rows;
   if (stride) *stride = kStatStride;
   if (!out) return WSR_OK;

@@ -49,19 +49,24 @@ struct IndexArgs {
 };
 
 // counters[] (zeroed before every batch): 0 total items, 2 event capacity used,
-// 4 error flags, 6 end of the lean items (items [0, lean) run in lean_kernel,
-// the rest in segment_kernel); each work queue has one head per XCD-sized
-// shard, each on its own 64-byte line (kCtrHead0 + 16*s lean, kCtrGHead0 +
-// 16*s general), so the dequeues of the persistent workers do not serialise
-// on a single line.
-enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrHead0 = 16,
+// 4 error flags, 6 end of the lean items, 8 end of the conjunctive lean items
+// (items [0, lean conj) run in lean_kernel's conjunctive instance, [lean
+// conj, lean) -- the lean phrase queries' -- in its phrase instance, the rest
+// in segment_kernel); each work queue has one head per XCD-sized shard, each
+// on its own 64-byte line (kCtrHead0 + 16*s lean conjunctive, kCtrPHead0 +
+// 16*s lean phrase, kCtrGHead0 + 16*s general), so the dequeues of the
+// persistent workers do not serialise on a single line.
+enum { kCtrItems = 0, kCtrEvCap = 2, kCtrError = 4, kCtrLean = 6, kCtrLeanConj = 8, kCtrHead0 = 16,
        kQueueShards = 8,
-       kCtrGHead0 = kCtrHead0 + 16 * kQueueShards,
+       kCtrPHead0 = kCtrHead0 + 16 * kQueueShards,
+       kCtrGHead0 = kCtrPHead0 + 16 * kQueueShards,
        kNumCounters = kCtrGHead0 + 16 * kQueueShards };
 // QueryPlan::driver = driver slot | cost bucket << kPlanBucketShift | kPlanLean
+// (| kPlanPhrase: a lean phrase query, the phrase instance's items)
 constexpr uint32_t kPlanSlotMask = 0x7FFu;   // (kMaxQueryTerms <= 2048)
 constexpr int kPlanBucketShift = 12;
 constexpr uint32_t kPlanLean = 1u << 16;
+constexpr uint32_t kPlanPhrase = 1u << 17;
 static_assert(kMaxQueryTerms <= static_cast<int>(kPlanSlotMask) + 1, "driver slot field");
 constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
 // per-workgroup statistics written by the segment kernels (no atomics):
@@ -146,7 +151,7 @@ constexpr int kPhraseScratch = kMaxPhraseTerms * 256;
 // plan queries (2 launches); part: per plan workgroup of kPlanThreads queries
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int lean_grid_ph, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st);
 hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                            uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
@@ -154,8 +159,9 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
                            uint64_t* pub, uint32_t* ph, hipStream_t st);
 
 // lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride];
-// phrase: the batch holds phrase queries (lean ones have two terms);
-// two: every query of the batch has two terms (or none) and k <= kMaxK
+// phrase: the lean phrase queries' items (the phrase instance; their lean
+// ones have two terms), else the conjunctive lean items;
+// two: every query of those items has two terms and k <= kMaxK
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,

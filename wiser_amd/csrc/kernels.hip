@@ -448,14 +448,15 @@ __device__ __forceinline__ const int32_t* qlist_of(const QueryIn* qs, int qi) {
 }
 
 // ----------------------------------------------------------------- plan --
-// Item order: class-major (lean items first, then general ones), then cost
-// bucket-major, heaviest bucket first (query order inside a bucket, a query's
-// items consecutive), so the persistent workers take the long items first and
-// the short ones fill the tail (longest-first list scheduling).
-constexpr int kPlanKeys = 2 * kCostBuckets;   // classes: lean, general
+// Item order: class-major (conjunctive lean items first, then the lean phrase
+// queries', then general ones), then cost bucket-major, heaviest bucket first
+// (query order inside a bucket, a query's items consecutive), so the
+// persistent workers take the long items first and the short ones fill the
+// tail (longest-first list scheduling).
+constexpr int kPlanKeys = 3 * kCostBuckets;   // classes: lean conjunctive, lean phrase, general
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
   const uint32_t bucket = (drv >> kPlanBucketShift) & 0xFu;
-  const uint32_t cls = (drv & kPlanLean) ? 0u : 1u;
+  const uint32_t cls = (drv & kPlanLean) ? ((drv & kPlanPhrase) ? 1u : 0u) : 2u;
   return cls * kCostBuckets + (kCostBuckets - 1 - bucket);
 }
 
@@ -610,7 +611,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       const uint32_t ic = static_cast<uint32_t>(item_cost);
       const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
       const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
-      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u);
+      // (a lean phrase query has two terms: the one-term "phrase" is a plain term)
+      const bool lean_ph = lean && nt > 1 && (q.flags & kQueryPhrase);
+      p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u) | (lean_ph ? kPlanPhrase : 0u);
       p.seg_blocks = seg;
       p.n_items = (nd + seg - 1) / seg;
       if (lean) {
@@ -690,7 +693,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
                                                         const PlanPart* __restrict__ part, int n_part,
                                                         uint32_t* __restrict__ counters,
                                                         uint64_t ev_capacity, uint32_t item_capacity,
-                                                        uint32_t lean_grid, uint32_t seg_grid,
+                                                        uint32_t lean_grid, uint32_t lean_grid_ph,
+                                                        uint32_t seg_grid,
                                                         uint32_t* __restrict__ item_q,
                                                         uint64_t* __restrict__ pub,
                                                         QueryDesc* __restrict__ desc) {
@@ -729,12 +733,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
   }
   __syncthreads();
   uint32_t key_base[kPlanKeys];
-  uint32_t run = 0, n_lean = 0;
+  uint32_t run = 0, n_lean = 0, n_conj = 0;
 #pragma unroll
   for (int k = 0; k < kPlanKeys; ++k) {
     key_base[k] = run + s_key_below[k];
     run += s_key_all[k];
-    if (k == kCostBuckets - 1) n_lean = run;
+    if (k == kCostBuckets - 1) n_conj = run;
+    if (k == 2 * kCostBuckets - 1) n_lean = run;
   }
   const uint32_t total_items = run;
   const bool fits = s_cap_all <= ev_capacity && total_items <= item_capacity;
@@ -793,6 +798,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
       if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
       counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
       counters[kCtrLean] = fits ? n_lean : 0u;
+      counters[kCtrLeanConj] = fits ? n_conj : 0u;
       counters[kCtrEvCap] = static_cast<uint32_t>(s_cap_all > 0xFFFFFFFFull ? 0xFFFFFFFFull : s_cap_all);
     }
     // Work queues: shard s serves relative items s, s+8, s+16, ...; worker w
@@ -800,6 +806,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
     // those first items (lean: one worker per wave; general: per workgroup).
     if (t < kQueueShards) {
       counters[kCtrHead0 + 16 * t] = (lean_grid + kQueueShards - 1 - t) / kQueueShards;
+      counters[kCtrPHead0 + 16 * t] = (lean_grid_ph + kQueueShards - 1 - t) / kQueueShards;
       counters[kCtrGHead0 + 16 * t] = (seg_grid + kQueueShards - 1 - t) / kQueueShards;
     }
   }
@@ -2294,9 +2301,32 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   const uint32_t lo = in_vgpr(ix.doc_lo), hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);
   const double idf = Q.a_idf;
   const float b_id = Q.b_id, idf_f = static_cast<float>(Q.a_idf);
-  // this item's block bounds, one per lane (blocks b0 + l)
+  // this item's block bounds, one per lane (blocks b0 + l), and those of the
+  // 64 blocks before it (a floor seed, below)
   const float bmax = b0 + l < b1 ? ix.bmax[Q.a_blk0 + b0 + l] * idf_f : 0.0f;
+  const bool pre_in = !wide && b0 > 64u - l;   // block b0 - 64 + l, list block >= 1
+  const float pre = ix.bmax[Q.a_blk0 + (pre_in ? b0 - 64u + l : 0u)];
   uint64_t floor_bits = prev_pub ? floor_max(floor0) : 0ull;   // (floor0: the caller's floor_lanes)
+  // Floor seed: each block holds a doc whose score is its block max, so the
+  // k-th largest block max of k blocks before this item bounds from below the
+  // k-th best score before it -- the reference heap's minimum at every doc of
+  // the item (the same argument as the floors of earlier items).  Lower bound
+  // of a block's f64 max score: idf * bmax * (1 - 2^-21) (bmax is rounded up
+  // by at most one f32 ulp; the score's own roundings are f64).  Blocks from
+  // the list's second on: their docs lie past the first block's last doc, so
+  // inside a doc-range shard's range whenever this item's are.
+  if (uni(static_cast<uint32_t>(__ballot(pre_in) != 0)) && k <= 64u) {
+    uint32_t v = pre_in ? __float_as_uint(pre) : 0u;   // (positive floats order as their bits)
+    uint32_t kth = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+      kth = wave_max(v);
+      const uint64_t at = __ballot(v == kth);
+      if (l == static_cast<uint32_t>(__builtin_ctzll(at))) v = 0u;
+    }
+    const double seed = idf * static_cast<double>(__uint_as_float(kth)) * (1.0 - 0x1.0p-21);
+    const uint64_t sb = static_cast<uint64_t>(__double_as_longlong(seed));
+    floor_bits = sb > floor_bits ? sb : floor_bits;
+  }
   auto as_f64 = [](uint64_t b) __attribute__((always_inline)) {
     return __longlong_as_double(static_cast<long long>(
         (static_cast<uint64_t>(uni(static_cast<uint32_t>(b >> 32))) << 32) | uni(static_cast<uint32_t>(b))));
@@ -2929,7 +2959,7 @@ __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t*
 // is what hides the dependent loads of short items and of the probe chains.
 // 5 workgroups (the conjunctive instance: 96 VGPRs, 27.7 KB LDS, 5 waves per
 // SIMD): with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against
-// 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 3 (kLeanWgsPhrase).
+// 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 4 (kLeanWgsPhrase).
 constexpr int kLeanWgs = 5;
 constexpr int kLeanWgsPhrase = 4;
 template <bool kPh, bool kTwo = false>
@@ -2948,13 +2978,20 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
   __syncthreads();
   LeanLdsT<kPh>& S = SW[w];
   const uint32_t wid = blockIdx.x * kLeanWaves + w;
-  const uint32_t n_lean = uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
+  // this instance's items: the conjunctive lean ones [0, lean conj), or (kPh)
+  // the lean phrase queries' [lean conj, lean)
+  const uint32_t n_conj = uni(__hip_atomic_load(&counters[kCtrLeanConj], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t lo = kPh ? n_conj : 0u;
+  const uint32_t n_lean = kPh ? uni(__hip_atomic_load(&counters[kCtrLean], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT))
+                              : n_conj;
+  uint32_t* heads = &counters[kPh ? kCtrPHead0 : kCtrHead0];
   uint32_t n_surv = 0, n_dblk = 0;
   uint32_t shard = wid % kQueueShards, tried = 0;
-  uint32_t item = wid;
+  uint32_t item = lo + wid;
   for (;;) {
-    if (item >= n_lean) item = next_item(&counters[kCtrHead0], 0, n_lean, shard, tried);
+    if (item >= n_lean) item = next_item(heads, lo, n_lean, shard, tried);
     if (item >= n_lean) break;
     const uint32_t qi = uni(item_q[item]);
     const QueryDesc Q = desc[qi];   // everything the item's setup needs, one record
@@ -2993,7 +3030,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
       const bool phrase =
           kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
       const int32_t* ql = qlist_of(qs, static_cast<int>(qi));
-      if (!kTwo && (Q.slots >> 16) == kNoSlot)   // one term
+      if (!kTwo && !kPh && (Q.slots >> 16) == kNoSlot)   // one term (never a phrase instance's item)
         single_segment<kPh>(ix, S, norm, Q, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, floor0, prev_pub, r, my_pub,
                             ev_out,
                             ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
@@ -3155,14 +3192,14 @@ __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t*
 // ------------------------------------------------------------ launchers --
 hipError_t launch_plan(const IndexArgs& ix, const QueryIn* q, int nq, QueryPlan* plan,
                        uint32_t* counters, uint64_t ev_capacity, uint32_t item_capacity,
-                       int lean_grid, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
+                       int lean_grid, int lean_grid_ph, int seg_grid, const FusedReplay& fr, uint32_t* item_q,
                        uint64_t* pub, QueryDesc* desc, PlanPart* part, hipStream_t st) {
   const int n_part = std::max(1, (nq + kPlanThreads - 1) / kPlanThreads);
   hipLaunchKernelGGL(plan_query_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, ix, q, nq, plan,
                      counters, fr, desc, part);
   hipLaunchKernelGGL(plan_fill_kernel, dim3(n_part), dim3(kPlanThreads), 0, st, nq, plan, part, n_part,
                      counters, ev_capacity, item_capacity, static_cast<uint32_t>(lean_grid),
-                     static_cast<uint32_t>(seg_grid), item_q, pub, desc);
+                     static_cast<uint32_t>(lean_grid_ph), static_cast<uint32_t>(seg_grid), item_q, pub, desc);
   return hipGetLastError();
 }
 
