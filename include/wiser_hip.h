@@ -346,6 +346,12 @@ int wsr_shard_step_emit(wsr_handle* h, wsr_batch* b, int32_t world, int32_t q_pe
                         void* host_send);
 int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
                           int64_t slot, const void* host_recv);
+/* wsr_shard_step_replay deferred: the regions are copied to the device now and
+ * the owner replay rides in the lean kernel of the next run of another batch
+ * of the engine (a fetch, wsr_batch_ready, the batch's next run or its destroy
+ * enqueues it on the batch's own stream first if no run has taken it). */
+int wsr_shard_step_replay_deferred(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
+                                   int64_t slot, const void* host_recv);
 /* wsr_shard_step_emit without the wait: the copy to host_send (page-locked,
  * wsr_pinned_alloc) is enqueued on the batch's stream; wsr_batch_stream_sync
  * waits for it, so a caller overlaps one batch's host exchange with the next

@@ -135,6 +135,7 @@ _sigs = {
     "wsr_shard_step_regions": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint64)]),
     "wsr_shard_step_emit": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_shard_step_replay": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),
+    "wsr_shard_step_replay_deferred": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P]),
     "wsr_debug_wg_stats": (C.c_int, [_P, _P, C.POINTER(C.c_uint32), C.c_int32,
                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_debug_fail_runs": (C.c_int, [C.c_int32]),

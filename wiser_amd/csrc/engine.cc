@@ -123,6 +123,10 @@ struct wsr_handle {
   std::vector<uint64_t> pos_bytes;  // position box bytes per list (positions on)
   std::vector<BlockDev> blocks;     // host copy (debug decode)
   std::vector<uint32_t> meta;
+  // host-exchange owner replays deferred into a later batch run's lean kernel
+  // (wsr_shard_step_replay_deferred), oldest first
+  std::mutex hdef_mu;
+  std::deque<wsr_batch*> hdef_q;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
   int gen_cap = 0;     // general workgroups launched at most
@@ -176,6 +180,11 @@ struct wsr_batch {
   // orders what the two do with the group)
   std::atomic<wsr_comm*> x_comm{nullptr};
   bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
+  // a host-exchange owner replay of this batch waiting for another batch's
+  // run to carry it (wsr_shard_step_replay_deferred); its regions are in
+  // d_xrecv once xev[0] (recorded after their copy on st) has passed
+  wsr_handle* hdef = nullptr;
+  int32_t hdef_rank = 0;
   int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
   int64_t x_slot = 0;           //     and slot (the replay half must match them)
   uint64_t algo_static = 0;  // sum of list spans + k*12 over the uploaded queries
@@ -185,21 +194,24 @@ struct wsr_batch {
   // general kernel goes to st2, forked from and joined back into st.  HIP maps
   // streams to its hardware queues (GPU_MAX_HW_QUEUES, 4) round-robin in
   // creation order, and kernels of one queue run in order: a batch creates
-  // three streams (st_pad is never used), so the lean kernels of consecutive
+  // three streams (st_pad carries only the conjunctive lean kernel of batches
+  // with phrase queries, beside the other two), so the lean kernels of consecutive
   // batches land on queues 3 apart, i.e. on all four in turn, instead of
   // alternating between two (with two streams per batch the C3 headline fell
   // from 21.7 to 18.9 M q/s and C2 from 35.0 to 29.6 M at unchanged per-batch
   // kernel times, profiles/r04a_bench.json).
   hipStream_t st = nullptr, st2 = nullptr, st_pad = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, join_ph = nullptr;
   bool ran = false;
 };
 static void replay_flush(wsr_comm* c, const wsr_batch* upto);
+static void host_replay_flush(wsr_batch* b);
 // Is a shard step's exchange of b outstanding?  First wait until every
 // exchange and owner replay asked for b is enqueued (by the communicator's
-// worker, or, deferred, by a later step group: enqueued now if still
-// pending), so that xev[1] is the record to wait on.
+// worker, or, deferred, by a later step group or batch run: enqueued now if
+// still pending), so that xev[1] is the record to wait on.
 static bool x_join(wsr_batch* b) {
+  if (b->hdef) host_replay_flush(b);
   if (wsr_comm* c = b->x_comm.load(std::memory_order_acquire)) replay_flush(c, b);
   while (b->x_enq.load(std::memory_order_acquire) != b->x_req) std::this_thread::yield();
   return b->x_pending;
@@ -647,6 +659,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipStreamCreateWithFlags(&b->st_pad, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&b->fork, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&b->join, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&b->join_ph, hipEventDisableTiming));
   } catch (const std::exception& e) {
     wsr_batch_destroy(h, b.release());
     return fail(WSR_E_HIP, e.what());
@@ -660,6 +673,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   if (x_join(b)) (void)hipEventSynchronize(b->xev[1]);   // a shard step's exchange reads its buffers
   if (b->st) (void)hipStreamSynchronize(b->st);
   if (b->st2) (void)hipStreamSynchronize(b->st2);
+  if (b->st_pad) (void)hipStreamSynchronize(b->st_pad);
   for (void* p : {static_cast<void*>(b->d_q), static_cast<void*>(b->d_plan),
                   static_cast<void*>(b->d_desc), static_cast<void*>(b->d_part),
                   static_cast<void*>(b->d_ctr), static_cast<void*>(b->d_events),
@@ -674,6 +688,7 @@ void wsr_batch_destroy(wsr_handle* h, wsr_batch* b) {
   for (auto& e : b->xev) if (e) (void)hipEventDestroy(e);
   if (b->fork) (void)hipEventDestroy(b->fork);
   if (b->join) (void)hipEventDestroy(b->join);
+  if (b->join_ph) (void)hipEventDestroy(b->join_ph);
   if (b->st) (void)hipStreamDestroy(b->st);
   if (b->st2) (void)hipStreamDestroy(b->st2);
   if (b->st_pad) (void)hipStreamDestroy(b->st_pad);
@@ -738,7 +753,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       nbmin = std::min(nbmin, h->lists[id].nblk);
     }
     if (ok && nbmin > 0) {
-      ev_need += (static_cast<uint64_t>(nbmin) + kSegCostMax) * 128;
+      // (a single-term item spans up to kSingleWindows items' blocks)
+      const uint64_t seg_max = d.n_terms == 1 ? std::min<uint64_t>(nbmin, uint64_t{kSegCostMax} * kSingleWindows)
+                                              : uint64_t{kSegCostMax};
+      ev_need += (static_cast<uint64_t>(nbmin) + seg_max) * 128;
       items_need += nbmin;
       int drv = 0;
       for (int t = 1; t < d.n_terms; ++t)
@@ -826,6 +844,8 @@ struct ShardEmit {
 };
 
 static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se = nullptr, const OwnerJob* oj = nullptr);
+static wsr_batch* take_host_replay(wsr_handle* h, const wsr_batch* b, OwnerJob* oj);
+static void host_replay_enqueue(wsr_batch* pb, wsr_handle* h);
 
 
 int wsr_batch_run(wsr_handle* h, wsr_batch* b) { return batch_run(h, b); }
@@ -847,6 +867,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   for (int32_t f = g_fail_runs.load(); f > 0;)
     if (g_fail_runs.compare_exchange_weak(f, f - 1)) return fail(WSR_E_HIP, "injected run failure");
+  wsr_batch* pb = nullptr;   // (a host replay taken, below)
+  bool pb_queued = false;
   try {
     HIP_OK(hipSetDevice(h->device));
     hipStream_t st = b->st;
@@ -854,6 +876,14 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     // stream) read this batch's buffers and write its results
     if (x_join(b)) HIP_OK(hipStreamWaitEvent(st, b->xev[1], 0));
     b->x_pending = false;
+    // a host-exchange owner replay another batch deferred (wsr_shard_step_
+    // replay_deferred) rides in this run's lean kernel, after its regions'
+    // copy; its end is recorded on this stream behind the lean kernel
+    OwnerJob hoj{};
+    if (!oj && (pb = take_host_replay(h, b, &hoj))) {
+      HIP_OK(hipStreamWaitEvent(st, pb->xev[0], 0));
+      oj = &hoj;
+    }
     HIP_OK(hipMemsetAsync(b->d_ctr, 0, sizeof(uint32_t) * (kNumCounters + (se ? se->owners : 0)), st));
     FusedReplay fr{b->d_qdone, b->d_hits, b->stride, b->d_nhits};
     if (se) {
@@ -884,28 +914,43 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
                            b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
                            b->has_phrase ? b->d_ph : nullptr, b->st2));
     uint32_t* lean_stats = b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid;
+    HIP_OK(hipEventRecord(b->join, b->st2));
     if (b->has_phrase) {
-      // the lean phrase queries' items in the phrase instance (its position
-      // check and registers), after the general kernel on the second stream;
-      // the conjunctive lean items keep the conjunctive instance's occupancy
-      // (a deferred owner replay runs in the conjunctive launch only)
+      // The lean phrase queries' items run in the phrase instance (its
+      // position check and registers) and the conjunctive lean items keep the
+      // conjunctive instance's occupancy: the phrase launch on the batch
+      // stream (where a phrase batch's lean kernel has always run, so that
+      // consecutive batches' kernels rotate over the hardware queues as
+      // before), the conjunctive one on the third stream beside it.  (A
+      // deferred owner replay runs in the conjunctive launch only.)
+      HIP_OK(hipStreamWaitEvent(b->st_pad, b->fork, 0));
+      HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
+                         b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->st_pad));
+      HIP_OK(hipEventRecord(b->join_ph, b->st_pad));
       FusedReplay frp = fr;
       frp.oj = OwnerJob{};
       HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                          lean_stats + static_cast<size_t>(kStatStride) * kLeanWaves * b->lean_wgs,
-                         b->lean_wgs_ph, frp, b->d_itemq, b->d_pub, b->d_desc, true, b->two_ph, b->st2));
+                         b->lean_wgs_ph, frp, b->d_itemq, b->d_pub, b->d_desc, true, b->two_ph, st));
+    } else {
+      HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
+                         b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, st));
     }
-    HIP_OK(hipEventRecord(b->join, b->st2));
-    HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
-                       b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, st));
     HIP_OK(hipEventRecord(b->ev[4], st));
+    if (pb) {
+      HIP_OK(hipEventRecord(pb->xev[1], st));
+      pb->x_pending = true;
+      pb_queued = true;
+    }
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
+    if (b->has_phrase) HIP_OK(hipStreamWaitEvent(st, b->join_ph, 0));
     HIP_OK(hipEventRecord(b->ev[2], st));
     if (!se && b->has_wide)
       HIP_OK(launch_wide_replay(b->d_q, b->d_plan, b->nq, b->d_events, b->d_evcnt, b->d_hits, b->stride,
                                 b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
   } catch (const std::exception& e) {
+    if (pb && !pb_queued) host_replay_enqueue(pb, h);   // (its own stream, then)
     return fail(WSR_E_HIP, e.what());
   }
   b->ran = true;
@@ -1841,6 +1886,77 @@ int wsr_shard_step_replay(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t wor
     return fail(WSR_E_HIP, e.what());
   }
   return step_replay(h, b, rank, world, q_per_owner, slot, b->st);
+}
+
+// Host-exchange owner replays deferred into a later run's lean kernel (the
+// counterpart of the communicator's deferral, wsr_shard_steps): a separate
+// owner replay launch -- thousands of one-wave workgroups -- costs more than
+// its work beside the persistent kernels of the next batches.
+int wsr_shard_step_replay_deferred(wsr_handle* h, wsr_batch* b, int32_t rank, int32_t world, int32_t q_per_owner,
+                                   int64_t slot, const void* host_recv) {
+  if (!h || !b || !host_recv || world < 1 || rank < 0 || rank >= world || q_per_owner <= 0 || slot <= 0 ||
+      !b->x_fused || b->x_world != world || b->x_qpr != q_per_owner || b->x_slot != slot ||
+      static_cast<int64_t>(q_per_owner) * world != b->nq)
+    return fail(WSR_E_INVALID, "call wsr_shard_step_emit with the same world, q_per_owner and slot first");
+  if (b->has_wide)   // (the LDS heap: the replay launch of its own)
+    return wsr_shard_step_replay(h, b, rank, world, q_per_owner, slot, host_recv);
+  try {
+    HIP_OK(hipSetDevice(h->device));
+    if (b->hdef) host_replay_flush(b);   // (an earlier one still waiting: first)
+    ensure_xev(b);
+    HIP_OK(hipMemcpyAsync(b->d_xrecv, host_recv, sizeof(Event) * region_events_of(q_per_owner, slot) * world,
+                          hipMemcpyHostToDevice, b->st));
+    HIP_OK(hipEventRecord(b->xev[0], b->st));
+  } catch (const std::exception& e) {
+    return fail(WSR_E_HIP, e.what());
+  }
+  std::lock_guard<std::mutex> g(h->hdef_mu);
+  b->hdef = h;
+  b->hdef_rank = rank;
+  h->hdef_q.push_back(b);
+  return WSR_OK;
+}
+
+// The oldest deferred host replay that a run of b can carry (not b's own),
+// off the queue; its OwnerJob in *oj.
+static wsr_batch* take_host_replay(wsr_handle* h, const wsr_batch* b, OwnerJob* oj) {
+  std::lock_guard<std::mutex> g(h->hdef_mu);
+  for (auto it = h->hdef_q.begin(); it != h->hdef_q.end(); ++it) {
+    wsr_batch* pb = *it;
+    if (pb == b) continue;
+    h->hdef_q.erase(it);
+    pb->hdef = nullptr;
+    const uint64_t region = region_events_of(pb->x_qpr, pb->x_slot);
+    const uint64_t meta_events = (static_cast<uint64_t>(pb->x_qpr) + 1) / 2;
+    *oj = OwnerJob{pb->d_q, reinterpret_cast<const int32_t*>(pb->d_xrecv), pb->d_xrecv + meta_events, pb->d_hits,
+                   pb->d_nhits, pb->d_ctr, region * (sizeof(Event) / sizeof(int32_t)), region,
+                   pb->hdef_rank * pb->x_qpr, pb->x_qpr, pb->x_world, pb->stride};
+    return pb;
+  }
+  return nullptr;
+}
+
+// A taken (or still queued, via host_replay_flush) replay on pb's own stream.
+static void host_replay_enqueue(wsr_batch* pb, wsr_handle* h) {
+  if (step_replay(h, pb, pb->hdef_rank, pb->x_world, pb->x_qpr, pb->x_slot, pb->st) == WSR_OK &&
+      hipEventRecord(pb->xev[1], pb->st) == hipSuccess)
+    pb->x_pending = true;
+}
+
+static void host_replay_flush(wsr_batch* b) {
+  wsr_handle* h = b->hdef;
+  if (!h) return;
+  {
+    std::lock_guard<std::mutex> g(h->hdef_mu);
+    if (!b->hdef) return;   // (taken by a run meanwhile)
+    for (auto it = h->hdef_q.begin(); it != h->hdef_q.end(); ++it)
+      if (*it == b) {
+        h->hdef_q.erase(it);
+        break;
+      }
+    b->hdef = nullptr;
+  }
+  host_replay_enqueue(b, h);
 }
 
 int wsr_batch_fetch_range(wsr_handle* h, wsr_batch* b, int32_t q0, int32_t nq, wsr_hit* hits,

@@ -83,6 +83,10 @@ constexpr int kMaxOwners = 1024;   // doc-range shards (ranks) of one exchange
 // profiles/r03_phrase_item_ab.txt).
 constexpr int kSegCost = 63;
 static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane");
+// A single-term item spans up to this many items' worth of blocks, which
+// single_segment runs window by window: most of its blocks are skipped by
+// their block bounds, so a short item would be mostly fixed cost.
+constexpr int kSingleWindows = 8;
 // item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5

@@ -604,6 +604,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
     if (ok) {
       uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
       seg = seg > ix.seg_cap ? ix.seg_cap : seg;
+      if (nt == 1) seg *= kSingleWindows;   // (single_segment: windows of 64 blocks)
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
       // for the per-item setup): the queue hands out heavy items first
@@ -2301,9 +2302,12 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   const uint32_t lo = in_vgpr(ix.doc_lo), hi_rel = in_vgpr(ix.doc_hi - ix.doc_lo);
   const double idf = Q.a_idf;
   const float b_id = Q.b_id, idf_f = static_cast<float>(Q.a_idf);
-  // this item's block bounds, one per lane (blocks b0 + l), and those of the
-  // 64 blocks before it (a floor seed, below)
-  const float bmax = b0 + l < b1 ? ix.bmax[Q.a_blk0 + b0 + l] * idf_f : 0.0f;
+  // The item runs window by window, 64 blocks each (its first window's
+  // directory is in S already); per window the block bounds, one per lane
+  // (blocks wb + l), and, for the first, those of the 64 blocks before the
+  // item (a floor seed, below).
+  uint32_t wb = b0, we = min(b0 + 64u, b1);
+  float bmax = wb + l < we ? ix.bmax[Q.a_blk0 + wb + l] * idf_f : 0.0f;
   const bool pre_in = !wide && b0 > 64u - l;   // block b0 - 64 + l, list block >= 1
   const float pre = ix.bmax[Q.a_blk0 + (pre_in ? b0 - 64u + l : 0u)];
   uint64_t floor_bits = prev_pub ? floor_max(floor0) : 0ull;   // (floor0: the caller's floor_lanes)
@@ -2336,22 +2340,23 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   double pub_val = 0.0, sent = 0.0;
   uint64_t floor_next = 0;
   uint32_t n_done = 0;
-  // the first block at or after b whose bound passes the threshold (b1: none)
+  // the first block of the window at or after b whose bound passes the
+  // threshold (we: none)
   auto next_block = [&](uint32_t b) __attribute__((always_inline)) {
-    const uint64_t m = __ballot(b0 + l >= b && bmax > thr_s);
-    return m ? b0 + static_cast<uint32_t>(__builtin_ctzll(m)) : b1;
+    const uint64_t m = __ballot(wb + l >= b && bmax > thr_s);
+    return m ? wb + static_cast<uint32_t>(__builtin_ctzll(m)) : we;
   };
   struct Regs {
     uint32_t w0 = 0, w1 = 0, w2 = 0, t0 = 0, t1 = 0, t2 = 0, wc = 0, b = 0;
   };
   auto issue = [&](uint32_t b, Regs& Y) __attribute__((always_inline)) {
-    const uint32_t bi = b < b1 ? b - b0 : 0u;
+    const uint32_t bi = b < we ? b - wb : 0u;
     const uint32_t m = uni(S.dmeta[bi]);
     const uint4 e = S.dblk[bi];
     uint32_t sh;
     pair_words(a_blob + uni(e.z) + 2, (m & 0xFF) ? (m & 0xFF) : 1u, l, Y.w0, Y.w1, Y.w2, sh);
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.t0, Y.t1, Y.t2, sh);
-    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < b1 ? b : b0)) * 32u + (l >> 1)];
+    Y.wc = reinterpret_cast<const uint32_t*>(ix.plen)[(Q.a_blk0 + (b < we ? b : wb)) * 32u + (l >> 1)];
     Y.b = b;
   };
   auto pair_shift = [&](uint32_t rel, uint32_t bits) __attribute__((always_inline)) {
@@ -2367,7 +2372,7 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   };
   // score block X.b (its loads were issued one block earlier)
   auto score = [&](const Regs& X) __attribute__((always_inline)) {
-    const uint32_t b = X.b, bi = b - b0;
+    const uint32_t b = X.b, bi = b - wb;
     const uint4 be = S.dblk[bi];
     const uint32_t m = uni(S.dmeta[bi]);
     const uint32_t wbits = (m & 0xFF) ? (m & 0xFF) : 1u, wtb = (m >> 8) ? (m >> 8) : 1u;
@@ -2449,19 +2454,32 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
     floor_next = floor_lanes(prev_pub, n_prev);
   };
   Regs R0, R1;
-  uint32_t b = next_block(b0);
-  issue(b, R0);
-  while (b < b1) {
-    b = next_block(b + 1);
-    issue(b, R1);
-    score(R0);
-    refresh();
-    if (R1.b >= b1) break;
-    b = next_block(b + 1);
+  for (;;) {
+    uint32_t b = next_block(wb);
     issue(b, R0);
-    score(R1);
-    refresh();
-    if (R0.b >= b1) break;
+    while (b < we) {
+      b = next_block(b + 1);
+      issue(b, R1);
+      score(R0);
+      refresh();
+      if (R1.b >= we) break;
+      b = next_block(b + 1);
+      issue(b, R0);
+      score(R1);
+      refresh();
+      if (R0.b >= we) break;
+    }
+    if (we >= b1) break;
+    // the next window: its directory and block bounds (one round of loads)
+    wb = we;
+    we = min(wb + 64u, b1);
+    __builtin_amdgcn_wave_barrier();
+    if (wb + l < we) {
+      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + wb + l];
+      S.dmeta[l] = ix.blk_meta[Q.a_blk0 + wb + l];
+    }
+    bmax = wb + l < we ? ix.bmax[Q.a_blk0 + wb + l] * idf_f : 0.0f;
+    __builtin_amdgcn_wave_barrier();
   }
   // (the last evb events stay in S.evs for finish_lean_item)
   if (my_pub && pub_val > last_pub && l == 0)

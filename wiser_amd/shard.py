@@ -203,8 +203,10 @@ class HostExchangeShardedSearcher:
         check(lib.wsr_batch_stream_sync(self.engine._h, b._b))
         send = torch.frombuffer((C.c_char * nbytes).from_address(ptr), dtype=torch.int64)
         recv = exchange_regions(send, self.world, self.group)
-        check(lib.wsr_shard_step_replay(self.engine._h, b._b, self.rank, self.world, qpr, slot,
-                                        C.c_void_p(recv.data_ptr())))
+        # deferred: the owner replay rides in the next run's lean kernel (or is
+        # enqueued on the batch's stream by its fetch), as the RCCL path defers it
+        check(lib.wsr_shard_step_replay_deferred(self.engine._h, b._b, self.rank, self.world, qpr, slot,
+                                                 C.c_void_p(recv.data_ptr())))
         self._keep[(id(b), b.nq)] = (b, recv)   # alive until the replay has run
 
     def flush(self):
