@@ -29,8 +29,11 @@ def main():
         classes[f"c4_{n}term"] = [it for it in mixed if len(it[0]) == n]
     classes["c4_3to5"] = [it for it in mixed if len(it[0]) >= 3]
     classes["c4_mix"] = mixed
-    for name in ("single_high", "single_low", "realistic_mix"):
+    for name in ("single_high", "single_low", "realistic_mix", "c5_phrase"):
         classes[name] = bench.leg_items(a, idx, name)[0]
+    # the realistic mix's two parts alone (the same queries)
+    classes["real_and"] = [it for it in classes["realistic_mix"] if not it[1]]
+    classes["real_phrase"] = [it for it in classes["realistic_mix"] if it[1]]
     engs = {}
     for name, items in classes.items():
         if want and name not in want:

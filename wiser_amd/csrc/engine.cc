@@ -153,6 +153,7 @@ struct wsr_batch {
   uint32_t* d_stats = nullptr;   // per general workgroup, then per lean wave: survivors, blocks
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
+  bool gen_phrase = false;       // ... one of the general class (segment_kernel's phrase instance)
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   bool two_conj = false;         // every conjunctive query: two terms (or empty), k <= kMaxK
   bool two_ph = false;           // every phrase query: k <= kMaxK (a lean one has two terms)
@@ -721,7 +722,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, lean_need_ph = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
-  bool has_phrase = false, has_wide = false, two_conj = true, two_ph = true;
+  bool has_phrase = false, has_wide = false, two_conj = true, two_ph = true, gen_phrase = false;
   std::vector<int32_t> ids;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
@@ -769,6 +770,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
       for (int t = 0; t < d.n_terms; ++t)
         if (t != drv && !dense(t)) lean = false;
       (lean ? (phrase ? lean_need_ph : lean_need) : gen_need) += nbmin;
+      gen_phrase = gen_phrase || (phrase && !lean);
       // every term's docid+tf span, and for a phrase query also its
       // position box (the bags the position check reads from)
       for (int t = 0; t < d.n_terms; ++t) {
@@ -818,6 +820,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->has_phrase = has_phrase;
   b->has_wide = has_wide;
   b->two_conj = two_conj;
+  b->gen_phrase = gen_phrase;
   b->two_ph = two_ph;
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
@@ -912,7 +915,7 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     HIP_OK(hipStreamWaitEvent(b->st2, b->fork, 0));
     HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                            b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
-                           b->has_phrase ? b->d_ph : nullptr, b->st2));
+                           b->gen_phrase ? b->d_ph : nullptr, b->st2));
     uint32_t* lean_stats = b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid;
     HIP_OK(hipEventRecord(b->join, b->st2));
     if (b->has_phrase) {

@@ -72,7 +72,7 @@ constexpr int kLeanWaves = 4;   // independent waves per lean_kernel workgroup
 // per-workgroup statistics written by the segment kernels (no atomics):
 // stats[wg * kStatStride + {0 survivors, 1 driver blocks, 2 other blocks}]
 constexpr int kStatStride = 4;
-enum { kErrLimit = 1, kErrCapacity = 2, kErrExchange = 4 };
+enum { kErrLimit = 1, kErrCapacity = 2, kErrExchange = 4, kErrClass = 8 };
 constexpr int kMaxOwners = 1024;   // doc-range shards (ranks) of one exchange
 
 // Target block decodes per work item, for every class (lean, general,
@@ -87,6 +87,10 @@ static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane
 // single_segment runs window by window: most of its blocks are skipped by
 // their block bounds, so a short item would be mostly fixed cost.
 constexpr int kSingleWindows = 8;
+// Driver blocks per item of a phrase query at most: a batch's phrase items
+// are its tail when they are few (the realistic mix: 15.4 -> 16.5 M q/s at 32
+// against 63, C5 unchanged; 16: 16.0 / 8.5 M, profiles/r05/phrase_seg_ab.txt).
+constexpr uint32_t kPhraseSegCap = 32;
 // item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5

@@ -605,6 +605,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       uint32_t seg = static_cast<uint32_t>(kSegCost / cost);
       seg = seg > ix.seg_cap ? ix.seg_cap : seg;
       if (nt == 1) seg *= kSingleWindows;   // (single_segment: windows of 64 blocks)
+      if (nt > 1 && (q.flags & kQueryPhrase)) seg = seg > kPhraseSegCap ? kPhraseSegCap : seg;
       seg = seg < 1 ? 1 : (seg > nd ? nd : seg);
       // cost class of one item (log2 of its block decodes, plus a fixed part
       // for the per-item setup): the queue hands out heavy items first
@@ -2532,6 +2533,15 @@ __global__ __launch_bounds__(64, kSegWaves) void segment_kernel(IndexArgs ix, co
     // phrase query: every term's posting of each candidate is recorded in this
     // workgroup's slice of ph_all, then the positions are checked
     const bool phrase = kPhrase && nt > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
+    // (the conjunctive instance runs a batch whose phrase queries are all lean,
+    // by the host's restatement of the class rule: a general phrase item here
+    // would lose its position check, so it fails the batch loudly instead)
+    if (!kPhrase && nt > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase)) {
+      if (l == 0) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrClass));
+      finish_item<false>(qs, plan, qi, P.n_items, item, nullptr, r, events + P.ev_base, 0, events, ev_cnt, fr);
+      item = 0xFFFFFFFFu;
+      continue;
+    }
     uint32_t* ph = kPhrase ? ph_all + static_cast<uint64_t>(blockIdx.x) * kPhraseScratch : nullptr;
     const uint32_t b0 = r * seg;
     const uint32_t b1 = min(b0 + seg, A.nblk);
