@@ -129,6 +129,7 @@ struct wsr_handle {
   std::deque<wsr_batch*> hdef_q;
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
+  int lean_wgs_ph = 0; // ... its phrase instance's
   int gen_cap = 0;     // general workgroups launched at most
 };
 
@@ -154,6 +155,8 @@ struct wsr_batch {
   uint32_t* d_ph = nullptr;      // phrase scratch, gen_cap * kPhraseScratch (lazily)
   bool has_phrase = false;       // the uploaded queries include a phrase query
   bool gen_phrase = false;       // ... one of the general class (segment_kernel's phrase instance)
+  bool has_conj_lean = true;     // the host's class rule found a conjunctive lean query
+  bool has_gen = true;           // ... a general one
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   bool two_conj = false;         // every conjunctive query: two terms (or empty), k <= kMaxK
   bool two_ph = false;           // every phrase query: k <= kMaxK (a lean one has two terms)
@@ -411,9 +414,14 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // concurrent lean kernel keeps its occupancy
     const int gen_per_cu = static_cast<int>(env_number("WSR_GEN_PER_CU", 4));
     h->gen_cap = prop.multiProcessorCount * std::max(1, std::min(std::min(occ, 32), gen_per_cu));
-    int locc = lean_kernel_occupancy();
+    int locc = lean_kernel_occupancy(false);
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
+    // the phrase instance holds more registers: its resident grid is smaller
+    // (workgroups past it would start only as resident ones leave)
+    int pocc = lean_kernel_occupancy(true);
+    if (pocc < 1) pocc = 1;
+    h->lean_wgs_ph = prop.multiProcessorCount * std::min(std::min(pocc, locc), 16);   // (stats rows: <= lean_wgs)
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -821,6 +829,8 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->has_wide = has_wide;
   b->two_conj = two_conj;
   b->gen_phrase = gen_phrase;
+  b->has_conj_lean = lean_need > 0;
+  b->has_gen = gen_need > 0;
   b->two_ph = two_ph;
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
@@ -828,7 +838,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
       1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
   b->lean_wgs_ph = static_cast<int>(std::max<uint64_t>(
-      1, std::min<uint64_t>(h->lean_wgs, (lean_need_ph + kLeanWaves - 1) / kLeanWaves)));
+      1, std::min<uint64_t>(h->lean_wgs_ph, (lean_need_ph + kLeanWaves - 1) / kLeanWaves)));
   b->algo_static = algo;
   b->ran = false;
   return WSR_OK;
@@ -903,19 +913,27 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     HIP_OK(hipEventRecord(b->ev[0], st));
     IndexArgs pa = h->args;   // (the batch's item length)
     pa.seg_cap = b->seg_cap;
+    // A batch with phrase queries launches the conjunctive lean kernel and the
+    // general one only when the host's restatement of the class rule found
+    // such queries (an empty persistent launch waited for CU slots beside the
+    // others: 54 us on C5, profiles/r05p); the plan flags kErrClass if a class
+    // without a launch holds items.  (Shard steps launch everything: their
+    // owners read every query's emission.)
+    const bool run_conj = se || !b->has_phrase || b->has_conj_lean;
+    const bool run_gen = se || !b->has_phrase || b->has_gen;
     HIP_OK(launch_plan(pa, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
-                       kLeanWaves * b->lean_wgs, kLeanWaves * b->lean_wgs_ph, b->seg_grid, fr, b->d_itemq,
-                       b->d_pub, b->d_desc,
-                       b->d_part, st));
+                       run_conj ? kLeanWaves * b->lean_wgs : 0, b->has_phrase ? kLeanWaves * b->lean_wgs_ph : 0,
+                       run_gen ? b->seg_grid : 0, fr, b->d_itemq, b->d_pub, b->d_desc, b->d_part, st));
     HIP_OK(hipEventRecord(b->ev[1], st));
     // general items on the second stream, lean items here; both drain their
     // own queue, then the streams join
     HIP_OK(hipEventRecord(b->fork, st));
     HIP_OK(hipStreamWaitEvent(b->st2, b->fork, 0));
-    HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
-                           b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
-                           b->gen_phrase ? b->d_ph : nullptr, b->st2));
+    if (run_gen)
+      HIP_OK(launch_segments(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
+                             b->d_stats, b->seg_grid, fr, b->d_itemq, b->d_pub,
+                             b->gen_phrase ? b->d_ph : nullptr, b->st2));
     uint32_t* lean_stats = b->d_stats + static_cast<size_t>(kStatStride) * b->seg_grid;
     HIP_OK(hipEventRecord(b->join, b->st2));
     if (b->has_phrase) {
@@ -927,8 +945,9 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
       // before), the conjunctive one on the third stream beside it.  (A
       // deferred owner replay runs in the conjunctive launch only.)
       HIP_OK(hipStreamWaitEvent(b->st_pad, b->fork, 0));
-      HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
-                         b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->st_pad));
+      if (run_conj)
+        HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
+                           b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->st_pad));
       HIP_OK(hipEventRecord(b->join_ph, b->st_pad));
       FusedReplay frp = fr;
       frp.oj = OwnerJob{};

@@ -174,7 +174,7 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
                        uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, hipStream_t st);
-int lean_kernel_occupancy();
+int lean_kernel_occupancy(bool phrase);   // workgroups per CU
 // queries with k > kMaxK (their segments emitted every survivor): heap in LDS
 hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,
                               const uint32_t* ev_cnt, HitDev* hits, int hit_stride, int32_t* n_hits,

@@ -798,6 +798,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(int nq, QueryPl
   if (blockIdx.x == 0) {
     if (t == 0) {
       if (!fits) atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrCapacity));
+      // a class whose kernel the host did not launch (grid 0: its restatement
+      // of the class rule found no such query) must hold no item: loud if it does
+      if ((lean_grid == 0 && n_conj > 0) || (lean_grid_ph == 0 && n_lean > n_conj) ||
+          (seg_grid == 0 && total_items > n_lean))
+        atomicOr(&counters[kCtrError], static_cast<uint32_t>(kErrClass));
       counters[kCtrItems] = fits ? total_items : 0u;  // never write past the workspace
       counters[kCtrLean] = fits ? n_lean : 0u;
       counters[kCtrLeanConj] = fits ? n_conj : 0u;
@@ -3266,9 +3271,10 @@ hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* p
   return hipGetLastError();
 }
 
-int lean_kernel_occupancy() {
+int lean_kernel_occupancy(bool phrase) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, lean_kernel<false>, 64 * kLeanWaves, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, phrase ? lean_kernel<true, true> : lean_kernel<false>,
+                                                   64 * kLeanWaves, 0) != hipSuccess)
     return 1;
   return n;
 }
