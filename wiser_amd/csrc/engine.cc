@@ -130,6 +130,7 @@ struct wsr_handle {
   int grid = 0;        // general segment kernel: workgroups (one wave each)
   int lean_wgs = 0;    // lean kernel: workgroups of kLeanWaves waves
   int lean_wgs_ph = 0; // ... its phrase instance's
+  int lean_wgs_two = 0; // ... its two-term instance's (one workgroup per CU past residency)
   int gen_cap = 0;     // general workgroups launched at most
 };
 
@@ -421,7 +422,13 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     // (workgroups past it would start only as resident ones leave)
     int pocc = lean_kernel_occupancy(true);
     if (pocc < 1) pocc = 1;
-    h->lean_wgs_ph = prop.multiProcessorCount * std::min(std::min(pocc, locc), 16);   // (stats rows: <= lean_wgs)
+    h->lean_wgs_ph = prop.multiProcessorCount * std::min(std::min(pocc, locc), 16);
+    // Batches whose conjunctive items are all two-term (the headline's) run one
+    // workgroup per CU past the resident grid: it starts as the first resident
+    // waves leave and takes items from the queue's tail (C3 24.0 -> 24.5 M q/s,
+    // C2 and C4 unchanged; 2 to 11 more: no better, 11 -6 %; single-term
+    // batches -2 %, so they keep the resident grid: profiles/r05/leg_ab.txt r05u-w)
+    h->lean_wgs_two = prop.multiProcessorCount * std::min(locc + 1, 16);
   } catch (const std::exception& e) {
     wsr_close(h.release());
     return fail(WSR_E_HIP, e.what());
@@ -661,7 +668,8 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
-                                      (std::max(h->grid, 1) + 2 * kLeanWaves * std::max(h->lean_wgs, 1))));
+                                      (std::max(h->grid, 1) +
+                                       kLeanWaves * (std::max(h->lean_wgs_two, 1) + std::max(h->lean_wgs_ph, 1)))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&b->st2, hipStreamNonBlocking));
@@ -836,7 +844,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
   b->lean_wgs = static_cast<int>(std::max<uint64_t>(
-      1, std::min<uint64_t>(h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
+      1, std::min<uint64_t>(two_conj ? h->lean_wgs_two : h->lean_wgs, (lean_need + kLeanWaves - 1) / kLeanWaves)));
   b->lean_wgs_ph = static_cast<int>(std::max<uint64_t>(
       1, std::min<uint64_t>(h->lean_wgs_ph, (lean_need_ph + kLeanWaves - 1) / kLeanWaves)));
   b->algo_static = algo;
