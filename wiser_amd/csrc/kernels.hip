@@ -935,6 +935,10 @@ __device__ __forceinline__ double bm25_term(double idf, uint32_t tf, double norm
   return idf * tfn;
 }
 
+// global-address-space views (loads through them are global_load, not flat_load)
+typedef __attribute__((address_space(1))) const uint64_t GlobalU64;
+typedef __attribute__((address_space(1))) const uint32_t GlobalU32;
+
 // --------------------------------------------------------------- replay --
 // Events handed from one workgroup to another inside the segment kernel
 // (fused replay) travel with agent-scope relaxed atomics, which gfx950 issues
@@ -951,10 +955,14 @@ __device__ __forceinline__ void store_event_coherent(Event* dst, const Event& e)
 template <bool kCoherent>
 __device__ __forceinline__ void load_event(const Event* src, double* sc, int32_t* dc) {
   if (kCoherent) {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(src);
+    // global (not flat) loads: a flat load also counts in lgkmcnt, so every
+    // LDS or scalar wait would wait for it too; the doc alone (no load into
+    // the pad's register, which the compiler reuses and then must wait for)
+    const GlobalU64* w = (const GlobalU64*)src;
     *sc = __longlong_as_double(static_cast<long long>(
         __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    *dc = static_cast<int32_t>(__hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    *dc = static_cast<int32_t>(__hip_atomic_load((const GlobalU32*)w + 2, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
   } else {
     *sc = src->score;
     *dc = src->doc;
@@ -963,7 +971,8 @@ __device__ __forceinline__ void load_event(const Event* src, double* sc, int32_t
 
 template <bool kCoherent>
 __device__ __forceinline__ uint32_t load_count(const uint32_t* p) {
-  if (kCoherent) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (kCoherent)
+    return __hip_atomic_load((const GlobalU32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return *p;
 }
 
