@@ -243,3 +243,44 @@ def test_bloom_pruning_follows_reference(bloom_indexes, tmp_path, factor):
         assert n_diff == 0
     assert eng.image_info()["pos_bytes"] > 0
     eng.close()
+
+
+def test_phrase_only_batch_stats_are_its_own(positions_index):
+    """A batch of phrase queries alone launches neither the conjunctive lean
+    kernel nor the general one (engine.cc batch_run); its statistics must not
+    read those kernels' rows, which still hold the batch's previous run."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    d, seqs = positions_index
+    eng = _engine(d, "dense")
+    qs = phrase_cases(seqs, 400, seed=5)
+    ph = [q for q in qs if len(q) == 2]
+    conj = [q for q in qs if len(q) >= 2]
+
+    def upload(b, queries, phrase):
+        arr = (_capi.Query * len(queries))()
+        for i, q in enumerate(queries):
+            arr[i] = eng.resolve(w.SearchQuery(q, n_results=10, is_phrase=phrase))[0]
+        b.upload(arr)
+
+    a = w.ResidentBatch(eng, len(conj), 10)
+    upload(a, conj, False)
+    a.run()
+    a.fetch()
+    assert a.stats().survivors > 0
+    upload(a, ph, True)   # the same batch object: its conjunctive rows keep the last run's counts
+    a.run()
+    _, na = a.fetch()
+    na = list(na)[:len(ph)]
+    sa = a.stats()
+    b = w.ResidentBatch(eng, len(conj), 10)
+    upload(b, ph, True)
+    b.run()
+    _, nb = b.fetch()
+    nb = list(nb)[:len(ph)]
+    sb = b.stats()
+    assert na == nb
+    assert (sa.survivors, sa.driver_blocks, sa.algo_bytes) == (sb.survivors, sb.driver_blocks, sb.algo_bytes)
+    a.close()
+    b.close()
+    eng.close()

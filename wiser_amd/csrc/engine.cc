@@ -158,6 +158,7 @@ struct wsr_batch {
   bool gen_phrase = false;       // ... one of the general class (segment_kernel's phrase instance)
   bool has_conj_lean = true;     // the host's class rule found a conjunctive lean query
   bool has_gen = true;           // ... a general one
+  bool ran_conj = true, ran_gen = true;   // the last run launched them (their stats rows are its own)
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   bool two_conj = false;         // every conjunctive query: two terms (or empty), k <= kMaxK
   bool two_ph = false;           // every phrase query: k <= kMaxK (a lean one has two terms)
@@ -929,6 +930,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     // owners read every query's emission.)
     const bool run_conj = se || !b->has_phrase || b->has_conj_lean;
     const bool run_gen = se || !b->has_phrase || b->has_gen;
+    b->ran_conj = run_conj;
+    b->ran_gen = run_gen;
     HIP_OK(launch_plan(pa, b->d_q, b->nq, b->d_plan, b->d_ctr, b->ev_cap,
                        static_cast<uint32_t>(std::min<uint64_t>(b->item_cap, 0xFFFFFFFFull)),
                        run_conj ? kLeanWaves * b->lean_wgs : 0, b->has_phrase ? kLeanWaves * b->lean_wgs_ph : 0,
@@ -1098,6 +1101,8 @@ int wsr_batch_stats_get(wsr_handle* h, wsr_batch* b, wsr_batch_stats* out) {
     HIP_OK(hipMemcpy(ws.data(), b->d_stats, ws.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     uint64_t sv = 0, db = 0, ob = 0;
     for (int i = 0; i < rows; ++i) {
+      // (rows of a kernel the last run did not launch hold an earlier run's values)
+      if (i < b->seg_grid ? !b->ran_gen : (i < b->seg_grid + kLeanWaves * b->lean_wgs && !b->ran_conj)) continue;
       sv += ws[kStatStride * i]; db += ws[kStatStride * i + 1]; ob += ws[kStatStride * i + 2];
     }
     out->work_items = ctr[kCtrItems];
@@ -2048,7 +2053,8 @@ int wsr_debug_wg_stats(wsr_handle* h, wsr_batch* b, uint32_t* out, int32_t max_w
                        int32_t* n_wg, int32_t* stride) {
   if (!h || !b) return fail(WSR_E_INVALID, "null argument");
   std::lock_guard<std::mutex> g(h->mu);
-  // general workgroups, then lean waves (the conjunctive instance's, then the phrase instance's)
+  // general workgroups, then lean waves (the conjunctive instance's, then the phrase instance's);
+  // the rows of a kernel the last run did not launch (b->ran_conj / ran_gen) are stale
   const int rows = b->seg_grid + kLeanWaves * (b->lean_wgs + (b->has_phrase ? b->lean_wgs_ph : 0));
   if (n_wg) *n_wg = rows;
   if (stride) *stride = kStatStride;
