@@ -388,6 +388,9 @@ def roofline_of(acc, nbk, launch_ms, source):
             "kernel": "lean_kernel||segment_kernel"}
 
 
+LEG_MIN_BATCHES = int(os.environ.get("WSR_LEG_MIN_BATCHES", "16"))
+
+
 def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
     """A secondary workload on one GPU: items = [(terms, is_phrase)] in
     batches of `batch` resident queries; the timed region runs every batch
@@ -397,6 +400,21 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
     batches, chunks = [], []
     for s in range(0, len(items), batch):
         chunk = items[s:s + batch]
+        arr = (_capi.Query * len(chunk))()
+        for i, (terms, ph) in enumerate(chunk):
+            arr[i] = eng.resolve(w.SearchQuery(terms, n_results=k, is_phrase=ph))[0]
+        b = w.ResidentBatch(eng, batch, k)
+        b.upload(arr)
+        batches.append(b)
+        chunks.append(chunk)
+    # A batch runs again only after its last run: a log of few batches (C5's
+    # 10k queries: 3) caps the batches in flight at that count, so the leg would
+    # time its batches' latency, not the device's rate.  Copies of the batches
+    # (the same queries, each run in full) keep LEG_MIN_BATCHES resident, as the
+    # headline's 25 do.
+    n_distinct = len(batches)
+    for c in range(n_distinct, max(n_distinct, LEG_MIN_BATCHES)):
+        chunk = chunks[c % n_distinct]
         arr = (_capi.Query * len(chunk))()
         for i, (terms, ph) in enumerate(chunk):
             arr[i] = eng.resolve(w.SearchQuery(terms, n_results=k, is_phrase=ph))[0]
@@ -430,18 +448,24 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
     snaps = []
     if check:   # batch 0's last timed run, checked after every timed loop (snapshot)
         snaps.append(snapshot(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=[p for _, p in chunks[0]]))
-    nq = len(items) * passes
+    nq = sum(len(c) for c in chunks) * passes   # (every resident batch, copies included)
     for b in batches:
         b.close()
     nbk = len(batches)
     out = {"value": round(nq / el, 1), "unit": "queries/s", "queries": len(items),
-           "batch": batch, "passes": passes, "ms_per_batch": round(el / (passes * nbk) * 1e3, 4),
+           "batch": batch, "batches_resident": nbk, "passes": passes, "ms_per_batch": round(el / (passes * nbk) * 1e3, 4),
            "p50_alone_ms": round(statistics.median(lat), 3),
            "segment_ms_per_batch": round(acc["seg"] / nbk, 4),
            "survivors_per_batch": int(acc["surv"] / nbk),
            "driver_blocks_per_batch": int(acc["dblk"] / nbk),
            "roofline": roofline_of(acc, nbk, timed_seg, "timed region"),
            "parity_checked_queries": 0}
+    # the device's rate over the whole loop: a batch's algorithmic bytes per
+    # batch interval (with many launches in flight each one's duration is
+    # stretched by the others, so the per-launch figure reads low)
+    per_batch = acc["algo"] / nbk / (el / (passes * nbk)) / 1e9
+    out["roofline"]["achieved_per_batch"] = round(per_batch, 1)
+    out["roofline"]["frac_per_batch"] = round(per_batch / HBM_PEAK_GBS, 4)
 
     def deferred():   # oracle work, after every timed loop of the run (see snapshot)
         out["parity_checked_queries"] = sum(verify_snapshot(sn) for sn in snaps)
