@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Per-launch fabric bytes of the segment phase (scripts/gpu_prof.sh,
 # scripts/pmc_bytes.py), one profile per workload: attached to lines of that
 # workload only, with the file named in roofline.traffic_source.
-PMC_PROFILES = {w: f"r05g/{w}_pmc_segment.json"
+PMC_PROFILES = {w: f"r05h/{w}_pmc_segment.json"
                 for w in ("c3", "c2", "c4_mixed_1to5", "c5_phrase", "single_high", "realistic_mix")}
 # The sources a counter profile describes (the kernels, their launch and the
 # image they read): scripts/pmc_bytes.py records their hash in the profile and

@@ -414,8 +414,11 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
     h->grid = prop.multiProcessorCount * std::min(occ, 32);
     // general workers hold 12 KB of LDS each: at most 4 per CU, so that the
     // concurrent lean kernel keeps its occupancy
+    // (one workgroup per CU past that: it starts as the first resident ones
+    // leave; C4 +1.6 %, the mixed log +0.6 %, the rest unchanged,
+    // profiles/r05/leg_ab.txt r05ar / r05as)
     const int gen_per_cu = static_cast<int>(env_number("WSR_GEN_PER_CU", 4));
-    h->gen_cap = prop.multiProcessorCount * std::max(1, std::min(std::min(occ, 32), gen_per_cu));
+    h->gen_cap = prop.multiProcessorCount * std::max(1, std::min(std::min(occ, 32), gen_per_cu) + 1);
     int locc = lean_kernel_occupancy(false);
     if (locc < 1) locc = 1;
     h->lean_wgs = prop.multiProcessorCount * std::min(locc, 16);
@@ -669,7 +672,7 @@ int wsr_batch_create(wsr_handle* h, int32_t max_q, int32_t stride, wsr_batch** o
     HIP_OK(hipMalloc(&b->d_nhits, sizeof(int32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_qdone, sizeof(uint32_t) * max_q));
     HIP_OK(hipMalloc(&b->d_stats, sizeof(uint32_t) * kStatStride *
-                                      (std::max(h->grid, 1) +
+                                      (std::max(std::max(h->grid, h->gen_cap), 1) +   // (seg_grid <= gen_cap)
                                        kLeanWaves * (std::max(h->lean_wgs_two, 1) + std::max(h->lean_wgs_ph, 1)))));
     for (auto& e : b->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
