@@ -49,3 +49,22 @@ def test_bench_two_ranks_gloo(built, tmp_path):
     assert d["hbm_per_rank"]["total_bytes"] > 0
     assert d["config"]["parallelism"].startswith(("hybrid-docshard2", "docshard2"))
     assert "REHEARSAL" in d["exchange"]["kind"]
+
+
+def test_bench_gpus2_spawns_its_launcher(built, tmp_path):
+    """`bench.py --gpus 2` with no launcher around it starts one
+    itself (a child torch.distributed.run) and reports n_gpus 2, not a silent
+    one-rank measurement."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--exchange", "gloo",
+           "--workload", "c2", "--docs", "50000", "--vocab", "50000", "--queries", "20000", "--steps", "20",
+           "--warmup", "2", "--no-extra", "--no-cpu", "--check", "64", "--mode", "shard", "--heavy-blocks", "0",
+           "--index-dir", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["parity_checked_queries"] > 0
+    assert d["config"]["parallelism"] == "docshard2"

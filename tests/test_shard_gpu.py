@@ -384,3 +384,48 @@ def test_step_regions_overflow_is_loud(synth_small):
     qs = [[head[i % 8], head[(i + 1) % 8]] for i in range(64)]
     with pytest.raises(_capi.WiserError, match="exchange slot"):
         _run_step_regions(d, qs, 10, 2, slot=4)
+
+
+def test_host_replay_taken_by_phrase_only_run(positions_index):
+    """a deferred host-exchange owner replay taken by a plain
+    run of a phrase-only batch (no conjunctive lean item) must still run -- the
+    conjunctive launch that carries it is forced -- and the owner's fetch must
+    wait for it.  Both batches equal the oracle."""
+    import torch.distributed as dist
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import HostExchangeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    from conftest import phrase_cases
+    d, seqs = positions_index
+    rng = random.Random(23)
+    words = [f"w{i}" for i in range(60)]
+    conj = [rng.sample(words[:30], 2) for _ in range(128)]
+    phr = [p for p in phrase_cases(seqs, 400, seed=29) if len(p) == 2][:96]
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:29617", rank=0, world_size=1)
+    try:
+        S = HostExchangeShardedSearcher(d, 0, 1, positions=True)
+        eng = S.engine
+        o = OracleVacuum(d)
+        ba = w.ResidentBatch(eng, len(conj), 10)
+        ba.upload((_capi.Query * len(conj))(*[eng.resolve(w.SearchQuery(q, n_results=10))[0] for q in conj]))
+        bp = w.ResidentBatch(eng, len(phr), 10)
+        bp.upload((_capi.Query * len(phr))(
+            *[eng.resolve(w.SearchQuery(q, n_results=10, is_phrase=True))[0] for q in phr]))
+        for _ in range(2):
+            S.step(ba, len(conj), 64 * len(conj))
+            S.flush()          # ba's owner replay now waits for another batch's run
+            bp.run()           # a phrase-only run takes it
+            hits, nh = bp.fetch()
+            for i, q in enumerate(phr):
+                got = [(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])]
+                assert got == o.search(q, 10, phrase=True)[0], q
+            hits, nh = S.fetch_owned(ba, len(conj))
+            got = [[(hits[i * 10 + j].doc_id, hits[i * 10 + j].score) for j in range(nh[i])]
+                   for i in range(len(conj))]
+            assert got == [o.search(q, 10)[0] for q in conj]
+        ba.close()
+        bp.close()
+        S.close()
+    finally:
+        dist.destroy_process_group()

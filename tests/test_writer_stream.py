@@ -69,3 +69,21 @@ def test_first_bad_row(built, tmp_path, chunk):
     finally:
         os.environ.pop("WSR_WRITER_CHUNK_DOCS", None)
     assert not os.path.exists(str(tmp_path / "o1" / ".wsr_runs"))
+
+
+def test_log_generators_fail_on_unwritable_path(built, tmp_path):
+    """a query-log generator whose output cannot be written fails
+    the call instead of returning WSR_OK with no file."""
+    import pytest
+    import wiser_amd as w
+    d = str(tmp_path / "idx")
+    w.build_synthetic(d, n_docs=20000, vocab=20000, seed=3, threads=2)
+    bad = str(tmp_path / "no_such_dir" / "q.log")
+    for gen in (lambda p: w.gen_two_term_log(d, p, n_queries=10),
+                lambda p: w.gen_mixed_log(d, p, n_queries=10),
+                lambda p: w.gen_single_term_log(d, p, True, n_queries=10)):
+        with pytest.raises(Exception):
+            gen(bad)
+        ok = str(tmp_path / "q.log")
+        assert gen(ok) == 10
+        assert len(open(ok).read().splitlines()) == 10

@@ -174,11 +174,11 @@ struct wsr_batch {
   uint64_t x_slots = 0;     // region events * pairs the two exchange buffers were sized for
   int x_pairs = 0;
   hipEvent_t xev[2] = {nullptr, nullptr};   // emission done -> comm stream; exchange done -> replay
-  bool x_pending = false;   // a shard step's exchange + owner replay (xev[1]) not yet joined
+  std::atomic<bool> x_pending{false};   // a shard step's exchange + owner replay (xev[1]) not yet joined
   // exchanges asked of the communicator's worker thread for this batch, and
   // those it has enqueued (xev[1] recorded): xev[1] is only waited on once
   // they agree (x_join)
-  uint64_t x_req = 0;
+  std::atomic<uint64_t> x_req{0};
   std::atomic<uint64_t> x_enq{0};
   // a step group's owner replay of this batch deferred (wsr_shard_steps) and
   // not yet enqueued: x_join has x_comm enqueue it first (atomic: a fetch on
@@ -188,8 +188,10 @@ struct wsr_batch {
   bool x_fused = false;     // the last run emitted into the exchange regions (fill counters after d_ctr)
   // a host-exchange owner replay of this batch waiting for another batch's
   // run to carry it (wsr_shard_step_replay_deferred); its regions are in
-  // d_xrecv once xev[0] (recorded after their copy on st) has passed
-  wsr_handle* hdef = nullptr;
+  // d_xrecv once xev[0] (recorded after their copy on st) has passed.  Set and
+  // cleared under the handle's hdef_mu; a run that takes it counts it in
+  // x_req before clearing it, so x_join waits for its enqueue
+  std::atomic<wsr_handle*> hdef{nullptr};
   int32_t hdef_rank = 0;
   int x_world = 0, x_qpr = 0;   // ... for this world and q_per_owner
   int64_t x_slot = 0;           //     and slot (the replay half must match them)
@@ -219,7 +221,8 @@ static void host_replay_flush(wsr_batch* b);
 static bool x_join(wsr_batch* b) {
   if (b->hdef) host_replay_flush(b);
   if (wsr_comm* c = b->x_comm.load(std::memory_order_acquire)) replay_flush(c, b);
-  while (b->x_enq.load(std::memory_order_acquire) != b->x_req) std::this_thread::yield();
+  while (b->x_enq.load(std::memory_order_acquire) != b->x_req.load(std::memory_order_acquire))
+    std::this_thread::yield();
   return b->x_pending;
 }
 
@@ -931,7 +934,9 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
     // others: 54 us on C5, profiles/r05p); the plan flags kErrClass if a class
     // without a launch holds items.  (Shard steps launch everything: their
     // owners read every query's emission.)
-    const bool run_conj = se || !b->has_phrase || b->has_conj_lean;
+    // (a taken owner replay rides in the conjunctive launch: it runs then
+    // even with no conjunctive lean item of its own)
+    const bool run_conj = se || oj || !b->has_phrase || b->has_conj_lean;
     const bool run_gen = se || !b->has_phrase || b->has_gen;
     b->ran_conj = run_conj;
     b->ran_gen = run_gen;
@@ -962,6 +967,10 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
       if (run_conj)
         HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
                            b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->st_pad));
+      if (pb) {   // the replay's end: behind the conjunctive launch that carried it
+        HIP_OK(hipEventRecord(pb->xev[1], b->st_pad));
+        pb_queued = true;
+      }
       HIP_OK(hipEventRecord(b->join_ph, b->st_pad));
       FusedReplay frp = fr;
       frp.oj = OwnerJob{};
@@ -973,10 +982,14 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
                          b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, st));
     }
     HIP_OK(hipEventRecord(b->ev[4], st));
-    if (pb) {
+    if (pb && !pb_queued) {
       HIP_OK(hipEventRecord(pb->xev[1], st));
-      pb->x_pending = true;
       pb_queued = true;
+    }
+    if (pb) {
+      pb->x_pending = true;
+      pb->x_enq.fetch_add(1, std::memory_order_release);   // (take_host_replay counted it in x_req)
+      pb = nullptr;
     }
     HIP_OK(hipStreamWaitEvent(st, b->join, 0));
     if (b->has_phrase) HIP_OK(hipStreamWaitEvent(st, b->join_ph, 0));
@@ -986,7 +999,11 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
                                 b->d_nhits, st));
     HIP_OK(hipEventRecord(b->ev[3], st));
   } catch (const std::exception& e) {
-    if (pb && !pb_queued) host_replay_enqueue(pb, h);   // (its own stream, then)
+    if (pb) {
+      if (!pb_queued) host_replay_enqueue(pb, h);   // (its own stream, then)
+      else pb->x_pending = true;
+      pb->x_enq.fetch_add(1, std::memory_order_release);
+    }
     return fail(WSR_E_HIP, e.what());
   }
   b->ran = true;
@@ -1849,7 +1866,7 @@ int wsr_shard_steps(wsr_handle* h, wsr_batch* const* bs, int32_t n, wsr_comm* c,
   {
     std::lock_guard<std::mutex> lk(c->mu);
     for (int i = 0; i < n; ++i) {
-      ++bs[i]->x_req;
+      bs[i]->x_req.fetch_add(1, std::memory_order_acq_rel);
       if (g->defer) bs[i]->x_comm.store(c, std::memory_order_release);
     }
     c->jobs.push_back(g);
@@ -1949,8 +1966,8 @@ int wsr_shard_step_replay_deferred(wsr_handle* h, wsr_batch* b, int32_t rank, in
     return fail(WSR_E_HIP, e.what());
   }
   std::lock_guard<std::mutex> g(h->hdef_mu);
-  b->hdef = h;
   b->hdef_rank = rank;
+  b->hdef.store(h);
   h->hdef_q.push_back(b);
   return WSR_OK;
 }
@@ -1963,7 +1980,10 @@ static wsr_batch* take_host_replay(wsr_handle* h, const wsr_batch* b, OwnerJob* 
     wsr_batch* pb = *it;
     if (pb == b) continue;
     h->hdef_q.erase(it);
-    pb->hdef = nullptr;
+    // counted before hdef is cleared: an x_join that sees it cleared waits
+    // until the taking run has recorded xev[1] (x_enq)
+    pb->x_req.fetch_add(1, std::memory_order_acq_rel);
+    pb->hdef.store(nullptr);
     const uint64_t region = region_events_of(pb->x_qpr, pb->x_slot);
     const uint64_t meta_events = (static_cast<uint64_t>(pb->x_qpr) + 1) / 2;
     *oj = OwnerJob{pb->d_q, reinterpret_cast<const int32_t*>(pb->d_xrecv), pb->d_xrecv + meta_events, pb->d_hits,
@@ -1982,17 +2002,17 @@ static void host_replay_enqueue(wsr_batch* pb, wsr_handle* h) {
 }
 
 static void host_replay_flush(wsr_batch* b) {
-  wsr_handle* h = b->hdef;
+  wsr_handle* h = b->hdef.load();
   if (!h) return;
   {
     std::lock_guard<std::mutex> g(h->hdef_mu);
-    if (!b->hdef) return;   // (taken by a run meanwhile)
+    if (!b->hdef.load()) return;   // (taken by a run meanwhile; x_join waits for its enqueue)
     for (auto it = h->hdef_q.begin(); it != h->hdef_q.end(); ++it)
       if (*it == b) {
         h->hdef_q.erase(it);
         break;
       }
-    b->hdef = nullptr;
+    b->hdef.store(nullptr);
   }
   host_replay_enqueue(b, h);
 }

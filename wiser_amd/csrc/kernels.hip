@@ -46,6 +46,7 @@
 #include <cstdint>
 
 #include "kernels.h"
+#include "regheap.h"
 
 namespace wiser {
 
@@ -1292,9 +1293,58 @@ struct HeapSink {
   }
 };
 
+// The same heap for k <= kRegHeapK held in registers (regheap.h): every step
+// of a walk is an f64 compare and a uniform branch over registers of fixed
+// index, no permute or readlane chain.  The replay's heap insertions were the
+// batch's tail (~1,300 cycles each on WaveHeap).
+struct RegHeapSink {
+  RegHeap H;
+  uint32_t k = 0;
+  template <class Emit>
+  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&&) {
+    const double top = H.n < k ? -1.0 : H.s[0];
+    uint64_t cm = __ballot(valid && sc > top);
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      H.insert(k, readlane_f64(sc, fl),
+               static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl)));
+    }
+  }
+  // SortHeap: pop m times, the i-th popped to lane m - 1 - i, one store
+  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t m = H.n;
+    double os = 0.0;
+    int32_t od = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+      if (l == m - 1 - i) { os = H.s[0]; od = H.d[0]; }
+      H.pop();
+    }
+    if (l < m) {
+      HitDev h;
+      h.doc = od;
+      h.pad = 0;
+      h.score = os;
+      out[l] = h;
+    }
+    if (l == 0) *n_out = static_cast<int32_t>(m);
+  }
+};
 
 // One wave per query: the events of its segments (doc-id order) through the
-// restated heap (HeapSink::step: the heap's own insertion test).
+// restated heap (Sink::step: the heap's own insertion test).
+template <bool kCoherent, class Sink>
+__device__ __forceinline__ void replay_query_sink(const QueryPlan& P, uint32_t k, const Event* events,
+                                                  const uint32_t* ev_cnt, HitDev* out, int32_t* n_out) {
+  Sink sink;
+  sink.k = k;
+  consume_stream<kCoherent>(
+      sink, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
+      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
+      [](double, int32_t) {});
+  sink.finish(out, n_out);
+}
 template <bool kCoherent>
 __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
                                              const QueryPlan* __restrict__ plan, int qi,
@@ -1303,13 +1353,11 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
                                              int32_t* __restrict__ n_hits) {
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
-  HeapSink sink;
-  sink.k = k;
-  consume_stream<kCoherent>(
-      sink, P.n_items, [&](uint32_t r) { return load_count<kCoherent>(ev_cnt + P.item_base + r); },
-      [&](uint32_t r) { return events + P.ev_base + static_cast<uint64_t>(r) * P.seg_blocks * 128; },
-      [](double, int32_t) {});
-  sink.finish(hits + static_cast<int64_t>(qi) * hit_stride, &n_hits[qi]);
+  HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
+  if (k <= static_cast<uint32_t>(kRegHeapK))
+    replay_query_sink<kCoherent, RegHeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
+  else
+    replay_query_sink<kCoherent, HeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
 }
 
 // A one-item query's events straight from the lean kernel's LDS buffer (lane
@@ -1325,10 +1373,18 @@ __device__ __noinline__ void replay_lds_call(double sc, int32_t dc, uint32_t n, 
   n_out = reinterpret_cast<int32_t*>(static_cast<uint64_t>(uni(static_cast<uint32_t>(no))) |
                                      (static_cast<uint64_t>(uni(static_cast<uint32_t>(no >> 32))) << 32));
   n = uni(n);
-  HeapSink sink;
-  sink.k = uni(k);
-  sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
-  sink.finish(out, n_out);
+  k = uni(k);
+  if (k <= static_cast<uint32_t>(kRegHeapK)) {
+    RegHeapSink sink;
+    sink.k = k;
+    sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
+    sink.finish(out, n_out);
+  } else {
+    HeapSink sink;
+    sink.k = k;
+    sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
+    sink.finish(out, n_out);
+  }
 }
 
 // out-of-line copy for the segment kernel (keeps its register allocation
@@ -3171,6 +3227,11 @@ __device__ __forceinline__ void owner_replay_query(const QueryIn* __restrict__ q
     LdsHeapSink sink;
     sink.hs = s_hs;
     sink.hd = s_hd;
+    sink.k = k;
+    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
+    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
+  } else if (k <= static_cast<uint32_t>(kRegHeapK)) {
+    RegHeapSink sink;
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);

@@ -1343,6 +1343,15 @@ void df_groups(const std::string& dir, std::vector<std::string>* low, std::vecto
   if (low->empty() || high->empty() || low->size() + high->size() < 2)
     throw std::runtime_error("df table has an empty low or high group");
 }
+
+// One query per line; a file that cannot be opened or written fails the call.
+void write_log(const std::string& out_path, const std::vector<std::string>& lines) {
+  std::ofstream f(out_path, std::ios::trunc);
+  if (!f) throw std::runtime_error("cannot open query log " + out_path);
+  for (auto& q : lines) f << q << "\n";
+  f.close();
+  if (!f) throw std::runtime_error("cannot write query log " + out_path);
+}
 }  // namespace
 
 int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t seed,
@@ -1366,8 +1375,7 @@ int64_t gen_two_term_log(const std::string& dir, int64_t n_queries, uint64_t see
     std::string q = t1 + " " + t2;
     if (seen.insert(q).second) out.push_back(q);
   }
-  std::ofstream f(out_path, std::ios::trunc);
-  for (auto& q : out) f << q << "\n";
+  write_log(out_path, out);
   return static_cast<int64_t>(out.size());
 }
 
@@ -1402,8 +1410,7 @@ int64_t gen_mixed_log(const std::string& dir, int64_t n_queries, uint64_t seed,
     for (auto& t : terms) q += (q.empty() ? "" : " ") + t;
     if (seen.insert(q).second) out.push_back(q);
   }
-  std::ofstream f(out_path, std::ios::trunc);
-  for (auto& q : out) f << q << "\n";
+  write_log(out_path, out);
   return static_cast<int64_t>(out.size());
 }
 
@@ -1413,8 +1420,11 @@ int64_t gen_single_term_log(const std::string& dir, bool high, int64_t n_queries
   df_groups(dir, &low, &hi);
   const auto& grp = high ? hi : low;
   std::mt19937_64 g(seed);
-  std::ofstream f(out_path, std::ios::trunc);
-  for (int64_t i = 0; i < n_queries; ++i) f << grp[g() % grp.size()] << "\n";
+  if (grp.empty()) throw std::runtime_error("no terms in the requested df group");
+  std::vector<std::string> out;
+  out.reserve(static_cast<size_t>(std::max<int64_t>(n_queries, 0)));
+  for (int64_t i = 0; i < n_queries; ++i) out.push_back(grp[g() % grp.size()]);
+  write_log(out_path, out);
   return n_queries;
 }
 
@@ -1431,8 +1441,9 @@ int64_t gen_phrase_log(const std::string& dir, int64_t n_queries, uint64_t seed,
   const int64_t n = std::min<int64_t>(n_queries, static_cast<int64_t>(pool.size()));
   for (int64_t i = 0; i < n; ++i)
     std::swap(pool[i], pool[i + static_cast<int64_t>(g() % (pool.size() - i))]);
-  std::ofstream f(out_path, std::ios::trunc);
-  for (int64_t i = 0; i < n; ++i) f << '"' << pool[i] << "\"\n";   // gen_synthetic_log.py:262
+  std::vector<std::string> out;
+  for (int64_t i = 0; i < n; ++i) out.push_back('"' + pool[i] + '"');   // gen_synthetic_log.py:262
+  write_log(out_path, out);
   return n;
 }
 
