@@ -391,15 +391,23 @@ def roofline_of(acc, nbk, launch_ms, source):
 LEG_MIN_BATCHES = int(os.environ.get("WSR_LEG_MIN_BATCHES", "16"))
 
 
-def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
+def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds, class_form=False):
     """A secondary workload on one GPU: items = [(terms, is_phrase)] in
     batches of `batch` resident queries; the timed region runs every batch
-    `passes` times (consecutive batches in flight, as the main leg)."""
+    `passes` times (consecutive batches in flight, as the main leg).
+    class_form: the batches are cut by the engine's batch former
+    (wsr_class_order: the log's conjunctive queries, then its phrase queries,
+    each cut into batches of `batch`), not in log order."""
     import wiser_amd as w
     from wiser_amd import _capi
     batches, chunks = [], []
-    for s in range(0, len(items), batch):
-        chunk = items[s:s + batch]
+    groups = [items[s:s + batch] for s in range(0, len(items), batch)]
+    if class_form:
+        allq = (_capi.Query * len(items))()
+        for i, (terms, ph) in enumerate(items):
+            allq[i] = eng.resolve(w.SearchQuery(terms, n_results=k, is_phrase=ph))[0]
+        groups = [[items[i] for i in g] for g in w.class_batches(allq, batch)]
+    for chunk in groups:
         arr = (_capi.Query * len(chunk))()
         for i, (terms, ph) in enumerate(chunk):
             arr[i] = eng.resolve(w.SearchQuery(terms, n_results=k, is_phrase=ph))[0]
@@ -443,16 +451,20 @@ def run_leg(eng, idx, items, k, batch, passes, check, cpu_seconds):
     el = time.perf_counter() - t0
     seg = [b.stats() for b in batches]   # each batch's last run: inside the timed loop
     timed_seg = sum(st.segment_ms for st in seg) / len(seg)
-    for b in batches[::-1]:   # device error flags of every batch's last run (fetch raises)
-        hits, nh = b.fetch()
     snaps = []
-    if check:   # batch 0's last timed run, checked after every timed loop (snapshot)
-        snaps.append(snapshot(idx, [t for t, _ in chunks[0]], hits, nh, k, check, phrase=[p for _, p in chunks[0]]))
+    for i in range(len(batches) - 1, -1, -1):   # device error flags of every batch's last run (fetch raises)
+        hits, nh = batches[i].fetch()
+        # batch 0's last timed run and the last distinct batch's (a class-form
+        # leg's phrase batch), checked after every timed loop (snapshot)
+        if check and (i == 0 or (i == n_distinct - 1 and class_form)):
+            snaps.append(snapshot(idx, [t for t, _ in chunks[i]], hits, nh, k, check,
+                                  phrase=[p for _, p in chunks[i]]))
     nq = sum(len(c) for c in chunks) * passes   # (every resident batch, copies included)
     for b in batches:
         b.close()
     nbk = len(batches)
     out = {"value": round(nq / el, 1), "unit": "queries/s", "queries": len(items),
+           "distinct_queries": len(items), "distinct_batches": n_distinct,
            "batch": batch, "batches_resident": nbk, "passes": passes, "ms_per_batch": round(el / (passes * nbk) * 1e3, 4),
            "p50_alone_ms": round(statistics.median(lat), 3),
            "segment_ms_per_batch": round(acc["seg"] / nbk, 4),
@@ -669,8 +681,22 @@ def extra_legs(a, idx, qlog, local, threads):
             t = time.time()
             eng.Load()
             load_s = round(time.time() - t, 1)
-        leg = run_leg(eng, lidx, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 4)
+        mixed = name == "realistic_mix"
+        leg = run_leg(eng, lidx, items, a.k, a.batch, 4, a.check, 0 if a.no_cpu else a.cpu_seconds / 4,
+                      class_form=mixed)
         leg["workload"] = what
+        if leg["batches_resident"] > leg["distinct_batches"]:
+            leg["workload"] += (f"; {leg['distinct_batches']} distinct batches, each run in full, resident as "
+                                f"{leg['batches_resident']} (copies)")
+        if mixed:
+            # the value: batches cut by the engine's batch former (wsr_class_order:
+            # class-pure batches); the log's own order (phrases inside every
+            # batch) beside it
+            leg["workload"] += ("; batches cut by the engine's batch former (wsr_class_order: the log's "
+                                "conjunctive queries, then its phrases, each class in batches of 4096)")
+            inter = run_leg(eng, lidx, items, a.k, a.batch, 4, 0, 0)
+            leg["interleaved"] = {"value": inter["value"], "ms_per_batch": inter["ms_per_batch"],
+                                  "note": "the same log cut in log order: ~10 % phrases in every batch"}
         if positions:
             leg["load_s"] = load_s
             leg["image"] = eng.image_info()

@@ -209,6 +209,18 @@ int wsr_resolve_text(wsr_handle* h, const char* text, int64_t len, int32_t k, in
 int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int32_t hit_stride,
                     int32_t max_q, wsr_hit* hits, int32_t* n_hits, int32_t* nq);
 
+/* The batch former for a stream of queries cut into batches.  The reference
+ * scores every query on its own (grpc_server_impl.h:382-389, a query_pool.h
+ * log mixes classes), so which queries share a batch is the engine's choice:
+ * order[0..nq) receives a stable permutation of the queries that puts each
+ * execution class together -- conjunctive queries (AND of any length, single
+ * terms) first, then phrase queries of two or more terms -- and *n_conj the
+ * size of the first class.  Batches cut from this order are class-pure: a
+ * phrase query's position check then runs in batches of its own instead of
+ * riding, a few hundred at a time, at the tail of every conjunctive batch
+ * (DESIGN.md §4i).  Needs no handle. */
+int wsr_class_order(const wsr_query* q, int32_t nq, int32_t* order, int32_t* n_conj);
+
 /* ---- resident batches ------------------------------------------------ */
 int wsr_batch_create(wsr_handle* h, int32_t max_queries, int32_t hit_stride, wsr_batch** out);
 void wsr_batch_destroy(wsr_handle* h, wsr_batch* b);

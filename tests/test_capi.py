@@ -66,3 +66,32 @@ def test_struct_layouts(built, tmp_path):
                    C.sizeof(_capi.OpenOpts), _capi.OpenOpts.positions.offset,
                    C.sizeof(_capi.BatchStats), C.sizeof(_capi.BuildStats)]
     assert C.sizeof(_capi.Query) == 88 and C.sizeof(_capi.Hit) == 16
+
+
+def test_class_order_is_stable_and_class_pure(built):
+    from wiser_amd import _capi
+    """wsr_class_order (the engine's batch former): conjunctive queries first
+    (a one-term phrase counts as a single-term query), then phrases of two or
+    more terms, each class in its input order; class_batches cuts each class
+    on its own."""
+    import random
+    import wiser_amd as w
+    rng = random.Random(5)
+    n = 1000
+    arr = (_capi.Query * n)()
+    kinds = []
+    for i in range(n):
+        nt = rng.choice([1, 2, 2, 3])
+        ph = rng.random() < 0.15
+        arr[i].n_terms = nt
+        arr[i].flags = 1 if ph else 0
+        kinds.append(ph and nt > 1)
+    order, nc = w.class_order(arr)
+    assert sorted(order) == list(range(n))
+    assert nc == kinds.count(False)
+    assert order[:nc] == [i for i in range(n) if not kinds[i]]
+    assert order[nc:] == [i for i in range(n) if kinds[i]]
+    bs = w.class_batches(arr, 128)
+    assert [i for b in bs for i in b] == order
+    assert all(len(b) <= 128 and len({kinds[i] for i in b}) == 1 for b in bs)
+    assert _capi.lib.wsr_class_order(None, 3, None, None) == -1

@@ -284,3 +284,41 @@ def test_phrase_only_batch_stats_are_its_own(positions_index):
     a.close()
     b.close()
     eng.close()
+
+
+def test_class_batches_resident(positions_index):
+    """The engine's batch former (wsr_class_order) over a mixed log: class-pure
+    resident batches, run back to back with several in flight, every result
+    equal to the oracle's and scattered back to its query."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from oracle.oracle import OracleVacuum
+    d, seqs = positions_index
+    eng = w.VacuumEngine(d, positions=True)
+    eng.Load()
+    orc = OracleVacuum(d)
+    rng = random.Random(31)
+    qs = phrase_cases(seqs, 900, seed=37)
+    items = [(q, rng.random() < 0.3) for q in qs]
+    arr = (_capi.Query * len(items))(*[eng.resolve(w.SearchQuery(q, n_results=10, is_phrase=ph))[0]
+                                       for q, ph in items])
+    groups = w.class_batches(arr, 128)
+    assert len({items[i][1] and len(items[i][0]) > 1 for i in groups[0]}) == 1
+    bs = []
+    for g in groups:
+        b = w.ResidentBatch(eng, len(g), 10)
+        b.upload((_capi.Query * len(g))(*[arr[i] for i in g]))
+        bs.append(b)
+    for _ in range(2):
+        for b in bs:
+            b.run()
+    got = {}
+    for g, b in zip(groups, bs):
+        hits, nh = b.fetch()
+        for j, i in enumerate(g):
+            got[i] = [(hits[j * 10 + t].doc_id, hits[j * 10 + t].score) for t in range(nh[j])]
+        b.close()
+    for i, (q, ph) in enumerate(items):
+        assert got[i] == orc.search(list(q), 10, phrase=ph)[0], (q, ph)
+    eng.close()
+    orc.close()

@@ -110,6 +110,7 @@ _sigs = {
                                    C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int64]),
     "wsr_search_text": (C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                   C.POINTER(Hit), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "wsr_class_order": (C.c_int, [C.POINTER(Query), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "wsr_batch_create": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_batch_destroy": (None, [_P, _P]),
     "wsr_batch_upload": (C.c_int, [_P, _P, C.POINTER(Query), C.c_int32]),

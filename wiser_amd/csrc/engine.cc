@@ -1274,6 +1274,19 @@ int wsr_search_text(wsr_handle* h, const char* text, int64_t len, int32_t k, int
   return wsr_search_batch(h, q.data(), *nq_out, hit_stride, hits, n_hits);
 }
 
+int wsr_class_order(const wsr_query* q, int32_t nq, int32_t* order, int32_t* n_conj) {
+  if (nq < 0 || (nq && (!q || !order)) || !n_conj) return fail(WSR_E_INVALID, "bad class_order arguments");
+  // (a one-term phrase is a single-term query: the same class as in the plan)
+  auto phrase = [&](int32_t i) { return (q[i].flags & WSR_QUERY_PHRASE) != 0 && q[i].n_terms > 1; };
+  int32_t n = 0;
+  for (int32_t i = 0; i < nq; ++i)
+    if (!phrase(i)) order[n++] = i;
+  *n_conj = n;
+  for (int32_t i = 0; i < nq; ++i)
+    if (phrase(i)) order[n++] = i;
+  return WSR_OK;
+}
+
 int wsr_shard_fill(wsr_handle* h, wsr_batch* b, int32_t n_owners, int64_t* owner_totals) {
   if (!h || !b || !b->x_fused || !owner_totals || n_owners <= 0 || n_owners > b->x_world)
     return fail(WSR_E_INVALID, "call wsr_shard_step (or wsr_shard_step_emit) first");

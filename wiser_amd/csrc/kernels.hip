@@ -1295,8 +1295,13 @@ struct HeapSink {
 
 // The same heap for k <= kRegHeapK held in registers (regheap.h): every step
 // of a walk is an f64 compare and a uniform branch over registers of fixed
-// index, no permute or readlane chain.  The replay's heap insertions were the
-// batch's tail (~1,300 cycles each on WaveHeap).
+// index, no permute or readlane chain.  Measured slower than WaveHeap: the
+// compiler keeps the 48 uniform values in SGPRs, spills them to VGPR lanes and
+// copies the whole array at every join of the walk's branches (1,250 against
+// 550 ns per insertion at k = 10, profiles/r06/heap_bench_r06b.txt), and the
+// bench fell 22.8 -> 18.4 M q/s; held in VGPRs (in_vgpr) it copies them with
+// ~2,400 v_mov and spills as well.  Off (kRegHeapReplay).
+constexpr bool kRegHeapReplay = false;
 struct RegHeapSink {
   RegHeap H;
   uint32_t k = 0;
@@ -1354,7 +1359,7 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
   HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
-  if (k <= static_cast<uint32_t>(kRegHeapK))
+  if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK))
     replay_query_sink<kCoherent, RegHeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
   else
     replay_query_sink<kCoherent, HeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
@@ -1374,7 +1379,7 @@ __device__ __noinline__ void replay_lds_call(double sc, int32_t dc, uint32_t n, 
                                      (static_cast<uint64_t>(uni(static_cast<uint32_t>(no >> 32))) << 32));
   n = uni(n);
   k = uni(k);
-  if (k <= static_cast<uint32_t>(kRegHeapK)) {
+  if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK)) {
     RegHeapSink sink;
     sink.k = k;
     sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
@@ -1852,6 +1857,13 @@ __device__ __forceinline__ void pair_values(uint32_t w0, uint32_t w1, uint32_t w
 // profiles/r02_sc_ab.txt; 16 and 32 are within the noise, with 6 % and 21 %
 // more events: profiles/r02_su_refresh_interval_ab.txt).
 constexpr uint32_t kFloorRefresh = 8;
+// Extra iterations of slack in the conjunctive lean pipeline (kDeep of
+// lean_segment): 0 -- H consumes the O1 probes D issued one iteration
+// earlier and C the rank records H issued one iteration earlier; 1 -- H runs
+// two blocks behind D (the probes have a whole iteration in flight); 2 -- C
+// also runs two blocks behind H.  Each stage of slack keeps one more register
+// set live across the loop.
+constexpr int kLeanDeep = 0;
 // Capacity of the LDS event buffer: flushed after every chunk that added
 // events (64 since round 3: C2 leg 31.5 -> 33.2 M q/s, C4 11.8 -> 12.5 M
 // against 128, C3 headline unchanged; 4 KB less LDS per workgroup,
@@ -1884,7 +1896,7 @@ struct LeanLdsT {
 // D loads its bucket entry, H matches the offset and loads the hit's tf word,
 // C resolves the rare probe past a bucket's fourth posting from its offset
 // bytes.  The same pipeline otherwise.
-template <bool kPh, bool kTwo = false, bool kBk = false>
+template <bool kPh, bool kTwo = false, bool kBk = false, int kDeep = 0>
 __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                              const QueryDesc& Q, const int32_t* qlist,
                                              bool phrase, uint32_t b0, uint32_t b1, bool dtail,
@@ -2142,8 +2154,8 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     pair_words(a_blob + uni(e.w) + 2, (m >> 8) ? (m >> 8) : 1u, l, Y.wt0, Y.wt1, Y.wt2, sh);
   };
   auto stage_C = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    // C(j-2): compaction of block j-2 (its H fields are in X)
-    if (j >= b0 + 2) {
+    // C(j-2-kDeep): compaction of that block (its H fields are in X)
+    if (j >= b0 + 2 + kDeep) {
       // O1 posting ranks (hits): rank word + bits below; the tf byte is read by
       // rank when the chunk is scored (flag bit 31)
       // (the record's tf bytes cover the word's first four postings)
@@ -2193,7 +2205,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       qdoc[e0] = X.ha0; qc4[e0] = X.hc0; qtd[e0] = X.ht0; qto[e0] = to0;
       qdoc[e1] = X.ha1; qc4[e1] = X.hc1; qtd[e1] = X.ht1; qto[e1] = to1;
       if (kPh) {   // block j-2's postings 2l, 2l+1 and their O1 ranks
-        const uint32_t pd0 = (Q.a_blk0 + j - 2) * 128u + 2 * l;
+        const uint32_t pd0 = (Q.a_blk0 + j - 2 - kDeep) * 128u + 2 * l;
         qpd[e0] = pd0; qpo[e0] = rk0;
         qpd[e1] = pd0 + 1; qpo[e1] = rk1;
       }
@@ -2204,9 +2216,11 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       for (int c = 0; c < 2 && qtail - qhead >= 64; ++c) score_chunk(64);
     }
   };
-  auto stage_H = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    // H(j-1): block j-1 (D fields in X): O1 hits, its driver tfs and length
-    // codes extracted, into Y's H fields
+  auto stage_H = [&](Regs& X, Regs& Yh, uint32_t j) __attribute__((always_inline)) {
+    // H(j-1) (kDeep >= 1: H(j-2)): the block whose D fields are in X: O1 hits,
+    // its driver tfs and length codes extracted, into Yh's H fields (kDeep 2:
+    // X's, read by C two iterations later)
+    Regs& Y = kDeep >= 2 ? X : Yh;
     if constexpr (kBk) {
       const uint32_t q0 = X.da0 - lo, q1 = X.da1 - lo;
       const uint32_t m = (1u << bsh) - 1u;
@@ -2257,8 +2271,10 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
       Y.ht1 = X.dt1;
     }
   };
-  auto stage_D = [&](Regs& X, Regs& Y, uint32_t j) __attribute__((always_inline)) {
-    // D(j): decode block j from X's words into Y, issue its loads
+  auto stage_D = [&](Regs& X, Regs& Yd, uint32_t j) __attribute__((always_inline)) {
+    // D(j): decode block j from X's words into Yd (kDeep >= 1: into X, read
+    // by H two iterations later), issue its loads
+    Regs& Y = kDeep >= 1 ? X : Yd;
     {
       const bool live = j < bend;
       // (the block issue_words loaded: j < b1 there, and the values of a block
@@ -2329,9 +2345,9 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
     stage_D(X, Y, j);
   };
   issue_words(b0, R0);
-  for (uint32_t j = b0; j < bend + 2; j += 2) {
+  for (uint32_t j = b0; j < bend + 2 + kDeep; j += 2) {
     body(R0, R1, j);
-    if (j + 1 >= bend + 2) break;
+    if (j + 1 >= bend + 2 + kDeep) break;
     body(R1, R0, j + 1);
   }
   if (qtail != qhead) score_chunk(qtail - qhead);
@@ -3058,7 +3074,7 @@ __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t*
 // 5 workgroups (the conjunctive instance: 96 VGPRs, 27.7 KB LDS, 5 waves per
 // SIMD): with the pre-probe bound the main leg went 23.5 -> 24.9 M q/s against
 // 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 4 (kLeanWgsPhrase).
-constexpr int kLeanWgs = 5;
+constexpr int kLeanWgs = kLeanDeep ? 4 : 5;   // (a deeper pipeline's register sets: 4)
 constexpr int kLeanWgsPhrase = 4;
 template <bool kPh, bool kTwo = false>
 __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) void lean_kernel(
@@ -3133,10 +3149,10 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
                             ev_out,
                             ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
       else if (uni(static_cast<uint32_t>(Q.o_bm >> kProbeShiftBit)))   // O1 has offset buckets
-        lean_segment<kPh, kTwo, true>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
+        lean_segment<kPh, kTwo, true, kPh ? 0 : kLeanDeep>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
                                       floor0, prev_pub, r, my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
       else
-        lean_segment<kPh, kTwo, false>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
+        lean_segment<kPh, kTwo, false, kPh ? 0 : kLeanDeep>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
                                        floor0, prev_pub, r, my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
     }
     // The item's end from the events still in LDS where it can (finish_item
@@ -3230,7 +3246,7 @@ __device__ __forceinline__ void owner_replay_query(const QueryIn* __restrict__ q
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
-  } else if (k <= static_cast<uint32_t>(kRegHeapK)) {
+  } else if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK)) {
     RegHeapSink sink;
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});

@@ -26,7 +26,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import _capi
 from ._capi import check, lib
@@ -492,6 +492,30 @@ def gen_realistic_log(index_dir: str, out_path: str, n_queries: int = 20_000, ph
     with open(out_path, "w") as f:
         f.write("\n".join(lines) + "\n")
     return len(lines)
+
+
+def class_order(queries) -> Tuple[List[int], int]:
+    """wsr_class_order: a stable order of `queries` (a ctypes array of
+    _capi.Query) with the conjunctive queries first and the phrase queries
+    after them -> (order, n_conj).  Batches cut from it are class-pure."""
+    n = len(queries)
+    order = (C.c_int32 * max(n, 1))()
+    nc = C.c_int32()
+    check(lib.wsr_class_order(queries, n, order, C.byref(nc)))
+    return list(order[:n]), nc.value
+
+
+def class_batches(queries, batch: int) -> List[List[int]]:
+    """The engine's batch former for a query stream: indices of `queries`
+    (ctypes Query array) in batches of at most `batch`, each class cut
+    separately (wsr_class_order), so no batch mixes phrase and conjunctive
+    queries."""
+    order, nc = class_order(queries)
+    out = []
+    for lo, hi in ((0, nc), (nc, len(order))):
+        for s in range(lo, hi, batch):
+            out.append(order[s:min(s + batch, hi)])
+    return out
 
 
 def read_query_log(path: str):
