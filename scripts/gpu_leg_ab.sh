@@ -14,7 +14,7 @@ for rep in a b; do
     for lib in "$@"; do
       n=$(basename "${lib:-tree}" .so)
       WISER_HIP_LIB=$lib timeout -k 10 400 python3 scripts/leg_run.py $leg 6 > "$O/${leg}_${n}_$rep.json" 2> "$O/${leg}_${n}_$rep.err"
-      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], 'value', d['value'], 'ms/batch', d['ms_per_batch'], 'frac', d['roofline']['frac'])" "$O/${leg}_${n}_$rep.json" $leg $n
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], sys.argv[3], 'value', d['value'], 'ms/batch', d['ms_per_batch'], 'p50_alone', d.get('p50_alone_ms'), 'frac', d['roofline']['frac'])" "$O/${leg}_${n}_$rep.json" $leg $n
     done
   done
 done

@@ -93,7 +93,13 @@ constexpr int kSingleWindows = 8;
 constexpr uint32_t kPhraseSegCap = 32;
 // item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
-constexpr int kCostBuckets = 4;   // log2(cost) < 3, 3, 4, >= 5
+// item cost buckets: log2(cost) < 3, 3, 4, >= 5, and (the heaviest) the items
+// of a query of at least kHeavyQueryItems items
+constexpr int kCostBuckets = 5;
+// A query of this many items or more is queued before every other item of
+// its class: its replay, the batch's longest chain of heap insertions, then
+// starts while the lighter items still run, instead of ending the batch.
+constexpr uint32_t kHeavyQueryItems = 4;
 constexpr float kItemFixedCost = 4.0f;
 
 // Replay fused into the segment kernel: the workgroup that completes a

@@ -453,7 +453,8 @@ __device__ __forceinline__ const int32_t* qlist_of(const QueryIn* qs, int qi) {
 // queries', then general ones), then cost bucket-major, heaviest bucket first
 // (query order inside a bucket, a query's items consecutive), so the
 // persistent workers take the long items first and the short ones fill the
-// tail (longest-first list scheduling).
+// tail (longest-first list scheduling).  The first bucket holds the items of
+// queries of kHeavyQueryItems items or more, whose replays are the longest.
 constexpr int kPlanKeys = 3 * kCostBuckets;   // classes: lean conjunctive, lean phrase, general
 __device__ __forceinline__ uint32_t plan_key(uint32_t drv) {
   const uint32_t bucket = (drv >> kPlanBucketShift) & 0xFu;
@@ -613,12 +614,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_query_kernel(IndexArgs ix, 
       const float item_cost = static_cast<float>(seg) * cost + kItemFixedCost;
       const uint32_t ic = static_cast<uint32_t>(item_cost);
       const uint32_t lg = 31u - __clz(ic > 4u ? ic : 4u);    // >= 2
-      const uint32_t bucket = min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 1));
+      const uint32_t n_items = (nd + seg - 1) / seg;
+      const uint32_t bucket = n_items >= kHeavyQueryItems ? static_cast<uint32_t>(kCostBuckets - 1)
+                                                          : min(lg - 2u, static_cast<uint32_t>(kCostBuckets - 2));
       // (a lean phrase query has two terms: the one-term "phrase" is a plain term)
       const bool lean_ph = lean && nt > 1 && (q.flags & kQueryPhrase);
       p.driver = d | (bucket << kPlanBucketShift) | (lean ? kPlanLean : 0u) | (lean_ph ? kPlanPhrase : 0u);
       p.seg_blocks = seg;
-      p.n_items = (nd + seg - 1) / seg;
+      p.n_items = n_items;
       if (lean) {
         // the lean kernel's record (bases are added by plan_fill_kernel)
         // (the driver's and O1's records: a second round of loads, side by side)
@@ -1634,6 +1637,11 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
   }
 }
 
+// PosStream keeps the pack dwords it last read and takes a bag's next
+// positions from them while they cover them (one load per bag of small
+// deltas instead of one per position).
+constexpr bool kPosWindow = true;
+
 // waves per SIMD the segment kernel is compiled for (register budget)
 constexpr int kSegWaves = 3;
 
@@ -1658,6 +1666,11 @@ struct PosStream {
   uint32_t bits, pk;     // its width and index (pk = ~0: none yet)
   uint32_t e, end;       // next entry, one past the bag
   int32_t cur;           // last position popped
+  // the last two aligned dwords read from the pack, from bit wb of the pack's
+  // data (kPosWindow): a bag's next values usually lie in them, so a bag of
+  // small deltas costs one load instead of one per position
+  uint32_t w0, w1;
+  int32_t wb;
   __device__ __forceinline__ void init(const IndexArgs& ix, uint32_t slot, uint32_t tf) {
     e = ix.pos_start[slot];
     end = e + tf;
@@ -1665,6 +1678,8 @@ struct PosStream {
     pk = 0xFFFFFFFFu;
     data = ix.pos_blob;
     bits = 1;
+    w0 = w1 = 0;
+    wb = -(1 << 30);
   }
   // pop the next position (false past the bag's end)
   __device__ __forceinline__ bool next(const IndexArgs& ix, const PosDev& P) {
@@ -1677,8 +1692,23 @@ struct PosStream {
         data = ix.pos_blob + P.base + w.x + 2;
         bits = w.y;
         pk = p;
+        wb = -(1 << 30);
       }
-      v = pack_value(data, bits, e & 127u);
+      const int32_t bit = static_cast<int32_t>((e & 127u) * bits);
+      if (kPosWindow) {
+        if (bit - wb < 0 || bit - wb + static_cast<int32_t>(bits) > 64) {
+          const uint8_t* a = data + (bit >> 3);
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(a, 4));
+          w0 = w[0];
+          w1 = w[1];
+          wb = static_cast<int32_t>(reinterpret_cast<const uint8_t*>(w) - data) * 8;
+        }
+        const uint32_t sh = static_cast<uint32_t>(bit - wb);
+        const uint64_t x = ((static_cast<uint64_t>(w1) << 32) | w0) >> sh;
+        v = static_cast<uint32_t>(x) & (bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u));
+      } else {
+        v = pack_value(data, bits, e & 127u);
+      }
     } else {
       v = ix.pos_tail[P.tail + (e - (P.npk << 7))];
     }
@@ -2373,6 +2403,7 @@ __device__ __forceinline__ void lean_segment(const IndexArgs& ix, LeanLdsT<kPh>&
 // block each posting's own bound (its tf and length, f32) leaves only the
 // candidates for the f64 score and the running top-k.  Safety of the f32
 // bounds: as the lean pipeline's pre-probe pruning (kPruneMargin).
+constexpr bool kSingleQueue = true;
 template <bool kPh>
 __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh>& S, const double* norm_tab,
                                                const QueryDesc& Q, uint32_t b0, uint32_t b1, bool dtail,
@@ -2457,6 +2488,57 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
     __builtin_amdgcn_wave_barrier();
     evb = 0;
   };
+  // kSingleQueue: survivors wait in a ring of 256 in LDS (doc, tf, length
+  // code) and are scored 64 at a time, one per lane: a block keeps ~3 of
+  // its 128 postings, so scoring each block's 128 lanes in f64 spent most of
+  // its instructions on postings already dropped
+  uint32_t* qdoc = S.q;
+  uint32_t* qtf = S.q + 256;
+  uint32_t* qc4 = S.q + 512;
+  uint32_t qhead = 0, qtail = 0;
+  auto score_chunk = [&](uint32_t n) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t e = (qhead + l) & 255u;
+    const bool alive = l < n;
+    const uint32_t doc = qdoc[e], tf = qtf[e], c4 = qc4[e];
+    __builtin_amdgcn_wave_barrier();
+    qhead += n;
+    double sc = 0.0;   // BM25 of the one term (scoring.h:133-144: summed from 0.0)
+    sc += bm25_term(idf, alive ? tf : 0u, norm_tab[alive ? (c4 & 255u) : 0u]);
+    const double kth = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+    uint64_t cm = __ballot(alive && (wide || (sc > flo && (pt_n < k || sc > kth))));
+    while (cm) {
+      const int fl = __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const double sv = readlane_f64(sc, fl);
+      const uint32_t dv = __builtin_amdgcn_readlane(doc, fl);
+      const uint32_t pos = wide ? 0u : __popcll(__ballot(l < pt_n && pt >= sv));
+      if (wide || pos < k) {
+        if (evb == kLeanEvs) flush();
+        if (l == 0) {
+          Event ev;
+          ev.score = sv;
+          ev.doc = static_cast<int32_t>(dv);
+          ev.pad = 0;
+          S.evs[evb] = ev;
+        }
+        ++ev_n;
+        ++evb;
+        if (!wide) {
+          const double up = wave_shr1_f64(pt);
+          if (l > pos) pt = up;
+          else if (l == pos) pt = sv;
+          pt_n = pt_n + 1 > k ? k : pt_n + 1;
+        }
+      }
+    }
+    if (!wide) {
+      const double kn = pt_n >= k ? readlane_f64(pt, static_cast<int>(k) - 1) : 0.0;
+      const double pv = kn > flo ? kn : flo;
+      pub_val = pv > pub_val ? pv : pub_val;
+      thr_s = static_cast<float>(pv) * kPruneMargin;
+    }
+  };
   // score block X.b (its loads were issued one block earlier)
   auto score = [&](const Regs& X) __attribute__((always_inline)) {
     const uint32_t b = X.b, bi = b - wb;
@@ -2482,6 +2564,22 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
     const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
     if ((m0 | m1) == 0) return;
     n_surv += __popcll(m0) + __popcll(m1);
+    if constexpr (kSingleQueue) {
+      // append the block's survivors, in doc order, to the LDS queue (misses
+      // write the free slot before its head: at most 63 + 128 are live);
+      // every full 64 are scored one per lane
+      const uint64_t lt = lanemask_lt();
+      const uint32_t r0 = qtail + __popcll(m0 & lt) + __popcll(m1 & lt);
+      const uint32_t r1 = r0 + (p0 ? 1u : 0u);
+      const uint32_t spare = (qhead - 1u) & 255u;
+      const uint32_t e0 = p0 ? (r0 & 255u) : spare, e1 = p1 ? (r1 & 255u) : spare;
+      qdoc[e0] = a0; qtf[e0] = t0; qc4[e0] = c0;
+      qdoc[e1] = a1; qtf[e1] = t1; qc4[e1] = c1;
+      qtail += __popcll(m0) + __popcll(m1);
+#pragma nounroll
+      for (int c = 0; c < 2 && qtail - qhead >= 64; ++c) score_chunk(64);
+      return;
+    }
     // BM25 of the one term (scoring.h:133-144: summed from 0.0)
     double s0 = 0.0, s1 = 0.0;
     s0 += bm25_term(idf, p0 ? t0 : 0u, norm_tab[p0 ? c0 : 0u]);
@@ -2525,6 +2623,9 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   };
   auto refresh = [&]() __attribute__((always_inline)) {
     if (wide || ++n_done % kFloorRefresh) return;
+    // (the queue's partial chunk too: block skipping needs the threshold its
+    // survivors raise, at most kFloorRefresh blocks late)
+    if (kSingleQueue && qtail != qhead) score_chunk(qtail - qhead);
     const uint64_t fb = floor_max(floor_next);
     if (fb > floor_bits) {
       floor_bits = fb;
@@ -2558,6 +2659,7 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
     }
     if (we >= b1) break;
     // the next window: its directory and block bounds (one round of loads)
+    // (its blocks' survivors go on queueing behind this window's)
     wb = we;
     we = min(wb + 64u, b1);
     __builtin_amdgcn_wave_barrier();
@@ -2568,6 +2670,7 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
     bmax = wb + l < we ? ix.bmax[Q.a_blk0 + wb + l] * idf_f : 0.0f;
     __builtin_amdgcn_wave_barrier();
   }
+  if (kSingleQueue && qtail != qhead) score_chunk(qtail - qhead);
   // (the last evb events stay in S.evs for finish_lean_item)
   if (my_pub && pub_val > last_pub && l == 0)
     __hip_atomic_fetch_max(my_pub, static_cast<uint64_t>(__double_as_longlong(pub_val)), __ATOMIC_RELAXED,
