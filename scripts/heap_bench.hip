@@ -139,6 +139,61 @@ __global__ void reg_bench_kernel(const double* vals, int n, uint32_t k, uint64_t
 }
 }  // namespace wiser
 
+namespace wiser {
+// Where an insertion's cycles go: the candidate loop alone
+// (readlanes and the top test, no heap operation), pushes alone (into a heap
+// emptied every k), pops alone (of a heap refilled every k), and the LDS heap
+// of the wide queries (LdsHeapSink: a wave-uniform walk over LDS) at k = 10.
+__global__ void parts_bench_kernel(const double* vals, int n, uint32_t k, uint32_t mode, uint64_t* ticks,
+                                   double* out) {
+  __shared__ double s_hs[kMaxKWide];
+  __shared__ int32_t s_hd[kMaxKWide];
+  k = uni(k);
+  mode = uni(mode);
+  const uint32_t l = threadIdx.x & 63;
+  double sc = vals[l];
+  WaveHeap H;
+  LdsHeapSink L;
+  L.hs = s_hs;
+  L.hd = s_hd;
+  L.k = k;
+  double acc = 0.0;
+  uint32_t cnt = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int c = 0; c < n; c += 64) {
+    const double nx = c + 64 < n ? vals[c + 64 + l] : 0.0;
+    if (mode == 3) {
+      L.step(sc, c + static_cast<int32_t>(l), true, [](double, int32_t) {});
+    } else {
+      const double top = H.n < k ? -1.0 : H.at(0);
+      uint64_t cm = __ballot(sc > top || mode != 0);
+      while (cm) {
+        const int fl = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const double sv = readlane_f64(sc, fl);
+        const int32_t dv = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(c + l), fl));
+        if (mode == 0) {            // the loop alone
+          acc += sv;
+          ++cnt;
+        } else if (mode == 1) {     // pushes alone
+          if (H.n == k) H.n = 0;
+          H.push(sv, dv);
+        } else {                    // pops alone (refilled by pushes, not timed apart)
+          if (H.n <= 1) {
+            for (uint32_t i = 0; i < k; ++i) H.push(sv + i, dv);
+          }
+          H.pop();
+        }
+      }
+    }
+    sc = nx;
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  out[l] = acc + H.hs + cnt + (L.n ? L.at(0) : 0.0);
+  if (l == 0) ticks[0] = t1 - t0;
+}
+}  // namespace wiser
+
 int main() {
   const int n = 64 * 64;   // 4,096 events, rising: 4,096 insertions
   std::vector<double> h(n);
@@ -195,6 +250,21 @@ int main() {
     if (bad) return 1;
   }
   double* od; hipMalloc(&od, 64 * sizeof(double));
+  {
+    std::vector<double> h2(n);
+    for (int i = 0; i < n; ++i) h2[i] = 1.0 + i * 1e-3;
+    hipMemcpy(d, h2.data(), n * sizeof(double), hipMemcpyHostToDevice);
+    const char* names[] = {"candidate loop alone", "pushes alone", "pops alone (+1 refill push per pop... see note)",
+                           "LDS heap (LdsHeapSink)"};
+    for (uint32_t mode = 0; mode < 4; ++mode) {
+      for (int rep = 0; rep < 2; ++rep) {
+        hipLaunchKernelGGL(wiser::parts_bench_kernel, dim3(1), dim3(64), 0, 0, d, n, 10u, mode, t, od);
+        uint64_t ht[2];
+        hipMemcpy(ht, t, 16, hipMemcpyDeviceToHost);
+        std::printf("parts k 10 mode %u (%s): %.1f ns per event\n", mode, names[mode], ht[0] * 10.0 / n);
+      }
+    }
+  }
   for (uint32_t k : {10u, 64u}) {
     for (int rep = 0; rep < 2; ++rep) {
       hipLaunchKernelGGL(wiser::lane_bench_kernel, dim3(1), dim3(64), 0, 0, d, n, k, t, od);

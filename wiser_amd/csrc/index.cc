@@ -591,7 +591,10 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
     std::vector<uint32_t> pk, tail;
   };
   std::vector<PosPart> pos_parts(positions ? L : 0);
-  if (positions) img.pos_start.assign(nb * kPackSize, 0);
+  if (positions) {
+    img.pos_start.assign(nb * kPackSize, 0);
+    img.pos_bag.assign(nb * kPackSize, 0);
+  }
   // phrase bloom filters: shape from the header's "end" fields; one 16-byte
   // slot per filter, so bit arrays of more than 16 bytes stay on the host
   const BloomShape bshape(static_cast<int>(idx.bloom_entries()), idx.bloom_ratio());
@@ -793,9 +796,16 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
       if (!with_tail) pt.tail.clear();
       pt.bytes.assign(file + b_lo, file + std::max(b_lo, b_hi));
       const uint64_t e0 = k0 * kPackSize;
+      const uint64_t n_pk = k1 - k0;   // the slice's packs (pt.pk pairs)
       for (uint64_t r = r0; r < r1; ++r)
-        for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i)
-          img.pos_start[(ld.blk0 + r - r0) * kPackSize + i] = static_cast<uint32_t>(cum[r * kPackSize + i] - e0);
+        for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i) {
+          const uint64_t slot = (ld.blk0 + r - r0) * kPackSize + i;
+          const uint64_t er = cum[r * kPackSize + i] - e0;
+          img.pos_start[slot] = static_cast<uint32_t>(er);
+          const uint64_t kk = er / kPackSize;
+          if (kk < n_pk && pt.pk[2 * kk] < (1u << 26))
+            img.pos_bag[slot] = (pt.pk[2 * kk] << 6) | pt.pk[2 * kk + 1];
+        }
     }
     if (with_blm) {
       // The list's two bloom sections (flash_engine_dumper.h:620-646): the 8

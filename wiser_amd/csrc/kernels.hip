@@ -1641,6 +1641,9 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
 // positions from them while they cover them (one load per bag of small
 // deltas instead of one per position).
 constexpr bool kPosWindow = true;
+// PosStream takes its first pack record from pos_bag (loaded with pos_start)
+// instead of a dependent pos_pk load.
+constexpr bool kPosBag = true;
 
 // waves per SIMD the segment kernel is compiled for (register budget)
 constexpr int kSegWaves = 3;
@@ -1671,13 +1674,21 @@ struct PosStream {
   // small deltas costs one load instead of one per position
   uint32_t w0, w1;
   int32_t wb;
-  __device__ __forceinline__ void init(const IndexArgs& ix, uint32_t slot, uint32_t tf) {
+  // (P: the list's box; its pack record for the bag's first pack comes with
+  // the bag's start, pos_bag, so the first position needs no pos_pk load)
+  __device__ __forceinline__ void init(const IndexArgs& ix, const PosDev& P, uint32_t slot, uint32_t tf) {
     e = ix.pos_start[slot];
+    const uint32_t g = kPosBag ? ix.pos_bag[slot] : 0u;
     end = e + tf;
     cur = 0;
     pk = 0xFFFFFFFFu;
     data = ix.pos_blob;
     bits = 1;
+    if (g) {
+      pk = e >> 7;
+      data = ix.pos_blob + P.base + (g >> 6) + 2;
+      bits = g & 63u;
+    }
     w0 = w1 = 0;
     wb = -(1 << 30);
   }
@@ -1776,8 +1787,8 @@ __device__ __forceinline__ bool phrase_match2(const IndexArgs& ix, uint32_t l0, 
   }
   const PosDev P0 = ix.pos_lists[l0], P1 = ix.pos_lists[l1];
   PosStream s0, s1;
-  s0.init(ix, slot0, tf0);
-  s1.init(ix, slot1, tf1);
+  s0.init(ix, P0, slot0, tf0);
+  s1.init(ix, P1, slot1, tf1);
   if (!s0.next(ix, P0) || !s1.next(ix, P1)) return false;
   for (;;) {
     const int32_t a = s0.cur + 1, b = s1.cur;
@@ -1793,8 +1804,8 @@ __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* ql
   if (nt == 2) {   // ProcessTwoTerm: a merge of bag 0 against bag 1 shifted by one
     const PosDev P0 = ix.pos_lists[qlist[0]], P1 = ix.pos_lists[qlist[1]];
     PosStream s0, s1;
-    s0.init(ix, ph[v], ph[128 + v]);
-    s1.init(ix, ph[256 + v], ph[384 + v]);
+    s0.init(ix, P0, ph[v], ph[128 + v]);
+    s1.init(ix, P1, ph[256 + v], ph[384 + v]);
     if (!s0.next(ix, P0) || !s1.next(ix, P1)) return false;
     for (;;) {
       const int32_t a = s0.cur + 1, b = s1.cur;
@@ -1806,8 +1817,9 @@ __device__ __noinline__ bool phrase_match(const IndexArgs& ix, const int32_t* ql
   PosStream st[kMaxPhraseTerms];
 #pragma unroll
   for (uint32_t i = 0; i < kMaxPhraseTerms; ++i) {
-    st[i].init(ix, ph[i * 256 + v], i < nt ? ph[i * 256 + 128 + v] : 0u);
-    if (i < nt && !st[i].next(ix, ix.pos_lists[qlist[i]])) return false;
+    const PosDev Pi = ix.pos_lists[i < nt ? qlist[i] : qlist[0]];
+    st[i].init(ix, Pi, i < nt ? ph[i * 256 + v] : 0u, i < nt ? ph[i * 256 + 128 + v] : 0u);
+    if (i < nt && !st[i].next(ix, Pi)) return false;
   }
   int32_t a = 0;
   for (;;) {
