@@ -118,28 +118,6 @@ __global__ void lane_bench_kernel(const double* vals, int n, uint32_t k, uint64_
 }  // namespace wiser
 
 namespace wiser {
-// the register heap (regheap.h) as the replay runs it for k <= kRegHeapK
-__global__ void reg_bench_kernel(const double* vals, int n, uint32_t k, uint64_t* ticks, HitDev* out,
-                                 int32_t* nout) {
-  RegHeapSink sink;
-  sink.k = uni(k);
-  const uint32_t l = threadIdx.x & 63;
-  double sc = vals[l];
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const uint64_t c0 = __builtin_amdgcn_s_memtime();
-  for (int c = 0; c < n; c += 64) {
-    const double nx = c + 64 < n ? vals[c + 64 + l] : 0.0;
-    sink.step(sc, c + static_cast<int32_t>(l), true, [](double, int32_t) {});
-    sc = nx;
-  }
-  const uint64_t c1 = __builtin_amdgcn_s_memtime();
-  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-  sink.finish(out, nout);
-  if (l == 0) { ticks[0] = t1 - t0; ticks[1] = c1 - c0; }
-}
-}  // namespace wiser
-
-namespace wiser {
 // Where an insertion's cycles go: the candidate loop alone
 // (readlanes and the top test, no heap operation), pushes alone (into a heap
 // emptied every k), pops alone (of a heap refilled every k), and the LDS heap
@@ -209,45 +187,6 @@ int main() {
       std::printf("k %u: %d insertions, %.3f us (%.1f ns each), %.1f s_memtime ticks each\n", k, n,
                   ht[0] / 100.0, ht[0] * 10.0 / n, static_cast<double>(ht[1]) / n);
     }
-  }
-  for (uint32_t k : {10u, 16u}) {
-    for (int rep = 0; rep < 3; ++rep) {
-      hipLaunchKernelGGL(wiser::reg_bench_kernel, dim3(1), dim3(64), 0, 0, d, n, k, t, o, no);
-      uint64_t ht[2];
-      hipMemcpy(ht, t, 16, hipMemcpyDeviceToHost);
-      std::printf("reg heap k %u: %d insertions, %.3f us (%.1f ns each), %.1f s_memtime ticks each\n", k, n,
-                  ht[0] / 100.0, ht[0] * 10.0 / n, static_cast<double>(ht[1]) / n);
-    }
-  }
-  // the two heaps on tie-heavy random streams: identical results, doc order included
-  {
-    std::vector<double> r(n);
-    uint64_t x = 88172645463325252ull;
-    int bad = 0;
-    wiser::HitDev* o2; int32_t* no2;
-    hipMalloc(&o2, 64 * sizeof(wiser::HitDev)); hipMalloc(&no2, 4);
-    for (int trial = 0; trial < 64; ++trial) {
-      const int levels = 1 + trial % 7;
-      for (int i = 0; i < n; ++i) {
-        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-        r[i] = 1.0 + static_cast<double>(x % levels) * 0.5 + (trial % 4 == 3 ? i * 1e-4 : 0.0);
-      }
-      hipMemcpy(d, r.data(), n * sizeof(double), hipMemcpyHostToDevice);
-      const uint32_t k = 1 + trial % 16;
-      hipLaunchKernelGGL(wiser::heap_bench_kernel, dim3(1), dim3(64), 0, 0, d, n, k, t, o, no);
-      hipLaunchKernelGGL(wiser::reg_bench_kernel, dim3(1), dim3(64), 0, 0, d, n, k, t, o2, no2);
-      std::vector<wiser::HitDev> a(64), b(64);
-      int32_t na = 0, nb = 0;
-      hipMemcpy(a.data(), o, 64 * sizeof(wiser::HitDev), hipMemcpyDeviceToHost);
-      hipMemcpy(b.data(), o2, 64 * sizeof(wiser::HitDev), hipMemcpyDeviceToHost);
-      hipMemcpy(&na, no, 4, hipMemcpyDeviceToHost);
-      hipMemcpy(&nb, no2, 4, hipMemcpyDeviceToHost);
-      bool same = na == nb;
-      for (int i = 0; same && i < na; ++i) same = a[i].doc == b[i].doc && a[i].score == b[i].score;
-      if (!same) ++bad;
-    }
-    std::printf("reg heap vs wave heap on 64 tie-heavy streams: %d mismatches\n", bad);
-    if (bad) return 1;
   }
   double* od; hipMalloc(&od, 64 * sizeof(double));
   {

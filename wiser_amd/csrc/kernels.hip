@@ -46,7 +46,6 @@
 #include <cstdint>
 
 #include "kernels.h"
-#include "regheap.h"
 
 namespace wiser {
 
@@ -1296,50 +1295,6 @@ struct HeapSink {
   }
 };
 
-// The same heap for k <= kRegHeapK held in registers (regheap.h): every step
-// of a walk is an f64 compare and a uniform branch over registers of fixed
-// index, no permute or readlane chain.  Measured slower than WaveHeap: the
-// compiler keeps the 48 uniform values in SGPRs, spills them to VGPR lanes and
-// copies the whole array at every join of the walk's branches (1,250 against
-// 550 ns per insertion at k = 10, profiles/r06/heap_bench_r06b.txt), and the
-// bench fell 22.8 -> 18.4 M q/s; held in VGPRs (in_vgpr) it copies them with
-// ~2,400 v_mov and spills as well.  Off (kRegHeapReplay).
-constexpr bool kRegHeapReplay = false;
-struct RegHeapSink {
-  RegHeap H;
-  uint32_t k = 0;
-  template <class Emit>
-  __device__ __forceinline__ void step(double sc, int32_t dc, bool valid, Emit&&) {
-    const double top = H.n < k ? -1.0 : H.s[0];
-    uint64_t cm = __ballot(valid && sc > top);
-    while (cm) {
-      const int fl = __builtin_ctzll(cm);
-      cm &= cm - 1;
-      H.insert(k, readlane_f64(sc, fl),
-               static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(dc), fl)));
-    }
-  }
-  // SortHeap: pop m times, the i-th popped to lane m - 1 - i, one store
-  __device__ __forceinline__ void finish(HitDev* out, int32_t* n_out) {
-    const uint32_t l = threadIdx.x & 63;
-    const uint32_t m = H.n;
-    double os = 0.0;
-    int32_t od = 0;
-    for (uint32_t i = 0; i < m; ++i) {
-      if (l == m - 1 - i) { os = H.s[0]; od = H.d[0]; }
-      H.pop();
-    }
-    if (l < m) {
-      HitDev h;
-      h.doc = od;
-      h.pad = 0;
-      h.score = os;
-      out[l] = h;
-    }
-    if (l == 0) *n_out = static_cast<int32_t>(m);
-  }
-};
-
 // One wave per query: the events of its segments (doc-id order) through the
 // restated heap (Sink::step: the heap's own insertion test).
 template <bool kCoherent, class Sink>
@@ -1362,10 +1317,7 @@ __device__ __forceinline__ void replay_query(const QueryIn* __restrict__ qs,
   const QueryPlan P = plan[qi];
   const uint32_t k = uni(qs[qi].k > 0 ? static_cast<uint32_t>(qs[qi].k) : 0u);
   HitDev* out = hits + static_cast<int64_t>(qi) * hit_stride;
-  if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK))
-    replay_query_sink<kCoherent, RegHeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
-  else
-    replay_query_sink<kCoherent, HeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
+  replay_query_sink<kCoherent, HeapSink>(P, k, events, ev_cnt, out, &n_hits[qi]);
 }
 
 // A one-item query's events straight from the lean kernel's LDS buffer (lane
@@ -1382,17 +1334,10 @@ __device__ __noinline__ void replay_lds_call(double sc, int32_t dc, uint32_t n, 
                                      (static_cast<uint64_t>(uni(static_cast<uint32_t>(no >> 32))) << 32));
   n = uni(n);
   k = uni(k);
-  if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK)) {
-    RegHeapSink sink;
-    sink.k = k;
-    sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
-    sink.finish(out, n_out);
-  } else {
-    HeapSink sink;
-    sink.k = k;
-    sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
-    sink.finish(out, n_out);
-  }
+  HeapSink sink;
+  sink.k = k;
+  sink.step(sc, dc, (threadIdx.x & 63) < n, [](double, int32_t) {});
+  sink.finish(out, n_out);
 }
 
 // out-of-line copy for the segment kernel (keeps its register allocation
@@ -3358,11 +3303,6 @@ __device__ __forceinline__ void owner_replay_query(const QueryIn* __restrict__ q
     LdsHeapSink sink;
     sink.hs = s_hs;
     sink.hd = s_hd;
-    sink.k = k;
-    consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
-    sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
-  } else if (kRegHeapReplay && k <= static_cast<uint32_t>(kRegHeapK)) {
-    RegHeapSink sink;
     sink.k = k;
     consume_stream(sink, static_cast<uint32_t>(n_shards), count_of, base_of, [](double, int32_t) {});
     sink.finish(hits + static_cast<int64_t>(gq) * hit_stride, &n_hits[gq]);
