@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Per-launch fabric bytes of the segment phase (scripts/gpu_prof.sh,
 # scripts/pmc_bytes.py), one profile per workload: attached to lines of that
 # workload only, with the file named in roofline.traffic_source.
-PMC_PROFILES = {w: f"r05h/{w}_pmc_segment.json"
+PMC_PROFILES = {w: f"r06p/{w}_pmc_segment.json"
                 for w in ("c3", "c2", "c4_mixed_1to5", "c5_phrase", "single_high", "realistic_mix")}
 # The sources a counter profile describes (the kernels, their launch and the
 # image they read): scripts/pmc_bytes.py records their hash in the profile and
@@ -377,15 +377,16 @@ def cpu_model():
     return None
 
 
-def roofline_of(acc, nbk, launch_ms, source):
+def roofline_of(acc, nbk, launch_ms, source, kernel="lean_kernel||segment_kernel"):
     """Algorithmic bytes per launch (wsr_list_bytes) over the
-    segment phase's launch duration."""
+    launch duration of `kernel` (the segment phase, fork -> join, unless
+    named)."""
     algo = acc["algo"] / nbk
     ach = algo / (launch_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "algo_bytes_per_launch": int(algo),
             "avg_launch_ms": round(launch_ms, 4), "launch_ms_source": source,
-            "kernel": "lean_kernel||segment_kernel"}
+            "kernel": kernel}
 
 
 LEG_MIN_BATCHES = int(os.environ.get("WSR_LEG_MIN_BATCHES", "16"))
@@ -1437,7 +1438,11 @@ def main():
         cpu = cpu_baseline(idx, lines, a.k, a.cpu_seconds, "the headline workload's log")
 
     if rank == 0:
-        roof = roofline_of(acc, nbk, seg_avg_ms, seg_src)
+        # the dominant kernel, lean_kernel (its HIP events on the batch stream,
+        # plan end -> lean end; the general segment_kernel runs beside it on a
+        # second stream and is given with the fork -> join time below)
+        roof = roofline_of(acc, nbk, lean_avg_ms, seg_src + ", lean_kernel (HIP events on its stream)",
+                           "lean_kernel")
         roof.update({"traffic": None, "traffic_source": None})
         if mode == "replica":
             pmc = load_pmc(wkey)
@@ -1451,6 +1456,8 @@ def main():
             # beside it on a second stream (HIP events fork -> join on the
             # batch's stream; isolated: one batch at a time, nothing overlapping)
             "lean_kernel_ms": round(lean_avg_ms, 4),
+            "fork_join_ms": round(seg_avg_ms, 4),
+            "frac_fork_join": round((acc["algo"] / nbk) / (seg_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "isolated_launch_ms": round(iso_ms, 4),
             "isolated_frac": round((acc["algo"] / nbk) / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "algo_bytes_rule": "SURVEY 8d: per query the docid+tf span bytes of every term's list "

@@ -39,7 +39,8 @@ def main():
             items, what, positions = bench.leg_items(a, idx, leg)
     eng = w.VacuumEngine(idx, device=0, threads=bench.HOST_THREADS, positions=positions)
     eng.Load()
-    out = bench.run_leg(eng, idx, items, a.k, a.batch, passes, 0, 0)
+    # (realistic_mix: batches cut by the engine's batch former, as in bench.py)
+    out = bench.run_leg(eng, idx, items, a.k, a.batch, passes, 0, 0, class_form=leg == "realistic_mix")
     out["config"] = {"workload": what}
     out["src_sha"] = bench.src_sha()
     eng.close()

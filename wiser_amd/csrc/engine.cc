@@ -113,7 +113,6 @@ struct wsr_handle {
   uint32_t* d_pos_pk = nullptr;
   uint32_t* d_pos_tail = nullptr;
   uint32_t* d_pos_start = nullptr;
-  uint32_t* d_pos_bag = nullptr;
   uint8_t* d_blm = nullptr;
   uint32_t* d_blm_hash = nullptr;
   bool positions = false;
@@ -240,7 +239,7 @@ wsr_image_info image_info_of(const HostImage& img, size_t n_c4) {
   if (img.has_blooms) o.pos_bytes += dev_bytes(img.blm) + dev_bytes(img.blm_hash);
   if (img.has_positions)
     o.pos_bytes += dev_bytes(img.pos_blob) + dev_bytes(img.pos_lists) + dev_bytes(img.pos_pk) +
-                   dev_bytes(img.pos_tail) + dev_bytes(img.pos_start) + dev_bytes(img.pos_bag);
+                   dev_bytes(img.pos_tail) + dev_bytes(img.pos_start);
   o.dense_bytes = dev_bytes(img.dense) + dev_bytes(img.dense_rank) + dev_bytes(img.bkt);
   o.tf8_bytes = dev_bytes(img.tf8);
   o.blob_bytes = dev_bytes(img.blob);
@@ -356,17 +355,14 @@ int wsr_open(const char* dir, const wsr_open_opts* opts, wsr_handle** out) {
       h->info.pos_bytes += dev_upload(&h->d_pos_pk, img.pos_pk);
       h->info.pos_bytes += dev_upload(&h->d_pos_tail, img.pos_tail);
       h->info.pos_bytes += dev_upload(&h->d_pos_start, img.pos_start);
-      h->info.pos_bytes += dev_upload(&h->d_pos_bag, img.pos_bag);
       h->args.pos_blob = h->d_pos_blob;
       h->args.pos_lists = h->d_pos_lists;
       h->args.pos_pk = reinterpret_cast<const uint2*>(h->d_pos_pk);
       h->args.pos_tail = h->d_pos_tail;
-      h->args.pos_start = h->d_pos_start;
-      h->args.pos_bag = h->d_pos_bag;
+      h->args.pos_start = reinterpret_cast<const uint2*>(h->d_pos_start);
       h->pos_bytes = img.pos_list_bytes;
       std::vector<uint8_t>().swap(img.pos_blob);
       std::vector<uint32_t>().swap(img.pos_start);
-      std::vector<uint32_t>().swap(img.pos_bag);
     }
     h->info.dense_bytes = dev_upload(&h->d_dense, img.dense);
     h->info.dense_bytes += dev_upload(&h->d_dense_rk, img.dense_rank);
@@ -463,8 +459,7 @@ void wsr_close(wsr_handle* h) {
                   static_cast<void*>(h->d_plen), static_cast<void*>(h->d_bmax), static_cast<void*>(h->d_tails),
                   static_cast<void*>(h->d_pos_blob), static_cast<void*>(h->d_pos_lists),
                   static_cast<void*>(h->d_pos_pk), static_cast<void*>(h->d_pos_tail),
-                  static_cast<void*>(h->d_pos_start), static_cast<void*>(h->d_pos_bag),
-                  static_cast<void*>(h->d_blm),
+                  static_cast<void*>(h->d_pos_start), static_cast<void*>(h->d_blm),
                   static_cast<void*>(h->d_blm_hash)})
     if (p) (void)hipFree(p);
   delete h;

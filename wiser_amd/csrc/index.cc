@@ -592,8 +592,7 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
   };
   std::vector<PosPart> pos_parts(positions ? L : 0);
   if (positions) {
-    img.pos_start.assign(nb * kPackSize, 0);
-    img.pos_bag.assign(nb * kPackSize, 0);
+    img.pos_start.assign(2 * nb * kPackSize, 0);
   }
   // phrase bloom filters: shape from the header's "end" fields; one 16-byte
   // slot per filter, so bit arrays of more than 16 bytes stay on the host
@@ -801,10 +800,10 @@ HostImage build_image(const VacuumIndex& idx, uint32_t doc_lo, uint32_t doc_hi, 
         for (uint64_t i = 0; i < kPackSize && r * kPackSize + i < n; ++i) {
           const uint64_t slot = (ld.blk0 + r - r0) * kPackSize + i;
           const uint64_t er = cum[r * kPackSize + i] - e0;
-          img.pos_start[slot] = static_cast<uint32_t>(er);
+          img.pos_start[2 * slot] = static_cast<uint32_t>(er);
           const uint64_t kk = er / kPackSize;
           if (kk < n_pk && pt.pk[2 * kk] < (1u << 26))
-            img.pos_bag[slot] = (pt.pk[2 * kk] << 6) | pt.pk[2 * kk + 1];
+            img.pos_start[2 * slot + 1] = (pt.pk[2 * kk] << 6) | pt.pk[2 * kk + 1];
         }
     }
     if (with_blm) {

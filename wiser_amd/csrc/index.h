@@ -144,12 +144,12 @@ struct HostImage {
   std::vector<PosDev> pos_lists;            // indexed by list id
   std::vector<uint32_t> pos_pk;             // per full pack: byte offset, bit width (pairs)
   std::vector<uint32_t> pos_tail;
-  std::vector<uint32_t> pos_start;          // bag start entry per posting slot (as plen)
-  // per posting slot, the pack its bag starts in: (byte offset of the pack from
-  // the box base << 6) | its bit width; 0 when the bag starts in the VInts
-  // remainder or the offset needs more than 26 bits (the kernel then reads
-  // pos_pk).  One load with pos_start instead of a dependent pos_pk load.
-  std::vector<uint32_t> pos_bag;
+  // per posting slot (as plen), two words: the bag's start entry, and the pack
+  // it starts in: (byte offset of the pack from the box base << 6) | its bit
+  // width, 0 when the bag starts in the VInts remainder or the offset needs
+  // more than 26 bits (the kernel then reads pos_pk).  One 8-byte load, one
+  // line, instead of the start and then a dependent pos_pk load.
+  std::vector<uint32_t> pos_start;
   std::vector<uint64_t> pos_list_bytes;     // bytes of each list's position box (algorithmic bytes)
   // two-way phrase bloom filters (build_image(..., blooms = true), positions
   // images of bloom indexes whose bit arrays fit 16 bytes): per posting slot

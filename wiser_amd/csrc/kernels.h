@@ -38,8 +38,8 @@ struct IndexArgs {
   const PosDev* pos_lists;  // indexed by list id
   const uint2* pos_pk;      // per full pack: byte offset from PosDev::base, bit width
   const uint32_t* pos_tail; // decoded VInts remainders
-  const uint32_t* pos_start;// bag start entry of every posting, 128 slots per image block
-  const uint32_t* pos_bag;  // the pack its bag starts in: offset << 6 | width (0: read pos_pk)
+  const uint2* pos_start;   // per posting (128 slots per image block): the bag's start entry,
+                            // the pack it starts in (offset << 6 | width; 0: read pos_pk)
   // phrase bloom filters (null / 0 unless a bloom index was opened with
   // positions and bloom_factor > 0): per posting slot two 16-byte bit arrays
   // (prior, next), per list its term's two hashes; bloom_factor as

@@ -1586,7 +1586,7 @@ __device__ __forceinline__ void finish_item(const QueryIn* qs, const QueryPlan* 
 // positions from them while they cover them (one load per bag of small
 // deltas instead of one per position).
 constexpr bool kPosWindow = true;
-// PosStream takes its first pack record from pos_bag (loaded with pos_start)
+// PosStream takes its first pack record from the bag's word pair (pos_start)
 // instead of a dependent pos_pk load.
 constexpr bool kPosBag = true;
 
@@ -1619,11 +1619,12 @@ struct PosStream {
   // small deltas costs one load instead of one per position
   uint32_t w0, w1;
   int32_t wb;
-  // (P: the list's box; its pack record for the bag's first pack comes with
-  // the bag's start, pos_bag, so the first position needs no pos_pk load)
+  // (P: the list's box; the record of the bag's first pack comes with the
+  // bag's start, in one 8-byte word, so the first position needs no pos_pk load)
   __device__ __forceinline__ void init(const IndexArgs& ix, const PosDev& P, uint32_t slot, uint32_t tf) {
-    e = ix.pos_start[slot];
-    const uint32_t g = kPosBag ? ix.pos_bag[slot] : 0u;
+    const uint2 sb = ix.pos_start[slot];
+    e = sb.x;
+    const uint32_t g = kPosBag ? sb.y : 0u;
     end = e + tf;
     cur = 0;
     pk = 0xFFFFFFFFu;
