@@ -89,9 +89,12 @@ static_assert(kSegCost < 64, "a segment's driver directory is one entry per lane
 // their block bounds, so a short item would be mostly fixed cost.
 constexpr int kSingleWindows = 8;
 // Driver blocks per item of a phrase query at most: a batch's phrase items
-// are its tail when they are few (the realistic mix: 15.4 -> 16.5 M q/s at 32
-// against 63, C5 unchanged; 16: 16.0 / 8.5 M, profiles/r05/phrase_seg_ab.txt).
-constexpr uint32_t kPhraseSegCap = 32;
+// are its tail when they are few (the realistic mix in log order: 15.4 -> 16.5
+// M q/s at 32 against 63, C5 unchanged; 16: 16.0 / 8.5 M, round 5).  Since the
+// batch former puts phrases in batches of their own (round 6), 48: C5 15.3 ->
+// 16.1 M, the class-ordered mix 27.6 -> 27.2 M (63: 16.1 / 27.2 M;
+// profiles/r06/phrase_cap_ab/).
+constexpr uint32_t kPhraseSegCap = 48;
 // item cost classes for the longest-first queue order (QueryPlan::driver >> kPlanBucketShift);
 // kItemFixedCost = an item's setup (dequeue, directory loads), in block decodes
 // item cost buckets: log2(cost) < 3, 3, 4, >= 5, and (the heaviest) the items
