@@ -342,6 +342,19 @@ typedef struct wsr_comm_stats {
   int64_t groups, steps, replays_in_lean, replays_on_stream;
 } wsr_comm_stats;
 int wsr_comm_stats_get(wsr_comm* c, wsr_comm_stats* out);
+/* Loopback communicators (tests and one-GPU rehearsals, never a measurement):
+ * the world ranks of a group live in ONE process, each with its own engine
+ * (usually its doc-range shard image on the same device), and the step
+ * groups' all-to-all is done by device copies between their exchange buffers
+ * in place of ncclAllToAll -- the same regions, runs, slots and owner replays
+ * as the RCCL path, so wsr_shard_steps at world > 1 runs exactly as it does
+ * over xGMI except for the transport.  Every rank must submit the same step
+ * groups in the same order (as with RCCL); a rank's collective completes on
+ * its stream only once every rank has read its send buffer. */
+typedef struct wsr_loopback wsr_loopback;
+int wsr_loopback_create(int32_t world, wsr_loopback** out);
+void wsr_loopback_destroy(wsr_loopback* l);   /* after closing its communicators */
+int wsr_comm_open_loopback(wsr_loopback* l, int32_t rank, int32_t device, wsr_comm** out);
 /* wsr_shard_step's two device halves with the transfer left to the caller (a
  * multi-rank rehearsal on one GPU, where RCCL refuses two ranks, or a host
  * exchange): the engine's own region buffers, in the exact layout the step's

@@ -429,3 +429,60 @@ def test_host_replay_taken_by_phrase_only_run(positions_index):
         S.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,defer", [(2, "1"), (3, "1"), (3, "0"), (8, "1")])
+def test_loopback_shard_steps(synth_small, monkeypatch, world, defer):
+    """wsr_shard_steps itself at world > 1 (the W > 1 parity tests
+    moved regions by copies outside the step): W doc-range shard engines in
+    this process, each with a loopback communicator, so the step groups'
+    regions, runs of regions, slots and deferred owner replays run exactly as
+    over RCCL, with the all-to-all done by device copies.  Groups of changing
+    size and order, more groups than exchange buffer sets, a batch stepped
+    again while its replay is pending; every rank's owned slice equal to the
+    oracle."""
+    import wiser_amd as w
+    from wiser_amd import _capi
+    from wiser_amd.shard import LoopbackGroup, NativeShardedSearcher
+    from oracle.oracle import OracleVacuum
+    monkeypatch.setenv("WSR_REPLAY_DEFER", defer)
+    d, _ = synth_small
+    log = os.path.join(d, f"qshard_loop{world}.log")
+    qpr = 96
+    nb = 4
+    w.gen_two_term_log(d, log, n_queries=nb * world * qpr, seed=29 + world)
+    qs = [l.split() for l in open(log).read().splitlines()]
+    parts = [qs[i * world * qpr:(i + 1) * world * qpr] for i in range(nb)]
+    o = OracleVacuum(d)
+    exp = [[o.search(q, 10)[0] for q in part] for part in parts]
+    L = LoopbackGroup(world)
+    S = [NativeShardedSearcher(d, r, world, share_id=None, loopback=L) for r in range(world)]
+    bs = []
+    try:
+        for s in S:
+            row = []
+            for part in parts:
+                b = w.ResidentBatch(s.engine, world * qpr, 10)
+                b.upload((_capi.Query * len(part))(
+                    *[s.engine.resolve(w.SearchQuery(q, n_results=10))[0] for q in part]))
+                row.append(b)
+            bs.append(row)
+        slot = 64 * qpr
+        for order in ([0, 1], [2], [3, 0], [1, 2, 3], [0], [2, 1], [3]):
+            for r, s in enumerate(S):   # every rank submits the group before the next group
+                s.steps([bs[r][i] for i in order], qpr, slot)
+        for r, s in enumerate(S):
+            for i in range(nb):
+                hits, nh = s.fetch_owned(bs[r][i], qpr)
+                got = [[(hits[q * 10 + j].doc_id, hits[q * 10 + j].score) for j in range(nh[q])]
+                       for q in range(qpr)]
+                assert got == exp[i][r * qpr:(r + 1) * qpr], (world, r, i)
+        st = S[0].comm_stats()
+        assert st["groups"] == 7 and st["steps"] == 12
+    finally:
+        for row in bs:
+            for b in row:
+                b.close()
+        for s in S:
+            s.close()
+        L.close()

@@ -126,6 +126,9 @@ _sigs = {
     "wsr_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
     "wsr_comm_open": (C.c_int, [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_close": (None, [_P]),
+    "wsr_loopback_create": (C.c_int, [C.c_int32, C.POINTER(_P)]),
+    "wsr_loopback_destroy": (None, [_P]),
+    "wsr_comm_open_loopback": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
     "wsr_comm_flush": (C.c_int, [_P]),
     "wsr_comm_stats_get": (C.c_int, [_P, C.POINTER(CommStats)]),
     "wsr_shard_step": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64]),

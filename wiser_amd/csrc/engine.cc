@@ -14,6 +14,7 @@
 #include <memory>
 #include <cstdlib>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1355,8 +1356,32 @@ struct XSlot {
   size_t n_done = 0;                  // (recorded)
   std::shared_ptr<XGroup> last;       // the group that used it last
 };
+// Loopback group (wsr_loopback_create): the all-to-all of W communicators of
+// one process by device copies.  Call n of every rank meets in calls[n]:
+// each rank records its send buffer ready, waits on the host until all W have
+// (phase 1), copies region r of every rank's send buffer into slot g of its
+// receive buffer behind that rank's ready event, records its reads done and
+// waits until all W have (phase 2), then makes its stream wait for every
+// rank's reads -- so a rank's collective completes only once its send buffer
+// has been read by all, as ncclAllToAll's does, and no rank records its
+// per-communicator events again before every rank has waited on them.
+struct wsr_loopback {
+  int world = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  struct Call {
+    std::vector<const void*> send;
+    std::vector<hipEvent_t> ready, read;
+    int arrived = 0, read_done = 0, left = 0;
+  };
+  std::map<uint64_t, Call> calls;
+};
+
 struct wsr_comm {
   ncclComm_t comm = nullptr;
+  wsr_loopback* loop = nullptr;   // a loopback communicator (no RCCL)
+  uint64_t loop_seq = 0;
+  hipEvent_t loop_ready = nullptr, loop_read = nullptr;
   hipStream_t stream = nullptr;
   int world = 0, rank = 0, device = 0;
   // WSR_HOST_TIMING=1: host time per phase of wsr_shard_step (enqueue only),
@@ -1401,6 +1426,49 @@ static uint64_t now_ns() {
 static int step_replay_from(wsr_handle* h, wsr_batch* b, int rank, int W, int32_t q_per_owner, const Event* recv,
                             uint64_t owner_stride, hipStream_t st);
 
+// The loopback group's all-to-all (wsr_loopback above): bytes per rank pair.
+static void loopback_alltoall(wsr_comm* c, const Event* send, Event* recv, uint64_t bytes) {
+  wsr_loopback* L = c->loop;
+  const int W = L->world, r = c->rank;
+  HIP_OK(hipEventRecord(c->loop_ready, c->stream));
+  const uint64_t n = c->loop_seq++;
+  wsr_loopback::Call* call;
+  {
+    std::unique_lock<std::mutex> lk(L->mu);
+    call = &L->calls[n];
+    if (call->send.empty()) {
+      call->send.assign(W, nullptr);
+      call->ready.assign(W, nullptr);
+      call->read.assign(W, nullptr);
+    }
+    call->send[r] = send;
+    call->ready[r] = c->loop_ready;
+    ++call->arrived;
+    L->cv.notify_all();
+    L->cv.wait(lk, [&] { return call->arrived == W; });
+  }
+  const uint8_t* src_base = nullptr;
+  for (int g = 0; g < W; ++g) {
+    HIP_OK(hipStreamWaitEvent(c->stream, call->ready[g], 0));
+    src_base = static_cast<const uint8_t*>(call->send[g]);
+    HIP_OK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(recv) + g * bytes, src_base + r * bytes, bytes,
+                          hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_OK(hipEventRecord(c->loop_read, c->stream));
+  {
+    std::unique_lock<std::mutex> lk(L->mu);
+    call->read[r] = c->loop_read;
+    ++call->read_done;
+    L->cv.notify_all();
+    L->cv.wait(lk, [&] { return call->read_done == W; });
+  }
+  for (int g = 0; g < W; ++g) HIP_OK(hipStreamWaitEvent(c->stream, call->read[g], 0));
+  {
+    std::lock_guard<std::mutex> lk(L->mu);
+    if (++call->left == W) L->calls.erase(n);
+  }
+}
+
 // One job: wait for the group's emissions (and for the slot's previous
 // replays), one ncclAllToAll of the owners' runs of regions, then -- not
 // deferred -- the owner replays and the end event of every batch.
@@ -1422,9 +1490,13 @@ static void run_xjob(wsr_comm* c, const XJob& jp) {
     // query sharded, profiles/r04t/)
     for (wsr_batch* b : j.bs) HIP_OK(hipStreamWaitEvent(c->stream, b->xev[0], 0));
     for (hipEvent_t e : j.wait_done) HIP_OK(hipStreamWaitEvent(c->stream, e, 0));
-    const ncclResult_t r = ncclAllToAll(S.send, S.recv, run * (sizeof(Event) / sizeof(uint64_t)),
-                                        ncclUint64, c->comm, c->stream);
-    if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+    if (c->loop) {
+      loopback_alltoall(c, S.send, S.recv, run * sizeof(Event));
+    } else {
+      const ncclResult_t r = ncclAllToAll(S.send, S.recv, run * (sizeof(Event) / sizeof(uint64_t)),
+                                          ncclUint64, c->comm, c->stream);
+      if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllToAll: ") + ncclGetErrorString(r));
+    }
     HIP_OK(hipEventRecord(S.xa, c->stream));
   } catch (const std::exception& e) {
     rc = WSR_E_HIP;
@@ -1521,6 +1593,38 @@ int wsr_comm_open(const uint8_t* id, int32_t world, int32_t rank, int32_t device
   return WSR_OK;
 }
 
+int wsr_loopback_create(int32_t world, wsr_loopback** out) {
+  if (!out || world < 1 || world > kMaxOwners) return fail(WSR_E_INVALID, "bad loopback arguments");
+  *out = new wsr_loopback();
+  (*out)->world = world;
+  return WSR_OK;
+}
+
+void wsr_loopback_destroy(wsr_loopback* l) { delete l; }
+
+int wsr_comm_open_loopback(wsr_loopback* l, int32_t rank, int32_t device, wsr_comm** out) {
+  if (!l || !out || rank < 0 || rank >= l->world) return fail(WSR_E_INVALID, "bad loopback comm arguments");
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return fail(WSR_E_HIP, "hipSetDevice failed");
+  std::unique_ptr<wsr_comm> c(new wsr_comm());
+  c->loop = l;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->loop_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->loop_read, hipEventDisableTiming) != hipSuccess) {
+    if (c->loop_ready) (void)hipEventDestroy(c->loop_ready);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    return fail(WSR_E_HIP, "hipStreamCreate / hipEventCreate failed");
+  }
+  c->world = l->world;
+  c->rank = rank;
+  c->device = device;
+  c->defer = env_number("WSR_REPLAY_DEFER", 1) != 0;
+  wsr_comm* cp = c.get();
+  cp->worker = std::thread([cp] { exchange_worker(cp); });
+  *out = c.release();
+  return WSR_OK;
+}
+
 void wsr_comm_close(wsr_comm* c) {
   if (!c) return;
   (void)wsr_comm_flush(c);   // (every deferred replay enqueued before the worker stops)
@@ -1544,6 +1648,8 @@ void wsr_comm_close(wsr_comm* c) {
     if (S.recv) (void)hipFree(S.recv);
   }
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->loop_ready) (void)hipEventDestroy(c->loop_ready);
+  if (c->loop_read) (void)hipEventDestroy(c->loop_read);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

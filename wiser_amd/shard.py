@@ -79,14 +79,36 @@ def slot_for_fill(max_fill: int, qpr: int) -> int:
     return int(max(2 * max_fill, 8 * qpr, 1024))
 
 
+class LoopbackGroup:
+    """wsr_loopback: the world ranks of a sharded engine in ONE process (one
+    NativeShardedSearcher each, loopback=this), their step groups' all-to-all
+    done by device copies between the ranks' exchange buffers -- the RCCL
+    path's regions, runs, slots and deferred owner replays at world > 1, with
+    only the transport replaced (tests, one-GPU rehearsals).  Every rank must
+    submit the same step groups in the same order; destroy after closing the
+    searchers."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self._l = C.c_void_p()
+        check(lib.wsr_loopback_create(world, C.byref(self._l)))
+
+    def close(self):
+        if self._l:
+            lib.wsr_loopback_destroy(self._l)
+            self._l = None
+
+
 class NativeShardedSearcher:
     """One rank of a doc-range sharded engine whose whole step runs in C++
     (wsr_shard_step: run with fused emission + one ncclAllToAll + owner replay)."""
 
     def __init__(self, index_dir: str, rank: int, world: int, share_id, device: int = 0,
-                 threads: int = 0, positions: bool = False):
+                 threads: int = 0, positions: bool = False, loopback=None):
         """share_id(bytes_or_None) -> bytes: the launcher's rendezvous; rank 0
-        passes the RCCL id it made, every rank gets rank 0's id back."""
+        passes the RCCL id it made, every rank gets rank 0's id back.
+        loopback: a LoopbackGroup instead (every rank in this process, the
+        all-to-all by device copies: tests and one-GPU rehearsals)."""
         from .engine import VacuumEngine
         self.rank, self.world = rank, world
         self.n_docs = index_doc_count(index_dir)
@@ -94,13 +116,16 @@ class NativeShardedSearcher:
         self.engine = VacuumEngine(index_dir, device=device, threads=threads,
                                    doc_range=self.doc_range if world > 1 else None, positions=positions)
         self.engine.Load()
-        uid = (C.c_uint8 * 128)()
-        if rank == 0:
-            check(lib.wsr_comm_unique_id(uid))
-        got = share_id(bytes(uid) if rank == 0 else None)
-        uid = (C.c_uint8 * 128).from_buffer_copy(got)
         c = C.c_void_p()
-        check(lib.wsr_comm_open(uid, world, rank, device, C.byref(c)))
+        if loopback is not None:
+            check(lib.wsr_comm_open_loopback(loopback._l, rank, device, C.byref(c)))
+        else:
+            uid = (C.c_uint8 * 128)()
+            if rank == 0:
+                check(lib.wsr_comm_unique_id(uid))
+            got = share_id(bytes(uid) if rank == 0 else None)
+            uid = (C.c_uint8 * 128).from_buffer_copy(got)
+            check(lib.wsr_comm_open(uid, world, rank, device, C.byref(c)))
         self._c = c
 
     def step(self, b, qpr: int, slot: int):
