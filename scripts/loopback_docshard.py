@@ -29,7 +29,8 @@ def main():
     from wiser_amd.shard import LoopbackGroup, NativeShardedSearcher, slot_for_fill
     idx, qlog, _ = bench.ensure_c3(a)
     lines = [l.split() for l in open(qlog).read().splitlines()]
-    B, nb, group, passes = 4096, 8, 8, 6
+    B, nb, group, passes = 4096, 16, 4, 3   # 4 groups in rotation: the deferred replays
+    # (kReplayLag = 2 groups) ride the lean kernels as in bench.py's loop
     chunks = [lines[i * B:(i + 1) * B] for i in range(nb)]
 
     def qarr(eng, chunk):
