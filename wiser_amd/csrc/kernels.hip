@@ -2384,6 +2384,20 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
   // item (a floor seed, below).
   uint32_t wb = b0, we = min(b0 + 64u, b1);
   float bmax = wb + l < we ? ix.bmax[Q.a_blk0 + wb + l] * idf_f : 0.0f;
+  // the next window's directory and bounds, loaded one window ahead (a
+  // window switch is then LDS stores, not a round trip to memory)
+  uint4 nx_dblk = {0u, 0u, 0u, 0u};
+  uint32_t nx_dmeta = 0u;
+  float nx_bmax = 0.0f;
+  auto prefetch_window = [&](uint32_t from) __attribute__((always_inline)) {
+    const uint32_t to = min(from + 64u, b1);
+    if (from + l < to) {
+      nx_dblk = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + from + l];
+      nx_dmeta = ix.blk_meta[Q.a_blk0 + from + l];
+      nx_bmax = ix.bmax[Q.a_blk0 + from + l] * idf_f;
+    }
+  };
+  prefetch_window(we);
   const bool pre_in = !wide && b0 > 64u - l;   // block b0 - 64 + l, list block >= 1
   const float pre = ix.bmax[Q.a_blk0 + (pre_in ? b0 - 64u + l : 0u)];
   uint64_t floor_bits = prev_pub ? floor_max(floor0) : 0ull;   // (floor0: the caller's floor_lanes)
@@ -2616,17 +2630,19 @@ __device__ __forceinline__ void single_segment(const IndexArgs& ix, LeanLdsT<kPh
       if (R0.b >= we) break;
     }
     if (we >= b1) break;
-    // the next window: its directory and block bounds (one round of loads)
+    // the next window: its directory and block bounds from the registers
+    // loaded a window earlier, and the loads of the one after it
     // (its blocks' survivors go on queueing behind this window's)
     wb = we;
     we = min(wb + 64u, b1);
     __builtin_amdgcn_wave_barrier();
     if (wb + l < we) {
-      S.dblk[l] = reinterpret_cast<const uint4*>(ix.blocks)[Q.a_blk0 + wb + l];
-      S.dmeta[l] = ix.blk_meta[Q.a_blk0 + wb + l];
+      S.dblk[l] = nx_dblk;
+      S.dmeta[l] = nx_dmeta;
     }
-    bmax = wb + l < we ? ix.bmax[Q.a_blk0 + wb + l] * idf_f : 0.0f;
+    bmax = wb + l < we ? nx_bmax : 0.0f;
     __builtin_amdgcn_wave_barrier();
+    prefetch_window(we);
   }
   if (kSingleQueue && qtail != qhead) score_chunk(qtail - qhead);
   // (the last evb events stay in S.evs for finish_lean_item)
