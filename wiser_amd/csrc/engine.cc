@@ -163,6 +163,7 @@ struct wsr_batch {
   bool has_wide = false;         // ... a query with k > kMaxK (wide_replay_kernel)
   bool two_conj = false;         // every conjunctive query: two terms (or empty), k <= kMaxK
   bool two_ph = false;           // every phrase query: k <= kMaxK (a lean one has two terms)
+  bool one_conj = false;         // every conjunctive query: one term (or empty)
   uint32_t seg_cap = kSegCost;   // driver blocks per work item at most (wsr_batch_set_item_blocks)
   int seg_grid = 0;
   int lean_wgs = 0;      // the conjunctive lean instance's grid
@@ -746,7 +747,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   // persistent grids: lean items run in lean_kernel, the rest in segment_kernel
   uint64_t lean_need = 0, lean_need_ph = 0, gen_need = 0;
   const float dense_ratio = h->args.dense_ratio;
-  bool has_phrase = false, has_wide = false, two_conj = true, two_ph = true, gen_phrase = false;
+  bool has_phrase = false, has_wide = false, two_conj = true, two_ph = true, one_conj = true, gen_phrase = false;
   std::vector<int32_t> ids;
   for (int i = 0; i < nq; ++i) {
     const wsr_query& s = q[i];
@@ -758,7 +759,10 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
     has_phrase = has_phrase || phrase;
     has_wide = has_wide || s.k > kMaxK;
     if (phrase) two_ph = two_ph && s.k <= kMaxK;
-    else two_conj = two_conj && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
+    else {
+      two_conj = two_conj && s.k <= kMaxK && (s.n_terms == 2 || s.n_terms <= 0 || s.k <= 0);
+      one_conj = one_conj && (s.n_terms == 1 || s.n_terms <= 0 || s.k <= 0);
+    }
     QueryIn& d = in[i];
     d.n_terms = s.n_terms < 0 ? 0 : s.n_terms;
     d.k = s.k < 0 ? 0 : s.k;
@@ -848,6 +852,7 @@ int wsr_batch_upload(wsr_handle* h, wsr_batch* b, const wsr_query* q, int32_t nq
   b->has_conj_lean = lean_need > 0;
   b->has_gen = gen_need > 0;
   b->two_ph = two_ph;
+  b->one_conj = one_conj && !two_conj;   // (a batch of empty queries only: the two-term instance)
   // persistent grid: never more workgroups than work items can exist
   // (at least one worker each: a grid also drains items the estimate missed)
   b->seg_grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(h->gen_cap, gen_need)));
@@ -967,7 +972,8 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
       HIP_OK(hipStreamWaitEvent(b->st_pad, b->fork, 0));
       if (run_conj)
         HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
-                           b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->st_pad));
+                           b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->one_conj,
+                           b->st_pad));
       if (pb) {   // the replay's end: behind the conjunctive launch that carried it
         HIP_OK(hipEventRecord(pb->xev[1], b->st_pad));
         pb_queued = true;
@@ -977,10 +983,10 @@ static int batch_run(wsr_handle* h, wsr_batch* b, const ShardEmit* se, const Own
       frp.oj = OwnerJob{};
       HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt,
                          lean_stats + static_cast<size_t>(kStatStride) * kLeanWaves * b->lean_wgs,
-                         b->lean_wgs_ph, frp, b->d_itemq, b->d_pub, b->d_desc, true, b->two_ph, st));
+                         b->lean_wgs_ph, frp, b->d_itemq, b->d_pub, b->d_desc, true, b->two_ph, false, st));
     } else {
       HIP_OK(launch_lean(h->args, b->d_q, b->d_plan, b->nq, b->d_ctr, b->d_events, b->d_evcnt, lean_stats,
-                         b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, st));
+                         b->lean_wgs, fr, b->d_itemq, b->d_pub, b->d_desc, false, b->two_conj, b->one_conj, st));
     }
     HIP_OK(hipEventRecord(b->ev[4], st));
     if (pb && !pb_queued) {

@@ -179,11 +179,13 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 // lean_grid workgroups of kLeanWaves waves; stats of wave w at stats[w * kStatStride];
 // phrase: the lean phrase queries' items (the phrase instance; their lean
 // ones have two terms), else the conjunctive lean items;
-// two: every query of those items has two terms and k <= kMaxK
+// two: every query of those items has two terms and k <= kMaxK;
+// one (conjunctive only): every query of those items has one term
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, hipStream_t st);
+                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, bool one,
+                       hipStream_t st);
 int lean_kernel_occupancy(bool phrase);   // workgroups per CU
 // queries with k > kMaxK (their segments emitted every survivor): heap in LDS
 hipError_t launch_wide_replay(const QueryIn* q, const QueryPlan* plan, int nq, const Event* events,

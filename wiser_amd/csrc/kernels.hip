@@ -3153,7 +3153,10 @@ __device__ __noinline__ void owner_replay_tail(const QueryIn* qs, const int32_t*
 // 4 (profiles/r02_pr2_ab.txt).  The phrase instance: 4 (kLeanWgsPhrase).
 constexpr int kLeanWgs = kLeanDeep ? 4 : 5;   // (a deeper pipeline's register sets: 4)
 constexpr int kLeanWgsPhrase = 4;
-template <bool kPh, bool kTwo = false>
+// kOne: every item of the launch is a single-term query's (single_high,
+// single_low, a batch former's single-term batches): only single_segment is
+// compiled in, so the instance keeps its registers for it (no spills).
+template <bool kPh, bool kTwo = false, bool kOne = false>
 __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) void lean_kernel(
     IndexArgs ix, const QueryIn* __restrict__ qs, const QueryPlan* __restrict__ plan, int nq,
     uint32_t* __restrict__ counters, Event* __restrict__ events, uint32_t* __restrict__ ev_cnt,
@@ -3221,6 +3224,10 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
       const bool phrase =
           kPh && (Q.nt & 0xFFFFu) > 1 && (uni(static_cast<uint32_t>(qs[qi].flags)) & kQueryPhrase);
       const int32_t* ql = qlist_of(qs, static_cast<int>(qi));
+      if constexpr (kOne) {
+        single_segment<kPh>(ix, S, norm, Q, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, floor0, prev_pub, r, my_pub,
+                            ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
+      } else {
       if (!kTwo && !kPh && (Q.slots >> 16) == kNoSlot)   // one term (never a phrase instance's item)
         single_segment<kPh>(ix, S, norm, Q, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1, floor0, prev_pub, r, my_pub,
                             ev_out,
@@ -3231,6 +3238,7 @@ __global__ __launch_bounds__(64 * kLeanWaves, kPh ? kLeanWgsPhrase : kLeanWgs) v
       else
         lean_segment<kPh, kTwo, false, kPh ? 0 : kLeanDeep>(ix, S, norm, Q, ql, phrase, b0, b1, dtail, tdoc0, tdoc1, ttf0, ttf1,
                                        floor0, prev_pub, r, my_pub, ev_out, ev_n, evb, pt, pt_n, last_pub, n_surv, n_dblk);
+      }
     }
     // The item's end from the events still in LDS where it can (finish_item
     // otherwise): every event of the item is there when ev_n == evb.
@@ -3410,11 +3418,15 @@ hipError_t launch_segments(const IndexArgs& ix, const QueryIn* q, const QueryPla
 hipError_t launch_lean(const IndexArgs& ix, const QueryIn* q, const QueryPlan* plan, int nq,
                        uint32_t* counters, Event* events, uint32_t* ev_cnt, uint32_t* stats,
                        int lean_wgs, const FusedReplay& fr, const uint32_t* item_q,
-                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, hipStream_t st) {
+                       uint64_t* pub, const QueryDesc* desc, bool phrase, bool two, bool one,
+                       hipStream_t st) {
   // (a persistent grid sized for the conjunctive instance: waves of a larger
   // instance that find no room start later and find the queue drained)
   const dim3 g(lean_wgs), b(64 * kLeanWaves);
-  if (phrase && two)
+  if (!phrase && one)
+    hipLaunchKernelGGL((lean_kernel<false, false, true>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
+                       stats, fr, item_q, pub, desc);
+  else if (phrase && two)
     hipLaunchKernelGGL((lean_kernel<true, true>), g, b, 0, st, ix, q, plan, nq, counters, events, ev_cnt,
                        stats, fr, item_q, pub, desc);
   else if (phrase)
