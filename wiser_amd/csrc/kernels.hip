@@ -1589,6 +1589,8 @@ constexpr bool kPosWindow = true;
 // PosStream takes its first pack record from the bag's word pair (pos_start)
 // instead of a dependent pos_pk load.
 constexpr bool kPosBag = true;
+// phrase_match2 primes both bags' first windows before the merge pops
+constexpr bool kPosPrime = true;
 
 // waves per SIMD the segment kernel is compiled for (register budget)
 constexpr int kSegWaves = 3;
@@ -1637,6 +1639,17 @@ struct PosStream {
     }
     w0 = w1 = 0;
     wb = -(1 << 30);
+  }
+  // (kPosPrime) the window of the bag's first position, loaded before either
+  // stream of a pair pops, so the two bags' first pack reads share one round
+  // trip (the pack record came with the start; without it, next() loads it)
+  __device__ __forceinline__ void prime() {
+    if (!kPosWindow || e >= end || pk != (e >> 7)) return;
+    const int32_t bit = static_cast<int32_t>((e & 127u) * bits);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(__builtin_align_down(data + (bit >> 3), 4));
+    w0 = w[0];
+    w1 = w[1];
+    wb = static_cast<int32_t>(reinterpret_cast<const uint8_t*>(w) - data) * 8;
   }
   // pop the next position (false past the bag's end)
   __device__ __forceinline__ bool next(const IndexArgs& ix, const PosDev& P) {
@@ -1735,6 +1748,10 @@ __device__ __forceinline__ bool phrase_match2(const IndexArgs& ix, uint32_t l0, 
   PosStream s0, s1;
   s0.init(ix, P0, slot0, tf0);
   s1.init(ix, P1, slot1, tf1);
+  if (kPosPrime) {
+    s0.prime();
+    s1.prime();
+  }
   if (!s0.next(ix, P0) || !s1.next(ix, P1)) return false;
   for (;;) {
     const int32_t a = s0.cur + 1, b = s1.cur;
